@@ -1,0 +1,171 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark: forward + inverse negacyclic NTT, N = 2^16, L = 44 limbs
+(BASELINE.json configs[1]; limbs 0..43 of the examples/3_ckks.cu:796-803 chain).
+
+One step = forward NTT followed by inverse NTT of one [44][65536] uint64 batch that is
+already resident in HBM.  Each step uses the next buffer of a ring whose total size
+(> 256 MiB) exceeds the Infinity Cache, so every forward transform reads its input from HBM.
+value = algorithmic bytes (16 B per coefficient per transform, the convention of the
+reference's benchmark/ntt_bench.cu:96-97) of all steps on all ranks / max-over-ranks time.
+
+Multi-GPU: one process per GPU; each rank transforms its own independent batches (weak
+scaling, no data-path collective: ciphertext limbs are independent).
+
+roofline: the forward transform (column pass + row pass kernels) timed with HIP events on
+the stream the kernels run on; achieved = 46,137,344 B / average forward duration.
+cpu_baseline: the oracle's scalar C restatement (oracle/liboracle.so) on a bounded sample.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "phantom-fhe-boot_amd", "py"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+N = 1 << 16
+L = 44
+C3_BITS = [60] + [50] * 44 + [60] * 15
+BYTES_PER_TRANSFORM = 16 * N * L  # 46,137,344
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+RING_BYTES = 320 << 20  # > 256 MiB Infinity Cache
+
+
+def cpu_baseline(mods, seconds=12.0):
+    """Scalar oracle NTT (forward + inverse of the same [44][65536] batch), 1 thread."""
+    import oracle_lib as O
+    plan = O.lib().or_ntt_plan_create(N, L, O.P(O.arr(mods)))
+    a = O.random_limbs(np.random.default_rng(0x5EED), N, mods)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        O.lib().or_ntt_plan_fwd(plan, O.P(a), L, 1)
+        O.lib().or_ntt_plan_inv(plan, O.P(a), L, 1)
+        steps += 1
+    dt = time.perf_counter() - t0
+    O.lib().or_ntt_plan_destroy(plan)
+    return {
+        "value": round(2 * BYTES_PER_TRANSFORM * steps / dt / 1e9, 3),
+        "unit": "GB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{steps} steps of fwd+inv NTT on one [44][65536] batch, scalar C oracle, {dt:.1f}s",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import phantom_amd as PA
+    lib = PA.load()
+    mods = PA.coeff_modulus_create(N, C3_BITS)[:L]
+    tables = PA.NttTables(N, mods)
+
+    nbuf = max(2, RING_BYTES // (8 * N * L) + 1)
+    rng = np.random.default_rng(0x5EED + rank)
+    base = np.concatenate([rng.integers(0, q, size=N, dtype=np.uint64) for q in mods])
+    ring = [torch.from_numpy(base.view(np.int64)).cuda() for _ in range(nbuf)]
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    def step(i, ev=None):
+        d = ring[i % nbuf].data_ptr()
+        if ev is not None:
+            ev[0].record(stream)
+        PA.check(lib.phantom_nwt_forward_inplace(d, tables.handle, L, 0, sh))
+        if ev is not None:
+            ev[1].record(stream)
+        PA.check(lib.phantom_nwt_backward_inplace(d, tables.handle, L, 0, sh))
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i, events[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    fwd_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    if world > 1:
+        t = torch.tensor([elapsed, fwd_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, fwd_ms = float(t[0]), float(t[1])
+
+    # parity spot-check of the last buffer state is done by tests/; here just sanity
+    total_bytes = 2 * BYTES_PER_TRANSFORM * args.steps * world
+    value = total_bytes / elapsed / 1e9
+    achieved = BYTES_PER_TRANSFORM / (fwd_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        out = {
+            "metric": "NTT GB/s vs HBM roofline (fwd+inv NTT, N=2^16, L=44)",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic uniform residues in [0, q_i), seed 0x5EED",
+            "config": {
+                "workload": "C2: forward+inverse negacyclic NTT, N=65536, 44 RNS limbs of the 3_ckks.cu C3 chain",
+                "poly_modulus_degree": N,
+                "limbs": L,
+                "batch_per_rank": 1,
+                "buffer_ring": nbuf,
+                "parallelism": f"replicas x{world} (independent batches per rank)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "forward NTT (ntt_col_pass + ntt_row_pass)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "fwd_ms": round(fwd_ms, 5),
+                "traffic": None,
+            },
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(mods)
+        print(json.dumps(out), flush=True)
+    tables.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,58 @@
+// ntt.h — negacyclic NTT / INTT over RNS limbs on gfx950.
+//
+// Replaces the reference's launcher family of include/ntt.cuh:157-226
+// (nwt_2d_radix8_forward_inplace, nwt_2d_radix8_backward_inplace, the _scale,
+// _include_special_mod, _exclude_range and out-of-place variants).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace phx {
+
+// Device-resident NTT tables for a list of moduli (the reference's DNTTTable,
+// include/ntt.cuh:36-129).  Layout [num_moduli][n] for every table.
+struct NttTables {
+  size_t n = 0;
+  int log_n = 0;
+  size_t num_moduli = 0;
+  uint64_t* modulus = nullptr;   // [num_moduli]
+  uint64_t* barrett = nullptr;   // [num_moduli][2] floor(2^128/q) {lo, hi}
+  uint64_t* tw = nullptr;        // tw[brv(i)] = psi^i
+  uint64_t* tw_shoup = nullptr;
+  uint64_t* itw = nullptr;       // itw[brv(i)] = psi^-i (n^-1 NOT folded in; applied separately)
+  uint64_t* itw_shoup = nullptr;
+  uint64_t* n_inv = nullptr;     // [num_moduli]
+  uint64_t* n_inv_shoup = nullptr;
+};
+
+// Which table row each buffer limb uses.  Buffer limb i (0 <= i < num_limbs) maps to
+// table row (i < split ? first_a + i : first_b + (i - split)); limbs in
+// [skip_begin, skip_end) are left untouched (the reference's exclude_range).
+struct LimbMap {
+  int num_limbs = 0;
+  int split = 0;
+  int first_a = 0;
+  int first_b = 0;
+  int skip_begin = 0;
+  int skip_end = 0;
+  static LimbMap contiguous(int num_limbs, int first) {
+    LimbMap m;
+    m.num_limbs = num_limbs; m.split = num_limbs; m.first_a = first; m.first_b = 0;
+    return m;
+  }
+};
+
+// Forward NTT, out-of-place allowed (out may equal in).  Output fully reduced, bit-reversed
+// order (A[i] = a(psi^(2 brv(i) + 1))), identical to nwt_2d_radix8_forward_inplace.
+hipError_t ntt_forward(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
+                       hipStream_t stream);
+
+// Inverse NTT.  When scale/scale_shoup are given (one value per buffer limb, indexed by
+// buffer limb), the output is additionally multiplied by scale[i] (the reference's
+// nwt_2d_radix8_backward_scale used by modup, src/ntt/ntt_modup.cu:356-393).
+hipError_t ntt_inverse(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
+                       const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream);
+
+}  // namespace phx

@@ -1,0 +1,88 @@
+#include "ntt_tables.h"
+
+#include <stdexcept>
+#include <thread>
+
+#include "hip_check.h"
+#include "numth.h"
+
+namespace phantom {
+
+using namespace phantom::arith;
+
+HostNttTable make_host_ntt_table(size_t n, uint64_t q) {
+  const int logn = log2_exact(n);
+  if (logn < 0) throw std::invalid_argument("ring degree must be a power of two");
+  HostNttTable h;
+  h.q = q;
+  h.psi = minimal_primitive_root(2 * n, q);
+  const uint64_t ipsi = inv_mod(h.psi, q);
+  h.tw.resize(n); h.tw_shoup.resize(n); h.itw.resize(n); h.itw_shoup.resize(n);
+  uint64_t p = 1, ip = 1;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t r = reverse_bits(static_cast<uint32_t>(i), logn);
+    h.tw[r] = p;
+    h.itw[r] = ip;
+    p = mul_mod(p, h.psi, q);
+    ip = mul_mod(ip, ipsi, q);
+  }
+  for (size_t i = 0; i < n; ++i) {
+    h.tw_shoup[i] = shoup(h.tw[i], q);
+    h.itw_shoup[i] = shoup(h.itw[i], q);
+  }
+  h.n_inv = inv_mod(n % q, q);
+  h.n_inv_shoup = shoup(h.n_inv, q);
+  return h;
+}
+
+DeviceNttTables::DeviceNttTables(size_t n, const std::vector<uint64_t>& moduli, hipStream_t stream)
+    : moduli_(moduli) {
+  const size_t L = moduli.size();
+  t_.n = n;
+  t_.log_n = log2_exact(n);
+  t_.num_moduli = L;
+  if (t_.log_n < 10 || t_.log_n > 17) throw std::invalid_argument("unsupported polynomial degree");
+
+  std::vector<HostNttTable> host(L);
+  {
+    // table generation is O(n L) host work per context; spread it over a few threads
+    const unsigned nt = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 16u);
+    std::vector<std::thread> th;
+    for (unsigned w = 0; w < nt; ++w)
+      th.emplace_back([&, w] {
+        for (size_t i = w; i < L; i += nt) host[i] = make_host_ntt_table(n, moduli[i]);
+      });
+    for (auto& x : th) x.join();
+  }
+  std::vector<uint64_t> flat(n * L), mod(L), bar(2 * L), ninv(L), ninvs(L);
+  for (size_t i = 0; i < L; ++i) {
+    mod[i] = moduli[i];
+    barrett_ratio(moduli[i], &bar[2 * i]);
+    ninv[i] = host[i].n_inv;
+    ninvs[i] = host[i].n_inv_shoup;
+  }
+  auto alloc_copy = [&](uint64_t*& dst, const std::vector<uint64_t>& src) {
+    PHX_CHECK(hipMalloc(&dst, src.size() * sizeof(uint64_t)));
+    PHX_CHECK(hipMemcpyAsync(dst, src.data(), src.size() * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+  };
+  alloc_copy(t_.modulus, mod);
+  alloc_copy(t_.barrett, bar);
+  alloc_copy(t_.n_inv, ninv);
+  alloc_copy(t_.n_inv_shoup, ninvs);
+  auto gather = [&](uint64_t*& dst, std::vector<uint64_t> HostNttTable::*member) {
+    for (size_t i = 0; i < L; ++i) std::copy((host[i].*member).begin(), (host[i].*member).end(), flat.begin() + i * n);
+    alloc_copy(dst, flat);
+    PHX_CHECK(hipStreamSynchronize(stream));  // flat is reused
+  };
+  gather(t_.tw, &HostNttTable::tw);
+  gather(t_.tw_shoup, &HostNttTable::tw_shoup);
+  gather(t_.itw, &HostNttTable::itw);
+  gather(t_.itw_shoup, &HostNttTable::itw_shoup);
+}
+
+DeviceNttTables::~DeviceNttTables() {
+  for (uint64_t* p : {t_.modulus, t_.barrett, t_.tw, t_.tw_shoup, t_.itw, t_.itw_shoup, t_.n_inv, t_.n_inv_shoup})
+    if (p) (void)hipFree(p);
+}
+
+}  // namespace phantom

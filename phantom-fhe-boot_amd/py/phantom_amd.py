@@ -1,0 +1,110 @@
+"""ctypes binding of libphantom_amd.so (include/phantom_amd.h) for tests and bench.py.
+
+The product is the C-ABI library; this module only loads it and declares signatures.
+It raises if the library is missing — there is no Python or CPU fallback.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libphantom_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "phantom_amd.h")
+
+u64p = ctypes.POINTER(ctypes.c_uint64)
+vp = ctypes.c_void_p
+sz = ctypes.c_size_t
+
+_SIGS = {
+    "phantom_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "phantom_last_error": (ctypes.c_char_p, []),
+    "phantom_version": (ctypes.c_char_p, []),
+    "phantom_coeff_modulus_create": (ctypes.c_int, [sz, ctypes.POINTER(ctypes.c_int), sz, u64p]),
+    "phantom_ntt_tables_create": (ctypes.c_int, [sz, u64p, sz, ctypes.POINTER(vp)]),
+    "phantom_ntt_tables_destroy": (ctypes.c_int, [vp]),
+    "phantom_ntt_tables_host": (ctypes.c_int, [vp, sz, u64p, u64p, u64p, u64p, u64p]),
+    "phantom_nwt_forward_inplace": (ctypes.c_int, [vp, vp, sz, sz, vp]),
+    "phantom_nwt_backward_inplace": (ctypes.c_int, [vp, vp, sz, sz, vp]),
+    "phantom_nwt_backward": (ctypes.c_int, [vp, vp, vp, sz, sz, vp]),
+    "phantom_nwt_backward_scale": (ctypes.c_int, [vp, vp, vp, sz, sz, vp, vp, vp]),
+    "phantom_nwt_forward_include_special_mod_exclude_range": (ctypes.c_int, [vp, vp, sz, sz, sz, sz, sz, sz, vp]),
+    "phantom_nwt_backward_inplace_include_special_mod": (ctypes.c_int, [vp, vp, sz, sz, sz, sz, vp]),
+}
+
+_lib = None
+
+
+class PhantomError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libphantom_amd.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        # One HIP runtime per process: torch bundles its own libamdhip64 (soname
+        # libamdhip64.so.7).  Loading torch first makes this library bind to that same
+        # runtime instead of pulling a second copy from /opt/rocm.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not os.path.exists(LIB_PATH):
+            raise PhantomError(f"{LIB_PATH} missing: run __graft_entry__.build() (no fallback path exists)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            if hasattr(lib, name):
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(status):
+    if status != 0:
+        lib = load()
+        raise PhantomError(f"{lib.phantom_status_string(status).decode()}: {lib.phantom_last_error().decode()}")
+
+
+def declared_symbols(header=HEADER_PATH):
+    """Names of every function declared in include/phantom_amd.h."""
+    import re
+    txt = open(header).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(phantom_[a-z0-9_]+)\s*\(", txt)))
+
+
+def u64_array(values):
+    arr = (ctypes.c_uint64 * len(values))(*values)
+    return arr
+
+
+def coeff_modulus_create(n, bit_sizes):
+    lib = load()
+    bs = (ctypes.c_int * len(bit_sizes))(*bit_sizes)
+    out = (ctypes.c_uint64 * len(bit_sizes))()
+    check(lib.phantom_coeff_modulus_create(n, bs, len(bit_sizes), out))
+    return list(out)
+
+
+class NttTables:
+    """Owning handle of a phantom_ntt_tables (device NTT tables for a modulus list)."""
+
+    def __init__(self, n, moduli):
+        lib = load()
+        self.n = n
+        self.moduli = list(moduli)
+        h = vp()
+        check(lib.phantom_ntt_tables_create(n, u64_array(self.moduli), len(self.moduli), ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            load().phantom_ntt_tables_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
