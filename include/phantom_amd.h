@@ -79,6 +79,59 @@ int phantom_nwt_backward_inplace_include_special_mod(uint64_t *inout, const phan
                                                      size_t coeff_modulus_size, size_t start_modulus_idx,
                                                      size_t size_QP, size_t size_P, hipStream_t stream);
 
+/* ---- context (PhantomContext, include/context.cuh:133-272; src/context.cu:121-232) ------ */
+typedef struct phantom_context phantom_context;
+/* moduli: the full key-level chain (data primes then special_modulus_size special primes),
+ * as produced by CoeffModulus::Create; scheme is CKKS. */
+int phantom_context_create(size_t poly_modulus_degree, const uint64_t *moduli, size_t count,
+                           size_t special_modulus_size, phantom_context **out);
+int phantom_context_destroy(phantom_context *ctx);
+/* number of data primes at chain_index (chain 0 = key level Q u P, 1 = Q, ...) */
+size_t phantom_context_coeff_modulus_size(const phantom_context *ctx, size_t chain_index);
+
+/* ---- CKKS evaluation on raw device ciphertexts --------------------------------------- */
+/* tensor_prod_2x2_rns_poly (src/polymath.cu:501-536) via bgv_ckks_multiply (src/evaluate.cu:415-473):
+ * ct1, ct2 are [2][L][n] at chain_index, out [3][L][n] (out may alias ct1's storage if sized for 3) */
+int phantom_multiply(const phantom_context *ctx, size_t chain_index, const uint64_t *ct1, const uint64_t *ct2,
+                     uint64_t *out, hipStream_t stream);
+/* relinearize_inplace (src/evaluate.cu:1552-1589) -> keyswitch_inplace (src/eval_key_switch.cu:112-212):
+ * ct is [3][L][n]; on return its first two polys hold the relinearized ciphertext.
+ * key_digits: host array of dnum device pointers, each a [2][size_QP][n] key digit. */
+int phantom_relinearize(const phantom_context *ctx, size_t chain_index, uint64_t *ct,
+                        const uint64_t *const *key_digits, size_t dnum, hipStream_t stream);
+/* keyswitch_inplace core: ct [2][L][n] += KeySwitch(c2 [L][n]) */
+int phantom_keyswitch(const phantom_context *ctx, size_t chain_index, uint64_t *ct, const uint64_t *c2,
+                      const uint64_t *const *key_digits, size_t dnum, hipStream_t stream);
+/* DRNSTool::modup (src/rns_bconv.cu:530-628): c2 [L][n] NTT form -> t_mod_up [beta][L+P][n] */
+int phantom_modup(const phantom_context *ctx, size_t chain_index, const uint64_t *c2, uint64_t *t_mod_up,
+                  hipStream_t stream);
+/* key_switch_inner_prod (include/evaluate.cuh:27-29, src/eval_key_switch.cu:88-109) */
+int phantom_keyswitch_inner_prod(const phantom_context *ctx, size_t chain_index, const uint64_t *t_mod_up,
+                                 const uint64_t *const *key_digits, size_t dnum, uint64_t *cx, hipStream_t stream);
+/* DRNSTool::moddown_from_NTT (src/rns_bconv.cu:791-843): cx_i [L+P][n] NTT form (P limbs clobbered)
+ * -> out [L][n] = (cx_i - NTT(bconv(INTT(cx_i|P)))) * P^-1 */
+int phantom_moddown_from_ntt(const phantom_context *ctx, size_t chain_index, uint64_t *cx_i, uint64_t *out,
+                             hipStream_t stream);
+/* rescale_to_next (src/evaluate.cu:1779-1801) -> divide_and_round_q_last_ntt (src/rns.cu:1160-1184):
+ * in [polys][L][n] at chain_index -> out [polys][L-1][n] */
+int phantom_rescale_to_next(const phantom_context *ctx, size_t chain_index, const uint64_t *in, uint64_t *out,
+                            size_t polys, hipStream_t stream);
+/* apply_galois_ntt (src/galois.cu:104-119) with the PrecomputeAutoMapKernel table (src/util.cu:941-958) */
+int phantom_apply_galois_ntt(const phantom_context *ctx, uint32_t galois_elt, const uint64_t *in, uint64_t *out,
+                             size_t coeff_modulus_size, hipStream_t stream);
+/* elementwise ops over limbs [limb_offset, limb_offset + L) of the key-level chain
+ * (add_rns_poly / sub_rns_poly / multiply_rns_poly / negate, src/polymath.cu) */
+#define PHANTOM_POLY_ADD 0
+#define PHANTOM_POLY_SUB 1
+#define PHANTOM_POLY_MUL 2
+#define PHANTOM_POLY_NEGATE 3
+int phantom_poly_op(const phantom_context *ctx, int op, const uint64_t *a, const uint64_t *b, uint64_t *out,
+                    size_t limb_offset, size_t coeff_modulus_size, hipStream_t stream);
+/* switchModulusKernel as used by RaiseMod (src/evaluate.cu:2414-2503): coefficient-form limb 0
+ * lifted to L limbs (centered representative of the q0 residue) */
+int phantom_switch_modulus_raise(const phantom_context *ctx, const uint64_t *in_q0, uint64_t *out,
+                                 size_t coeff_modulus_size, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -252,6 +252,7 @@ static void ntt_inv_one(uint64_t *a, const tables_t *t) {
 }
 
 void or_ntt_fwd(uint64_t *data, size_t n, size_t L, const uint64_t *moduli) {
+#pragma omp parallel for schedule(dynamic)
     for (size_t l = 0; l < L; l++) {
         tables_t t;
         tables_make(&t, n, moduli[l]);
@@ -261,6 +262,7 @@ void or_ntt_fwd(uint64_t *data, size_t n, size_t L, const uint64_t *moduli) {
 }
 
 void or_ntt_inv(uint64_t *data, size_t n, size_t L, const uint64_t *moduli) {
+#pragma omp parallel for schedule(dynamic)
     for (size_t l = 0; l < L; l++) {
         tables_t t;
         tables_make(&t, n, moduli[l]);
@@ -392,6 +394,7 @@ void or_bconv(const uint64_t *in, uint64_t *out, size_t n, const uint64_t *ibase
             qhat_mod_p[i * obase_size + j] = pr;
         }
     }
+#pragma omp parallel for schedule(static)
     for (size_t k = 0; k < n; k++) {
         for (size_t j = 0; j < obase_size; j++) {
             u128 acc = 0;
@@ -466,6 +469,7 @@ void or_keyswitch_inner_prod(const uint64_t *t_mod_up, const uint64_t *const *ev
                              size_t size_ql, size_t size_q, size_t size_p, size_t beta, const uint64_t *qp_full) {
     const size_t size_qlp = size_ql + size_p;
     const size_t size_qp = size_q + size_p;
+#pragma omp parallel for schedule(static)
     for (size_t nid = 0; nid < size_qlp; nid++) {
         size_t twr = nid >= size_ql ? size_q + (nid - size_ql) : nid;
         uint64_t q = qp_full[twr];

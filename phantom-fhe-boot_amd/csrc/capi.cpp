@@ -1,6 +1,6 @@
 // capi.cpp — extern "C" boundary of libphantom_amd.so (declared in include/phantom_amd.h).
 // Converts C++ exceptions into status codes; every compute call is an async enqueue.
-#include "../../include/phantom_amd.h"
+#include "phantom_amd.h"
 
 #include <cstring>
 #include <memory>

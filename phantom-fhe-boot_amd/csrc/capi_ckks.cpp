@@ -1,0 +1,200 @@
+// capi_ckks.cpp — C-ABI entry points for context-level CKKS evaluation on raw device buffers
+// (declared in include/phantom_amd.h).  Thin wrappers over the C++ façade in host/.
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../host/buffer.h"
+#include "../host/capi_internal.h"
+#include "../host/context.h"
+#include "../host/evaluate.h"
+#include "../host/numth.h"
+#include "phantom_amd.h"
+#include "rns.h"
+
+struct phantom_context {
+  std::unique_ptr<phantom::PhantomContext> ctx;
+  std::mutex mu;
+  std::map<std::vector<const uint64_t*>, phantom::DeviceBuffer<const uint64_t*>> key_ptrs;  // cached device arrays
+  std::map<uint32_t, phantom::DeviceBuffer<uint32_t>> perms;                               // galois tables
+
+  const uint64_t* const* device_key_array(const uint64_t* const* host, size_t dnum, size_t need) {
+    if (!host || dnum < need) throw std::invalid_argument("not enough key-switching key digits");
+    std::vector<const uint64_t*> v(host, host + dnum);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = key_ptrs.find(v);
+    if (it == key_ptrs.end()) {
+      phantom::DeviceBuffer<const uint64_t*> d;
+      d.upload(v, nullptr);
+      it = key_ptrs.emplace(v, std::move(d)).first;
+    }
+    return it->second.get();
+  }
+};
+
+using phantom::capi::fail;
+using phantom::capi::from_hip;
+
+namespace {
+const phantom::RnsTool& tool(const phantom_context* c, size_t chain_index) {
+  if (!c) throw std::invalid_argument("null context");
+  if (chain_index < 1 || chain_index >= c->ctx->total_parm_size()) throw std::invalid_argument("invalid chain index");
+  return c->ctx->get_context_data(chain_index).gpu_rns_tool();
+}
+}  // namespace
+
+extern "C" {
+
+int phantom_context_create(size_t n, const uint64_t* moduli, size_t count, size_t special, phantom_context** out) {
+  PHX_CAPI_GUARD({
+    if (!moduli || !out) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    phantom::EncryptionParameters p(phantom::scheme_type::ckks);
+    p.set_poly_modulus_degree(n);
+    std::vector<phantom::arith::Modulus> m;
+    for (size_t i = 0; i < count; ++i) m.emplace_back(moduli[i]);
+    p.set_coeff_modulus(m);
+    p.set_special_modulus_size(special);
+    auto c = std::make_unique<phantom_context>();
+    c->ctx = std::make_unique<phantom::PhantomContext>(p, nullptr);
+    *out = c.release();
+    return PHANTOM_OK;
+  });
+}
+
+int phantom_context_destroy(phantom_context* ctx) {
+  if (ctx) (void)hipDeviceSynchronize();
+  delete ctx;
+  return PHANTOM_OK;
+}
+
+size_t phantom_context_coeff_modulus_size(const phantom_context* ctx, size_t chain_index) {
+  if (!ctx || chain_index >= ctx->ctx->total_parm_size()) return 0;
+  return ctx->ctx->get_context_data(chain_index).coeff_modulus_size();
+}
+
+int phantom_multiply(const phantom_context* ctx, size_t chain_index, const uint64_t* ct1, const uint64_t* ct2,
+                     uint64_t* out, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& rt = tool(ctx, chain_index);
+    return from_hip(phx::tensor_prod_2x2(ct1, ct2, out, ctx->ctx->mod_QP(), ctx->ctx->poly_degree(), rt.size_Ql(),
+                                         stream));
+  });
+}
+
+int phantom_keyswitch(const phantom_context* ctx, size_t chain_index, uint64_t* ct, const uint64_t* c2,
+                      const uint64_t* const* key_digits, size_t dnum, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& rt = tool(ctx, chain_index);
+    auto* c = const_cast<phantom_context*>(ctx);
+    const uint64_t* const* evk = c->device_key_array(key_digits, dnum, rt.beta());
+    phantom::keyswitch_raw(*ctx->ctx, chain_index, ct, c2, evk, stream);
+    return from_hip(hipGetLastError());
+  });
+}
+
+int phantom_relinearize(const phantom_context* ctx, size_t chain_index, uint64_t* ct,
+                        const uint64_t* const* key_digits, size_t dnum, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& rt = tool(ctx, chain_index);
+    const size_t L = rt.size_Ql(), n = ctx->ctx->poly_degree();
+    return phantom_keyswitch(ctx, chain_index, ct, ct + 2 * L * n, key_digits, dnum, stream);
+  });
+}
+
+int phantom_modup(const phantom_context* ctx, size_t chain_index, const uint64_t* c2, uint64_t* t_mod_up,
+                  hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    tool(ctx, chain_index).modup(t_mod_up, c2, ctx->ctx->gpu_rns_tables(), stream);
+    return from_hip(hipGetLastError());
+  });
+}
+
+int phantom_keyswitch_inner_prod(const phantom_context* ctx, size_t chain_index, const uint64_t* t_mod_up,
+                                 const uint64_t* const* key_digits, size_t dnum, uint64_t* cx, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& rt = tool(ctx, chain_index);
+    auto* c = const_cast<phantom_context*>(ctx);
+    const uint64_t* const* evk = c->device_key_array(key_digits, dnum, rt.beta());
+    const auto& pc = *ctx->ctx;
+    return from_hip(phx::keyswitch_inner_prod(t_mod_up, evk, cx, pc.mod_QP().q, pc.mod_QP().barrett, pc.poly_degree(),
+                                              rt.size_Ql(), pc.size_Q(), pc.size_P(), rt.beta(), stream));
+  });
+}
+
+int phantom_moddown_from_ntt(const phantom_context* ctx, size_t chain_index, uint64_t* cx_i, uint64_t* out,
+                             hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    tool(ctx, chain_index).moddown_add(out, cx_i, false, ctx->ctx->gpu_rns_tables(), stream);
+    return from_hip(hipGetLastError());
+  });
+}
+
+int phantom_rescale_to_next(const phantom_context* ctx, size_t chain_index, const uint64_t* in, uint64_t* out,
+                            size_t polys, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& rt = tool(ctx, chain_index);
+    if (rt.size_Ql() < 2) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "end of modulus switching chain reached");
+    rt.rescale_ntt(in, out, polys, ctx->ctx->gpu_rns_tables(), stream);
+    return from_hip(hipGetLastError());
+  });
+}
+
+int phantom_apply_galois_ntt(const phantom_context* ctx, uint32_t galois_elt, const uint64_t* in, uint64_t* out,
+                             size_t L, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (!ctx) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null context");
+    const size_t n = ctx->ctx->poly_degree();
+    if (!(galois_elt & 1) || galois_elt >= 2 * n) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "invalid Galois element");
+    auto* c = const_cast<phantom_context*>(ctx);
+    const uint32_t* perm;
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      auto it = c->perms.find(galois_elt);
+      if (it == c->perms.end()) {
+        const int logn = phantom::arith::log2_exact(n);
+        std::vector<uint32_t> p(n);
+        for (uint32_t j = 0; j < n; ++j) {
+          const uint64_t idx = ((2ull * j + 1) * galois_elt) % (2ull * n);
+          p[phantom::arith::reverse_bits(j, logn)] = phantom::arith::reverse_bits(static_cast<uint32_t>(idx >> 1), logn);
+        }
+        phantom::DeviceBuffer<uint32_t> d;
+        d.upload(p, nullptr);
+        it = c->perms.emplace(galois_elt, std::move(d)).first;
+      }
+      perm = it->second.get();
+    }
+    return from_hip(phx::galois_ntt(in, out, perm, n, L, stream));
+  });
+}
+
+int phantom_poly_op(const phantom_context* ctx, int op, const uint64_t* a, const uint64_t* b, uint64_t* out,
+                    size_t off, size_t L, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (!ctx) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null context");
+    const auto& pc = *ctx->ctx;
+    if (off + L > pc.size_QP()) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "limb range exceeds the chain");
+    const phx::ModView m{pc.mod_QP().q + off, pc.mod_QP().barrett + 2 * off};
+    const size_t n = pc.poly_degree();
+    switch (op) {
+      case PHANTOM_POLY_ADD: return from_hip(phx::poly_add(a, b, out, m, n, L, stream));
+      case PHANTOM_POLY_SUB: return from_hip(phx::poly_sub(a, b, out, m, n, L, stream));
+      case PHANTOM_POLY_MUL: return from_hip(phx::poly_mul(a, b, out, m, n, L, stream));
+      case PHANTOM_POLY_NEGATE: return from_hip(phx::poly_negate(a, out, m, n, L, stream));
+      default: return fail(PHANTOM_ERR_INVALID_ARGUMENT, "unknown op");
+    }
+  });
+}
+
+int phantom_switch_modulus_raise(const phantom_context* ctx, const uint64_t* in_q0, uint64_t* out, size_t L,
+                                 hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (!ctx) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null context");
+    const auto& pc = *ctx->ctx;
+    if (L > pc.size_Q()) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "too many limbs");
+    return from_hip(phx::switch_modulus_raise(in_q0, out, pc.mod_QP().q, pc.mod_QP().barrett, pc.poly_degree(), L,
+                                              stream));
+  });
+}
+
+}  // extern "C"

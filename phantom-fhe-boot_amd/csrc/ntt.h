@@ -25,6 +25,11 @@ struct NttTables {
   uint64_t* itw_shoup = nullptr;
   uint64_t* n_inv = nullptr;     // [num_moduli]
   uint64_t* n_inv_shoup = nullptr;
+  // FP64 path (farith.h), usable for q < 2^50
+  double* modulus_f = nullptr;   // [num_moduli] q
+  double* modulus_inv = nullptr; // [num_moduli] fl(1/q)
+  uint8_t* is_f64 = nullptr;     // [num_moduli] 1 if q < 2^50
+  double* twf = nullptr;         // [num_moduli][n] forward twiddles as centered doubles (|w| <= q/2)
 };
 
 // Which table row each buffer limb uses.  Buffer limb i (0 <= i < num_limbs) maps to

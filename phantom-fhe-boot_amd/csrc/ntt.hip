@@ -1,21 +1,35 @@
 // ntt.hip — two-pass negacyclic NTT / INTT for gfx950.
 //
 // Decomposition (the same factorisation the reference's 2-D radix-8 NTT uses,
-// src/ntt/fntt_2d.cu:9-198, re-designed for wave64 and 64-bit Shoup arithmetic):
+// src/ntt/fntt_2d.cu:9-198, re-designed for wave64 and this engine's arithmetic):
 //   n = S1 * S2.  The first log2(S1) Cooley-Tukey stages only pair elements of the same
-//   column (index mod S2), the last log2(S2) stages only pair elements of the same row
-//   (contiguous S2-element block).  Pass C ("column pass") runs the first stages on a
-//   tile of COLS consecutive columns, pass R ("row pass") runs the last stages on a tile
-//   of whole rows.  Each tile goes HBM -> registers -> (radix-16 rounds with LDS
-//   transposes between them) -> LDS -> HBM with coalesced accesses.
+//   column (index mod S2); the last log2(S2) stages only pair elements of the same row
+//   (contiguous S2-element block).  The column pass runs the first stages on tiles of COLS
+//   consecutive columns, the row pass runs the last stages on tiles of whole rows.  Each
+//   tile goes HBM -> registers -> (radix-16 rounds, LDS transposes between rounds) -> HBM.
 //
-// Stage g of a sub-transform of size S = 2^s pairs local indices p and p + S/2^(g+1)
-// inside block iloc = p >> (s - g); the twiddle is tw[B * 2^g + iloc] with B = 1 for
-// the column pass and B = S1 + row for the row pass, which is exactly the global
-// table index m + i of the reference's in-place CT loop (m = 2^g or S1 * 2^g).
+// Stage g of a sub-transform of size S = 2^s pairs local indices p and p + S/2^(g+1) inside
+// block iloc = p >> (s - g); the twiddle is tw[B * 2^g + iloc] with B = 1 for the column
+// pass and B = S1 + row for the row pass: exactly the table index m + i of the reference's
+// in-place CT loop (m = 2^g or S1 * 2^g).
+//
+// Arithmetic per limb (wave-uniform branch): primes q < 2^50 use exact FP64 arithmetic
+// (farith.h; ~half the instructions of a 64-bit integer Shoup butterfly on gfx950), other
+// primes use integer Shoup butterflies (arith.h).  In the FP64 forward path the column pass
+// leaves IEEE doubles (exact integers, |x| <= 3q) in the buffer for the row pass, which
+// writes canonical residues; the integer path keeps the reference's lazy [0, 4q) values.
+//
+// Latency hiding: both passes are persistent — a workgroup (column pass) or a wavefront
+// (row pass) walks a strided list of tiles and prefetches the next tile's data into
+// registers before computing the current one.
 #include "ntt.h"
 
+#include <algorithm>
+#include <type_traits>
+#include <utility>
+
 #include "arith.h"
+#include "farith.h"
 
 namespace phx {
 namespace {
@@ -24,6 +38,9 @@ constexpr int E_LOG = 4;  // elements per thread per round = 16 (radix-16 rounds
 constexpr int E = 1 << E_LOG;
 constexpr int COLS = 16;  // columns per column-pass tile (16 x 8 B = one 128 B line per row)
 constexpr int BLOCK = 256;
+#ifndef PHX_NTT_GRID_MULT
+#define PHX_NTT_GRID_MULT 2  // persistent workgroups per CU
+#endif
 
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 
@@ -32,10 +49,10 @@ template <int S_LOG, int R>
 struct Round {
   static constexpr int g0 = R * E_LOG;
   static constexpr int er = cmin(E_LOG, S_LOG - g0);
-  static constexpr int a_hi = S_LOG - 1 - g0;       // highest active bit
-  static constexpr int a_lo = S_LOG - g0 - er;      // lowest active bit
-  static constexpr int ex = E_LOG - er;             // extra (inactive) bits held per thread
-  // bit position of the thread's E_LOG-bit window is [a_lo, a_lo + E_LOG)
+  static constexpr int a_hi = S_LOG - 1 - g0;   // highest active bit
+  static constexpr int a_lo = S_LOG - g0 - er;  // lowest active bit
+  static constexpr int ex = E_LOG - er;         // extra (inactive) bits held per thread
+  // the thread's E_LOG-bit window occupies bit positions [a_lo, a_lo + E_LOG)
   __device__ static __forceinline__ uint32_t p_thread(uint32_t t) {
     return (t & ((1u << a_lo) - 1u)) | ((t >> a_lo) << (a_lo + E_LOG));
   }
@@ -51,40 +68,100 @@ struct Sub {
   static constexpr int ROUNDS = (S_LOG + E_LOG - 1) / E_LOG;
 };
 
-// forward CT round: values in [0, 4q)
-template <int S_LOG, int R>
-__device__ __forceinline__ void ct_round(uint64_t (&v)[E], uint32_t pt, uint32_t B, const uint64_t* __restrict__ tw,
-                                         const uint64_t* __restrict__ tws, uint64_t q) {
+// ---------------------------------------------------------------------------------------
+// per-limb arithmetic context
+// ---------------------------------------------------------------------------------------
+struct LimbCtx {
+  uint64_t q;
+  double qd, qinv;
+  const uint64_t* tw;   // integer table (forward or inverse)
+  const uint64_t* tws;  // its Shoup quotients
+  const double* twf;    // FP64 table (centered), forward only
+};
+
+// Distinct twiddles of one round: stage gl has 2^(gl + ex) of them, keyed by the element's
+// active bits above the pair bit and its extra bits; slots are packed stage after stage.
+template <int EX>
+__host__ __device__ constexpr int tw_slot(int gl, int key) { return (((1 << gl) - 1) << EX) + key; }
+template <int EX>
+__host__ __device__ constexpr int tw_key(int gl, int j) { return ((j >> (E_LOG - gl)) << EX) | (j & ((1 << EX) - 1)); }
+
+// Twiddles of one round, loaded into registers before the next tile's prefetch is issued
+// (vmcnt counts loads in issue order, so a twiddle load issued after the prefetch would
+// make the compute wait for the prefetch).  w[gl][k]: stage gl, k-th butterfly.
+template <int S_LOG, int R, typename W>
+__device__ __forceinline__ void load_tw(W (&w)[E], const W* __restrict__ tab, uint32_t pt, uint32_t B) {
   using Rd = Round<S_LOG, R>;
 #pragma unroll
   for (int gl = 0; gl < Rd::er; ++gl) {
     const int g = Rd::g0 + gl;
-    const int h = 1 << (E_LOG - 1 - gl);
 #pragma unroll
-    for (int j = 0; j < E; ++j) {
-      if (j & h) continue;
+    for (int key = 0; key < (1 << (gl + Rd::ex)); ++key) {
+      // a representative element j with this key: active bits above the pair bit from key's
+      // high part, extra bits from key's low part
+      const int j = ((key >> Rd::ex) << (E_LOG - gl)) | (key & ((1 << Rd::ex) - 1));
       const uint32_t p = pt | Rd::p_elem(j);
-      const uint32_t idx = (B << g) + (p >> (S_LOG - g));
-      ct_bfly(v[j], v[j | h], tw[idx], tws[idx], q);
+      w[tw_slot<Rd::ex>(gl, key)] = tab[(B << g) + (p >> (S_LOG - g))];
     }
   }
 }
 
-// inverse GS round: stages in reverse order, values in [0, 2q)
+// forward CT round, integer path: values in [0, 4q)
 template <int S_LOG, int R>
-__device__ __forceinline__ void gs_round(uint64_t (&v)[E], uint32_t pt, uint32_t B, const uint64_t* __restrict__ itw,
-                                         const uint64_t* __restrict__ itws, uint64_t q) {
+__device__ __forceinline__ void ct_round_int(uint64_t (&v)[E], const uint64_t (&w)[E], const uint64_t (&ws)[E],
+                                             uint64_t q) {
   using Rd = Round<S_LOG, R>;
 #pragma unroll
-  for (int gl = Rd::er - 1; gl >= 0; --gl) {
-    const int g = Rd::g0 + gl;
+  for (int gl = 0; gl < Rd::er; ++gl) {
     const int h = 1 << (E_LOG - 1 - gl);
 #pragma unroll
     for (int j = 0; j < E; ++j) {
       if (j & h) continue;
-      const uint32_t p = pt | Rd::p_elem(j);
-      const uint32_t idx = (B << g) + (p >> (S_LOG - g));
-      gs_bfly(v[j], v[j | h], itw[idx], itws[idx], q);
+      const int sl = tw_slot<Rd::ex>(gl, tw_key<Rd::ex>(gl, j));
+      ct_bfly(v[j], v[j | h], w[sl], ws[sl], q);
+    }
+  }
+}
+
+// forward CT round, FP64 path.  GOFF = global stage index of local stage 0 of this
+// sub-transform; every value is reduced before global stages 3, 6, 9, ... (farith.h bounds).
+template <int S_LOG, int R, int GOFF>
+__device__ __forceinline__ void ct_round_f64(double (&v)[E], const double (&w)[E], double qd, double qinv) {
+  using Rd = Round<S_LOG, R>;
+#ifdef PHX_NTT_NO_COMPUTE
+  return;
+#endif
+#pragma unroll
+  for (int gl = 0; gl < Rd::er; ++gl) {
+    const int g = Rd::g0 + gl;
+    if ((GOFF + g) % 3 == 0 && (GOFF + g) > 0) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) v[j] = freduce(v[j], qd, qinv);
+    }
+    const int h = 1 << (E_LOG - 1 - gl);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      if (j & h) continue;
+      const double t = fmodmul(v[j | h], w[tw_slot<Rd::ex>(gl, tw_key<Rd::ex>(gl, j))], qd, qinv);
+      v[j | h] = v[j] - t;
+      v[j] = v[j] + t;
+    }
+  }
+}
+
+// inverse GS round (integer path): stages in reverse order, values in [0, 2q)
+template <int S_LOG, int R>
+__device__ __forceinline__ void gs_round_int(uint64_t (&v)[E], const uint64_t (&w)[E], const uint64_t (&ws)[E],
+                                             uint64_t q) {
+  using Rd = Round<S_LOG, R>;
+#pragma unroll
+  for (int gl = Rd::er - 1; gl >= 0; --gl) {
+    const int h = 1 << (E_LOG - 1 - gl);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      if (j & h) continue;
+      const int sl = tw_slot<Rd::ex>(gl, tw_key<Rd::ex>(gl, j));
+      gs_bfly(v[j], v[j | h], w[sl], ws[sl], q);
     }
   }
 }
@@ -93,14 +170,20 @@ struct KArgs {
   const uint64_t* in;
   uint64_t* out;
   const uint64_t* modulus;
-  const uint64_t* tw;       // forward or inverse table base
+  const double* modulus_f;    // q as double
+  const double* modulus_inv;  // 1/q rounded
+  const uint8_t* is_f64;      // per table row: FP64 path usable (q < 2^50)
+  const uint64_t* tw;         // forward or inverse integer table base
   const uint64_t* tws;
+  const double* twf;          // forward FP64 table
   const uint64_t* n_inv;
   const uint64_t* n_inv_shoup;
-  const uint64_t* scale;        // optional, per buffer limb
+  const uint64_t* scale;      // optional, per buffer limb
   const uint64_t* scale_shoup;
   LimbMap map;
   int n;
+  int limbs;                  // number of processed limbs (excluding skipped)
+  int f64_fwd;                // 1: forward transform may use the FP64 path
 };
 
 __device__ __forceinline__ void resolve_limb(const LimbMap& m, int y, int& buf_limb, int& row) {
@@ -110,218 +193,292 @@ __device__ __forceinline__ void resolve_limb(const LimbMap& m, int y, int& buf_l
   row = i < m.split ? m.first_a + i : m.first_b + (i - m.split);
 }
 
-// LDS padding: one 8-byte pad word every 16 words (rows) / one 16-word pad row every 16 rows (columns)
+__device__ __forceinline__ LimbCtx limb_ctx(const KArgs& a, int row, bool& f64) {
+  LimbCtx c;
+  c.q = a.modulus[row];
+  c.qd = a.modulus_f[row];
+  c.qinv = a.modulus_inv[row];
+  c.tw = a.tw + (size_t)row * a.n;
+  c.tws = a.tws + (size_t)row * a.n;
+  c.twf = a.twf + (size_t)row * a.n;
+  f64 = a.f64_fwd && a.is_f64[row];
+  return c;
+}
+
+// LDS padding: one pad word every 16 words (row tiles) / one 16-word pad row every 16 rows
+// (column tiles) — keeps the transposed round's ds_read_b64 accesses conflict-free.
 __device__ __forceinline__ uint32_t rpad(uint32_t p) { return p + (p >> 4); }
+__device__ __forceinline__ uint32_t cidx(uint32_t p, uint32_t c) { return p * COLS + c + (p >> 4) * COLS; }
 
-// ---------------------------------------------------------------------------------------
-// Row pass: a tile of ROWS whole rows (S2 contiguous words each) of one limb.
-// FWD: rounds 0..ROUNDS-1 of the last log2(S2) CT stages; INV: the same stages in reverse
-// (the first log2(S2) GS stages of the inverse transform).
-// ---------------------------------------------------------------------------------------
-template <int S1_LOG, int S2_LOG, bool INV>
-__global__ __launch_bounds__(BLOCK) void ntt_row_pass(KArgs a) {
-  using SB = Sub<S2_LOG>;
-  constexpr int S2 = SB::S, T = SB::T, ROWS = cmin(BLOCK / T, 1 << S1_LOG), RSTR = S2 + S2 / 16;
-  __shared__ uint64_t lds[ROWS * RSTR];
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  [&]<int... I>(std::integer_sequence<int, I...>) { (f(std::integral_constant<int, I>{}), ...); }
+  (std::make_integer_sequence<int, N>{});
+}
 
-  int buf_limb, trow;
-  resolve_limb(a.map, blockIdx.y, buf_limb, trow);
-  const uint64_t q = a.modulus[trow];
-  const uint64_t* tw = a.tw + (size_t)trow * a.n;
-  const uint64_t* tws = a.tws + (size_t)trow * a.n;
-  const uint64_t* src = a.in + (size_t)buf_limb * a.n;
-  uint64_t* dst = a.out + (size_t)buf_limb * a.n;
+// All twiddles of one sub-transform for one thread, in registers.
+template <int S_LOG>
+struct TwF64 {
+  double w[Sub<S_LOG>::ROUNDS][E];
+};
+template <int S_LOG>
+struct TwInt {
+  uint64_t w[Sub<S_LOG>::ROUNDS][E];
+  uint64_t ws[Sub<S_LOG>::ROUNDS][E];
+};
 
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lr = tid / T, t = tid % T;
-  const uint32_t row = blockIdx.x * ROWS + lr;
-  const uint32_t B = (1u << S1_LOG) + row;
-  uint64_t* L = lds + lr * RSTR;
+template <int S_LOG>
+__device__ __forceinline__ void load_all(TwF64<S_LOG>& tw, const double* tab, uint32_t t, uint32_t B) {
+  static_for<Sub<S_LOG>::ROUNDS>([&](auto r) {
+    constexpr int R = decltype(r)::value;
+    load_tw<S_LOG, R>(tw.w[R], tab, Round<S_LOG, R>::p_thread(t), B);
+  });
+}
+template <int S_LOG>
+__device__ __forceinline__ void load_all(TwInt<S_LOG>& tw, const uint64_t* tab, const uint64_t* tabs, uint32_t t,
+                                         uint32_t B) {
+  static_for<Sub<S_LOG>::ROUNDS>([&](auto r) {
+    constexpr int R = decltype(r)::value;
+    load_tw<S_LOG, R>(tw.w[R], tab, Round<S_LOG, R>::p_thread(t), B);
+    load_tw<S_LOG, R>(tw.ws[R], tabs, Round<S_LOG, R>::p_thread(t), B);
+  });
+}
 
-  uint64_t v[E];
-  // coalesced load, round-0 layout p = t + j*T
-#pragma unroll
-  for (int j = 0; j < E; ++j) v[j] = src[(size_t)row * S2 + t + j * T];
-
-  if constexpr (!INV) {
-    ct_round<S2_LOG, 0>(v, Round<S2_LOG, 0>::p_thread(t), B, tw, tws, q);
-    if constexpr (SB::ROUNDS > 1) {
-#pragma unroll
-      for (int j = 0; j < E; ++j) L[rpad(Round<S2_LOG, 0>::p_thread(t) | Round<S2_LOG, 0>::p_elem(j))] = v[j];
-      __syncthreads();
-      constexpr int R1 = 1;
-      const uint32_t pt1 = Round<S2_LOG, R1>::p_thread(t);
-#pragma unroll
-      for (int j = 0; j < E; ++j) v[j] = L[rpad(pt1 | Round<S2_LOG, R1>::p_elem(j))];
-      ct_round<S2_LOG, R1>(v, pt1, B, tw, tws, q);
-      if constexpr (SB::ROUNDS > 2) {
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < E; ++j) L[rpad(pt1 | Round<S2_LOG, R1>::p_elem(j))] = v[j];
-        __syncthreads();
-        constexpr int R2 = 2;
-        const uint32_t pt2 = Round<S2_LOG, R2>::p_thread(t);
-#pragma unroll
-        for (int j = 0; j < E; ++j) v[j] = L[rpad(pt2 | Round<S2_LOG, R2>::p_elem(j))];
-        ct_round<S2_LOG, R2>(v, pt2, B, tw, tws, q);
-        static_assert(SB::ROUNDS <= 3, "row pass supports up to 3 rounds");
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < E; ++j) L[rpad(pt2 | Round<S2_LOG, R2>::p_elem(j))] = v[j];
-      } else {
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < E; ++j) L[rpad(pt1 | Round<S2_LOG, R1>::p_elem(j))] = v[j];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < E; ++j) v[j] = L[rpad(t + j * T)];
+// One full sub-transform (all rounds) on registers v, which hold the load layout
+// p = t + j*T on entry and on exit.  L is this thread-group's LDS tile of element type V
+// indexed by idx(p); sync() orders the LDS exchanges (workgroup or wavefront barrier).
+template <int S_LOG, int GOFF, bool FWD, typename V, typename TW, typename Idx, typename Sync>
+__device__ __forceinline__ void sub_transform(V (&v)[E], const TW& tw, V* L, Idx idx, Sync sync, uint32_t t,
+                                              uint64_t q, double qd, double qinv) {
+  using SB = Sub<S_LOG>;
+  constexpr int RN = SB::ROUNDS;
+  constexpr bool F = !std::is_same_v<V, uint64_t>;
+  auto round = [&](auto r) {
+    constexpr int R = decltype(r)::value;
+    if constexpr (F) {
+      static_assert(FWD, "FP64 path is forward-only");
+      ct_round_f64<S_LOG, R, GOFF>(v, tw.w[R], qd, qinv);
+    } else if constexpr (FWD) {
+      ct_round_int<S_LOG, R>(v, tw.w[R], tw.ws[R], q);
+    } else {
+      gs_round_int<S_LOG, R>(v, tw.w[R], tw.ws[R], q);
     }
-    // final stages of the forward transform: reduce to [0, q)
-    const uint64_t q2 = q << 1;
+  };
+  auto put = [&](uint32_t pt, auto r) {
+    constexpr int R = decltype(r)::value;
 #pragma unroll
-    for (int j = 0; j < E; ++j) dst[(size_t)row * S2 + t + j * T] = csub(csub(v[j], q2), q);
+    for (int j = 0; j < E; ++j) L[idx(pt | Round<S_LOG, R>::p_elem(j))] = v[j];
+  };
+  auto get = [&](uint32_t pt, auto r) {
+    constexpr int R = decltype(r)::value;
+#pragma unroll
+    for (int j = 0; j < E; ++j) v[j] = L[idx(pt | Round<S_LOG, R>::p_elem(j))];
+  };
+  if constexpr (FWD) {
+    round(std::integral_constant<int, 0>{});
+    static_for<RN - 1>([&](auto rm1) {
+      constexpr int R = decltype(rm1)::value + 1;
+      put(Round<S_LOG, R - 1>::p_thread(t), std::integral_constant<int, R - 1>{});
+      sync();
+      get(Round<S_LOG, R>::p_thread(t), std::integral_constant<int, R>{});
+      sync();
+      round(std::integral_constant<int, R>{});
+    });
+    if constexpr (RN > 1) {
+      put(Round<S_LOG, RN - 1>::p_thread(t), std::integral_constant<int, RN - 1>{});
+      sync();
+      get(Round<S_LOG, 0>::p_thread(t), std::integral_constant<int, 0>{});
+      sync();
+    }
   } else {
-    // inverse: rounds in reverse order
-    constexpr int RL = SB::ROUNDS - 1;
-    if constexpr (SB::ROUNDS > 1) {
-#pragma unroll
-      for (int j = 0; j < E; ++j) L[rpad(t + j * T)] = v[j];
-      __syncthreads();
-      const uint32_t ptl = Round<S2_LOG, RL>::p_thread(t);
-#pragma unroll
-      for (int j = 0; j < E; ++j) v[j] = L[rpad(ptl | Round<S2_LOG, RL>::p_elem(j))];
-      gs_round<S2_LOG, RL>(v, ptl, B, tw, tws, q);
-      if constexpr (SB::ROUNDS > 2) {
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < E; ++j) L[rpad(ptl | Round<S2_LOG, RL>::p_elem(j))] = v[j];
-        __syncthreads();
-        const uint32_t ptm = Round<S2_LOG, 1>::p_thread(t);
-#pragma unroll
-        for (int j = 0; j < E; ++j) v[j] = L[rpad(ptm | Round<S2_LOG, 1>::p_elem(j))];
-        gs_round<S2_LOG, 1>(v, ptm, B, tw, tws, q);
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < E; ++j) L[rpad(ptm | Round<S2_LOG, 1>::p_elem(j))] = v[j];
-      } else {
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < E; ++j) L[rpad(ptl | Round<S2_LOG, RL>::p_elem(j))] = v[j];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < E; ++j) v[j] = L[rpad(t + j * T)];
+    if constexpr (RN > 1) {
+      put(Round<S_LOG, 0>::p_thread(t), std::integral_constant<int, 0>{});
+      sync();
+      get(Round<S_LOG, RN - 1>::p_thread(t), std::integral_constant<int, RN - 1>{});
+      sync();
     }
-    gs_round<S2_LOG, 0>(v, Round<S2_LOG, 0>::p_thread(t), B, tw, tws, q);
-#pragma unroll
-    for (int j = 0; j < E; ++j) dst[(size_t)row * S2 + t + j * T] = v[j];  // [0, 2q), column pass follows
+    static_for<RN - 1>([&](auto i) {
+      constexpr int R = RN - 1 - decltype(i)::value;  // RN-1 .. 1
+      round(std::integral_constant<int, R>{});
+      put(Round<S_LOG, R>::p_thread(t), std::integral_constant<int, R>{});
+      sync();
+      get(Round<S_LOG, R - 1>::p_thread(t), std::integral_constant<int, R - 1>{});
+      sync();
+    });
+    round(std::integral_constant<int, 0>{});
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Column pass: a tile of COLS consecutive columns (stride S2) of one limb, all S1 rows.
-// FWD: the first log2(S1) CT stages (values stay lazy in [0, 4q) for the row pass);
-// INV: the last log2(S1) GS stages, then n^-1 (and the optional per-limb scale).
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t cidx(uint32_t p, uint32_t c) { return p * COLS + c + (p >> 4) * COLS; }
+__device__ __forceinline__ void fence_loads() { __builtin_amdgcn_sched_barrier(0); }
 
-template <int S1_LOG, int S2_LOG, bool INV>
-__global__ __launch_bounds__(BLOCK) void ntt_col_pass(KArgs a) {
+// ---------------------------------------------------------------------------------------
+// Column pass: tile = COLS consecutive columns x S1 rows of one limb; 256-thread workgroup.
+// FWD: first log2(S1) CT stages (FP64: output doubles |x| <= 3q; int: lazy [0, 4q)).
+// INV: last log2(S1) GS stages, then n^-1 and the optional per-limb scale.
+// ---------------------------------------------------------------------------------------
+template <int S1_LOG, int S2_LOG, bool FWD>
+__global__ __launch_bounds__(BLOCK) void ntt_col(KArgs a) {
   using SB = Sub<S1_LOG>;
-  constexpr int S1 = SB::S, T = SB::T, S2 = 1 << S2_LOG;
-  constexpr int NT = COLS * T;  // threads actually used
+  constexpr int T = SB::T, S2 = 1 << S2_LOG, NT = COLS * T, CT = S2 / COLS;
   static_assert(NT <= BLOCK, "column tile too large");
-  __shared__ uint64_t lds[(S1 + S1 / 16) * COLS];
-
-  int buf_limb, trow;
-  resolve_limb(a.map, blockIdx.y, buf_limb, trow);
-  const uint64_t q = a.modulus[trow];
-  const uint64_t* tw = a.tw + (size_t)trow * a.n;
-  const uint64_t* tws = a.tws + (size_t)trow * a.n;
-  const uint64_t* src = a.in + (size_t)buf_limb * a.n;
-  uint64_t* dst = a.out + (size_t)buf_limb * a.n;
+  __shared__ uint64_t lds[(SB::S + SB::S / 16) * COLS];
 
   const uint32_t tid = threadIdx.x;
   const bool active = tid < NT;
   const uint32_t c = tid % COLS, t = tid / COLS;
-  const uint32_t col = blockIdx.x * COLS + c;
-  constexpr uint32_t B = 1;
+  const int ntiles = a.limbs * CT;
+  auto idx = [c](uint32_t p) { return cidx(p, c); };
+  auto sync = [] { __syncthreads(); };
 
-  uint64_t v[E];
-  if (active) {
-#pragma unroll
-    for (int j = 0; j < E; ++j) v[j] = src[(size_t)(t + j * T) * S2 + col];
-  }
-
-  if constexpr (!INV) {
-    if (active) ct_round<S1_LOG, 0>(v, Round<S1_LOG, 0>::p_thread(t), B, tw, tws, q);
-    if constexpr (SB::ROUNDS > 1) {
-      static_assert(SB::ROUNDS == 2, "column pass supports 2 rounds");
-      if (active) {
-#pragma unroll
-        for (int j = 0; j < E; ++j) lds[cidx(Round<S1_LOG, 0>::p_thread(t) | Round<S1_LOG, 0>::p_elem(j), c)] = v[j];
-      }
-      __syncthreads();
-      const uint32_t pt1 = Round<S1_LOG, 1>::p_thread(t);
-      if (active) {
-#pragma unroll
-        for (int j = 0; j < E; ++j) v[j] = lds[cidx(pt1 | Round<S1_LOG, 1>::p_elem(j), c)];
-        ct_round<S1_LOG, 1>(v, pt1, B, tw, tws, q);
-      }
-      __syncthreads();
-      if (active) {
-#pragma unroll
-        for (int j = 0; j < E; ++j) lds[cidx(pt1 | Round<S1_LOG, 1>::p_elem(j), c)] = v[j];
-      }
-      __syncthreads();
-      if (active) {
-#pragma unroll
-        for (int j = 0; j < E; ++j) v[j] = lds[cidx(t + j * T, c)];
-      }
-    }
+  uint64_t cur[E], nxt[E];
+  auto load = [&](int tile, uint64_t (&dst)[E]) {
+    int buf_limb, row;
+    resolve_limb(a.map, tile / CT, buf_limb, row);
+    const uint64_t* src = a.in + (size_t)buf_limb * a.n + (tile % CT) * COLS + c;
     if (active) {
 #pragma unroll
-      for (int j = 0; j < E; ++j) dst[(size_t)(t + j * T) * S2 + col] = v[j];  // lazy [0, 4q)
+      for (int j = 0; j < E; ++j) dst[j] = __builtin_nontemporal_load(src + (size_t)(t + j * T) * S2);
     }
-  } else {
-    if constexpr (SB::ROUNDS > 1) {
-      static_assert(SB::ROUNDS == 2, "column pass supports 2 rounds");
+  };
+  int tile = blockIdx.x;
+  if (tile < ntiles) load(tile, cur);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int next = tile + gridDim.x;
+    int buf_limb, row;
+    resolve_limb(a.map, tile / CT, buf_limb, row);
+    bool f64;
+    const LimbCtx lc = limb_ctx(a, row, f64);
+    uint64_t* dst = a.out + (size_t)buf_limb * a.n + (tile % CT) * COLS + c;
+    if (FWD && f64) {
+      TwF64<S1_LOG> tw;
+      if (active) load_all(tw, lc.twf, t, 1);
+      fence_loads();
+      if (next < ntiles) load(next, nxt);
+      fence_loads();
+      double v[E];
+#pragma unroll
+      for (int j = 0; j < E; ++j) v[j] = u64_to_f64(cur[j]);
+      if constexpr (FWD)
+        sub_transform<S1_LOG, 0, true>(v, tw, reinterpret_cast<double*>(lds), idx, sync, t, lc.q, lc.qd, lc.qinv);
       if (active) {
 #pragma unroll
-        for (int j = 0; j < E; ++j) lds[cidx(t + j * T, c)] = v[j];
+        for (int j = 0; j < E; ++j) dst[(size_t)(t + j * T) * S2] = as_bits(v[j]);
       }
-      __syncthreads();
-      const uint32_t pt1 = Round<S1_LOG, 1>::p_thread(t);
+    } else {
+      TwInt<S1_LOG> tw;
+      if (active) load_all(tw, lc.tw, lc.tws, t, 1);
+      fence_loads();
+      if (next < ntiles) load(next, nxt);
+      fence_loads();
+      sub_transform<S1_LOG, 0, FWD>(cur, tw, lds, idx, sync, t, lc.q, lc.qd, lc.qinv);
       if (active) {
+        if constexpr (FWD) {
 #pragma unroll
-        for (int j = 0; j < E; ++j) v[j] = lds[cidx(pt1 | Round<S1_LOG, 1>::p_elem(j), c)];
-        gs_round<S1_LOG, 1>(v, pt1, B, tw, tws, q);
-      }
-      __syncthreads();
-      if (active) {
+          for (int j = 0; j < E; ++j) dst[(size_t)(t + j * T) * S2] = cur[j];  // lazy [0, 4q)
+        } else {
+          const uint64_t ni = a.n_inv[row], nis = a.n_inv_shoup[row];
+          const bool scaled = a.scale != nullptr;
+          const uint64_t sc = scaled ? a.scale[buf_limb] : 0, scs = scaled ? a.scale_shoup[buf_limb] : 0;
 #pragma unroll
-        for (int j = 0; j < E; ++j) lds[cidx(pt1 | Round<S1_LOG, 1>::p_elem(j), c)] = v[j];
-      }
-      __syncthreads();
-      if (active) {
-#pragma unroll
-        for (int j = 0; j < E; ++j) v[j] = lds[cidx(t + j * T, c)];
+          for (int j = 0; j < E; ++j) {
+            uint64_t x = mul_shoup(cur[j], ni, nis, lc.q);
+            if (scaled) x = mul_shoup(x, sc, scs, lc.q);
+            dst[(size_t)(t + j * T) * S2] = x;
+          }
+        }
       }
     }
-    if (active) {
-      gs_round<S1_LOG, 0>(v, Round<S1_LOG, 0>::p_thread(t), B, tw, tws, q);
-      const uint64_t ni = a.n_inv[trow], nis = a.n_inv_shoup[trow];
-      const bool scaled = a.scale != nullptr;
-      const uint64_t sc = scaled ? a.scale[buf_limb] : 0, scs = scaled ? a.scale_shoup[buf_limb] : 0;
 #pragma unroll
-      for (int j = 0; j < E; ++j) {
-        uint64_t x = mul_shoup(v[j], ni, nis, q);
-        if (scaled) x = mul_shoup(x, sc, scs, q);
-        dst[(size_t)(t + j * T) * S2 + col] = x;
-      }
-    }
+    for (int j = 0; j < E; ++j) cur[j] = nxt[j];
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Row pass: each wavefront owns RW = 64/T whole rows at a time (T lanes per row), so the
+// LDS transposes are wave-private and need no workgroup barrier.
+// FWD: last log2(S2) CT stages, canonical output.  INV: first log2(S2) GS stages.
+// ---------------------------------------------------------------------------------------
+template <int S1_LOG, int S2_LOG, bool FWD>
+__global__ __launch_bounds__(BLOCK) void ntt_row(KArgs a) {
+  using SB = Sub<S2_LOG>;
+  constexpr int S2 = SB::S, T = SB::T, RW = cmin(64 / T, 1 << S1_LOG), RSTR = S2 + S2 / 16;
+  constexpr int WAVES = BLOCK / 64;
+  constexpr int GROUPS = (1 << S1_LOG) / RW;  // row groups per limb
+  __shared__ uint64_t lds[WAVES * RW * RSTR];
+
+  const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+  const uint32_t lr = lane / T, t = lane % T;
+  uint64_t* lrow = lds + (wave * RW + lr) * RSTR;
+  const int nitems = a.limbs * GROUPS;
+  const int stride = gridDim.x * WAVES;
+  auto idx = [](uint32_t p) { return rpad(p); };
+  auto sync = [] { __builtin_amdgcn_wave_barrier(); };
+
+  uint64_t cur[E], nxt[E];
+  auto load = [&](int item, uint64_t (&dst)[E]) {
+    int buf_limb, row;
+    resolve_limb(a.map, item / GROUPS, buf_limb, row);
+    const uint32_t r = (item % GROUPS) * RW + lr;
+    const uint64_t* src = a.in + (size_t)buf_limb * a.n + (size_t)r * S2 + t;
+#pragma unroll
+    for (int j = 0; j < E; ++j) dst[j] = src[j * T];
+  };
+  int item = blockIdx.x * WAVES + wave;
+  if (item < nitems) load(item, cur);
+  for (; item < nitems; item += stride) {
+    const int next = item + stride;
+    int buf_limb, row;
+    resolve_limb(a.map, item / GROUPS, buf_limb, row);
+    bool f64;
+    const LimbCtx lc = limb_ctx(a, row, f64);
+    const uint32_t r = (item % GROUPS) * RW + lr;
+    const uint32_t B = (1u << S1_LOG) + r;
+    uint64_t* dst = a.out + (size_t)buf_limb * a.n + (size_t)r * S2 + t;
+    if (FWD && f64) {
+      TwF64<S2_LOG> tw;
+      load_all(tw, lc.twf, t, B);
+      fence_loads();
+      if (next < nitems) load(next, nxt);
+      fence_loads();
+      double v[E];
+#pragma unroll
+      for (int j = 0; j < E; ++j) v[j] = as_f64(cur[j]);
+      if constexpr (FWD)
+        sub_transform<S2_LOG, S1_LOG, true>(v, tw, reinterpret_cast<double*>(lrow), idx, sync, t, lc.q, lc.qd,
+                                            lc.qinv);
+#pragma unroll
+      for (int j = 0; j < E; ++j) __builtin_nontemporal_store(f64_to_canonical(v[j], lc.qd, lc.qinv), dst + j * T);
+    } else {
+      TwInt<S2_LOG> tw;
+      load_all(tw, lc.tw, lc.tws, t, B);
+      fence_loads();
+      if (next < nitems) load(next, nxt);
+      fence_loads();
+      sub_transform<S2_LOG, S1_LOG, FWD>(cur, tw, lrow, idx, sync, t, lc.q, lc.qd, lc.qinv);
+      if constexpr (FWD) {
+        const uint64_t q2 = lc.q << 1;
+#pragma unroll
+        for (int j = 0; j < E; ++j) __builtin_nontemporal_store(csub(csub(cur[j], q2), lc.q), dst + j * T);
+      } else {
+#pragma unroll
+        for (int j = 0; j < E; ++j) dst[j * T] = cur[j];  // [0, 2q), column pass follows
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) cur[j] = nxt[j];
+  }
+}
+
+int g_num_cus = 0;
+
+int num_cus() {
+  if (!g_num_cus) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) g_num_cus = p.multiProcessorCount;
+    if (g_num_cus <= 0) g_num_cus = 256;
+  }
+  return g_num_cus;
 }
 
 template <int S1_LOG, int S2_LOG>
@@ -331,23 +488,30 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   if (limbs <= 0) return hipSuccess;
   KArgs a;
   a.in = in; a.out = out; a.modulus = tb.modulus;
+  a.modulus_f = tb.modulus_f; a.modulus_inv = tb.modulus_inv; a.is_f64 = tb.is_f64;
   a.tw = inverse ? tb.itw : tb.tw;
   a.tws = inverse ? tb.itw_shoup : tb.tw_shoup;
+  a.twf = tb.twf;
   a.n_inv = tb.n_inv; a.n_inv_shoup = tb.n_inv_shoup;
   a.scale = scale; a.scale_shoup = scale_shoup;
-  a.map = map; a.n = (int)tb.n;
+  a.map = map; a.n = (int)tb.n; a.limbs = limbs;
+  a.f64_fwd = inverse ? 0 : 1;
   constexpr int S1 = 1 << S1_LOG, S2 = 1 << S2_LOG;
-  constexpr int ROWS = cmin(BLOCK / Sub<S2_LOG>::T, S1);
-  const dim3 grid_r(S1 / ROWS, limbs), grid_c(S2 / COLS, limbs);
-  const dim3 block_r(ROWS * Sub<S2_LOG>::T);
+  constexpr int RW = cmin(64 / Sub<S2_LOG>::T, S1);
+  const int col_tiles = limbs * (S2 / COLS);
+  const int row_items = limbs * (S1 / RW);
+  const int cus = num_cus();
+  const dim3 grid_c(std::min(col_tiles, cus * PHX_NTT_GRID_MULT)),
+      grid_r(std::min((row_items + 3) / 4, cus * PHX_NTT_GRID_MULT));
+  const dim3 block(BLOCK);
   if (!inverse) {
-    hipLaunchKernelGGL((ntt_col_pass<S1_LOG, S2_LOG, false>), grid_c, dim3(BLOCK), 0, stream, a);
+    hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true>), grid_c, block, 0, stream, a);
     a.in = out;
-    hipLaunchKernelGGL((ntt_row_pass<S1_LOG, S2_LOG, false>), grid_r, block_r, 0, stream, a);
+    hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true>), grid_r, block, 0, stream, a);
   } else {
-    hipLaunchKernelGGL((ntt_row_pass<S1_LOG, S2_LOG, true>), grid_r, block_r, 0, stream, a);
+    hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false>), grid_r, block, 0, stream, a);
     a.in = out;
-    hipLaunchKernelGGL((ntt_col_pass<S1_LOG, S2_LOG, true>), grid_c, dim3(BLOCK), 0, stream, a);
+    hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false>), grid_c, block, 0, stream, a);
   }
   return hipGetLastError();
 }

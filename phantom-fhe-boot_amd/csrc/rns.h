@@ -1,0 +1,100 @@
+// rns.h — RNS polynomial kernels on gfx950: elementwise arithmetic (src/polymath.cu), fast
+// base conversion (src/rns_bconv.cu), hybrid key-switch pieces (src/rns_bconv.cu:530-843,
+// src/eval_key_switch.cu), CKKS rescale (src/rns.cu:1128-1184), NTT-domain automorphism
+// (src/galois.cu:104-119) and the bootstrap helpers (src/evaluate.cu:2414-2554).
+//
+// Every launcher enqueues on `stream` and returns hipGetLastError().  Modulus arrays are
+// device arrays indexed by limb; `barrett` is [limb][2] = floor(2^128/q) {lo, hi}.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace phx {
+
+// Per-limb modulus view (device pointers).
+struct ModView {
+  const uint64_t* q = nullptr;
+  const uint64_t* barrett = nullptr;  // [L][2]
+};
+
+// ---- elementwise, all [L][n] limb-major, one modulus per limb -------------------------
+hipError_t poly_add(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
+                    hipStream_t s);
+hipError_t poly_sub(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
+                    hipStream_t s);
+hipError_t poly_negate(const uint64_t* a, uint64_t* out, ModView m, size_t n, size_t L, hipStream_t s);
+hipError_t poly_mul(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
+                    hipStream_t s);
+// out = a * b + c
+hipError_t poly_mul_add(const uint64_t* a, const uint64_t* b, const uint64_t* c, uint64_t* out, ModView m,
+                        size_t n, size_t L, hipStream_t s);
+// out[l] = a[l] * scalar[l] (scalar, scalar_shoup: device arrays of L)
+hipError_t poly_mul_scalar(const uint64_t* a, const uint64_t* scalar, const uint64_t* scalar_shoup, uint64_t* out,
+                           ModView m, size_t n, size_t L, hipStream_t s);
+// out[l] = a[l] + scalar[l]
+hipError_t poly_add_scalar(const uint64_t* a, const uint64_t* scalar, uint64_t* out, ModView m, size_t n,
+                           size_t L, hipStream_t s);
+// (c0, c1) x (d0, d1) -> (c0 d0, c0 d1 + c1 d0, c1 d1); ct1/ct2 are [2][L][n], out [3][L][n]
+// (tensor_prod_2x2_rns_poly, src/polymath.cu:501-536).  out may alias ct1.
+hipError_t tensor_prod_2x2(const uint64_t* ct1, const uint64_t* ct2, uint64_t* out, ModView m, size_t n, size_t L,
+                           hipStream_t s);
+
+// ---- base conversion ------------------------------------------------------------------
+// Fast base conversion (bconv_mult + bconv_matmul, src/rns_bconv.cu:40-179, 455-485):
+//   t_i = [x_i * qhat_inv_i]_{q_i}            (skipped when qhat_inv == nullptr: x already scaled)
+//   y_j = sum_i t_i * qhat_mod_p[i][j] mod p_j
+// Output limb j goes to out[(j < skip_at ? j : j + skip_len) * n].
+struct BconvArgs {
+  const uint64_t* in;            // [ibase][n]
+  uint64_t* out;
+  const uint64_t* ibase;         // [ibase]
+  const uint64_t* qhat_inv;      // [ibase] or nullptr
+  const uint64_t* qhat_inv_shoup;
+  const uint64_t* qhat_mod_p;    // [ibase][obase]
+  const uint64_t* obase;         // [obase]
+  const uint64_t* obase_barrett; // [obase][2]
+  int ibase_size = 0;
+  int obase_size = 0;
+  int skip_at = 1 << 30;
+  int skip_len = 0;
+};
+hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s);
+
+// ---- hybrid key switching -------------------------------------------------------------
+// modup_copy_partQl_kernel (src/rns_bconv.cu:522-528): t_mod_up[beta][qlp] gets the digit's own
+// NTT-form limbs of c2 for every digit.
+hipError_t modup_copy_digits(const uint64_t* c2, uint64_t* t_mod_up, size_t n, size_t size_ql, size_t size_qlp,
+                             size_t alpha, hipStream_t s);
+// key_switch_inner_prod_c2_and_evk (src/eval_key_switch.cu:26-85).  evk: device array of
+// beta pointers to [2][size_QP][n] key digits; modulus/barrett over the full QP chain.
+hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const* evk, uint64_t* cx,
+                                const uint64_t* qp_mod, const uint64_t* qp_barrett, size_t n, size_t size_ql,
+                                size_t size_q, size_t size_p, size_t beta, hipStream_t s);
+// moddown tail + add_to_ct (src/ntt/ntt_moddown.cu:199-214, src/rns_bconv.cu:763-789):
+//   ct[j] = ct[j] + (cx[j] - delta[j]) * Pinv[j] mod q_j   (accumulate = true)
+//   ct[j] =         (cx[j] - delta[j]) * Pinv[j] mod q_j   (accumulate = false)
+hipError_t moddown_finish(uint64_t* ct, const uint64_t* cx, const uint64_t* delta, const uint64_t* pinv,
+                          const uint64_t* pinv_shoup, const uint64_t* q, size_t n, size_t size_ql, bool accumulate,
+                          hipStream_t s);
+
+// ---- rescale --------------------------------------------------------------------------
+// divide_and_round_reduce_q_last_kernel (src/rns.cu:1128-1139): tmp[j] = c_last mod q_j, j < L-1
+hipError_t rescale_spread_last(const uint64_t* c_last, uint64_t* tmp, const uint64_t* q, const uint64_t* barrett,
+                               size_t n, size_t L_next, hipStream_t s);
+// divide_and_round_ntt_inv_scalar_kernel (src/rns.cu:1141-1158): out[j] = (c[j] - tmp[j]) * qlast_inv[j]
+hipError_t rescale_finish(const uint64_t* c, const uint64_t* tmp, uint64_t* out, const uint64_t* inv,
+                          const uint64_t* inv_shoup, const uint64_t* q, size_t n, size_t L_next, hipStream_t s);
+
+// ---- automorphism ---------------------------------------------------------------------
+// apply_galois_ntt_permutation_direct (src/galois.cu:104-119): out[l][j] = in[l][perm[j]]
+hipError_t galois_ntt(const uint64_t* in, uint64_t* out, const uint32_t* perm, size_t n, size_t L,
+                      hipStream_t s);
+
+// ---- bootstrap helpers ----------------------------------------------------------------
+// switchModulusKernel (src/evaluate.cu:2414-2457): lift limb-0 coefficients (mod q0) to L limbs
+hipError_t switch_modulus_raise(const uint64_t* in_q0, uint64_t* out, const uint64_t* q, const uint64_t* barrett,
+                                size_t n, size_t L, hipStream_t s);
+
+}  // namespace phx

@@ -1,0 +1,453 @@
+// rns.hip — elementwise RNS arithmetic, base conversion, key-switch and rescale kernels.
+// HBM-bound streaming kernels: 16 B per lane accesses (two coefficients), grid-stride
+// loops sized to a few waves per SIMD; per-limb constants come through the scalar cache.
+#include "rns.h"
+
+#include <algorithm>
+
+#include "arith.h"
+
+namespace phx {
+namespace {
+
+constexpr int kBlock = 256;
+
+int grid_for(size_t work_items) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ? p.multiProcessorCount
+                                                                                              : 256;
+  }
+  const size_t blocks = (work_items + kBlock - 1) / kBlock;
+  return static_cast<int>(std::max<size_t>(1, std::min<size_t>(blocks, static_cast<size_t>(cus) * 8)));
+}
+
+using u64x2 = ulonglong2;
+
+__device__ __forceinline__ u64x2 ld2(const uint64_t* p) { return *reinterpret_cast<const u64x2*>(p); }
+__device__ __forceinline__ void st2(uint64_t* p, uint64_t a, uint64_t b) {
+  *reinterpret_cast<u64x2*>(p) = make_ulonglong2(a, b);
+}
+
+// generic binary elementwise over [L][n] with per-limb modulus
+template <typename Op>
+__global__ __launch_bounds__(kBlock) void ew2_kernel(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
+                                                     uint64_t* out, ModView m, uint32_t log_n, size_t pairs, Op op) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const uint64_t q = m.q[l];
+    const u64x2 x = ld2(a + e);
+    const u64x2 y = ld2(b + e);
+    st2(out + e, op(x.x, y.x, q, m, l), op(x.y, y.y, q, m, l));
+  }
+}
+
+struct AddOp {
+  __device__ uint64_t operator()(uint64_t x, uint64_t y, uint64_t q, const ModView&, uint32_t) const {
+    return add_mod(x, y, q);
+  }
+};
+struct SubOp {
+  __device__ uint64_t operator()(uint64_t x, uint64_t y, uint64_t q, const ModView&, uint32_t) const {
+    return sub_mod(x, y, q);
+  }
+};
+struct MulOp {
+  __device__ uint64_t operator()(uint64_t x, uint64_t y, uint64_t q, const ModView& m, uint32_t l) const {
+    return mul_mod(x, y, q, m.barrett[2 * l], m.barrett[2 * l + 1]);
+  }
+};
+
+__global__ __launch_bounds__(kBlock) void negate_kernel(const uint64_t* __restrict__ a, uint64_t* out, ModView m,
+                                                        uint32_t log_n, size_t pairs) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint64_t q = m.q[e >> log_n];
+    const u64x2 x = ld2(a + e);
+    st2(out + e, neg_mod(x.x, q), neg_mod(x.y, q));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void mul_add_kernel(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
+                                                         const uint64_t* __restrict__ c, uint64_t* out, ModView m,
+                                                         uint32_t log_n, size_t pairs) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const uint64_t q = m.q[l], r0 = m.barrett[2 * l], r1 = m.barrett[2 * l + 1];
+    const u64x2 x = ld2(a + e), y = ld2(b + e), z = ld2(c + e);
+    u128 p0 = mul_wide(x.x, y.x), p1 = mul_wide(x.y, y.y);
+    add128(p0, u128{z.x, 0});
+    add128(p1, u128{z.y, 0});
+    st2(out + e, barrett_reduce_128(p0, q, r0, r1), barrett_reduce_128(p1, q, r0, r1));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void mul_scalar_kernel(const uint64_t* __restrict__ a, const uint64_t* sc,
+                                                            const uint64_t* scs, uint64_t* out, ModView m,
+                                                            uint32_t log_n, size_t pairs) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const uint64_t q = m.q[l], w = sc[l], ws = scs[l];
+    const u64x2 x = ld2(a + e);
+    st2(out + e, mul_shoup(x.x, w, ws, q), mul_shoup(x.y, w, ws, q));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void add_scalar_kernel(const uint64_t* __restrict__ a, const uint64_t* sc,
+                                                            uint64_t* out, ModView m, uint32_t log_n, size_t pairs) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const uint64_t q = m.q[l], w = sc[l];
+    const u64x2 x = ld2(a + e);
+    st2(out + e, add_mod(x.x, w, q), add_mod(x.y, w, q));
+  }
+}
+
+// d0 = a0 b0, d1 = a0 b1 + a1 b0 (one Barrett on the 128-bit sum), d2 = a1 b1
+__global__ __launch_bounds__(kBlock) void tensor_kernel(const uint64_t* ct1, const uint64_t* ct2, uint64_t* out,
+                                                        ModView m, uint32_t log_n, size_t pairs, size_t stride) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const uint64_t q = m.q[l], r0 = m.barrett[2 * l], r1 = m.barrett[2 * l + 1];
+    const u64x2 a0 = ld2(ct1 + e), a1 = ld2(ct1 + stride + e);
+    const u64x2 b0 = ld2(ct2 + e), b1 = ld2(ct2 + stride + e);
+    u128 c1x = mul_wide(a0.x, b1.x), c1y = mul_wide(a0.y, b1.y);
+    add128(c1x, mul_wide(a1.x, b0.x));
+    add128(c1y, mul_wide(a1.y, b0.y));
+    const uint64_t d0x = mul_mod(a0.x, b0.x, q, r0, r1), d0y = mul_mod(a0.y, b0.y, q, r0, r1);
+    const uint64_t d2x = mul_mod(a1.x, b1.x, q, r0, r1), d2y = mul_mod(a1.y, b1.y, q, r0, r1);
+    st2(out + e, d0x, d0y);
+    st2(out + stride + e, barrett_reduce_128(c1x, q, r0, r1), barrett_reduce_128(c1y, q, r0, r1));
+    st2(out + 2 * stride + e, d2x, d2y);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// fast base conversion: one thread per coefficient pair; the [ibase][obase] matrix and the
+// per-limb constants are wave-uniform (scalar loads).
+// ---------------------------------------------------------------------------------------
+constexpr int kMaxIbase = 64;
+
+template <bool PRESCALE>
+__global__ __launch_bounds__(kBlock) void bconv_kernel(BconvArgs a, uint32_t n, uint32_t pairs_per_limb) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < pairs_per_limb; i += gridDim.x * kBlock) {
+    const uint32_t k = 2 * i;
+    uint64_t tx[kMaxIbase], ty[kMaxIbase];
+    const int ib = a.ibase_size;
+    for (int s = 0; s < ib; ++s) {
+      const u64x2 x = ld2(a.in + (size_t)s * n + k);
+      if constexpr (PRESCALE) {
+        const uint64_t q = a.ibase[s], w = a.qhat_inv[s], ws = a.qhat_inv_shoup[s];
+        tx[s] = mul_shoup(x.x, w, ws, q);
+        ty[s] = mul_shoup(x.y, w, ws, q);
+      } else {
+        tx[s] = x.x;
+        ty[s] = x.y;
+      }
+    }
+    for (int j = 0; j < a.obase_size; ++j) {
+      u128 accx{0, 0}, accy{0, 0};
+      const uint64_t p = a.obase[j], r0 = a.obase_barrett[2 * j], r1 = a.obase_barrett[2 * j + 1];
+      for (int s = 0; s < ib; ++s) {
+        const uint64_t c = a.qhat_mod_p[(size_t)s * a.obase_size + j];
+        add128(accx, mul_wide(tx[s], c));
+        add128(accy, mul_wide(ty[s], c));
+        if (s % 15 == 14) {  // keep the sum below p * 2^64 for the Barrett quotient
+          accx = u128{barrett_reduce_128(accx, p, r0, r1), 0};
+          accy = u128{barrett_reduce_128(accy, p, r0, r1), 0};
+        }
+      }
+      const int oj = j < a.skip_at ? j : j + a.skip_len;
+      st2(a.out + (size_t)oj * n + k, barrett_reduce_128(accx, p, r0, r1), barrett_reduce_128(accy, p, r0, r1));
+    }
+  }
+}
+
+template <int IB>
+__global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32_t n, uint32_t pairs_per_limb,
+                                                              bool prescale) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < pairs_per_limb; i += gridDim.x * kBlock) {
+    const uint32_t k = 2 * i;
+    uint64_t tx[IB], ty[IB];
+#pragma unroll
+    for (int s = 0; s < IB; ++s) {
+      const u64x2 x = ld2(a.in + (size_t)s * n + k);
+      if (prescale) {
+        const uint64_t q = a.ibase[s], w = a.qhat_inv[s], ws = a.qhat_inv_shoup[s];
+        tx[s] = mul_shoup(x.x, w, ws, q);
+        ty[s] = mul_shoup(x.y, w, ws, q);
+      } else {
+        tx[s] = x.x;
+        ty[s] = x.y;
+      }
+    }
+    for (int j = 0; j < a.obase_size; ++j) {
+      u128 accx{0, 0}, accy{0, 0};
+#pragma unroll
+      for (int s = 0; s < IB; ++s) {
+        const uint64_t c = a.qhat_mod_p[(size_t)s * a.obase_size + j];
+        add128(accx, mul_wide(tx[s], c));
+        add128(accy, mul_wide(ty[s], c));
+      }
+      const uint64_t p = a.obase[j], r0 = a.obase_barrett[2 * j], r1 = a.obase_barrett[2 * j + 1];
+      const int oj = j < a.skip_at ? j : j + a.skip_len;
+      st2(a.out + (size_t)oj * n + k, barrett_reduce_128(accx, p, r0, r1), barrett_reduce_128(accy, p, r0, r1));
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void modup_copy_kernel(const uint64_t* c2, uint64_t* tmu, uint32_t log_n,
+                                                            size_t pairs, size_t size_qlp_n, size_t alpha_n) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const size_t beta = e / alpha_n;
+    *reinterpret_cast<u64x2*>(tmu + beta * size_qlp_n + e) = ld2(c2 + e);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void ks_inner_kernel(const uint64_t* __restrict__ tmu,
+                                                          const uint64_t* const* __restrict__ evk, uint64_t* cx,
+                                                          const uint64_t* qp, const uint64_t* qpb, uint32_t log_n,
+                                                          size_t pairs, uint32_t size_ql, uint32_t size_q,
+                                                          size_t size_qlp_n, size_t size_qp_n, uint32_t beta) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint32_t nid = static_cast<uint32_t>(e >> log_n);
+    const uint32_t twr = nid >= size_ql ? size_q + (nid - size_ql) : nid;
+    const size_t kk = e & ((size_t(1) << log_n) - 1);
+    const size_t eidx = ((size_t)twr << log_n) + kk;
+    u128 a0x{0, 0}, a0y{0, 0}, a1x{0, 0}, a1y{0, 0};
+    for (uint32_t b = 0; b < beta; ++b) {
+      const u64x2 c = ld2(tmu + b * size_qlp_n + e);
+      const uint64_t* key = evk[b];
+      const u64x2 k0 = ld2(key + eidx), k1 = ld2(key + size_qp_n + eidx);
+      add128(a0x, mul_wide(c.x, k0.x));
+      add128(a0y, mul_wide(c.y, k0.y));
+      add128(a1x, mul_wide(c.x, k1.x));
+      add128(a1y, mul_wide(c.y, k1.y));
+    }
+    const uint64_t q = qp[twr], r0 = qpb[2 * twr], r1 = qpb[2 * twr + 1];
+    st2(cx + e, barrett_reduce_128(a0x, q, r0, r1), barrett_reduce_128(a0y, q, r0, r1));
+    st2(cx + size_qlp_n + e, barrett_reduce_128(a1x, q, r0, r1), barrett_reduce_128(a1y, q, r0, r1));
+  }
+}
+
+template <bool ACC>
+__global__ __launch_bounds__(kBlock) void moddown_finish_kernel(uint64_t* ct, const uint64_t* cx, const uint64_t* delta,
+                                                                const uint64_t* pinv, const uint64_t* pinvs,
+                                                                const uint64_t* q, uint32_t log_n, size_t pairs) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const uint64_t m = q[l], w = pinv[l], ws = pinvs[l];
+    const u64x2 c = ld2(cx + e), d = ld2(delta + e);
+    uint64_t x = mul_shoup(sub_mod(c.x, d.x, m), w, ws, m);
+    uint64_t y = mul_shoup(sub_mod(c.y, d.y, m), w, ws, m);
+    if constexpr (ACC) {
+      const u64x2 o = ld2(ct + e);
+      x = add_mod(o.x, x, m);
+      y = add_mod(o.y, y, m);
+    }
+    st2(ct + e, x, y);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void rescale_spread_kernel(const uint64_t* c_last, uint64_t* tmp,
+                                                                const uint64_t* q, const uint64_t* qb, uint32_t log_n,
+                                                                size_t pairs) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const size_t k = e & ((size_t(1) << log_n) - 1);
+    const uint64_t m = q[l], r1 = qb[2 * l + 1];
+    const u64x2 c = ld2(c_last + k);
+    st2(tmp + e, barrett_reduce_64(c.x, m, r1), barrett_reduce_64(c.y, m, r1));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void rescale_finish_kernel(const uint64_t* c, const uint64_t* tmp, uint64_t* out,
+                                                                const uint64_t* inv, const uint64_t* invs,
+                                                                const uint64_t* q, uint32_t log_n, size_t pairs) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const uint64_t m = q[l], w = inv[l], ws = invs[l];
+    const u64x2 x = ld2(c + e), t = ld2(tmp + e);
+    st2(out + e, mul_shoup(sub_mod(x.x, t.x, m), w, ws, m), mul_shoup(sub_mod(x.y, t.y, m), w, ws, m));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void galois_kernel(const uint64_t* __restrict__ in, uint64_t* out,
+                                                        const uint32_t* __restrict__ perm, uint32_t log_n,
+                                                        size_t total) {
+  const size_t mask = (size_t(1) << log_n) - 1;
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < total; i += (size_t)gridDim.x * kBlock) {
+    const size_t base = i & ~mask;
+    out[i] = in[base + perm[i & mask]];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void raise_kernel(const uint64_t* in_q0, uint64_t* out, const uint64_t* q,
+                                                       const uint64_t* qb, uint32_t log_n, size_t total) {
+  const uint64_t q0 = q[0], half = q0 >> 1;
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < total; i += (size_t)gridDim.x * kBlock) {
+    const uint32_t l = static_cast<uint32_t>(i >> log_n);
+    const uint64_t v = in_q0[i & ((size_t(1) << log_n) - 1)];
+    const uint64_t m = q[l];
+    uint64_t r;
+    if (l == 0) {
+      r = v;
+    } else if (m > q0) {
+      r = v > half ? v + (m - q0) : v;
+    } else {
+      const uint64_t vv = v > half ? v + (m - q0 % m) : v;
+      r = barrett_reduce_64(vv, m, qb[2 * l + 1]);
+    }
+    out[i] = r;
+  }
+}
+
+}  // namespace
+
+hipError_t poly_add(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
+                    hipStream_t s) {
+  const size_t pairs = n * L / 2;
+  ew2_kernel<<<grid_for(pairs), kBlock, 0, s>>>(a, b, out, m, __builtin_ctzll(n), pairs, AddOp{});
+  return hipGetLastError();
+}
+
+hipError_t poly_sub(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
+                    hipStream_t s) {
+  const size_t pairs = n * L / 2;
+  ew2_kernel<<<grid_for(pairs), kBlock, 0, s>>>(a, b, out, m, __builtin_ctzll(n), pairs, SubOp{});
+  return hipGetLastError();
+}
+
+hipError_t poly_mul(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
+                    hipStream_t s) {
+  const size_t pairs = n * L / 2;
+  ew2_kernel<<<grid_for(pairs), kBlock, 0, s>>>(a, b, out, m, __builtin_ctzll(n), pairs, MulOp{});
+  return hipGetLastError();
+}
+
+hipError_t poly_negate(const uint64_t* a, uint64_t* out, ModView m, size_t n, size_t L, hipStream_t s) {
+  const size_t pairs = n * L / 2;
+  negate_kernel<<<grid_for(pairs), kBlock, 0, s>>>(a, out, m, __builtin_ctzll(n), pairs);
+  return hipGetLastError();
+}
+
+hipError_t poly_mul_add(const uint64_t* a, const uint64_t* b, const uint64_t* c, uint64_t* out, ModView m,
+                        size_t n, size_t L, hipStream_t s) {
+  const size_t pairs = n * L / 2;
+  mul_add_kernel<<<grid_for(pairs), kBlock, 0, s>>>(a, b, c, out, m, __builtin_ctzll(n), pairs);
+  return hipGetLastError();
+}
+
+hipError_t poly_mul_scalar(const uint64_t* a, const uint64_t* scalar, const uint64_t* scalar_shoup, uint64_t* out,
+                           ModView m, size_t n, size_t L, hipStream_t s) {
+  const size_t pairs = n * L / 2;
+  mul_scalar_kernel<<<grid_for(pairs), kBlock, 0, s>>>(a, scalar, scalar_shoup, out, m, __builtin_ctzll(n), pairs);
+  return hipGetLastError();
+}
+
+hipError_t poly_add_scalar(const uint64_t* a, const uint64_t* scalar, uint64_t* out, ModView m, size_t n, size_t L,
+                           hipStream_t s) {
+  const size_t pairs = n * L / 2;
+  add_scalar_kernel<<<grid_for(pairs), kBlock, 0, s>>>(a, scalar, out, m, __builtin_ctzll(n), pairs);
+  return hipGetLastError();
+}
+
+hipError_t tensor_prod_2x2(const uint64_t* ct1, const uint64_t* ct2, uint64_t* out, ModView m, size_t n, size_t L,
+                           hipStream_t s) {
+  const size_t pairs = n * L / 2;
+  tensor_kernel<<<grid_for(pairs), kBlock, 0, s>>>(ct1, ct2, out, m, __builtin_ctzll(n), pairs, n * L);
+  return hipGetLastError();
+}
+
+hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s) {
+  if (a.ibase_size <= 0 || a.ibase_size > kMaxIbase || a.obase_size <= 0) return hipErrorInvalidValue;
+  const uint32_t pairs = static_cast<uint32_t>(n / 2);
+  const int g = grid_for(pairs);
+  const bool pre = a.qhat_inv != nullptr;
+  switch (a.ibase_size) {
+#define PHX_BCONV_CASE(K) \
+  case K: bconv_fixed_kernel<K><<<g, kBlock, 0, s>>>(a, static_cast<uint32_t>(n), pairs, pre); break;
+    PHX_BCONV_CASE(1) PHX_BCONV_CASE(2) PHX_BCONV_CASE(3) PHX_BCONV_CASE(4) PHX_BCONV_CASE(5)
+    PHX_BCONV_CASE(6) PHX_BCONV_CASE(8) PHX_BCONV_CASE(10) PHX_BCONV_CASE(12) PHX_BCONV_CASE(15)
+#undef PHX_BCONV_CASE
+    default:
+      if (pre) bconv_kernel<true><<<g, kBlock, 0, s>>>(a, static_cast<uint32_t>(n), pairs);
+      else bconv_kernel<false><<<g, kBlock, 0, s>>>(a, static_cast<uint32_t>(n), pairs);
+  }
+  return hipGetLastError();
+}
+
+hipError_t modup_copy_digits(const uint64_t* c2, uint64_t* t_mod_up, size_t n, size_t size_ql, size_t size_qlp,
+                             size_t alpha, hipStream_t s) {
+  const size_t pairs = n * size_ql / 2;
+  modup_copy_kernel<<<grid_for(pairs), kBlock, 0, s>>>(c2, t_mod_up, __builtin_ctzll(n), pairs, size_qlp * n,
+                                                       alpha * n);
+  return hipGetLastError();
+}
+
+hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const* evk, uint64_t* cx,
+                                const uint64_t* qp_mod, const uint64_t* qp_barrett, size_t n, size_t size_ql,
+                                size_t size_q, size_t size_p, size_t beta, hipStream_t s) {
+  const size_t size_qlp = size_ql + size_p;
+  const size_t pairs = n * size_qlp / 2;
+  ks_inner_kernel<<<grid_for(pairs), kBlock, 0, s>>>(t_mod_up, evk, cx, qp_mod, qp_barrett, __builtin_ctzll(n), pairs,
+                                                     (uint32_t)size_ql, (uint32_t)size_q, size_qlp * n,
+                                                     (size_q + size_p) * n, (uint32_t)beta);
+  return hipGetLastError();
+}
+
+hipError_t moddown_finish(uint64_t* ct, const uint64_t* cx, const uint64_t* delta, const uint64_t* pinv,
+                          const uint64_t* pinv_shoup, const uint64_t* q, size_t n, size_t size_ql, bool accumulate,
+                          hipStream_t s) {
+  const size_t pairs = n * size_ql / 2;
+  if (accumulate)
+    moddown_finish_kernel<true><<<grid_for(pairs), kBlock, 0, s>>>(ct, cx, delta, pinv, pinv_shoup, q,
+                                                                   __builtin_ctzll(n), pairs);
+  else
+    moddown_finish_kernel<false><<<grid_for(pairs), kBlock, 0, s>>>(ct, cx, delta, pinv, pinv_shoup, q,
+                                                                    __builtin_ctzll(n), pairs);
+  return hipGetLastError();
+}
+
+hipError_t rescale_spread_last(const uint64_t* c_last, uint64_t* tmp, const uint64_t* q, const uint64_t* barrett,
+                               size_t n, size_t L_next, hipStream_t s) {
+  const size_t pairs = n * L_next / 2;
+  rescale_spread_kernel<<<grid_for(pairs), kBlock, 0, s>>>(c_last, tmp, q, barrett, __builtin_ctzll(n), pairs);
+  return hipGetLastError();
+}
+
+hipError_t rescale_finish(const uint64_t* c, const uint64_t* tmp, uint64_t* out, const uint64_t* inv,
+                          const uint64_t* inv_shoup, const uint64_t* q, size_t n, size_t L_next, hipStream_t s) {
+  const size_t pairs = n * L_next / 2;
+  rescale_finish_kernel<<<grid_for(pairs), kBlock, 0, s>>>(c, tmp, out, inv, inv_shoup, q, __builtin_ctzll(n),
+                                                           pairs);
+  return hipGetLastError();
+}
+
+hipError_t galois_ntt(const uint64_t* in, uint64_t* out, const uint32_t* perm, size_t n, size_t L,
+                      hipStream_t s) {
+  const size_t total = n * L;
+  galois_kernel<<<grid_for(total), kBlock, 0, s>>>(in, out, perm, __builtin_ctzll(n), total);
+  return hipGetLastError();
+}
+
+hipError_t switch_modulus_raise(const uint64_t* in_q0, uint64_t* out, const uint64_t* q, const uint64_t* barrett,
+                                size_t n, size_t L, hipStream_t s) {
+  const size_t total = n * L;
+  raise_kernel<<<grid_for(total), kBlock, 0, s>>>(in_q0, out, q, barrett, __builtin_ctzll(n), total);
+  return hipGetLastError();
+}
+
+}  // namespace phx

@@ -1,0 +1,79 @@
+// buffer.h — stream-ordered device buffers (the reference's cuda_auto_ptr,
+// include/cuda_wrapper.cuh:74-219), on hipMallocAsync / hipFreeAsync.  PhantomContext raises the
+// default pool's release threshold so freed blocks stay cached for reuse, as the reference
+// does for its CUDA pool (src/context.cu:127-131).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+#include <utility>
+#include <vector>
+
+#include "hip_check.h"
+
+namespace phantom {
+
+template <typename T>
+class DeviceBuffer {
+ public:
+  DeviceBuffer() = default;
+  DeviceBuffer(size_t count, hipStream_t stream) { allocate(count, stream); }
+  ~DeviceBuffer() { release(); }
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  DeviceBuffer(DeviceBuffer&& o) noexcept { swap(o); }
+  DeviceBuffer& operator=(DeviceBuffer&& o) noexcept {
+    if (this != &o) {
+      release();
+      swap(o);
+    }
+    return *this;
+  }
+
+  void allocate(size_t count, hipStream_t stream) {
+    release();
+    if (count) PHX_CHECK(hipMallocAsync(reinterpret_cast<void**>(&ptr_), count * sizeof(T), stream));
+    count_ = count;
+    stream_ = stream;
+  }
+  void release() {
+    if (ptr_) (void)hipFreeAsync(ptr_, stream_);
+    ptr_ = nullptr;
+    count_ = 0;
+  }
+  // setup-path upload: waits for the copy so the host source may be a temporary
+  void upload(const T* host, size_t count, hipStream_t stream) {
+    allocate(count, stream);
+    if (count) {
+      PHX_CHECK(hipMemcpyAsync(ptr_, host, count * sizeof(T), hipMemcpyHostToDevice, stream));
+      PHX_CHECK(hipStreamSynchronize(stream));
+    }
+  }
+  void upload(const std::vector<T>& v, hipStream_t stream) { upload(v.data(), v.size(), stream); }
+  std::vector<T> download(hipStream_t stream) const {
+    std::vector<T> v(count_);
+    if (count_) {
+      PHX_CHECK(hipMemcpyAsync(v.data(), ptr_, count_ * sizeof(T), hipMemcpyDeviceToHost, stream));
+      PHX_CHECK(hipStreamSynchronize(stream));
+    }
+    return v;
+  }
+
+  T* get() const { return ptr_; }
+  size_t size() const { return count_; }
+  hipStream_t stream() const { return stream_; }
+  explicit operator bool() const { return ptr_ != nullptr; }
+
+ private:
+  void swap(DeviceBuffer& o) noexcept {
+    std::swap(ptr_, o.ptr_);
+    std::swap(count_, o.count_);
+    std::swap(stream_, o.stream_);
+  }
+  T* ptr_ = nullptr;
+  size_t count_ = 0;
+  hipStream_t stream_ = nullptr;
+};
+
+}  // namespace phantom

@@ -4,7 +4,7 @@
 #include <new>
 #include <stdexcept>
 
-#include "../../include/phantom_amd.h"
+#include "phantom_amd.h"
 #include "hip_check.h"
 
 namespace phantom::capi {
@@ -15,9 +15,9 @@ int from_hip(hipError_t e);
 // Run `body` (which returns an int status) and map C++ exceptions to status codes, the way
 // the reference's exception classes map (std::invalid_argument, std::logic_error,
 // std::runtime_error from CUDA checks).
-#define PHX_CAPI_GUARD(body)                                                                  \
+#define PHX_CAPI_GUARD(...)                                                                   \
   try {                                                                                       \
-    body                                                                                      \
+    __VA_ARGS__                                                                                   \
   } catch (const ::phantom::hip_error& e) {                                                   \
     return ::phantom::capi::fail(PHANTOM_ERR_HIP, e.what());                                  \
   } catch (const std::invalid_argument& e) {                                                  \

@@ -1,0 +1,80 @@
+#include "ciphertext.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace phantom {
+
+void PhantomCiphertext::resize(const PhantomContext& ctx, size_t chain_index, size_t size, hipStream_t s,
+                               bool copy_old) {
+  const auto& cd = ctx.get_context_data(chain_index);
+  resize(size, cd.coeff_modulus_size(), ctx.poly_degree(), s, copy_old);
+  chain_index_ = chain_index;
+}
+
+void PhantomCiphertext::resize(size_t size, size_t L, size_t n, hipStream_t s, bool copy_old) {
+  const size_t old_count = size_ * L_ * n_, new_count = size * L * n;
+  if (new_count == 0) {
+    data_.release();
+  } else if (new_count != old_count) {
+    DeviceBuffer<uint64_t> fresh(new_count, s);
+    if (copy_old && data_) {
+      const size_t c = std::min(old_count, new_count);
+      PHX_CHECK(hipMemcpyAsync(fresh.get(), data_.get(), c * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    }
+    data_ = std::move(fresh);
+  }
+  size_ = size;
+  L_ = L;
+  n_ = n;
+}
+
+void PhantomCiphertext::copy_from(const PhantomCiphertext& o) {
+  chain_index_ = o.chain_index_;
+  size_ = o.size_;
+  n_ = o.n_;
+  L_ = o.L_;
+  scale_ = o.scale_;
+  correction_factor_ = o.correction_factor_;
+  noise_scale_deg_ = o.noise_scale_deg_;
+  is_ntt_form_ = o.is_ntt_form_;
+  const size_t count = size_ * L_ * n_;
+  hipStream_t s = o.data_.stream();
+  data_.allocate(count, s);
+  if (count) PHX_CHECK(hipMemcpyAsync(data_.get(), o.data_.get(), count * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+}
+
+std::vector<uint64_t> PhantomCiphertext::to_host(hipStream_t s) const {
+  std::vector<uint64_t> v(size_ * L_ * n_);
+  if (!v.empty()) {
+    PHX_CHECK(hipMemcpyAsync(v.data(), data_.get(), v.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    PHX_CHECK(hipStreamSynchronize(s));
+  }
+  return v;
+}
+
+void PhantomCiphertext::from_host(const PhantomContext& ctx, size_t chain_index, size_t size,
+                                  const std::vector<uint64_t>& v, hipStream_t s) {
+  resize(ctx, chain_index, size, s, false);
+  if (v.size() != size_ * L_ * n_) throw std::invalid_argument("ciphertext data size mismatch");
+  PHX_CHECK(hipMemcpyAsync(data_.get(), v.data(), v.size() * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  PHX_CHECK(hipStreamSynchronize(s));
+}
+
+void PhantomPlaintext::resize(const PhantomContext& ctx, size_t chain_index, hipStream_t s) {
+  const auto& cd = ctx.get_context_data(chain_index);
+  chain_index_ = chain_index;
+  L_ = cd.coeff_modulus_size();
+  n_ = ctx.poly_degree();
+  data_.allocate(L_ * n_, s);
+}
+
+void PhantomPlaintext::from_host(const PhantomContext& ctx, size_t chain_index, const std::vector<uint64_t>& v,
+                                 hipStream_t s) {
+  resize(ctx, chain_index, s);
+  if (v.size() != L_ * n_) throw std::invalid_argument("plaintext data size mismatch");
+  PHX_CHECK(hipMemcpyAsync(data_.get(), v.data(), v.size() * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  PHX_CHECK(hipStreamSynchronize(s));
+}
+
+}  // namespace phantom

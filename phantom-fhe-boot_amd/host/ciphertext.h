@@ -1,0 +1,79 @@
+// ciphertext.h — PhantomCiphertext / PhantomPlaintext (include/ciphertext.h, include/plaintext.h):
+// device-resident RNS polynomials in the reference's layout data[(poly * L + limb) * n + k].
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <vector>
+
+#include "buffer.h"
+#include "context.h"
+
+namespace phantom {
+
+class PhantomCiphertext {
+ public:
+  PhantomCiphertext() = default;
+  PhantomCiphertext(PhantomCiphertext&&) = default;
+  PhantomCiphertext& operator=(PhantomCiphertext&&) = default;
+  // deep device copy (the reference copies through cuda_auto_ptr, cuda_wrapper.cuh:94-104)
+  PhantomCiphertext(const PhantomCiphertext& o) { copy_from(o); }
+  PhantomCiphertext& operator=(const PhantomCiphertext& o) {
+    if (this != &o) copy_from(o);
+    return *this;
+  }
+
+  // ciphertext.h:50-80: reallocate for (chain_index, size); keeps the leading old data.
+  void resize(const PhantomContext& ctx, size_t chain_index, size_t size, hipStream_t s, bool copy_old = true);
+  void resize(size_t size, size_t coeff_modulus_size, size_t n, hipStream_t s, bool copy_old = true);
+
+  uint64_t* data() const { return data_.get(); }
+  size_t chain_index() const { return chain_index_; }
+  size_t size() const { return size_; }
+  size_t poly_modulus_degree() const { return n_; }
+  size_t coeff_modulus_size() const { return L_; }
+  double scale() const { return scale_; }
+  bool is_ntt_form() const { return is_ntt_form_; }
+  uint64_t correction_factor() const { return correction_factor_; }
+  size_t GetNoiseScaleDeg() const { return noise_scale_deg_; }
+
+  void set_scale(double s) { scale_ = s; }
+  void set_chain_index(size_t c) { chain_index_ = c; }
+  void set_ntt_form(bool b) { is_ntt_form_ = b; }
+  void SetNoiseScaleDeg(size_t d) { noise_scale_deg_ = d; }
+  void set_correction_factor(uint64_t c) { correction_factor_ = c; }
+
+  // host transfer helpers (the reference's save/load staging, ciphertext.h:184-225)
+  std::vector<uint64_t> to_host(hipStream_t s) const;
+  void from_host(const PhantomContext& ctx, size_t chain_index, size_t size, const std::vector<uint64_t>& v,
+                 hipStream_t s);
+
+ private:
+  void copy_from(const PhantomCiphertext& o);
+  size_t chain_index_ = 0, size_ = 0, n_ = 0, L_ = 0;
+  double scale_ = 1.0;
+  uint64_t correction_factor_ = 1;
+  size_t noise_scale_deg_ = 1;
+  bool is_ntt_form_ = true;
+  DeviceBuffer<uint64_t> data_;
+};
+
+class PhantomPlaintext {
+ public:
+  uint64_t* data() const { return data_.get(); }
+  size_t chain_index() const { return chain_index_; }
+  size_t coeff_modulus_size() const { return L_; }
+  size_t poly_modulus_degree() const { return n_; }
+  double scale() const { return scale_; }
+  bool is_ntt_form() const { return true; }
+  void set_scale(double s) { scale_ = s; }
+  void resize(const PhantomContext& ctx, size_t chain_index, hipStream_t s);
+  void from_host(const PhantomContext& ctx, size_t chain_index, const std::vector<uint64_t>& v, hipStream_t s);
+
+ private:
+  size_t chain_index_ = 0, n_ = 0, L_ = 0;
+  double scale_ = 1.0;
+  DeviceBuffer<uint64_t> data_;
+};
+
+}  // namespace phantom

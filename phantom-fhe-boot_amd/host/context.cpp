@@ -1,0 +1,59 @@
+#include "context.h"
+
+#include <stdexcept>
+#include <thread>
+
+#include "hip_check.h"
+
+namespace phantom {
+
+PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t stream)
+    : params_(params), stream_(stream) {
+  if (params.scheme() != scheme_type::ckks) throw std::invalid_argument("only CKKS is supported by this engine");
+  const auto& mods = params.coeff_modulus();
+  if (mods.size() < 2) throw std::invalid_argument("The coefficient modulus must be a vector of at least two primes");
+  n_ = params.poly_modulus_degree();
+  size_P_ = params.special_modulus_size();
+  if (size_P_ >= mods.size()) throw std::invalid_argument("special modulus size too large");
+  size_Q_ = mods.size() - size_P_;
+  for (const auto& m : mods) qp_.push_back(m.value());
+
+  // keep freed stream-ordered allocations cached (src/context.cu:127-131)
+  int dev = 0;
+  PHX_CHECK(hipGetDevice(&dev));
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+    uint64_t threshold = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &threshold);
+  }
+
+  ntt_ = std::make_unique<DeviceNttTables>(n_, qp_, stream_);
+  data_.push_back(std::make_unique<ContextData>(0, qp_));
+  for (size_t c = 1; c <= size_Q_; ++c) {
+    std::vector<uint64_t> ql(qp_.begin(), qp_.begin() + (size_Q_ - (c - 1)));
+    data_.push_back(std::make_unique<ContextData>(c, ql));
+  }
+  // per-level RNS tools (host constant generation is O(L^2) per level; run levels in parallel)
+  std::vector<std::unique_ptr<RnsTool>> tools(size_Q_ + 1);
+  {
+    std::vector<std::thread> th;
+    const unsigned nt = std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 8u);
+    std::vector<std::exception_ptr> errs(nt);
+    for (unsigned w = 0; w < nt; ++w)
+      th.emplace_back([&, w] {
+        try {
+          for (size_t c = 1 + w; c <= size_Q_; c += nt)
+            tools[c] = std::make_unique<RnsTool>(n_, qp_, size_P_, size_Q_ - (c - 1), stream_);
+        } catch (...) {
+          errs[w] = std::current_exception();
+        }
+      });
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+  }
+  for (size_t c = 1; c <= size_Q_; ++c) data_[c]->set_rns_tool(std::move(tools[c]));
+  PHX_CHECK(hipStreamSynchronize(stream_));
+}
+
+}  // namespace phantom

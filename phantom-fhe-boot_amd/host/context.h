@@ -1,0 +1,93 @@
+// context.h — EncryptionParameters, PhantomContext and per-level ContextData, mirroring the
+// reference's include/host/encryptionparams.h and include/context.cuh:16-272 (CKKS subset).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "modulus.h"
+#include "ntt_tables.h"
+#include "rns_tool.h"
+
+namespace phantom {
+
+enum class scheme_type : uint8_t { none = 0, bfv = 1, ckks = 2, bgv = 3 };
+
+// EncryptionParameters (include/host/encryptionparams.h): the CKKS fields this engine uses.
+class EncryptionParameters {
+ public:
+  explicit EncryptionParameters(scheme_type scheme = scheme_type::ckks) : scheme_(scheme) {}
+  void set_poly_modulus_degree(size_t n) { poly_modulus_degree_ = n; }
+  void set_coeff_modulus(const std::vector<arith::Modulus>& m) { coeff_modulus_ = m; }
+  void set_special_modulus_size(size_t s) { special_modulus_size_ = s; }
+  void set_galois_elts(const std::vector<uint32_t>& g) { galois_elts_ = g; }
+  scheme_type scheme() const { return scheme_; }
+  size_t poly_modulus_degree() const { return poly_modulus_degree_; }
+  const std::vector<arith::Modulus>& coeff_modulus() const { return coeff_modulus_; }
+  std::vector<arith::Modulus>& coeff_modulus() { return coeff_modulus_; }
+  size_t special_modulus_size() const { return special_modulus_size_; }
+  const std::vector<uint32_t>& galois_elts() const { return galois_elts_; }
+
+ private:
+  scheme_type scheme_;
+  size_t poly_modulus_degree_ = 0;
+  std::vector<arith::Modulus> coeff_modulus_;
+  size_t special_modulus_size_ = 1;
+  std::vector<uint32_t> galois_elts_;
+};
+
+// Per-level data: chain index 0 is the key level (Q u P), 1 the full data chain Q, and each
+// further index drops the last data prime (src/context.cu:133-159).
+class ContextData {
+ public:
+  ContextData(size_t chain_index, std::vector<uint64_t> moduli) : chain_index_(chain_index), moduli_(std::move(moduli)) {}
+  size_t chain_index() const { return chain_index_; }
+  const std::vector<uint64_t>& moduli() const { return moduli_; }
+  size_t coeff_modulus_size() const { return moduli_.size(); }
+  const RnsTool& gpu_rns_tool() const { return *rns_tool_; }
+  bool has_rns_tool() const { return rns_tool_ != nullptr; }
+  void set_rns_tool(std::unique_ptr<RnsTool> t) { rns_tool_ = std::move(t); }
+
+ private:
+  size_t chain_index_;
+  std::vector<uint64_t> moduli_;
+  std::unique_ptr<RnsTool> rns_tool_;
+};
+
+class PhantomContext {
+ public:
+  explicit PhantomContext(const EncryptionParameters& params, hipStream_t stream = nullptr);
+  PhantomContext(const PhantomContext&) = delete;
+  PhantomContext& operator=(const PhantomContext&) = delete;
+
+  const EncryptionParameters& params() const { return params_; }
+  size_t poly_degree() const { return n_; }
+  size_t size_Q() const { return size_Q_; }
+  size_t size_P() const { return size_P_; }
+  size_t size_QP() const { return size_Q_ + size_P_; }
+  const std::vector<uint64_t>& key_moduli() const { return qp_; }
+
+  const ContextData& get_context_data(size_t chain_index) const { return *data_.at(chain_index); }
+  size_t total_parm_size() const { return data_.size(); }
+  size_t get_first_index() const { return 1; }
+  size_t get_next_index(size_t i) const { return i + 1 < data_.size() ? i + 1 : i; }
+  size_t get_previous_index(size_t i) const { return i > 0 ? i - 1 : 0; }
+  size_t coeff_mod_size() const { return qp_.size(); }
+
+  // NTT tables and per-modulus device constants over the whole Q u P chain
+  const phx::NttTables& gpu_rns_tables() const { return ntt_->get(); }
+  phx::ModView mod_QP() const { return {ntt_->get().modulus, ntt_->get().barrett}; }
+  hipStream_t stream() const { return stream_; }
+
+ private:
+  EncryptionParameters params_;
+  size_t n_ = 0, size_Q_ = 0, size_P_ = 0;
+  std::vector<uint64_t> qp_;
+  std::unique_ptr<DeviceNttTables> ntt_;
+  std::vector<std::unique_ptr<ContextData>> data_;
+  hipStream_t stream_;
+};
+
+}  // namespace phantom

@@ -1,0 +1,183 @@
+#include "evaluate.h"
+
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+
+#include "../csrc/rns.h"
+#include "numth.h"
+
+namespace phantom {
+
+static void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw hip_error(e, what);
+}
+
+void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, const uint64_t* c2,
+                   const uint64_t* const* evk, hipStream_t s) {
+  if (ctx.size_P() == 0) throw std::invalid_argument("key switching requires special primes");
+  if (chain_index < 1 || chain_index >= ctx.total_parm_size()) throw std::invalid_argument("invalid chain index");
+  const size_t n = ctx.poly_degree();
+  // levelsDropped = chain_index - 1 (src/eval_key_switch.cu:145-148)
+  const RnsTool& rt = ctx.get_context_data(chain_index).gpu_rns_tool();
+  const size_t size_Ql = rt.size_Ql(), size_QlP = size_Ql + ctx.size_P(), beta = rt.beta();
+  DeviceBuffer<uint64_t> t_mod_up(beta * size_QlP * n, s);
+  rt.modup(t_mod_up.get(), c2, ctx.gpu_rns_tables(), s);
+  DeviceBuffer<uint64_t> cx(2 * size_QlP * n, s);
+  hip_ok(phx::keyswitch_inner_prod(t_mod_up.get(), evk, cx.get(), ctx.mod_QP().q, ctx.mod_QP().barrett, n, size_Ql,
+                                   ctx.size_Q(), ctx.size_P(), beta, s),
+         "keyswitch inner product");
+  t_mod_up.release();
+  for (size_t i = 0; i < 2; ++i)
+    rt.moddown_add(ct + i * size_Ql * n, cx.get() + i * size_QlP * n, true, ctx.gpu_rns_tables(), s);
+}
+
+void keyswitch_inplace(const PhantomContext& ctx, PhantomCiphertext& ct, const uint64_t* c2,
+                       const uint64_t* const* evk) {
+  keyswitch_raw(ctx, ct.chain_index(), ct.data(), c2, evk, ctx.stream());
+}
+
+static void check_same(const PhantomCiphertext& a, const PhantomCiphertext& b) {
+  if (a.chain_index() != b.chain_index()) throw std::invalid_argument("encrypted1 and encrypted2 parameter mismatch");
+  if (a.is_ntt_form() != b.is_ntt_form()) throw std::invalid_argument("NTT form mismatch");
+}
+
+void add_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b) {
+  check_same(a, b);
+  if (a.size() != b.size()) throw std::invalid_argument("poly number mismatch");
+  const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
+  for (size_t i = 0; i < a.size(); ++i)
+    hip_ok(phx::poly_add(a.data() + i * L * n, b.data() + i * L * n, a.data() + i * L * n, ctx.mod_QP(), n, L,
+                         ctx.stream()),
+           "add");
+}
+
+void sub_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b, bool negate) {
+  check_same(a, b);
+  const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
+  for (size_t i = 0; i < a.size(); ++i) {
+    uint64_t* x = a.data() + i * L * n;
+    const uint64_t* y = b.data() + i * L * n;
+    if (negate) hip_ok(phx::poly_sub(y, x, x, ctx.mod_QP(), n, L, ctx.stream()), "sub");
+    else hip_ok(phx::poly_sub(x, y, x, ctx.mod_QP(), n, L, ctx.stream()), "sub");
+  }
+}
+
+void negate_inplace(const PhantomContext& ctx, PhantomCiphertext& a) {
+  const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
+  for (size_t i = 0; i < a.size(); ++i)
+    hip_ok(phx::poly_negate(a.data() + i * L * n, a.data() + i * L * n, ctx.mod_QP(), n, L, ctx.stream()), "negate");
+}
+
+void add_plain_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomPlaintext& p) {
+  if (a.chain_index() != p.chain_index()) throw std::invalid_argument("encrypted and plain parameter mismatch");
+  hip_ok(phx::poly_add(a.data(), p.data(), a.data(), ctx.mod_QP(), ctx.poly_degree(), a.coeff_modulus_size(),
+                       ctx.stream()),
+         "add_plain");
+}
+
+void multiply_plain_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomPlaintext& p) {
+  if (a.chain_index() != p.chain_index()) throw std::invalid_argument("encrypted and plain parameter mismatch");
+  const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
+  for (size_t i = 0; i < a.size(); ++i)
+    hip_ok(phx::poly_mul(a.data() + i * L * n, p.data(), a.data() + i * L * n, ctx.mod_QP(), n, L, ctx.stream()),
+           "multiply_plain");
+  a.set_scale(a.scale() * p.scale());
+}
+
+void multiply_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b) {
+  check_same(a, b);
+  if (!a.is_ntt_form()) throw std::invalid_argument("encrypted1 and encrypted2 must be in NTT form");
+  if (a.size() != 2 || b.size() != 2) throw std::invalid_argument("only size-2 ciphertexts are supported");
+  const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
+  hipStream_t s = ctx.stream();
+  a.resize(ctx, a.chain_index(), 3, s);
+  // tensor_prod_2x2 reads (a0, a1) and writes (d0, d1, d2) in place: every element is read
+  // before the same thread writes it, so aliasing out with ct1 is safe.
+  hip_ok(phx::tensor_prod_2x2(a.data(), &a == &b ? a.data() : b.data(), a.data(), ctx.mod_QP(), n, L, s), "tensor");
+  a.set_scale(a.scale() * b.scale());
+}
+
+void relinearize_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomRelinKey& rlk) {
+  if (a.size() != 3) throw std::invalid_argument("destination_size must be 3");
+  if (!a.is_ntt_form()) throw std::invalid_argument("CKKS encrypted must be in NTT form");
+  const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
+  keyswitch_inplace(ctx, a, a.data() + 2 * L * n, rlk.public_keys_ptr());
+  a.resize(2, L, n, ctx.stream());
+}
+
+PhantomCiphertext rescale_to_next(const PhantomContext& ctx, const PhantomCiphertext& a) {
+  if (a.chain_index() + 1 >= ctx.total_parm_size()) throw std::invalid_argument("end of modulus switching chain reached");
+  const RnsTool& rt = ctx.get_context_data(a.chain_index()).gpu_rns_tool();
+  PhantomCiphertext d;
+  d.resize(ctx, a.chain_index() + 1, a.size(), ctx.stream(), false);
+  rt.rescale_ntt(a.data(), d.data(), a.size(), ctx.gpu_rns_tables(), ctx.stream());
+  d.set_ntt_form(a.is_ntt_form());
+  d.set_scale(a.scale() / static_cast<double>(rt.base_Ql().back()));
+  d.SetNoiseScaleDeg(a.GetNoiseScaleDeg());
+  return d;
+}
+
+PhantomCiphertext mod_switch_to_next(const PhantomContext& ctx, const PhantomCiphertext& a) {
+  if (a.chain_index() + 1 >= ctx.total_parm_size()) throw std::invalid_argument("end of modulus switching chain reached");
+  const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
+  PhantomCiphertext d;
+  d.resize(ctx, a.chain_index() + 1, a.size(), ctx.stream(), false);
+  for (size_t i = 0; i < a.size(); ++i)
+    PHX_CHECK(hipMemcpyAsync(d.data() + i * (L - 1) * n, a.data() + i * L * n, (L - 1) * n * sizeof(uint64_t),
+                             hipMemcpyDeviceToDevice, ctx.stream()));
+  d.set_scale(a.scale());
+  d.set_ntt_form(a.is_ntt_form());
+  d.SetNoiseScaleDeg(a.GetNoiseScaleDeg());
+  return d;
+}
+
+void mod_switch_to_inplace(const PhantomContext& ctx, PhantomCiphertext& a, size_t chain_index) {
+  if (chain_index < a.chain_index()) throw std::invalid_argument("cannot switch to higher level modulus");
+  while (a.chain_index() < chain_index) a = mod_switch_to_next(ctx, a);
+}
+
+// NTT-domain permutation tables per Galois element (PrecomputeAutoMapKernel, src/util.cu:941-958),
+// built once per (degree, element) and cached.
+static const uint32_t* galois_perm(size_t n, uint32_t elt, hipStream_t s) {
+  static std::mutex mu;
+  // intentionally never destroyed: device memory must not be freed after HIP teardown
+  static auto& cache = *new std::map<std::pair<size_t, uint32_t>, DeviceBuffer<uint32_t>>();
+  std::lock_guard<std::mutex> lk(mu);
+  auto key = std::make_pair(n, elt);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second.get();
+  const int logn = arith::log2_exact(n);
+  std::vector<uint32_t> perm(n);
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint64_t idx = ((2ull * j + 1) * elt) % (2ull * n);
+    perm[arith::reverse_bits(j, logn)] = arith::reverse_bits(static_cast<uint32_t>(idx >> 1), logn);
+  }
+  DeviceBuffer<uint32_t> d;
+  d.upload(perm, s);
+  const uint32_t* p = d.get();
+  cache.emplace(key, std::move(d));
+  return p;
+}
+
+void apply_galois_inplace(const PhantomContext& ctx, PhantomCiphertext& a, uint32_t elt, const PhantomGaloisKey& keys) {
+  if (a.size() != 2) throw std::invalid_argument("encrypted size must be 2");
+  const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
+  hipStream_t s = ctx.stream();
+  const uint32_t* perm = galois_perm(n, elt, s);
+  DeviceBuffer<uint64_t> temp(L * n, s);
+  uint64_t* c0 = a.data();
+  uint64_t* c1 = a.data() + L * n;
+  hip_ok(phx::galois_ntt(c0, temp.get(), perm, n, L, s), "galois c0");
+  PHX_CHECK(hipMemcpyAsync(c0, temp.get(), L * n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+  hip_ok(phx::galois_ntt(c1, temp.get(), perm, n, L, s), "galois c1");
+  PHX_CHECK(hipMemsetAsync(c1, 0, L * n * sizeof(uint64_t), s));
+  keyswitch_inplace(ctx, a, temp.get(), keys.get(elt).public_keys_ptr());
+}
+
+void rotate_inplace(const PhantomContext& ctx, PhantomCiphertext& a, int step, const PhantomGaloisKey& keys) {
+  apply_galois_inplace(ctx, a, galois_elt_from_step(step, ctx.poly_degree()), keys);
+}
+
+}  // namespace phantom

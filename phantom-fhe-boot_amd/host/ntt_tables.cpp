@@ -74,6 +74,29 @@ DeviceNttTables::DeviceNttTables(size_t n, const std::vector<uint64_t>& moduli, 
     alloc_copy(dst, flat);
     PHX_CHECK(hipStreamSynchronize(stream));  // flat is reused
   };
+  {
+    std::vector<double> qf(L), qi(L), twf(n * L);
+    std::vector<uint8_t> f64(L);
+    for (size_t i = 0; i < L; ++i) {
+      const uint64_t q = moduli[i];
+      qf[i] = static_cast<double>(q);
+      qi[i] = 1.0 / static_cast<double>(q);
+      f64[i] = q < (1ull << 50) ? 1 : 0;
+      for (size_t k = 0; k < n; ++k) {
+        const uint64_t w = host[i].tw[k];
+        twf[i * n + k] = w > (q - 1) / 2 ? -static_cast<double>(q - w) : static_cast<double>(w);
+      }
+    }
+    PHX_CHECK(hipMalloc(&t_.modulus_f, L * sizeof(double)));
+    PHX_CHECK(hipMalloc(&t_.modulus_inv, L * sizeof(double)));
+    PHX_CHECK(hipMalloc(&t_.is_f64, L));
+    PHX_CHECK(hipMalloc(&t_.twf, n * L * sizeof(double)));
+    PHX_CHECK(hipMemcpyAsync(t_.modulus_f, qf.data(), L * sizeof(double), hipMemcpyHostToDevice, stream));
+    PHX_CHECK(hipMemcpyAsync(t_.modulus_inv, qi.data(), L * sizeof(double), hipMemcpyHostToDevice, stream));
+    PHX_CHECK(hipMemcpyAsync(t_.is_f64, f64.data(), L, hipMemcpyHostToDevice, stream));
+    PHX_CHECK(hipMemcpyAsync(t_.twf, twf.data(), n * L * sizeof(double), hipMemcpyHostToDevice, stream));
+    PHX_CHECK(hipStreamSynchronize(stream));
+  }
   gather(t_.tw, &HostNttTable::tw);
   gather(t_.tw_shoup, &HostNttTable::tw_shoup);
   gather(t_.itw, &HostNttTable::itw);
@@ -82,6 +105,8 @@ DeviceNttTables::DeviceNttTables(size_t n, const std::vector<uint64_t>& moduli, 
 
 DeviceNttTables::~DeviceNttTables() {
   for (uint64_t* p : {t_.modulus, t_.barrett, t_.tw, t_.tw_shoup, t_.itw, t_.itw_shoup, t_.n_inv, t_.n_inv_shoup})
+    if (p) (void)hipFree(p);
+  for (void* p : {(void*)t_.modulus_f, (void*)t_.modulus_inv, (void*)t_.is_f64, (void*)t_.twf})
     if (p) (void)hipFree(p);
 }
 

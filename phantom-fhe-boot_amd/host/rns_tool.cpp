@@ -1,0 +1,192 @@
+#include "rns_tool.h"
+
+#include <cmath>
+#include <stdexcept>
+
+#include "numth.h"
+
+namespace phantom {
+
+using namespace phantom::arith;
+
+void DeviceBaseConverter::init(const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, hipStream_t s) {
+  ibase = in;
+  obase = out;
+  const size_t I = in.size(), O = out.size();
+  std::vector<uint64_t> qinv(I), qinvs(I), qhat(I * O), ob(2 * O);
+  for (size_t i = 0; i < I; ++i) {
+    uint64_t prod = 1 % in[i];
+    for (size_t k = 0; k < I; ++k)
+      if (k != i) prod = mul_mod(prod, in[k] % in[i], in[i]);
+    qinv[i] = inv_mod(prod, in[i]);
+    qinvs[i] = shoup(qinv[i], in[i]);
+    for (size_t j = 0; j < O; ++j) {
+      uint64_t pr = 1 % out[j];
+      for (size_t k = 0; k < I; ++k)
+        if (k != i) pr = mul_mod(pr, in[k] % out[j], out[j]);
+      qhat[i * O + j] = pr;
+    }
+  }
+  for (size_t j = 0; j < O; ++j) barrett_ratio(out[j], &ob[2 * j]);
+  d_ibase.upload(in, s);
+  d_obase.upload(out, s);
+  d_obase_barrett.upload(ob, s);
+  d_qhat_inv.upload(qinv, s);
+  d_qhat_inv_shoup.upload(qinvs, s);
+  d_qhat_mod_p.upload(qhat, s);
+}
+
+phx::BconvArgs DeviceBaseConverter::args(const uint64_t* in, uint64_t* out, bool prescale) const {
+  phx::BconvArgs a;
+  a.in = in;
+  a.out = out;
+  a.ibase = d_ibase.get();
+  a.qhat_inv = prescale ? d_qhat_inv.get() : nullptr;
+  a.qhat_inv_shoup = prescale ? d_qhat_inv_shoup.get() : nullptr;
+  a.qhat_mod_p = d_qhat_mod_p.get();
+  a.obase = d_obase.get();
+  a.obase_barrett = d_obase_barrett.get();
+  a.ibase_size = static_cast<int>(ibase.size());
+  a.obase_size = static_cast<int>(obase.size());
+  return a;
+}
+
+RnsTool::RnsTool(size_t n, const std::vector<uint64_t>& qp, size_t size_P, size_t size_Ql, hipStream_t s)
+    : n_(n), size_Q_(qp.size() - size_P), size_P_(size_P) {
+  if (size_Ql == 0 || size_Ql > size_Q_) throw std::invalid_argument("invalid level");
+  base_Ql_.assign(qp.begin(), qp.begin() + size_Ql);
+  base_P_.assign(qp.begin() + size_Q_, qp.end());
+  std::vector<uint64_t> bar(2 * size_Ql);
+  for (size_t i = 0; i < size_Ql; ++i) barrett_ratio(base_Ql_[i], &bar[2 * i]);
+  d_Ql_.upload(base_Ql_, s);
+  d_Ql_barrett_.upload(bar, s);
+
+  // rescale constants: q_last^-1 mod q_i (src/rns.cu:64-82)
+  if (size_Ql > 1) {
+    const uint64_t ql = base_Ql_.back();
+    std::vector<uint64_t> inv(size_Ql - 1), invs(size_Ql - 1);
+    for (size_t i = 0; i + 1 < size_Ql; ++i) {
+      inv[i] = inv_mod(ql % base_Ql_[i], base_Ql_[i]);
+      invs[i] = shoup(inv[i], base_Ql_[i]);
+    }
+    d_inv_qlast_.upload(inv, s);
+    d_inv_qlast_shoup_.upload(invs, s);
+  }
+
+  if (size_P == 0) return;
+  // hybrid key switching constants (src/rns.cu:97-187)
+  const size_t alpha = size_P;
+  std::vector<uint64_t> pm(size_Ql), pms(size_Ql), pim(size_Ql), pims(size_Ql);
+  for (size_t i = 0; i < size_Ql; ++i) {
+    const uint64_t q = base_Ql_[i];
+    uint64_t P = 1 % q;
+    for (uint64_t p : base_P_) P = mul_mod(P, p % q, q);
+    pm[i] = P;
+    pms[i] = shoup(P, q);
+    pim[i] = inv_mod(P, q);
+    pims[i] = shoup(pim[i], q);
+  }
+  d_bigP_mod_q_.upload(pm, s);
+  d_bigP_mod_q_shoup_.upload(pms, s);
+  d_bigPInv_mod_q_.upload(pim, s);
+  d_bigPInv_mod_q_shoup_.upload(pims, s);
+
+  std::vector<uint64_t> qlp(base_Ql_);
+  qlp.insert(qlp.end(), base_P_.begin(), base_P_.end());
+  const size_t beta = static_cast<size_t>(std::ceil(static_cast<double>(size_Ql) / static_cast<double>(alpha)));
+  std::vector<uint64_t> hatinv(size_Ql), hatinvs(size_Ql);
+  converters_.resize(beta);
+  for (size_t b = 0; b < beta; ++b) {
+    const size_t start = alpha * b;
+    const size_t part = b == beta - 1 ? size_Ql - alpha * (beta - 1) : alpha;
+    std::vector<uint64_t> pin(qlp.begin() + start, qlp.begin() + start + part), compl_;
+    for (size_t j = 0; j < qlp.size(); ++j)
+      if (j < start || j >= start + part) compl_.push_back(qlp[j]);
+    converters_[b].init(pin, compl_, s);
+    digit_start_.push_back(start);
+    digit_size_.push_back(part);
+    // partQlHatInv_mod_Ql_concat: the digit-local qHat^-1 of every Ql prime
+    for (size_t i = 0; i < part; ++i) {
+      uint64_t prod = 1 % pin[i];
+      for (size_t k = 0; k < part; ++k)
+        if (k != i) prod = mul_mod(prod, pin[k] % pin[i], pin[i]);
+      hatinv[start + i] = inv_mod(prod, pin[i]);
+      hatinvs[start + i] = shoup(hatinv[start + i], pin[i]);
+    }
+  }
+  d_partQlHatInv_.upload(hatinv, s);
+  d_partQlHatInv_shoup_.upload(hatinvs, s);
+  p_to_ql_.init(base_P_, base_Ql_, s);
+}
+
+static void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw hip_error(e, what);
+}
+
+void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables& ntt, hipStream_t s) const {
+  const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_, alpha = size_P_;
+  DeviceBuffer<uint64_t> t_cks(size_Ql * n_, s);
+  // INTT(c2) * partQlHatInv (nwt_2d_radix8_backward_scale)
+  hip_ok(phx::ntt_inverse(ntt, c2, t_cks.get(), phx::LimbMap::contiguous((int)size_Ql, 0), d_partQlHatInv_.get(),
+                          d_partQlHatInv_shoup_.get(), s),
+         "modup INTT");
+  hip_ok(phx::modup_copy_digits(c2, t_mod_up, n_, size_Ql, size_QlP, alpha, s), "modup copy");
+  for (size_t b = 0; b < converters_.size(); ++b) {
+    const size_t start = digit_start_[b], part = digit_size_[b];
+    uint64_t* dst = t_mod_up + b * size_QlP * n_;
+    phx::BconvArgs a = converters_[b].args(t_cks.get() + start * n_, dst, false);
+    a.skip_at = (int)start;
+    a.skip_len = (int)part;
+    hip_ok(phx::bconv(a, n_, s), "modup bconv");
+    // NTT of every limb but the digit's own (include_special_mod_exclude_range)
+    phx::LimbMap m;
+    m.num_limbs = (int)size_QlP;
+    m.split = (int)size_Ql;
+    m.first_a = 0;
+    m.first_b = (int)size_Q_;
+    m.skip_begin = (int)start;
+    m.skip_end = (int)(start + part);
+    hip_ok(phx::ntt_forward(ntt, dst, dst, m, s), "modup NTT");
+  }
+}
+
+void RnsTool::moddown_add(uint64_t* ct_i, uint64_t* cx_i, bool accumulate, const phx::NttTables& ntt,
+                          hipStream_t s) const {
+  const size_t size_Ql = base_Ql_.size();
+  uint64_t* cp = cx_i + size_Ql * n_;
+  phx::LimbMap pm;
+  pm.num_limbs = (int)size_P_;
+  pm.split = 0;
+  pm.first_a = 0;
+  pm.first_b = (int)size_Q_;
+  hip_ok(phx::ntt_inverse(ntt, cp, cp, pm, nullptr, nullptr, s), "moddown INTT(P)");
+  DeviceBuffer<uint64_t> delta(size_Ql * n_, s);
+  hip_ok(phx::bconv(p_to_ql_.args(cp, delta.get(), true), n_, s), "moddown bconv");
+  hip_ok(phx::ntt_forward(ntt, delta.get(), delta.get(), phx::LimbMap::contiguous((int)size_Ql, 0), s),
+         "moddown NTT");
+  hip_ok(phx::moddown_finish(ct_i, cx_i, delta.get(), d_bigPInv_mod_q_.get(), d_bigPInv_mod_q_shoup_.get(),
+                             d_Ql_.get(), n_, size_Ql, accumulate, s),
+         "moddown finish");
+}
+
+void RnsTool::rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const phx::NttTables& ntt,
+                          hipStream_t s) const {
+  const size_t L = base_Ql_.size();
+  if (L < 2) throw std::invalid_argument("end of modulus switching chain reached");
+  const size_t Ln = L - 1;
+  DeviceBuffer<uint64_t> last(n_, s), tmp(Ln * n_, s);
+  for (size_t c = 0; c < polys; ++c) {
+    const uint64_t* ci = in + c * L * n_;
+    uint64_t* co = out + c * Ln * n_;
+    hip_ok(phx::ntt_inverse(ntt, ci + Ln * n_, last.get(), phx::LimbMap::contiguous(1, (int)Ln), nullptr, nullptr, s),
+           "rescale INTT(last)");
+    hip_ok(phx::rescale_spread_last(last.get(), tmp.get(), d_Ql_.get(), d_Ql_barrett_.get(), n_, Ln, s),
+           "rescale spread");
+    hip_ok(phx::ntt_forward(ntt, tmp.get(), tmp.get(), phx::LimbMap::contiguous((int)Ln, 0), s), "rescale NTT");
+    hip_ok(phx::rescale_finish(ci, tmp.get(), co, d_inv_qlast_.get(), d_inv_qlast_shoup_.get(), d_Ql_.get(), n_, Ln,
+                               s),
+           "rescale finish");
+  }
+}
+
+}  // namespace phantom

@@ -1,0 +1,71 @@
+// rns_tool.h — per-level RNS constants and the key-switch / rescale drivers: the CKKS part
+// of the reference's DRNSTool (include/rns.cuh:16-387, constants at src/rns.cu:11-190,
+// modup src/rns_bconv.cu:530-628, moddown_from_NTT :791-843, divide_and_round_q_last_ntt
+// src/rns.cu:1160-1184).  BFV/BGV-only members (BEHZ/HPS) are out of scope.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <vector>
+
+#include "../csrc/ntt.h"
+#include "../csrc/rns.h"
+#include "buffer.h"
+
+namespace phantom {
+
+// Fast base converter constants (the reference's BaseConverter, include/host/rns.h:135-199)
+struct DeviceBaseConverter {
+  std::vector<uint64_t> ibase, obase;
+  DeviceBuffer<uint64_t> d_ibase, d_obase, d_obase_barrett;
+  DeviceBuffer<uint64_t> d_qhat_inv, d_qhat_inv_shoup;  // [ibase] (qHat_i^-1 mod q_i)
+  DeviceBuffer<uint64_t> d_qhat_mod_p;                  // [ibase][obase]
+  void init(const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, hipStream_t s);
+  phx::BconvArgs args(const uint64_t* in, uint64_t* out, bool prescale) const;
+};
+
+class RnsTool {
+ public:
+  // moduli_QP: the full key-level chain (size_Q data primes then size_P special primes);
+  // size_Ql: number of data primes at this level (size_Q at chain index 1).
+  RnsTool(size_t n, const std::vector<uint64_t>& moduli_QP, size_t size_P, size_t size_Ql, hipStream_t s);
+
+  size_t n() const { return n_; }
+  size_t size_Q() const { return size_Q_; }
+  size_t size_P() const { return size_P_; }
+  size_t size_QP() const { return size_Q_ + size_P_; }
+  size_t size_Ql() const { return base_Ql_.size(); }
+  size_t beta() const { return converters_.size(); }
+  const std::vector<uint64_t>& base_Ql() const { return base_Ql_; }
+
+  // modup (src/rns_bconv.cu:530-628): c2 [size_Ql][n] NTT form -> t_mod_up [beta][size_QlP][n]
+  void modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables& ntt, hipStream_t s) const;
+  // moddown_from_NTT (src/rns_bconv.cu:791-843) fused with add_to_ct_kernel: cx_i is
+  // [size_QlP][n] NTT form (its P limbs are clobbered); ct_i (+)= moddown(cx_i).
+  void moddown_add(uint64_t* ct_i, uint64_t* cx_i, bool accumulate, const phx::NttTables& ntt,
+                   hipStream_t s) const;
+  // divide_and_round_q_last_ntt (src/rns.cu:1160-1184): in [polys][size_Ql][n] -> out
+  // [polys][size_Ql-1][n], NTT form.  `in` is not modified.
+  void rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const phx::NttTables& ntt,
+                   hipStream_t s) const;
+
+  // device views over Ql
+  phx::ModView mod_Ql() const { return {d_Ql_.get(), d_Ql_barrett_.get()}; }
+  const uint64_t* bigP_mod_q() const { return d_bigP_mod_q_.get(); }
+  const uint64_t* bigP_mod_q_shoup() const { return d_bigP_mod_q_shoup_.get(); }
+
+ private:
+  size_t n_, size_Q_, size_P_;
+  std::vector<uint64_t> base_Ql_, base_P_;
+  DeviceBuffer<uint64_t> d_Ql_, d_Ql_barrett_;
+  // key switching
+  DeviceBuffer<uint64_t> d_partQlHatInv_, d_partQlHatInv_shoup_;
+  std::vector<DeviceBaseConverter> converters_;  // digit beta: part -> complement of QlP
+  std::vector<size_t> digit_start_, digit_size_;
+  DeviceBaseConverter p_to_ql_;
+  DeviceBuffer<uint64_t> d_bigP_mod_q_, d_bigP_mod_q_shoup_, d_bigPInv_mod_q_, d_bigPInv_mod_q_shoup_;
+  // rescale
+  DeviceBuffer<uint64_t> d_inv_qlast_, d_inv_qlast_shoup_;
+};
+
+}  // namespace phantom

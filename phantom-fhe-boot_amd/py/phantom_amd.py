@@ -28,6 +28,19 @@ _SIGS = {
     "phantom_nwt_backward_scale": (ctypes.c_int, [vp, vp, vp, sz, sz, vp, vp, vp]),
     "phantom_nwt_forward_include_special_mod_exclude_range": (ctypes.c_int, [vp, vp, sz, sz, sz, sz, sz, sz, vp]),
     "phantom_nwt_backward_inplace_include_special_mod": (ctypes.c_int, [vp, vp, sz, sz, sz, sz, vp]),
+    "phantom_context_create": (ctypes.c_int, [sz, u64p, sz, sz, ctypes.POINTER(vp)]),
+    "phantom_context_destroy": (ctypes.c_int, [vp]),
+    "phantom_context_coeff_modulus_size": (sz, [vp, sz]),
+    "phantom_multiply": (ctypes.c_int, [vp, sz, vp, vp, vp, vp]),
+    "phantom_relinearize": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, vp]),
+    "phantom_keyswitch": (ctypes.c_int, [vp, sz, vp, vp, ctypes.POINTER(vp), sz, vp]),
+    "phantom_modup": (ctypes.c_int, [vp, sz, vp, vp, vp]),
+    "phantom_keyswitch_inner_prod": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, vp, vp]),
+    "phantom_moddown_from_ntt": (ctypes.c_int, [vp, sz, vp, vp, vp]),
+    "phantom_rescale_to_next": (ctypes.c_int, [vp, sz, vp, vp, sz, vp]),
+    "phantom_apply_galois_ntt": (ctypes.c_int, [vp, ctypes.c_uint32, vp, vp, sz, vp]),
+    "phantom_poly_op": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, sz, sz, vp]),
+    "phantom_switch_modulus_raise": (ctypes.c_int, [vp, vp, vp, sz, vp]),
 }
 
 _lib = None
@@ -85,6 +98,39 @@ def coeff_modulus_create(n, bit_sizes):
     out = (ctypes.c_uint64 * len(bit_sizes))()
     check(lib.phantom_coeff_modulus_create(n, bs, len(bit_sizes), out))
     return list(out)
+
+
+class Context:
+    """Owning handle of a phantom_context (CKKS PhantomContext over a key-level chain)."""
+
+    def __init__(self, n, moduli, special_modulus_size):
+        lib = load()
+        self.n = n
+        self.moduli = list(moduli)
+        self.size_P = special_modulus_size
+        self.size_Q = len(self.moduli) - special_modulus_size
+        h = vp()
+        check(lib.phantom_context_create(n, u64_array(self.moduli), len(self.moduli), special_modulus_size,
+                                         ctypes.byref(h)))
+        self.handle = h
+
+    def ql(self, chain_index):
+        return self.moduli[:self.size_Q - (chain_index - 1)]
+
+    def close(self):
+        if self.handle:
+            load().phantom_context_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def ptr_array(ptrs):
+    return (vp * len(ptrs))(*ptrs)
 
 
 class NttTables:

@@ -1,0 +1,191 @@
+"""GPU parity of the CKKS hot path (multiply, modup, key-switch inner product, moddown,
+relinearize, rescale, automorphism, ModRaise lift) against the CPU oracle, bit-exact.
+
+Config 3: N = 2^16, Q = {60, 44 x 50}, P = 15 x 60 (examples/3_ckks.cu:796-803).
+A small chain (N = 2^12, 7 data primes, alpha = 3) exercises partial digits and lower levels.
+Key-switching keys are uniform random digits here (parity is a property of the arithmetic, not
+of key structure); tests/test_oracle.py checks the oracle's key switch decrypts correctly.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import phantom_amd as PA
+from gpu_util import ptr, stream, to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+C3_BITS = [60] + [50] * 44 + [60] * 15
+SMALL_BITS = [60, 50, 50, 50, 50, 50, 50, 60, 60, 60]
+
+
+def _make(n, bits, special):
+    mods = O.coeff_modulus_create(n, bits)
+    return PA.Context(n, mods, special)
+
+
+@pytest.fixture(scope="module")
+def c3():
+    return _make(1 << 16, C3_BITS, 15)
+
+
+@pytest.fixture(scope="module")
+def small():
+    return _make(1 << 12, SMALL_BITS, 3)
+
+
+def _lib():
+    return PA.load()
+
+
+def _rand_ct(rng, ctx, chain, polys):
+    ql = ctx.ql(chain)
+    return np.concatenate([O.random_limbs(rng, ctx.n, ql) for _ in range(polys)])
+
+
+def _keys(rng, ctx):
+    dnum = -(-ctx.size_Q // ctx.size_P)
+    keys = [np.concatenate([O.random_limbs(rng, ctx.n, ctx.moduli) for _ in range(2)]) for _ in range(dnum)]
+    return keys, [to_dev(k) for k in keys]
+
+
+def _oracle_keys(keys):
+    return (O.u64p * len(keys))(*[O.P(k) for k in keys])
+
+
+@pytest.mark.parametrize("fixture,chain", [("c3", 1), ("small", 1), ("small", 4)])
+def test_multiply(request, rng, fixture, chain):
+    ctx = request.getfixturevalue(fixture)
+    ql = ctx.ql(chain)
+    a, b = _rand_ct(rng, ctx, chain, 2), _rand_ct(rng, ctx, chain, 2)
+    da, db = to_dev(a), to_dev(b)
+    dout = to_dev(np.zeros(3 * len(ql) * ctx.n, dtype=np.uint64))
+    PA.check(_lib().phantom_multiply(ctx.handle, chain, ptr(da), ptr(db), ptr(dout), stream()))
+    want = np.zeros(3 * len(ql) * ctx.n, dtype=np.uint64)
+    O.lib().or_tensor_prod_2x2(O.P(a), O.P(b), O.P(want), ctx.n, len(ql), O.P(O.arr(ql)))
+    assert np.array_equal(to_host(dout), want)
+
+
+@pytest.mark.parametrize("fixture,chain", [("c3", 1), ("small", 1), ("small", 2), ("small", 6)])
+def test_modup(request, rng, fixture, chain):
+    ctx = request.getfixturevalue(fixture)
+    ql, p = ctx.ql(chain), ctx.moduli[ctx.size_Q:]
+    beta = -(-len(ql) // ctx.size_P)
+    c2 = O.random_limbs(rng, ctx.n, ql)
+    d = to_dev(c2)
+    dout = to_dev(np.zeros(beta * (len(ql) + len(p)) * ctx.n, dtype=np.uint64))
+    PA.check(_lib().phantom_modup(ctx.handle, chain, ptr(d), ptr(dout), stream()))
+    want = np.zeros(beta * (len(ql) + len(p)) * ctx.n, dtype=np.uint64)
+    O.lib().or_modup(O.P(c2), O.P(want), ctx.n, O.P(O.arr(ql)), len(ql), O.P(O.arr(p)), len(p))
+    assert np.array_equal(to_host(dout), want)
+
+
+@pytest.mark.parametrize("fixture,chain", [("c3", 1), ("small", 3)])
+def test_inner_product(request, rng, fixture, chain):
+    ctx = request.getfixturevalue(fixture)
+    ql, p = ctx.ql(chain), ctx.moduli[ctx.size_Q:]
+    qlp = ql + p
+    beta = -(-len(ql) // ctx.size_P)
+    tmu = np.concatenate([O.random_limbs(rng, ctx.n, qlp) for _ in range(beta)])
+    keys, dkeys = _keys(rng, ctx)
+    dt = to_dev(tmu)
+    dcx = to_dev(np.zeros(2 * len(qlp) * ctx.n, dtype=np.uint64))
+    kp = PA.ptr_array([ptr(k) for k in dkeys])
+    PA.check(_lib().phantom_keyswitch_inner_prod(ctx.handle, chain, ptr(dt), kp, len(dkeys), ptr(dcx), stream()))
+    want = np.zeros(2 * len(qlp) * ctx.n, dtype=np.uint64)
+    O.lib().or_keyswitch_inner_prod(O.P(tmu), _oracle_keys(keys), O.P(want), ctx.n, len(ql), ctx.size_Q, ctx.size_P,
+                                    beta, O.P(O.arr(ctx.moduli)))
+    assert np.array_equal(to_host(dcx), want)
+
+
+@pytest.mark.parametrize("fixture,chain", [("c3", 1), ("c3", 30), ("small", 1), ("small", 5)])
+def test_moddown(request, rng, fixture, chain):
+    ctx = request.getfixturevalue(fixture)
+    ql, p = ctx.ql(chain), ctx.moduli[ctx.size_Q:]
+    cx = O.random_limbs(rng, ctx.n, ql + p)
+    d = to_dev(cx)
+    dout = to_dev(np.zeros(len(ql) * ctx.n, dtype=np.uint64))
+    PA.check(_lib().phantom_moddown_from_ntt(ctx.handle, chain, ptr(d), ptr(dout), stream()))
+    want = np.zeros(len(ql) * ctx.n, dtype=np.uint64)
+    cxo = cx.copy()
+    O.lib().or_moddown_from_ntt(O.P(cxo), O.P(want), ctx.n, O.P(O.arr(ql)), len(ql), O.P(O.arr(p)), len(p))
+    assert np.array_equal(to_host(dout), want)
+
+
+@pytest.mark.parametrize("fixture,chain", [("c3", 1), ("small", 1), ("small", 4), ("small", 7)])
+def test_relinearize(request, rng, fixture, chain):
+    ctx = request.getfixturevalue(fixture)
+    ql = ctx.ql(chain)
+    ct = _rand_ct(rng, ctx, chain, 3)
+    keys, dkeys = _keys(rng, ctx)
+    d = to_dev(ct)
+    kp = PA.ptr_array([ptr(k) for k in dkeys])
+    PA.check(_lib().phantom_relinearize(ctx.handle, chain, ptr(d), kp, len(dkeys), stream()))
+    want = ct.copy()
+    O.lib().or_relinearize(O.P(want), ctx.n, len(ql), ctx.size_Q, ctx.size_P, _oracle_keys(keys),
+                           O.P(O.arr(ctx.moduli)))
+    got = to_host(d)
+    L = len(ql)
+    assert np.array_equal(got[:2 * L * ctx.n], want[:2 * L * ctx.n])
+
+
+@pytest.mark.parametrize("fixture,chain", [("c3", 1), ("c3", 44), ("small", 1), ("small", 6)])
+def test_rescale(request, rng, fixture, chain):
+    ctx = request.getfixturevalue(fixture)
+    ql = ctx.ql(chain)
+    L = len(ql)
+    ct = _rand_ct(rng, ctx, chain, 2)
+    d = to_dev(ct)
+    dout = to_dev(np.zeros(2 * (L - 1) * ctx.n, dtype=np.uint64))
+    PA.check(_lib().phantom_rescale_to_next(ctx.handle, chain, ptr(d), ptr(dout), 2, stream()))
+    want = np.zeros(2 * (L - 1) * ctx.n, dtype=np.uint64)
+    O.lib().or_rescale_ntt(O.P(ct), O.P(want), ctx.n, L, 2, O.P(O.arr(ql)))
+    assert np.array_equal(to_host(dout), want)
+    assert np.array_equal(to_host(d), ct)  # input untouched
+
+
+def test_rescale_at_last_level_is_rejected(small):
+    d = to_dev(np.zeros(2 * small.n, dtype=np.uint64))
+    rc = _lib().phantom_rescale_to_next(small.handle, 7, ptr(d), ptr(d), 2, stream())
+    assert rc == 1 and b"end of modulus switching chain" in _lib().phantom_last_error()
+
+
+@pytest.mark.parametrize("elt", [5, 25, 3125, 2 * (1 << 12) - 1])
+def test_galois(small, rng, elt):
+    L = 4
+    a = O.random_limbs(rng, small.n, small.moduli[:L])
+    d, dout = to_dev(a), to_dev(np.zeros_like(a))
+    PA.check(_lib().phantom_apply_galois_ntt(small.handle, elt, ptr(d), ptr(dout), L, stream()))
+    want = np.zeros_like(a)
+    O.lib().or_apply_galois_ntt(O.P(a), O.P(want), small.n, L, elt)
+    assert np.array_equal(to_host(dout), want)
+
+
+def test_switch_modulus_raise(small, rng):
+    L = small.size_Q
+    q0 = small.moduli[0]
+    v = O.random_limbs(rng, small.n, [q0])
+    d, dout = to_dev(v), to_dev(np.zeros(L * small.n, dtype=np.uint64))
+    PA.check(_lib().phantom_switch_modulus_raise(small.handle, ptr(d), ptr(dout), L, stream()))
+    want = np.zeros(L * small.n, dtype=np.uint64)
+    O.lib().or_switch_modulus_raise(O.P(v), O.P(want), small.n, q0, O.P(O.arr(small.moduli)), L)
+    assert np.array_equal(to_host(dout), want)
+
+
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+def test_poly_ops(small, rng, op):
+    off, L = 2, 5
+    mods = small.moduli[off:off + L]
+    a, b = O.random_limbs(rng, small.n, mods), O.random_limbs(rng, small.n, mods)
+    da, db, do = to_dev(a), to_dev(b), to_dev(np.zeros_like(a))
+    PA.check(_lib().phantom_poly_op(small.handle, op, ptr(da), ptr(db), ptr(do), off, L, stream()))
+    want = np.zeros_like(a)
+    m = O.arr(mods)
+    fn = [O.lib().or_poly_add, O.lib().or_poly_sub, O.lib().or_poly_mul][op] if op < 3 else None
+    if fn:
+        fn(O.P(a), O.P(b), O.P(want), small.n, L, O.P(m))
+    else:
+        O.lib().or_poly_negate(O.P(a), O.P(want), small.n, L, O.P(m))
+    assert np.array_equal(to_host(do), want)

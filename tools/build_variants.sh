@@ -1,0 +1,16 @@
+# Build libphantom_amd variants with NTT tuning knobs into tools/variants/<name>/lib (experiments only)
+set -e
+ROOT=$(cd $(dirname $0)/.. && pwd)
+build() {
+  name=$1; shift
+  d=$ROOT/tools/variants/$name
+  rm -rf $d && mkdir -p $d && cp -r $ROOT/phantom-fhe-boot_amd/csrc $ROOT/phantom-fhe-boot_amd/host $ROOT/phantom-fhe-boot_amd/Makefile $d/
+  mkdir -p $d/py && cp $ROOT/phantom-fhe-boot_amd/py/phantom_amd.py $d/py/
+  make -C $d -j8 INCDIR=$ROOT/include HIPFLAGS="-std=c++20 -O3 -fPIC -Wall -ffp-contract=off -I$ROOT/include --offload-arch=gfx950 $*" > $d/build.log 2>&1
+  echo built $name
+}
+build base
+build nocomp -DPHX_NTT_NO_COMPUTE
+build g1 -DPHX_NTT_GRID_MULT=1
+build g4 -DPHX_NTT_GRID_MULT=4
+build g1nocomp -DPHX_NTT_GRID_MULT=1 -DPHX_NTT_NO_COMPUTE

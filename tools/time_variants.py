@@ -1,0 +1,44 @@
+"""Time the forward/inverse NTT of each library variant under tools/variants/ (one process each)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CODE = r'''
+import sys, os, time, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+import phantom_amd as PA
+N, L = 1 << 16, 44
+lib = PA.load()
+mods = PA.coeff_modulus_create(N, [60] + [50] * 44 + [60] * 15)[:L]
+t = PA.NttTables(N, mods)
+rng = np.random.default_rng(1)
+base = np.concatenate([rng.integers(0, q, size=N, dtype=np.uint64) for q in mods])
+ring = [torch.from_numpy(base.view(np.int64)).cuda() for _ in range(15)]
+s = torch.cuda.current_stream()
+def run(fn, iters=60):
+    evs = []
+    for i in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s); PA.check(fn(ring[i % 15].data_ptr(), t.handle, L, 0, s.cuda_stream)); b.record(s)
+        evs.append((a, b))
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) * 1e3 for a, b in evs[10:])
+    return ts[len(ts) // 2]
+fwd = run(lib.phantom_nwt_forward_inplace)
+inv = run(lib.phantom_nwt_backward_inplace)
+print("RESULT", fwd, inv)
+'''
+res = {}
+for name in sorted(os.listdir(os.path.join(ROOT, "tools", "variants"))):
+    py = os.path.join(ROOT, "tools", "variants", name, "py")
+    out = subprocess.run([sys.executable, "-c", CODE, py], capture_output=True, text=True, timeout=300)
+    line = [l for l in out.stdout.splitlines() if l.startswith("RESULT")]
+    if line:
+        f, i = map(float, line[0].split()[1:])
+        res[name] = {"fwd_us": round(f, 2), "inv_us": round(i, 2)}
+    else:
+        res[name] = {"error": out.stderr[-500:]}
+    print(name, res[name], flush=True)
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", "variants.json"), "w"), indent=1)
