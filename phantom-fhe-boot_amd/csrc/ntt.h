@@ -30,7 +30,13 @@ struct NttTables {
   double* modulus_inv = nullptr; // [num_moduli] fl(1/q)
   uint8_t* is_f64 = nullptr;     // [num_moduli] 1 if q < 2^50
   double* twf = nullptr;         // [num_moduli][n] forward twiddles as centered doubles (|w| <= q/2)
+  // row-pass twiddles factored as tw = A_g(row) * B_g(iloc) (see ntt.hip), centered doubles
+  double* row_a = nullptr;       // [num_moduli][S1][16]: A_g(row) for stage g of the row pass
+  double* row_b = nullptr;       // [num_moduli][S2]: B_g(iloc) at index 2^g + iloc
 };
+
+// log2 of the column-pass size S1 for a given log2(n) (the row pass handles the rest)
+inline int ntt_split_log_s1(int log_n) { return log_n / 2; }
 
 // Which table row each buffer limb uses.  Buffer limb i (0 <= i < num_limbs) maps to
 // table row (i < split ? first_a + i : first_b + (i - split)); limbs in

@@ -39,7 +39,13 @@ constexpr int E = 1 << E_LOG;
 constexpr int COLS = 16;  // columns per column-pass tile (16 x 8 B = one 128 B line per row)
 constexpr int BLOCK = 256;
 #ifndef PHX_NTT_GRID_MULT
-#define PHX_NTT_GRID_MULT 2  // persistent workgroups per CU
+#define PHX_NTT_GRID_MULT 0  // persistent workgroups per CU (0: one workgroup per tile)
+#endif
+#ifndef PHX_NTT_WAVES_PER_EU
+#define PHX_NTT_WAVES_PER_EU 4  // __launch_bounds__ occupancy target (waves per SIMD)
+#endif
+#ifndef PHX_NTT_PREFETCH
+#define PHX_NTT_PREFETCH 0   // prefetch the next tile into registers
 #endif
 
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
@@ -102,6 +108,27 @@ __device__ __forceinline__ void load_tw(W (&w)[E], const W* __restrict__ tab, ui
       const int j = ((key >> Rd::ex) << (E_LOG - gl)) | (key & ((1 << Rd::ex) - 1));
       const uint32_t p = pt | Rd::p_elem(j);
       w[tw_slot<Rd::ex>(gl, key)] = tab[(B << g) + (p >> (S_LOG - g))];
+    }
+  }
+}
+
+// Row-pass FP64 twiddles computed on the fly: tw = A_g(row) * B_g(iloc) mod q (ntt.h), so the
+// row pass reads 8 per-row factors and a 2 KB per-limb table instead of an n-entry table.
+template <int S_LOG, int R>
+__device__ __forceinline__ void make_tw_row_f64(double (&w)[E], const double* __restrict__ A,
+                                                const double* __restrict__ Btab, uint32_t pt, double qd,
+                                                double qinv) {
+  using Rd = Round<S_LOG, R>;
+#pragma unroll
+  for (int gl = 0; gl < Rd::er; ++gl) {
+    const int g = Rd::g0 + gl;
+    const double ag = A[g];
+#pragma unroll
+    for (int key = 0; key < (1 << (gl + Rd::ex)); ++key) {
+      const int j = ((key >> Rd::ex) << (E_LOG - gl)) | (key & ((1 << Rd::ex) - 1));
+      const uint32_t p = pt | Rd::p_elem(j);
+      const double b = Btab[(1u << g) + (p >> (S_LOG - g))];
+      w[tw_slot<Rd::ex>(gl, key)] = freduce(fmodmul(b, ag, qd, qinv), qd, qinv);
     }
   }
 }
@@ -176,6 +203,8 @@ struct KArgs {
   const uint64_t* tw;         // forward or inverse integer table base
   const uint64_t* tws;
   const double* twf;          // forward FP64 table
+  const double* row_a;        // row-pass factored twiddles (ntt.h)
+  const double* row_b;
   const uint64_t* n_inv;
   const uint64_t* n_inv_shoup;
   const uint64_t* scale;      // optional, per buffer limb
@@ -194,6 +223,9 @@ __device__ __forceinline__ void resolve_limb(const LimbMap& m, int y, int& buf_l
 }
 
 __device__ __forceinline__ LimbCtx limb_ctx(const KArgs& a, int row, bool& f64) {
+  // row is wave-uniform: readfirstlane lets the per-limb constants come through scalar loads
+  // (a vector load here would carry an s_waitcnt vmcnt(0) that drains the tile prefetch)
+  row = __builtin_amdgcn_readfirstlane(row);
   LimbCtx c;
   c.q = a.modulus[row];
   c.qd = a.modulus_f[row];
@@ -201,7 +233,7 @@ __device__ __forceinline__ LimbCtx limb_ctx(const KArgs& a, int row, bool& f64) 
   c.tw = a.tw + (size_t)row * a.n;
   c.tws = a.tws + (size_t)row * a.n;
   c.twf = a.twf + (size_t)row * a.n;
-  f64 = a.f64_fwd && a.is_f64[row];
+  f64 = a.f64_fwd && c.q < (1ull << 50);
   return c;
 }
 
@@ -247,21 +279,32 @@ __device__ __forceinline__ void load_all(TwInt<S_LOG>& tw, const uint64_t* tab, 
 // One full sub-transform (all rounds) on registers v, which hold the load layout
 // p = t + j*T on entry and on exit.  L is this thread-group's LDS tile of element type V
 // indexed by idx(p); sync() orders the LDS exchanges (workgroup or wavefront barrier).
-template <int S_LOG, int GOFF, bool FWD, typename V, typename TW, typename Idx, typename Sync>
-__device__ __forceinline__ void sub_transform(V (&v)[E], const TW& tw, V* L, Idx idx, Sync sync, uint32_t t,
+// Twiddles of one round in registers (FP64: w; integer: w and Shoup quotients ws)
+struct RoundTwF64 {
+  double w[E];
+};
+struct RoundTwInt {
+  uint64_t w[E], ws[E];
+};
+
+// get_tw(integral_constant<R>) produces round R's twiddles; it runs right before the round so
+// only one round's twiddles are live (keeps VGPR use low enough for 4 waves per SIMD).
+template <int S_LOG, int GOFF, bool FWD, typename V, typename GetTw, typename Idx, typename Sync>
+__device__ __forceinline__ void sub_transform(V (&v)[E], GetTw get_tw, V* L, Idx idx, Sync sync, uint32_t t,
                                               uint64_t q, double qd, double qinv) {
   using SB = Sub<S_LOG>;
   constexpr int RN = SB::ROUNDS;
   constexpr bool F = !std::is_same_v<V, uint64_t>;
   auto round = [&](auto r) {
     constexpr int R = decltype(r)::value;
+    const auto tw = get_tw(r);
     if constexpr (F) {
       static_assert(FWD, "FP64 path is forward-only");
-      ct_round_f64<S_LOG, R, GOFF>(v, tw.w[R], qd, qinv);
+      ct_round_f64<S_LOG, R, GOFF>(v, tw.w, qd, qinv);
     } else if constexpr (FWD) {
-      ct_round_int<S_LOG, R>(v, tw.w[R], tw.ws[R], q);
+      ct_round_int<S_LOG, R>(v, tw.w, tw.ws, q);
     } else {
-      gs_round_int<S_LOG, R>(v, tw.w[R], tw.ws[R], q);
+      gs_round_int<S_LOG, R>(v, tw.w, tw.ws, q);
     }
   };
   auto put = [&](uint32_t pt, auto r) {
@@ -317,7 +360,7 @@ __device__ __forceinline__ void fence_loads() { __builtin_amdgcn_sched_barrier(0
 // INV: last log2(S1) GS stages, then n^-1 and the optional per-limb scale.
 // ---------------------------------------------------------------------------------------
 template <int S1_LOG, int S2_LOG, bool FWD>
-__global__ __launch_bounds__(BLOCK) void ntt_col(KArgs a) {
+__global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) {
   using SB = Sub<S1_LOG>;
   constexpr int T = SB::T, S2 = 1 << S2_LOG, NT = COLS * T, CT = S2 / COLS;
   static_assert(NT <= BLOCK, "column tile too large");
@@ -327,6 +370,7 @@ __global__ __launch_bounds__(BLOCK) void ntt_col(KArgs a) {
   const bool active = tid < NT;
   const uint32_t c = tid % COLS, t = tid / COLS;
   const int ntiles = a.limbs * CT;
+  const int ntiles_or_items = ntiles;
   auto idx = [c](uint32_t p) { return cidx(p, c); };
   auto sync = [] { __syncthreads(); };
 
@@ -350,11 +394,13 @@ __global__ __launch_bounds__(BLOCK) void ntt_col(KArgs a) {
     const LimbCtx lc = limb_ctx(a, row, f64);
     uint64_t* dst = a.out + (size_t)buf_limb * a.n + (tile % CT) * COLS + c;
     if (FWD && f64) {
-      TwF64<S1_LOG> tw;
-      if (active) load_all(tw, lc.twf, t, 1);
-      fence_loads();
-      if (next < ntiles) load(next, nxt);
-      fence_loads();
+      auto tw = [&](auto r) {
+        constexpr int R = decltype(r)::value;
+        RoundTwF64 x;
+        load_tw<S1_LOG, R>(x.w, lc.twf, Round<S1_LOG, R>::p_thread(t), 1);
+        return x;
+      };
+      if (PHX_NTT_PREFETCH && next < ntiles) load(next, nxt);
       double v[E];
 #pragma unroll
       for (int j = 0; j < E; ++j) v[j] = u64_to_f64(cur[j]);
@@ -365,11 +411,14 @@ __global__ __launch_bounds__(BLOCK) void ntt_col(KArgs a) {
         for (int j = 0; j < E; ++j) dst[(size_t)(t + j * T) * S2] = as_bits(v[j]);
       }
     } else {
-      TwInt<S1_LOG> tw;
-      if (active) load_all(tw, lc.tw, lc.tws, t, 1);
-      fence_loads();
-      if (next < ntiles) load(next, nxt);
-      fence_loads();
+      auto tw = [&](auto r) {
+        constexpr int R = decltype(r)::value;
+        RoundTwInt x;
+        load_tw<S1_LOG, R>(x.w, lc.tw, Round<S1_LOG, R>::p_thread(t), 1);
+        load_tw<S1_LOG, R>(x.ws, lc.tws, Round<S1_LOG, R>::p_thread(t), 1);
+        return x;
+      };
+      if (PHX_NTT_PREFETCH && next < ntiles) load(next, nxt);
       sub_transform<S1_LOG, 0, FWD>(cur, tw, lds, idx, sync, t, lc.q, lc.qd, lc.qinv);
       if (active) {
         if constexpr (FWD) {
@@ -388,8 +437,12 @@ __global__ __launch_bounds__(BLOCK) void ntt_col(KArgs a) {
         }
       }
     }
+    if constexpr (PHX_NTT_PREFETCH) {
 #pragma unroll
-    for (int j = 0; j < E; ++j) cur[j] = nxt[j];
+      for (int j = 0; j < E; ++j) cur[j] = nxt[j];
+    } else if (next < ntiles_or_items) {
+      load(next, cur);
+    }
   }
 }
 
@@ -399,7 +452,7 @@ __global__ __launch_bounds__(BLOCK) void ntt_col(KArgs a) {
 // FWD: last log2(S2) CT stages, canonical output.  INV: first log2(S2) GS stages.
 // ---------------------------------------------------------------------------------------
 template <int S1_LOG, int S2_LOG, bool FWD>
-__global__ __launch_bounds__(BLOCK) void ntt_row(KArgs a) {
+__global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) {
   using SB = Sub<S2_LOG>;
   constexpr int S2 = SB::S, T = SB::T, RW = cmin(64 / T, 1 << S1_LOG), RSTR = S2 + S2 / 16;
   constexpr int WAVES = BLOCK / 64;
@@ -410,6 +463,7 @@ __global__ __launch_bounds__(BLOCK) void ntt_row(KArgs a) {
   const uint32_t lr = lane / T, t = lane % T;
   uint64_t* lrow = lds + (wave * RW + lr) * RSTR;
   const int nitems = a.limbs * GROUPS;
+  const int ntiles_or_items = nitems;
   const int stride = gridDim.x * WAVES;
   auto idx = [](uint32_t p) { return rpad(p); };
   auto sync = [] { __builtin_amdgcn_wave_barrier(); };
@@ -423,23 +477,28 @@ __global__ __launch_bounds__(BLOCK) void ntt_row(KArgs a) {
 #pragma unroll
     for (int j = 0; j < E; ++j) dst[j] = src[j * T];
   };
-  int item = blockIdx.x * WAVES + wave;
+  int item = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + wave);
   if (item < nitems) load(item, cur);
   for (; item < nitems; item += stride) {
     const int next = item + stride;
     int buf_limb, row;
     resolve_limb(a.map, item / GROUPS, buf_limb, row);
+    buf_limb = __builtin_amdgcn_readfirstlane(buf_limb);
     bool f64;
     const LimbCtx lc = limb_ctx(a, row, f64);
     const uint32_t r = (item % GROUPS) * RW + lr;
     const uint32_t B = (1u << S1_LOG) + r;
     uint64_t* dst = a.out + (size_t)buf_limb * a.n + (size_t)r * S2 + t;
     if (FWD && f64) {
-      TwF64<S2_LOG> tw;
-      load_all(tw, lc.twf, t, B);
-      fence_loads();
-      if (next < nitems) load(next, nxt);
-      fence_loads();
+      const double* A = a.row_a + ((size_t)row * (1u << S1_LOG) + r) * 16;
+      const double* Bt = a.row_b + (size_t)row * S2;
+      auto tw = [&](auto rr) {
+        constexpr int RR = decltype(rr)::value;
+        RoundTwF64 x;
+        make_tw_row_f64<S2_LOG, RR>(x.w, A, Bt, Round<S2_LOG, RR>::p_thread(t), lc.qd, lc.qinv);
+        return x;
+      };
+      if (PHX_NTT_PREFETCH && next < nitems) load(next, nxt);
       double v[E];
 #pragma unroll
       for (int j = 0; j < E; ++j) v[j] = as_f64(cur[j]);
@@ -449,11 +508,14 @@ __global__ __launch_bounds__(BLOCK) void ntt_row(KArgs a) {
 #pragma unroll
       for (int j = 0; j < E; ++j) __builtin_nontemporal_store(f64_to_canonical(v[j], lc.qd, lc.qinv), dst + j * T);
     } else {
-      TwInt<S2_LOG> tw;
-      load_all(tw, lc.tw, lc.tws, t, B);
-      fence_loads();
-      if (next < nitems) load(next, nxt);
-      fence_loads();
+      auto tw = [&](auto rr) {
+        constexpr int RR = decltype(rr)::value;
+        RoundTwInt x;
+        load_tw<S2_LOG, RR>(x.w, lc.tw, Round<S2_LOG, RR>::p_thread(t), B);
+        load_tw<S2_LOG, RR>(x.ws, lc.tws, Round<S2_LOG, RR>::p_thread(t), B);
+        return x;
+      };
+      if (PHX_NTT_PREFETCH && next < nitems) load(next, nxt);
       sub_transform<S2_LOG, S1_LOG, FWD>(cur, tw, lrow, idx, sync, t, lc.q, lc.qd, lc.qinv);
       if constexpr (FWD) {
         const uint64_t q2 = lc.q << 1;
@@ -464,8 +526,12 @@ __global__ __launch_bounds__(BLOCK) void ntt_row(KArgs a) {
         for (int j = 0; j < E; ++j) dst[j * T] = cur[j];  // [0, 2q), column pass follows
       }
     }
+    if constexpr (PHX_NTT_PREFETCH) {
 #pragma unroll
-    for (int j = 0; j < E; ++j) cur[j] = nxt[j];
+      for (int j = 0; j < E; ++j) cur[j] = nxt[j];
+    } else if (next < ntiles_or_items) {
+      load(next, cur);
+    }
   }
 }
 
@@ -492,6 +558,8 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   a.tw = inverse ? tb.itw : tb.tw;
   a.tws = inverse ? tb.itw_shoup : tb.tw_shoup;
   a.twf = tb.twf;
+  a.row_a = tb.row_a;
+  a.row_b = tb.row_b;
   a.n_inv = tb.n_inv; a.n_inv_shoup = tb.n_inv_shoup;
   a.scale = scale; a.scale_shoup = scale_shoup;
   a.map = map; a.n = (int)tb.n; a.limbs = limbs;
@@ -501,8 +569,8 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   const int col_tiles = limbs * (S2 / COLS);
   const int row_items = limbs * (S1 / RW);
   const int cus = num_cus();
-  const dim3 grid_c(std::min(col_tiles, cus * PHX_NTT_GRID_MULT)),
-      grid_r(std::min((row_items + 3) / 4, cus * PHX_NTT_GRID_MULT));
+  const int gm = PHX_NTT_GRID_MULT > 0 ? PHX_NTT_GRID_MULT : 1 << 20;
+  const dim3 grid_c(std::min(col_tiles, cus * gm)), grid_r(std::min((row_items + 3) / 4, cus * gm));
   const dim3 block(BLOCK);
   if (!inverse) {
     hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true>), grid_c, block, 0, stream, a);

@@ -87,6 +87,31 @@ DeviceNttTables::DeviceNttTables(size_t n, const std::vector<uint64_t>& moduli, 
         twf[i * n + k] = w > (q - 1) / 2 ? -static_cast<double>(q - w) : static_cast<double>(w);
       }
     }
+    // row-pass factored twiddles: for row R and row-pass stage g (global stage k = s1 + g),
+    // tw[2^k + R 2^g + iloc] = psi^(2^(logn-1-k) (1 + 2 brv_s1(R))) * psi^(2^(logn-g) brv_g(iloc))
+    const int logn = t_.log_n, s1 = phx::ntt_split_log_s1(logn), s2 = logn - s1;
+    const size_t S1 = size_t(1) << s1, S2 = size_t(1) << s2;
+    std::vector<double> ra(L * S1 * 16, 0.0), rb(L * S2, 0.0);
+    auto centered = [](uint64_t w, uint64_t q) {
+      return w > (q - 1) / 2 ? -static_cast<double>(q - w) : static_cast<double>(w);
+    };
+    for (size_t i = 0; i < L; ++i) {
+      const uint64_t q = moduli[i], psi = host[i].psi;
+      for (size_t R = 0; R < S1; ++R)
+        for (int g = 0; g < s2; ++g) {
+          const uint64_t e = (uint64_t(1) << (logn - 1 - s1 - g)) * (1 + 2 * (uint64_t)reverse_bits((uint32_t)R, s1));
+          ra[(i * S1 + R) * 16 + g] = centered(pow_mod(psi, e, q), q);
+        }
+      for (int g = 0; g < s2; ++g)
+        for (size_t il = 0; il < (size_t(1) << g); ++il) {
+          const uint64_t e = (uint64_t(1) << (logn - g)) * (uint64_t)reverse_bits((uint32_t)il, g);
+          rb[i * S2 + (size_t(1) << g) + il] = centered(pow_mod(psi, e, q), q);
+        }
+    }
+    PHX_CHECK(hipMalloc(&t_.row_a, ra.size() * sizeof(double)));
+    PHX_CHECK(hipMalloc(&t_.row_b, rb.size() * sizeof(double)));
+    PHX_CHECK(hipMemcpyAsync(t_.row_a, ra.data(), ra.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    PHX_CHECK(hipMemcpyAsync(t_.row_b, rb.data(), rb.size() * sizeof(double), hipMemcpyHostToDevice, stream));
     PHX_CHECK(hipMalloc(&t_.modulus_f, L * sizeof(double)));
     PHX_CHECK(hipMalloc(&t_.modulus_inv, L * sizeof(double)));
     PHX_CHECK(hipMalloc(&t_.is_f64, L));
@@ -106,7 +131,8 @@ DeviceNttTables::DeviceNttTables(size_t n, const std::vector<uint64_t>& moduli, 
 DeviceNttTables::~DeviceNttTables() {
   for (uint64_t* p : {t_.modulus, t_.barrett, t_.tw, t_.tw_shoup, t_.itw, t_.itw_shoup, t_.n_inv, t_.n_inv_shoup})
     if (p) (void)hipFree(p);
-  for (void* p : {(void*)t_.modulus_f, (void*)t_.modulus_inv, (void*)t_.is_f64, (void*)t_.twf})
+  for (void* p : {(void*)t_.modulus_f, (void*)t_.modulus_inv, (void*)t_.is_f64, (void*)t_.twf, (void*)t_.row_a,
+                  (void*)t_.row_b})
     if (p) (void)hipFree(p);
 }
 

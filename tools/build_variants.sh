@@ -10,7 +10,8 @@ build() {
   echo built $name
 }
 build base
-build nocomp -DPHX_NTT_NO_COMPUTE
-build g1 -DPHX_NTT_GRID_MULT=1
-build g4 -DPHX_NTT_GRID_MULT=4
-build g1nocomp -DPHX_NTT_GRID_MULT=1 -DPHX_NTT_NO_COMPUTE
+build w2 -DPHX_NTT_WAVES_PER_EU=2
+build w3 -DPHX_NTT_WAVES_PER_EU=3
+build w4_g4 -DPHX_NTT_GRID_MULT=4
+build w4_pf_g4 -DPHX_NTT_PREFETCH=1 -DPHX_NTT_GRID_MULT=4
+build w2_pf_g2 -DPHX_NTT_WAVES_PER_EU=2 -DPHX_NTT_PREFETCH=1 -DPHX_NTT_GRID_MULT=2
