@@ -25,14 +25,16 @@ struct NttTables {
   uint64_t* itw_shoup = nullptr;
   uint64_t* n_inv = nullptr;     // [num_moduli]
   uint64_t* n_inv_shoup = nullptr;
-  // FP64 path (farith.h), usable for q < 2^50
+  // FP64 path (farith.h), used for q < 2^50.  All twiddles are centered doubles (|w| <= q/2).
   double* modulus_f = nullptr;   // [num_moduli] q
   double* modulus_inv = nullptr; // [num_moduli] fl(1/q)
-  uint8_t* is_f64 = nullptr;     // [num_moduli] 1 if q < 2^50
-  double* twf = nullptr;         // [num_moduli][n] forward twiddles as centered doubles (|w| <= q/2)
-  // row-pass twiddles factored as tw = A_g(row) * B_g(iloc) (see ntt.hip), centered doubles
-  double* row_a = nullptr;       // [num_moduli][S1][16]: A_g(row) for stage g of the row pass
-  double* row_b = nullptr;       // [num_moduli][S2]: B_g(iloc) at index 2^g + iloc
+  double* col_fwd = nullptr;     // [num_moduli][S1] tw[0..S1): the column-pass (first log2 S1) stages
+  double* col_inv = nullptr;     // [num_moduli][S1] itw[0..S1) with [1] = itw[1] n^-1 and [0] = n^-1
+  // row-pass twiddles factored as tw[(S1 + row) 2^g + iloc] = A_g(row) * B_g(iloc) (see ntt.hip)
+  double* row_a_fwd = nullptr;   // [num_moduli][S1][16]: A_g(row) for row-pass stage g
+  double* row_b_fwd = nullptr;   // [num_moduli][S2]: B_g(iloc) at index 2^g + iloc
+  double* row_a_inv = nullptr;   // the same factors of itw (inverses of the forward ones)
+  double* row_b_inv = nullptr;
 };
 
 // log2 of the column-pass size S1 for a given log2(n) (the row pass handles the rest)

@@ -1,27 +1,29 @@
 // ntt.hip — two-pass negacyclic NTT / INTT for gfx950.
 //
-// Decomposition (the same factorisation the reference's 2-D radix-8 NTT uses,
-// src/ntt/fntt_2d.cu:9-198, re-designed for wave64 and this engine's arithmetic):
-//   n = S1 * S2.  The first log2(S1) Cooley-Tukey stages only pair elements of the same
-//   column (index mod S2); the last log2(S2) stages only pair elements of the same row
-//   (contiguous S2-element block).  The column pass runs the first stages on tiles of COLS
-//   consecutive columns, the row pass runs the last stages on tiles of whole rows.  Each
-//   tile goes HBM -> registers -> (radix-16 rounds, LDS transposes between rounds) -> HBM.
+// Decomposition (the factorisation the reference's 2-D radix-8 NTT uses, src/ntt/fntt_2d.cu:9-198
+// and src/ntt/intt_2d.cu:9-207, re-designed for wave64 and this engine's arithmetic):
+//   n = S1 * S2, coefficient k = row * S2 + col.  The first log2(S1) Cooley-Tukey stages only
+//   pair elements of one column, the last log2(S2) only elements of one row.  The column pass
+//   runs those stages on tiles of COLS consecutive columns (16 x 8 B = one 128 B line per row),
+//   the row pass on whole rows; each tile goes HBM -> registers -> (radix-16 rounds, LDS
+//   transposes between rounds) -> HBM.  The inverse runs the Gentleman-Sande stages in the
+//   reverse order: row pass, then column pass.
 //
 // Stage g of a sub-transform of size S = 2^s pairs local indices p and p + S/2^(g+1) inside
-// block iloc = p >> (s - g); the twiddle is tw[B * 2^g + iloc] with B = 1 for the column
-// pass and B = S1 + row for the row pass: exactly the table index m + i of the reference's
-// in-place CT loop (m = 2^g or S1 * 2^g).
+// block iloc = p >> (s - g); its twiddle is tw[B 2^g + iloc] with B = 1 in the column pass and
+// B = S1 + row in the row pass: the table index m + i of the reference's in-place loops.
 //
 // Arithmetic per limb (wave-uniform branch): primes q < 2^50 use exact FP64 arithmetic
-// (farith.h; ~half the instructions of a 64-bit integer Shoup butterfly on gfx950), other
-// primes use integer Shoup butterflies (arith.h).  In the FP64 forward path the column pass
-// leaves IEEE doubles (exact integers, |x| <= 3q) in the buffer for the row pass, which
-// writes canonical residues; the integer path keeps the reference's lazy [0, 4q) values.
-//
-// Latency hiding: both passes are persistent — a workgroup (column pass) or a wavefront
-// (row pass) walks a strided list of tiles and prefetches the next tile's data into
-// registers before computing the current one.
+// (farith.h), other primes the integer Shoup butterflies of arith.h.
+//  * FP64 forward: the column pass stores exact-integer doubles (|x| < 7.75 q) for the row pass,
+//    which writes canonical residues.  Reductions are placed at compile time (Bound, farith.h).
+//  * FP64 inverse: GS butterflies; n^-1 is folded into the last stage (x' = (x + y) n^-1,
+//    y' = (x - y) itw[1] n^-1) as the reference does (src/ntt/intt_2d.cu:195-198).
+//  * Column-pass twiddles come from a per-limb S1-entry table (cache resident); row-pass
+//    twiddles are generated: tw = A_g(row) * B_g(iloc) (host/ntt_tables.cpp), the 15 twiddles
+//    of the first radix-16 round (the same for all lanes of a row) cooperatively through LDS.
+//  * Integer path: the reference's lazy ranges ([0, 4q) forward, [0, 2q) inverse), twiddles and
+//    Shoup quotients read from the full tables, n^-1 applied after the last stage.
 #include "ntt.h"
 
 #include <algorithm>
@@ -36,21 +38,15 @@ namespace {
 
 constexpr int E_LOG = 4;  // elements per thread per round = 16 (radix-16 rounds)
 constexpr int E = 1 << E_LOG;
-constexpr int COLS = 16;  // columns per column-pass tile (16 x 8 B = one 128 B line per row)
+constexpr int COLS = 16;  // columns per column-pass tile
 constexpr int BLOCK = 256;
-#ifndef PHX_NTT_GRID_MULT
-#define PHX_NTT_GRID_MULT 0  // persistent workgroups per CU (0: one workgroup per tile)
-#endif
 #ifndef PHX_NTT_WAVES_PER_EU
 #define PHX_NTT_WAVES_PER_EU 4  // __launch_bounds__ occupancy target (waves per SIMD)
-#endif
-#ifndef PHX_NTT_PREFETCH
-#define PHX_NTT_PREFETCH 0   // prefetch the next tile into registers
 #endif
 
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 
-// Round r of a size-2^S_LOG sub-transform: stages [g0, g0 + er).
+// Round R of a size-2^S_LOG sub-transform: stages [g0, g0 + er).
 template <int S_LOG, int R>
 struct Round {
   static constexpr int g0 = R * E_LOG;
@@ -74,17 +70,64 @@ struct Sub {
   static constexpr int ROUNDS = (S_LOG + E_LOG - 1) / E_LOG;
 };
 
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  [&]<int... I>(std::integer_sequence<int, I...>) { (f(std::integral_constant<int, I>{}), ...); }
+  (std::make_integer_sequence<int, N>{});
+}
+
 // ---------------------------------------------------------------------------------------
-// per-limb arithmetic context
+// FP64 reduction schedules (compile time): bit g of `mask` = reduce every value before stage g.
 // ---------------------------------------------------------------------------------------
-struct LimbCtx {
-  uint64_t q;
-  double qd, qinv;
-  const uint64_t* tw;   // integer table (forward or inverse)
-  const uint64_t* tws;  // its Shoup quotients
-  const double* twf;    // FP64 table (centered), forward only
+struct Sched {
+  uint32_t mask;
+  double out;  // bound of the pass output (units of q)
+};
+constexpr double dmax(double a, double b) { return a > b ? a : b; }
+// Cooley-Tukey stages g = 0 .. s-1: x' = x +- fmodmul(y, w)
+constexpr Sched sched_ct(int s, double x0, double w) {
+  Sched r{0u, x0};
+  double x = x0;
+  for (int g = 0; g < s; ++g) {
+    if (x + Bound::prod(x, w) > Bound::kLimit) {
+      r.mask |= 1u << g;
+      x = Bound::kReduced;
+    }
+    x = x + Bound::prod(x, w);
+  }
+  r.out = x;
+  return r;
+}
+// Gentleman-Sande stages g = s-1 .. 0: x' = x + y, y' = fmodmul(x - y, w); with `fold` the
+// last stage also multiplies x' by n^-1
+constexpr Sched sched_gs(int s, double x0, double w, bool fold) {
+  Sched r{0u, x0};
+  double x = x0;
+  for (int g = s - 1; g >= 0; --g) {
+    auto next = [&](double v) { return (fold && g == 0) ? Bound::prod(2 * v, w) : dmax(2 * v, Bound::prod(2 * v, w)); };
+    if (next(x) > Bound::kLimit) {
+      r.mask |= 1u << g;
+      x = Bound::kReduced;
+    }
+    x = next(x);
+  }
+  r.out = x;
+  return r;
+}
+
+template <int S1_LOG, int S2_LOG>
+struct Plan {
+  static constexpr Sched col_fwd = sched_ct(S1_LOG, 1.0, Bound::kTableW);
+  static constexpr Sched row_fwd = sched_ct(S2_LOG, col_fwd.out, Bound::kGenW);
+  static constexpr Sched row_inv = sched_gs(S2_LOG, 1.0, Bound::kGenW, false);
+  static constexpr Sched col_inv = sched_gs(S1_LOG, row_inv.out, Bound::kGenW, true);
+  static_assert(col_fwd.out < Bound::kLimit && row_fwd.out < Bound::kLimit, "bound");
+  static_assert(row_inv.out < Bound::kLimit && col_inv.out < Bound::kLimit, "bound");
 };
 
+// ---------------------------------------------------------------------------------------
+// twiddles of one round
+// ---------------------------------------------------------------------------------------
 // Distinct twiddles of one round: stage gl has 2^(gl + ex) of them, keyed by the element's
 // active bits above the pair bit and its extra bits; slots are packed stage after stage.
 template <int EX>
@@ -92,9 +135,13 @@ __host__ __device__ constexpr int tw_slot(int gl, int key) { return (((1 << gl) 
 template <int EX>
 __host__ __device__ constexpr int tw_key(int gl, int j) { return ((j >> (E_LOG - gl)) << EX) | (j & ((1 << EX) - 1)); }
 
-// Twiddles of one round, loaded into registers before the next tile's prefetch is issued
-// (vmcnt counts loads in issue order, so a twiddle load issued after the prefetch would
-// make the compute wait for the prefetch).  w[gl][k]: stage gl, k-th butterfly.
+// representative element j of key `key` at local stage gl
+template <int EX>
+__host__ __device__ constexpr int key_elem(int gl, int key) {
+  return ((key >> EX) << (E_LOG - gl)) | (key & ((1 << EX) - 1));
+}
+
+// twiddles read from a table: w[slot] = tab[(B << g) + (p >> (S_LOG - g))]
 template <int S_LOG, int R, typename W>
 __device__ __forceinline__ void load_tw(W (&w)[E], const W* __restrict__ tab, uint32_t pt, uint32_t B) {
   using Rd = Round<S_LOG, R>;
@@ -103,21 +150,16 @@ __device__ __forceinline__ void load_tw(W (&w)[E], const W* __restrict__ tab, ui
     const int g = Rd::g0 + gl;
 #pragma unroll
     for (int key = 0; key < (1 << (gl + Rd::ex)); ++key) {
-      // a representative element j with this key: active bits above the pair bit from key's
-      // high part, extra bits from key's low part
-      const int j = ((key >> Rd::ex) << (E_LOG - gl)) | (key & ((1 << Rd::ex) - 1));
-      const uint32_t p = pt | Rd::p_elem(j);
+      const uint32_t p = pt | Rd::p_elem(key_elem<Rd::ex>(gl, key));
       w[tw_slot<Rd::ex>(gl, key)] = tab[(B << g) + (p >> (S_LOG - g))];
     }
   }
 }
 
-// Row-pass FP64 twiddles computed on the fly: tw = A_g(row) * B_g(iloc) mod q (ntt.h), so the
-// row pass reads 8 per-row factors and a 2 KB per-limb table instead of an n-entry table.
+// row-pass FP64 twiddles generated per lane: tw = A[g] * Btab[2^g + iloc] (unreduced, |tw| <= kGenW q)
 template <int S_LOG, int R>
-__device__ __forceinline__ void make_tw_row_f64(double (&w)[E], const double* __restrict__ A,
-                                                const double* __restrict__ Btab, uint32_t pt, double qd,
-                                                double qinv) {
+__device__ __forceinline__ void gen_tw_row(double (&w)[E], const double* __restrict__ A,
+                                           const double* __restrict__ Btab, uint32_t pt, double qd, double qinv) {
   using Rd = Round<S_LOG, R>;
 #pragma unroll
   for (int gl = 0; gl < Rd::er; ++gl) {
@@ -125,12 +167,63 @@ __device__ __forceinline__ void make_tw_row_f64(double (&w)[E], const double* __
     const double ag = A[g];
 #pragma unroll
     for (int key = 0; key < (1 << (gl + Rd::ex)); ++key) {
-      const int j = ((key >> Rd::ex) << (E_LOG - gl)) | (key & ((1 << Rd::ex) - 1));
-      const uint32_t p = pt | Rd::p_elem(j);
-      const double b = Btab[(1u << g) + (p >> (S_LOG - g))];
-      w[tw_slot<Rd::ex>(gl, key)] = freduce(fmodmul(b, ag, qd, qinv), qd, qinv);
+      const uint32_t p = pt | Rd::p_elem(key_elem<Rd::ex>(gl, key));
+      w[tw_slot<Rd::ex>(gl, key)] = fmodmul(Btab[(1u << g) + (p >> (S_LOG - g))], ag, qd, qinv);
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// rounds
+// ---------------------------------------------------------------------------------------
+template <int S_LOG, int R, uint32_t MASK>
+__device__ __forceinline__ void ct_round_f64(double (&v)[E], const double (&w)[E], double qd, double qinv) {
+  using Rd = Round<S_LOG, R>;
+  static_for<Rd::er>([&](auto glc) {
+    constexpr int gl = decltype(glc)::value;
+    constexpr int g = Rd::g0 + gl;
+    if constexpr ((MASK >> g) & 1u) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) v[j] = freduce(v[j], qd, qinv);
+    }
+    constexpr int h = 1 << (E_LOG - 1 - gl);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      if (j & h) continue;
+      const double t = fmodmul(v[j | h], w[tw_slot<Rd::ex>(gl, tw_key<Rd::ex>(gl, j))], qd, qinv);
+      v[j | h] = v[j] - t;
+      v[j] = v[j] + t;
+    }
+  });
+}
+
+// GS round, stages in reverse order.  FOLD: the sub-transform's stage 0 is the transform's last
+// stage; x' = (x + y) c0 and y' = (x - y) c1 (c0 = n^-1 [* scale], c1 = itw[1] n^-1 [* scale]).
+template <int S_LOG, int R, uint32_t MASK, bool FOLD>
+__device__ __forceinline__ void gs_round_f64(double (&v)[E], const double (&w)[E], double qd, double qinv,
+                                             double c0, double c1) {
+  using Rd = Round<S_LOG, R>;
+  static_for<Rd::er>([&](auto ic) {
+    constexpr int gl = Rd::er - 1 - decltype(ic)::value;
+    constexpr int g = Rd::g0 + gl;
+    if constexpr ((MASK >> g) & 1u) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) v[j] = freduce(v[j], qd, qinv);
+    }
+    constexpr int h = 1 << (E_LOG - 1 - gl);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      if (j & h) continue;
+      const double x = v[j], y = v[j | h];
+      if constexpr (FOLD && g == 0) {
+        v[j] = fmodmul(x + y, c0, qd, qinv);
+        v[j | h] = fmodmul(x - y, c1, qd, qinv);
+      } else {
+        v[j] = x + y;
+        v[j | h] = fmodmul(x - y, w[tw_slot<Rd::ex>(gl, tw_key<Rd::ex>(gl, j))], qd, qinv);
+      }
+    }
+  });
 }
 
 // forward CT round, integer path: values in [0, 4q)
@@ -150,33 +243,7 @@ __device__ __forceinline__ void ct_round_int(uint64_t (&v)[E], const uint64_t (&
   }
 }
 
-// forward CT round, FP64 path.  GOFF = global stage index of local stage 0 of this
-// sub-transform; every value is reduced before global stages 3, 6, 9, ... (farith.h bounds).
-template <int S_LOG, int R, int GOFF>
-__device__ __forceinline__ void ct_round_f64(double (&v)[E], const double (&w)[E], double qd, double qinv) {
-  using Rd = Round<S_LOG, R>;
-#ifdef PHX_NTT_NO_COMPUTE
-  return;
-#endif
-#pragma unroll
-  for (int gl = 0; gl < Rd::er; ++gl) {
-    const int g = Rd::g0 + gl;
-    if ((GOFF + g) % 3 == 0 && (GOFF + g) > 0) {
-#pragma unroll
-      for (int j = 0; j < E; ++j) v[j] = freduce(v[j], qd, qinv);
-    }
-    const int h = 1 << (E_LOG - 1 - gl);
-#pragma unroll
-    for (int j = 0; j < E; ++j) {
-      if (j & h) continue;
-      const double t = fmodmul(v[j | h], w[tw_slot<Rd::ex>(gl, tw_key<Rd::ex>(gl, j))], qd, qinv);
-      v[j | h] = v[j] - t;
-      v[j] = v[j] + t;
-    }
-  }
-}
-
-// inverse GS round (integer path): stages in reverse order, values in [0, 2q)
+// inverse GS round, integer path: stages in reverse order, values in [0, 2q)
 template <int S_LOG, int R>
 __device__ __forceinline__ void gs_round_int(uint64_t (&v)[E], const uint64_t (&w)[E], const uint64_t (&ws)[E],
                                              uint64_t q) {
@@ -193,17 +260,28 @@ __device__ __forceinline__ void gs_round_int(uint64_t (&v)[E], const uint64_t (&
   }
 }
 
+// Move a thread-group's values from round RA's layout to round RB's through its LDS tile.
+template <int S_LOG, int RA, int RB, typename V, typename Idx, typename Sync>
+__device__ __forceinline__ void relayout(V (&v)[E], V* L, Idx idx, Sync sync, uint32_t t) {
+  const uint32_t pa = Round<S_LOG, RA>::p_thread(t), pb = Round<S_LOG, RB>::p_thread(t);
+#pragma unroll
+  for (int j = 0; j < E; ++j) L[idx(pa | Round<S_LOG, RA>::p_elem(j))] = v[j];
+  sync();
+#pragma unroll
+  for (int j = 0; j < E; ++j) v[j] = L[idx(pb | Round<S_LOG, RB>::p_elem(j))];
+  sync();
+}
+
 struct KArgs {
   const uint64_t* in;
   uint64_t* out;
   const uint64_t* modulus;
   const double* modulus_f;    // q as double
-  const double* modulus_inv;  // 1/q rounded
-  const uint8_t* is_f64;      // per table row: FP64 path usable (q < 2^50)
-  const uint64_t* tw;         // forward or inverse integer table base
+  const double* modulus_inv;  // fl(1/q)
+  const uint64_t* tw;         // integer table (forward or inverse)
   const uint64_t* tws;
-  const double* twf;          // forward FP64 table
-  const double* row_a;        // row-pass factored twiddles (ntt.h)
+  const double* col;          // FP64 column table (forward or inverse)
+  const double* row_a;        // FP64 row factors (forward or inverse)
   const double* row_b;
   const uint64_t* n_inv;
   const uint64_t* n_inv_shoup;
@@ -212,7 +290,6 @@ struct KArgs {
   LimbMap map;
   int n;
   int limbs;                  // number of processed limbs (excluding skipped)
-  int f64_fwd;                // 1: forward transform may use the FP64 path
 };
 
 __device__ __forceinline__ void resolve_limb(const LimbMap& m, int y, int& buf_limb, int& row) {
@@ -222,329 +299,253 @@ __device__ __forceinline__ void resolve_limb(const LimbMap& m, int y, int& buf_l
   row = i < m.split ? m.first_a + i : m.first_b + (i - m.split);
 }
 
-__device__ __forceinline__ LimbCtx limb_ctx(const KArgs& a, int row, bool& f64) {
+struct LimbCtx {
+  uint64_t q;
+  double qd, qinv;
+  bool f64;
+};
+__device__ __forceinline__ LimbCtx limb_ctx(const KArgs& a, int row) {
   // row is wave-uniform: readfirstlane lets the per-limb constants come through scalar loads
-  // (a vector load here would carry an s_waitcnt vmcnt(0) that drains the tile prefetch)
   row = __builtin_amdgcn_readfirstlane(row);
   LimbCtx c;
   c.q = a.modulus[row];
   c.qd = a.modulus_f[row];
   c.qinv = a.modulus_inv[row];
-  c.tw = a.tw + (size_t)row * a.n;
-  c.tws = a.tws + (size_t)row * a.n;
-  c.twf = a.twf + (size_t)row * a.n;
-  f64 = a.f64_fwd && c.q < (1ull << 50);
+  c.f64 = c.q < (1ull << 50);
   return c;
 }
 
+__device__ __forceinline__ double centered_f64(uint64_t w, uint64_t q) {
+  return w > (q >> 1) ? -u52_to_f64(q - w) : u52_to_f64(w);
+}
+
 // LDS padding: one pad word every 16 words (row tiles) / one 16-word pad row every 16 rows
-// (column tiles) — keeps the transposed round's ds_read_b64 accesses conflict-free.
+// (column tiles) — keeps the transposed rounds' ds_read_b64 accesses conflict-free.
 __device__ __forceinline__ uint32_t rpad(uint32_t p) { return p + (p >> 4); }
 __device__ __forceinline__ uint32_t cidx(uint32_t p, uint32_t c) { return p * COLS + c + (p >> 4) * COLS; }
 
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  [&]<int... I>(std::integer_sequence<int, I...>) { (f(std::integral_constant<int, I>{}), ...); }
-  (std::make_integer_sequence<int, N>{});
-}
-
-// All twiddles of one sub-transform for one thread, in registers.
-template <int S_LOG>
-struct TwF64 {
-  double w[Sub<S_LOG>::ROUNDS][E];
-};
-template <int S_LOG>
-struct TwInt {
-  uint64_t w[Sub<S_LOG>::ROUNDS][E];
-  uint64_t ws[Sub<S_LOG>::ROUNDS][E];
-};
-
-template <int S_LOG>
-__device__ __forceinline__ void load_all(TwF64<S_LOG>& tw, const double* tab, uint32_t t, uint32_t B) {
-  static_for<Sub<S_LOG>::ROUNDS>([&](auto r) {
-    constexpr int R = decltype(r)::value;
-    load_tw<S_LOG, R>(tw.w[R], tab, Round<S_LOG, R>::p_thread(t), B);
-  });
-}
-template <int S_LOG>
-__device__ __forceinline__ void load_all(TwInt<S_LOG>& tw, const uint64_t* tab, const uint64_t* tabs, uint32_t t,
-                                         uint32_t B) {
-  static_for<Sub<S_LOG>::ROUNDS>([&](auto r) {
-    constexpr int R = decltype(r)::value;
-    load_tw<S_LOG, R>(tw.w[R], tab, Round<S_LOG, R>::p_thread(t), B);
-    load_tw<S_LOG, R>(tw.ws[R], tabs, Round<S_LOG, R>::p_thread(t), B);
-  });
-}
-
-// One full sub-transform (all rounds) on registers v, which hold the load layout
-// p = t + j*T on entry and on exit.  L is this thread-group's LDS tile of element type V
-// indexed by idx(p); sync() orders the LDS exchanges (workgroup or wavefront barrier).
-// Twiddles of one round in registers (FP64: w; integer: w and Shoup quotients ws)
-struct RoundTwF64 {
-  double w[E];
-};
-struct RoundTwInt {
-  uint64_t w[E], ws[E];
-};
-
-// get_tw(integral_constant<R>) produces round R's twiddles; it runs right before the round so
-// only one round's twiddles are live (keeps VGPR use low enough for 4 waves per SIMD).
-template <int S_LOG, int GOFF, bool FWD, typename V, typename GetTw, typename Idx, typename Sync>
-__device__ __forceinline__ void sub_transform(V (&v)[E], GetTw get_tw, V* L, Idx idx, Sync sync, uint32_t t,
-                                              uint64_t q, double qd, double qinv) {
-  using SB = Sub<S_LOG>;
-  constexpr int RN = SB::ROUNDS;
-  constexpr bool F = !std::is_same_v<V, uint64_t>;
-  auto round = [&](auto r) {
-    constexpr int R = decltype(r)::value;
-    const auto tw = get_tw(r);
-    if constexpr (F) {
-      static_assert(FWD, "FP64 path is forward-only");
-      ct_round_f64<S_LOG, R, GOFF>(v, tw.w, qd, qinv);
-    } else if constexpr (FWD) {
-      ct_round_int<S_LOG, R>(v, tw.w, tw.ws, q);
-    } else {
-      gs_round_int<S_LOG, R>(v, tw.w, tw.ws, q);
-    }
-  };
-  auto put = [&](uint32_t pt, auto r) {
-    constexpr int R = decltype(r)::value;
-#pragma unroll
-    for (int j = 0; j < E; ++j) L[idx(pt | Round<S_LOG, R>::p_elem(j))] = v[j];
-  };
-  auto get = [&](uint32_t pt, auto r) {
-    constexpr int R = decltype(r)::value;
-#pragma unroll
-    for (int j = 0; j < E; ++j) v[j] = L[idx(pt | Round<S_LOG, R>::p_elem(j))];
-  };
-  if constexpr (FWD) {
-    round(std::integral_constant<int, 0>{});
-    static_for<RN - 1>([&](auto rm1) {
-      constexpr int R = decltype(rm1)::value + 1;
-      put(Round<S_LOG, R - 1>::p_thread(t), std::integral_constant<int, R - 1>{});
-      sync();
-      get(Round<S_LOG, R>::p_thread(t), std::integral_constant<int, R>{});
-      sync();
-      round(std::integral_constant<int, R>{});
-    });
-    if constexpr (RN > 1) {
-      put(Round<S_LOG, RN - 1>::p_thread(t), std::integral_constant<int, RN - 1>{});
-      sync();
-      get(Round<S_LOG, 0>::p_thread(t), std::integral_constant<int, 0>{});
-      sync();
-    }
-  } else {
-    if constexpr (RN > 1) {
-      put(Round<S_LOG, 0>::p_thread(t), std::integral_constant<int, 0>{});
-      sync();
-      get(Round<S_LOG, RN - 1>::p_thread(t), std::integral_constant<int, RN - 1>{});
-      sync();
-    }
-    static_for<RN - 1>([&](auto i) {
-      constexpr int R = RN - 1 - decltype(i)::value;  // RN-1 .. 1
-      round(std::integral_constant<int, R>{});
-      put(Round<S_LOG, R>::p_thread(t), std::integral_constant<int, R>{});
-      sync();
-      get(Round<S_LOG, R - 1>::p_thread(t), std::integral_constant<int, R - 1>{});
-      sync();
-    });
-    round(std::integral_constant<int, 0>{});
-  }
-}
-
-__device__ __forceinline__ void fence_loads() { __builtin_amdgcn_sched_barrier(0); }
-
 // ---------------------------------------------------------------------------------------
 // Column pass: tile = COLS consecutive columns x S1 rows of one limb; 256-thread workgroup.
-// FWD: first log2(S1) CT stages (FP64: output doubles |x| <= 3q; int: lazy [0, 4q)).
-// INV: last log2(S1) GS stages, then n^-1 and the optional per-limb scale.
+// Any round layout is coalesced here (16 lanes cover one 128 B row segment), so the pass loads
+// in the layout of its first round and stores from its last: RN - 1 LDS transposes.
+// FWD: first log2(S1) CT stages.  INV: last log2(S1) GS stages (n^-1 and the optional scale).
 // ---------------------------------------------------------------------------------------
 template <int S1_LOG, int S2_LOG, bool FWD>
 __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) {
   using SB = Sub<S1_LOG>;
-  constexpr int T = SB::T, S2 = 1 << S2_LOG, NT = COLS * T, CT = S2 / COLS;
+  using P = Plan<S1_LOG, S2_LOG>;
+  constexpr int T = SB::T, S2 = 1 << S2_LOG, NT = COLS * T, CT = S2 / COLS, RN = SB::ROUNDS;
+  constexpr int RF = FWD ? 0 : RN - 1;  // first round executed
+  constexpr int RL = FWD ? RN - 1 : 0;  // last round executed
   static_assert(NT <= BLOCK, "column tile too large");
   __shared__ uint64_t lds[(SB::S + SB::S / 16) * COLS];
 
   const uint32_t tid = threadIdx.x;
-  const bool active = tid < NT;
+  if (tid >= NT) return;  // no barrier below involves the idle threads' absence (NT is a multiple of 64)
   const uint32_t c = tid % COLS, t = tid / COLS;
   const int ntiles = a.limbs * CT;
-  const int ntiles_or_items = ntiles;
   auto idx = [c](uint32_t p) { return cidx(p, c); };
   auto sync = [] { __syncthreads(); };
+  const uint32_t pf = Round<S1_LOG, RF>::p_thread(t), pl = Round<S1_LOG, RL>::p_thread(t);
 
-  uint64_t cur[E], nxt[E];
-  auto load = [&](int tile, uint64_t (&dst)[E]) {
+  {  // one tile per workgroup (grid = ntiles)
+    const int tile = blockIdx.x;
+    if (tile >= ntiles) return;
     int buf_limb, row;
     resolve_limb(a.map, tile / CT, buf_limb, row);
-    const uint64_t* src = a.in + (size_t)buf_limb * a.n + (tile % CT) * COLS + c;
-    if (active) {
+    buf_limb = __builtin_amdgcn_readfirstlane(buf_limb);
+    const LimbCtx lc = limb_ctx(a, row);
+    const size_t off = (size_t)buf_limb * a.n + (tile % CT) * COLS + c;
+    const uint64_t* src = a.in + off;
+    uint64_t* dst = a.out + off;
+    uint64_t x[E];
 #pragma unroll
-      for (int j = 0; j < E; ++j) dst[j] = __builtin_nontemporal_load(src + (size_t)(t + j * T) * S2);
-    }
-  };
-  int tile = blockIdx.x;
-  if (tile < ntiles) load(tile, cur);
-  for (; tile < ntiles; tile += gridDim.x) {
-    const int next = tile + gridDim.x;
-    int buf_limb, row;
-    resolve_limb(a.map, tile / CT, buf_limb, row);
-    bool f64;
-    const LimbCtx lc = limb_ctx(a, row, f64);
-    uint64_t* dst = a.out + (size_t)buf_limb * a.n + (tile % CT) * COLS + c;
-    if (FWD && f64) {
-      auto tw = [&](auto r) {
-        constexpr int R = decltype(r)::value;
-        RoundTwF64 x;
-        load_tw<S1_LOG, R>(x.w, lc.twf, Round<S1_LOG, R>::p_thread(t), 1);
-        return x;
-      };
-      if (PHX_NTT_PREFETCH && next < ntiles) load(next, nxt);
+    for (int j = 0; j < E; ++j) x[j] = __builtin_nontemporal_load(src + (size_t)(pf | Round<S1_LOG, RF>::p_elem(j)) * S2);
+    if (lc.f64) {
+      const double* tab = a.col + (size_t)__builtin_amdgcn_readfirstlane(row) * SB::S;
       double v[E];
 #pragma unroll
-      for (int j = 0; j < E; ++j) v[j] = u64_to_f64(cur[j]);
-      if constexpr (FWD)
-        sub_transform<S1_LOG, 0, true>(v, tw, reinterpret_cast<double*>(lds), idx, sync, t, lc.q, lc.qd, lc.qinv);
-      if (active) {
+      for (int j = 0; j < E; ++j) v[j] = FWD ? u52_to_f64(x[j]) : as_f64(x[j]);
+      if constexpr (FWD) {
+        static_for<RN>([&](auto rc) {
+          constexpr int R = decltype(rc)::value;
+          if constexpr (R > 0) relayout<S1_LOG, R - 1, R>(v, reinterpret_cast<double*>(lds), idx, sync, t);
+          double w[E];
+          load_tw<S1_LOG, R>(w, tab, Round<S1_LOG, R>::p_thread(t), 1);
+          ct_round_f64<S1_LOG, R, P::col_fwd.mask>(v, w, lc.qd, lc.qinv);
+        });
 #pragma unroll
-        for (int j = 0; j < E; ++j) dst[(size_t)(t + j * T) * S2] = as_bits(v[j]);
+        for (int j = 0; j < E; ++j) dst[(size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2] = as_bits(v[j]);
+      } else {
+        double c0 = tab[0], c1 = tab[1];
+        if (a.scale) {
+          const double sc = centered_f64(a.scale[buf_limb], lc.q);
+          c0 = fmodmul(c0, sc, lc.qd, lc.qinv);
+          c1 = fmodmul(c1, sc, lc.qd, lc.qinv);
+        }
+        static_for<RN>([&](auto rc) {
+          constexpr int R = RN - 1 - decltype(rc)::value;
+          if constexpr (R < RN - 1) relayout<S1_LOG, R + 1, R>(v, reinterpret_cast<double*>(lds), idx, sync, t);
+          double w[E];
+          load_tw<S1_LOG, R>(w, tab, Round<S1_LOG, R>::p_thread(t), 1);
+          gs_round_f64<S1_LOG, R, P::col_inv.mask, true>(v, w, lc.qd, lc.qinv, c0, c1);
+        });
+#pragma unroll
+        for (int j = 0; j < E; ++j)
+          __builtin_nontemporal_store(f64_to_canonical(v[j], lc.qd, lc.qinv),
+                                      dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2);
       }
     } else {
-      auto tw = [&](auto r) {
-        constexpr int R = decltype(r)::value;
-        RoundTwInt x;
-        load_tw<S1_LOG, R>(x.w, lc.tw, Round<S1_LOG, R>::p_thread(t), 1);
-        load_tw<S1_LOG, R>(x.ws, lc.tws, Round<S1_LOG, R>::p_thread(t), 1);
-        return x;
-      };
-      if (PHX_NTT_PREFETCH && next < ntiles) load(next, nxt);
-      sub_transform<S1_LOG, 0, FWD>(cur, tw, lds, idx, sync, t, lc.q, lc.qd, lc.qinv);
-      if (active) {
-        if constexpr (FWD) {
+      const uint64_t* tw = a.tw + (size_t)__builtin_amdgcn_readfirstlane(row) * a.n;
+      const uint64_t* tws = a.tws + (size_t)__builtin_amdgcn_readfirstlane(row) * a.n;
+      uint64_t(&v)[E] = x;
+      static_for<RN>([&](auto rc) {
+        constexpr int R = FWD ? decltype(rc)::value : RN - 1 - decltype(rc)::value;
+        if constexpr (FWD && R > 0) relayout<S1_LOG, R - 1, R>(v, lds, idx, sync, t);
+        if constexpr (!FWD && R < RN - 1) relayout<S1_LOG, R + 1, R>(v, lds, idx, sync, t);
+        uint64_t w[E], ws[E];
+        load_tw<S1_LOG, R>(w, tw, Round<S1_LOG, R>::p_thread(t), 1);
+        load_tw<S1_LOG, R>(ws, tws, Round<S1_LOG, R>::p_thread(t), 1);
+        if constexpr (FWD)
+          ct_round_int<S1_LOG, R>(v, w, ws, lc.q);
+        else
+          gs_round_int<S1_LOG, R>(v, w, ws, lc.q);
+      });
+      if constexpr (FWD) {
 #pragma unroll
-          for (int j = 0; j < E; ++j) dst[(size_t)(t + j * T) * S2] = cur[j];  // lazy [0, 4q)
-        } else {
-          const uint64_t ni = a.n_inv[row], nis = a.n_inv_shoup[row];
-          const bool scaled = a.scale != nullptr;
-          const uint64_t sc = scaled ? a.scale[buf_limb] : 0, scs = scaled ? a.scale_shoup[buf_limb] : 0;
+        for (int j = 0; j < E; ++j) dst[(size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2] = v[j];  // lazy [0, 4q)
+      } else {
+        const uint64_t ni = a.n_inv[row], nis = a.n_inv_shoup[row];
+        const bool scaled = a.scale != nullptr;
+        const uint64_t sc = scaled ? a.scale[buf_limb] : 0, scs = scaled ? a.scale_shoup[buf_limb] : 0;
 #pragma unroll
-          for (int j = 0; j < E; ++j) {
-            uint64_t x = mul_shoup(cur[j], ni, nis, lc.q);
-            if (scaled) x = mul_shoup(x, sc, scs, lc.q);
-            dst[(size_t)(t + j * T) * S2] = x;
-          }
+        for (int j = 0; j < E; ++j) {
+          uint64_t x = mul_shoup(v[j], ni, nis, lc.q);
+          if (scaled) x = mul_shoup(x, sc, scs, lc.q);
+          dst[(size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2] = x;
         }
       }
-    }
-    if constexpr (PHX_NTT_PREFETCH) {
-#pragma unroll
-      for (int j = 0; j < E; ++j) cur[j] = nxt[j];
-    } else if (next < ntiles_or_items) {
-      load(next, cur);
     }
   }
 }
 
 // ---------------------------------------------------------------------------------------
 // Row pass: each wavefront owns RW = 64/T whole rows at a time (T lanes per row), so the
-// LDS transposes are wave-private and need no workgroup barrier.
+// LDS transposes are wave-private and need no workgroup barrier.  Loads and stores use the
+// round-0 layout (p = t + 16 j: 16 lanes cover one 128 B segment).
 // FWD: last log2(S2) CT stages, canonical output.  INV: first log2(S2) GS stages.
 // ---------------------------------------------------------------------------------------
 template <int S1_LOG, int S2_LOG, bool FWD>
 __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) {
   using SB = Sub<S2_LOG>;
-  constexpr int S2 = SB::S, T = SB::T, RW = cmin(64 / T, 1 << S1_LOG), RSTR = S2 + S2 / 16;
+  using P = Plan<S1_LOG, S2_LOG>;
+  constexpr int S2 = SB::S, T = SB::T, RW = cmin(64 / T, 1 << S1_LOG), RSTR = S2 + S2 / 16, RN = SB::ROUNDS;
   constexpr int WAVES = BLOCK / 64;
   constexpr int GROUPS = (1 << S1_LOG) / RW;  // row groups per limb
+  constexpr int ER0 = Round<S2_LOG, 0>::er;   // stages of round 0 (its twiddles are row-uniform)
+  static_assert(Round<S2_LOG, 0>::ex == 0, "round 0 must be a full radix-16 round");
   __shared__ uint64_t lds[WAVES * RW * RSTR];
+  __shared__ double tw0[WAVES * RW * 16];
 
   const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
   const uint32_t lr = lane / T, t = lane % T;
   uint64_t* lrow = lds + (wave * RW + lr) * RSTR;
+  double* trow = tw0 + (wave * RW + lr) * 16;
   const int nitems = a.limbs * GROUPS;
-  const int ntiles_or_items = nitems;
-  const int stride = gridDim.x * WAVES;
   auto idx = [](uint32_t p) { return rpad(p); };
   auto sync = [] { __builtin_amdgcn_wave_barrier(); };
 
-  uint64_t cur[E], nxt[E];
-  auto load = [&](int item, uint64_t (&dst)[E]) {
-    int buf_limb, row;
-    resolve_limb(a.map, item / GROUPS, buf_limb, row);
-    const uint32_t r = (item % GROUPS) * RW + lr;
-    const uint64_t* src = a.in + (size_t)buf_limb * a.n + (size_t)r * S2 + t;
-#pragma unroll
-    for (int j = 0; j < E; ++j) dst[j] = src[j * T];
-  };
-  int item = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + wave);
-  if (item < nitems) load(item, cur);
-  for (; item < nitems; item += stride) {
-    const int next = item + stride;
+  {  // one item (RW rows) per wavefront (grid = nitems / WAVES)
+    const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + wave);
+    if (item >= nitems) return;  // no workgroup barrier in this kernel
     int buf_limb, row;
     resolve_limb(a.map, item / GROUPS, buf_limb, row);
     buf_limb = __builtin_amdgcn_readfirstlane(buf_limb);
-    bool f64;
-    const LimbCtx lc = limb_ctx(a, row, f64);
+    row = __builtin_amdgcn_readfirstlane(row);
+    const LimbCtx lc = limb_ctx(a, row);
     const uint32_t r = (item % GROUPS) * RW + lr;
-    const uint32_t B = (1u << S1_LOG) + r;
-    uint64_t* dst = a.out + (size_t)buf_limb * a.n + (size_t)r * S2 + t;
-    if (FWD && f64) {
+    const size_t off = (size_t)buf_limb * a.n + (size_t)r * S2 + t;
+    const uint64_t* src = a.in + off;
+    uint64_t* dst = a.out + off;
+    if (lc.f64) {
       const double* A = a.row_a + ((size_t)row * (1u << S1_LOG) + r) * 16;
       const double* Bt = a.row_b + (size_t)row * S2;
-      auto tw = [&](auto rr) {
-        constexpr int RR = decltype(rr)::value;
-        RoundTwF64 x;
-        make_tw_row_f64<S2_LOG, RR>(x.w, A, Bt, Round<S2_LOG, RR>::p_thread(t), lc.qd, lc.qinv);
-        return x;
-      };
-      if (PHX_NTT_PREFETCH && next < nitems) load(next, nxt);
+      // round-0 twiddles of this row, computed once per row: trow[e] = A[log2 e] * B[e], e < 2^ER0
+      for (int e = t + 1; e < (1 << ER0); e += T) trow[e] = fmodmul(Bt[e], A[31 - __builtin_clz(e)], lc.qd, lc.qinv);
       double v[E];
 #pragma unroll
-      for (int j = 0; j < E; ++j) v[j] = as_f64(cur[j]);
-      if constexpr (FWD)
-        sub_transform<S2_LOG, S1_LOG, true>(v, tw, reinterpret_cast<double*>(lrow), idx, sync, t, lc.q, lc.qd,
-                                            lc.qinv);
+      for (int j = 0; j < E; ++j) {
+        const uint64_t x = src[j * T];
+        v[j] = FWD ? as_f64(x) : u52_to_f64(x);
+      }
+      sync();
+      auto get_tw = [&](auto rc, double (&w)[E]) {
+        constexpr int R = decltype(rc)::value;
+        if constexpr (R == 0) {
 #pragma unroll
-      for (int j = 0; j < E; ++j) __builtin_nontemporal_store(f64_to_canonical(v[j], lc.qd, lc.qinv), dst + j * T);
-    } else {
-      auto tw = [&](auto rr) {
-        constexpr int RR = decltype(rr)::value;
-        RoundTwInt x;
-        load_tw<S2_LOG, RR>(x.w, lc.tw, Round<S2_LOG, RR>::p_thread(t), B);
-        load_tw<S2_LOG, RR>(x.ws, lc.tws, Round<S2_LOG, RR>::p_thread(t), B);
-        return x;
+          for (int s = 0; s < (1 << ER0) - 1; ++s) w[s] = trow[s + 1];
+        } else {
+          gen_tw_row<S2_LOG, R>(w, A, Bt, Round<S2_LOG, R>::p_thread(t), lc.qd, lc.qinv);
+        }
       };
-      if (PHX_NTT_PREFETCH && next < nitems) load(next, nxt);
-      sub_transform<S2_LOG, S1_LOG, FWD>(cur, tw, lrow, idx, sync, t, lc.q, lc.qd, lc.qinv);
       if constexpr (FWD) {
+        static_for<RN>([&](auto rc) {
+          constexpr int R = decltype(rc)::value;
+          if constexpr (R > 0) relayout<S2_LOG, R - 1, R>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
+          double w[E];
+          get_tw(rc, w);
+          ct_round_f64<S2_LOG, R, P::row_fwd.mask>(v, w, lc.qd, lc.qinv);
+        });
+        if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
+#pragma unroll
+        for (int j = 0; j < E; ++j) __builtin_nontemporal_store(f64_to_canonical(v[j], lc.qd, lc.qinv), dst + j * T);
+      } else {
+        if constexpr (RN > 1) relayout<S2_LOG, 0, RN - 1>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
+        static_for<RN>([&](auto rc) {
+          constexpr int R = RN - 1 - decltype(rc)::value;
+          if constexpr (R < RN - 1) relayout<S2_LOG, R + 1, R>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
+          double w[E];
+          get_tw(std::integral_constant<int, R>{}, w);
+          gs_round_f64<S2_LOG, R, P::row_inv.mask, false>(v, w, lc.qd, lc.qinv, 0.0, 0.0);
+        });
+#pragma unroll
+        for (int j = 0; j < E; ++j) dst[j * T] = as_bits(v[j]);  // exact-integer doubles for the column pass
+      }
+    } else {
+      const uint32_t B = (1u << S1_LOG) + r;
+      const uint64_t* tw = a.tw + (size_t)row * a.n;
+      const uint64_t* tws = a.tws + (size_t)row * a.n;
+      uint64_t v[E];
+#pragma unroll
+      for (int j = 0; j < E; ++j) v[j] = src[j * T];
+      if constexpr (FWD) {
+        static_for<RN>([&](auto rc) {
+          constexpr int R = decltype(rc)::value;
+          if constexpr (R > 0) relayout<S2_LOG, R - 1, R>(v, lrow, idx, sync, t);
+          uint64_t w[E], ws[E];
+          load_tw<S2_LOG, R>(w, tw, Round<S2_LOG, R>::p_thread(t), B);
+          load_tw<S2_LOG, R>(ws, tws, Round<S2_LOG, R>::p_thread(t), B);
+          ct_round_int<S2_LOG, R>(v, w, ws, lc.q);
+        });
+        if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, lrow, idx, sync, t);
         const uint64_t q2 = lc.q << 1;
 #pragma unroll
-        for (int j = 0; j < E; ++j) __builtin_nontemporal_store(csub(csub(cur[j], q2), lc.q), dst + j * T);
+        for (int j = 0; j < E; ++j) __builtin_nontemporal_store(csub(csub(v[j], q2), lc.q), dst + j * T);
       } else {
+        if constexpr (RN > 1) relayout<S2_LOG, 0, RN - 1>(v, lrow, idx, sync, t);
+        static_for<RN>([&](auto rc) {
+          constexpr int R = RN - 1 - decltype(rc)::value;
+          if constexpr (R < RN - 1) relayout<S2_LOG, R + 1, R>(v, lrow, idx, sync, t);
+          uint64_t w[E], ws[E];
+          load_tw<S2_LOG, R>(w, tw, Round<S2_LOG, R>::p_thread(t), B);
+          load_tw<S2_LOG, R>(ws, tws, Round<S2_LOG, R>::p_thread(t), B);
+          gs_round_int<S2_LOG, R>(v, w, ws, lc.q);
+        });
 #pragma unroll
-        for (int j = 0; j < E; ++j) dst[j * T] = cur[j];  // [0, 2q), column pass follows
+        for (int j = 0; j < E; ++j) dst[j * T] = v[j];  // [0, 2q), column pass follows
       }
     }
-    if constexpr (PHX_NTT_PREFETCH) {
-#pragma unroll
-      for (int j = 0; j < E; ++j) cur[j] = nxt[j];
-    } else if (next < ntiles_or_items) {
-      load(next, cur);
-    }
   }
-}
-
-int g_num_cus = 0;
-
-int num_cus() {
-  if (!g_num_cus) {
-    int dev = 0;
-    hipDeviceProp_t p;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) g_num_cus = p.multiProcessorCount;
-    if (g_num_cus <= 0) g_num_cus = 256;
-  }
-  return g_num_cus;
 }
 
 template <int S1_LOG, int S2_LOG>
@@ -554,32 +555,30 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   if (limbs <= 0) return hipSuccess;
   KArgs a;
   a.in = in; a.out = out; a.modulus = tb.modulus;
-  a.modulus_f = tb.modulus_f; a.modulus_inv = tb.modulus_inv; a.is_f64 = tb.is_f64;
+  a.modulus_f = tb.modulus_f; a.modulus_inv = tb.modulus_inv;
   a.tw = inverse ? tb.itw : tb.tw;
   a.tws = inverse ? tb.itw_shoup : tb.tw_shoup;
-  a.twf = tb.twf;
-  a.row_a = tb.row_a;
-  a.row_b = tb.row_b;
+  a.col = inverse ? tb.col_inv : tb.col_fwd;
+  a.row_a = inverse ? tb.row_a_inv : tb.row_a_fwd;
+  a.row_b = inverse ? tb.row_b_inv : tb.row_b_fwd;
   a.n_inv = tb.n_inv; a.n_inv_shoup = tb.n_inv_shoup;
   a.scale = scale; a.scale_shoup = scale_shoup;
   a.map = map; a.n = (int)tb.n; a.limbs = limbs;
-  a.f64_fwd = inverse ? 0 : 1;
   constexpr int S1 = 1 << S1_LOG, S2 = 1 << S2_LOG;
   constexpr int RW = cmin(64 / Sub<S2_LOG>::T, S1);
   const int col_tiles = limbs * (S2 / COLS);
   const int row_items = limbs * (S1 / RW);
-  const int cus = num_cus();
-  const int gm = PHX_NTT_GRID_MULT > 0 ? PHX_NTT_GRID_MULT : 1 << 20;
-  const dim3 grid_c(std::min(col_tiles, cus * gm)), grid_r(std::min((row_items + 3) / 4, cus * gm));
-  const dim3 block(BLOCK);
+  const dim3 grid_c(col_tiles), grid_r((row_items + BLOCK / 64 - 1) / (BLOCK / 64));
+  // column tiles of small transforms need fewer than BLOCK threads (rounded up to a wavefront)
+  const dim3 block_c(std::max(64, COLS * Sub<S1_LOG>::T)), block_r(BLOCK);
   if (!inverse) {
-    hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true>), grid_c, block, 0, stream, a);
+    hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true>), grid_c, block_c, 0, stream, a);
     a.in = out;
-    hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true>), grid_r, block, 0, stream, a);
+    hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true>), grid_r, block_r, 0, stream, a);
   } else {
-    hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false>), grid_r, block, 0, stream, a);
+    hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false>), grid_r, block_r, 0, stream, a);
     a.in = out;
-    hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false>), grid_c, block, 0, stream, a);
+    hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false>), grid_c, block_c, 0, stream, a);
   }
   return hipGetLastError();
 }

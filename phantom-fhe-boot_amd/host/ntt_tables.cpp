@@ -75,51 +75,53 @@ DeviceNttTables::DeviceNttTables(size_t n, const std::vector<uint64_t>& moduli, 
     PHX_CHECK(hipStreamSynchronize(stream));  // flat is reused
   };
   {
-    std::vector<double> qf(L), qi(L), twf(n * L);
-    std::vector<uint8_t> f64(L);
-    for (size_t i = 0; i < L; ++i) {
-      const uint64_t q = moduli[i];
-      qf[i] = static_cast<double>(q);
-      qi[i] = 1.0 / static_cast<double>(q);
-      f64[i] = q < (1ull << 50) ? 1 : 0;
-      for (size_t k = 0; k < n; ++k) {
-        const uint64_t w = host[i].tw[k];
-        twf[i * n + k] = w > (q - 1) / 2 ? -static_cast<double>(q - w) : static_cast<double>(w);
-      }
-    }
-    // row-pass factored twiddles: for row R and row-pass stage g (global stage k = s1 + g),
-    // tw[2^k + R 2^g + iloc] = psi^(2^(logn-1-k) (1 + 2 brv_s1(R))) * psi^(2^(logn-g) brv_g(iloc))
+    // FP64 tables (csrc/ntt.hip): column-pass twiddles and the factored row-pass twiddles.
+    // For row R and row-pass stage g (global stage k = s1 + g),
+    //   tw[2^k + R 2^g + iloc] = psi^(2^(logn-1-k) (1 + 2 brv_s1(R))) * psi^(2^(logn-g) brv_g(iloc))
+    // and itw[...] is the product of the inverses of the same two factors.
     const int logn = t_.log_n, s1 = phx::ntt_split_log_s1(logn), s2 = logn - s1;
     const size_t S1 = size_t(1) << s1, S2 = size_t(1) << s2;
-    std::vector<double> ra(L * S1 * 16, 0.0), rb(L * S2, 0.0);
+    std::vector<double> qf(L), qi(L), cf(L * S1), ci(L * S1);
+    std::vector<double> raf(L * S1 * 16, 0.0), rbf(L * S2, 0.0), rai(L * S1 * 16, 0.0), rbi(L * S2, 0.0);
     auto centered = [](uint64_t w, uint64_t q) {
       return w > (q - 1) / 2 ? -static_cast<double>(q - w) : static_cast<double>(w);
     };
     for (size_t i = 0; i < L; ++i) {
-      const uint64_t q = moduli[i], psi = host[i].psi;
+      const uint64_t q = moduli[i], psi = host[i].psi, ipsi = inv_mod(psi, q);
+      qf[i] = static_cast<double>(q);
+      qi[i] = 1.0 / static_cast<double>(q);
+      for (size_t k = 0; k < S1; ++k) {
+        cf[i * S1 + k] = centered(host[i].tw[k], q);
+        uint64_t w = host[i].itw[k];
+        if (k == 1) w = mul_mod(w, host[i].n_inv, q);
+        if (k == 0) w = host[i].n_inv;
+        ci[i * S1 + k] = centered(w, q);
+      }
       for (size_t R = 0; R < S1; ++R)
         for (int g = 0; g < s2; ++g) {
           const uint64_t e = (uint64_t(1) << (logn - 1 - s1 - g)) * (1 + 2 * (uint64_t)reverse_bits((uint32_t)R, s1));
-          ra[(i * S1 + R) * 16 + g] = centered(pow_mod(psi, e, q), q);
+          raf[(i * S1 + R) * 16 + g] = centered(pow_mod(psi, e, q), q);
+          rai[(i * S1 + R) * 16 + g] = centered(pow_mod(ipsi, e, q), q);
         }
       for (int g = 0; g < s2; ++g)
         for (size_t il = 0; il < (size_t(1) << g); ++il) {
           const uint64_t e = (uint64_t(1) << (logn - g)) * (uint64_t)reverse_bits((uint32_t)il, g);
-          rb[i * S2 + (size_t(1) << g) + il] = centered(pow_mod(psi, e, q), q);
+          rbf[i * S2 + (size_t(1) << g) + il] = centered(pow_mod(psi, e, q), q);
+          rbi[i * S2 + (size_t(1) << g) + il] = centered(pow_mod(ipsi, e, q), q);
         }
     }
-    PHX_CHECK(hipMalloc(&t_.row_a, ra.size() * sizeof(double)));
-    PHX_CHECK(hipMalloc(&t_.row_b, rb.size() * sizeof(double)));
-    PHX_CHECK(hipMemcpyAsync(t_.row_a, ra.data(), ra.size() * sizeof(double), hipMemcpyHostToDevice, stream));
-    PHX_CHECK(hipMemcpyAsync(t_.row_b, rb.data(), rb.size() * sizeof(double), hipMemcpyHostToDevice, stream));
-    PHX_CHECK(hipMalloc(&t_.modulus_f, L * sizeof(double)));
-    PHX_CHECK(hipMalloc(&t_.modulus_inv, L * sizeof(double)));
-    PHX_CHECK(hipMalloc(&t_.is_f64, L));
-    PHX_CHECK(hipMalloc(&t_.twf, n * L * sizeof(double)));
-    PHX_CHECK(hipMemcpyAsync(t_.modulus_f, qf.data(), L * sizeof(double), hipMemcpyHostToDevice, stream));
-    PHX_CHECK(hipMemcpyAsync(t_.modulus_inv, qi.data(), L * sizeof(double), hipMemcpyHostToDevice, stream));
-    PHX_CHECK(hipMemcpyAsync(t_.is_f64, f64.data(), L, hipMemcpyHostToDevice, stream));
-    PHX_CHECK(hipMemcpyAsync(t_.twf, twf.data(), n * L * sizeof(double), hipMemcpyHostToDevice, stream));
+    auto up = [&](double*& dst, const std::vector<double>& src) {
+      PHX_CHECK(hipMalloc(&dst, src.size() * sizeof(double)));
+      PHX_CHECK(hipMemcpyAsync(dst, src.data(), src.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    };
+    up(t_.modulus_f, qf);
+    up(t_.modulus_inv, qi);
+    up(t_.col_fwd, cf);
+    up(t_.col_inv, ci);
+    up(t_.row_a_fwd, raf);
+    up(t_.row_b_fwd, rbf);
+    up(t_.row_a_inv, rai);
+    up(t_.row_b_inv, rbi);
     PHX_CHECK(hipStreamSynchronize(stream));
   }
   gather(t_.tw, &HostNttTable::tw);
@@ -131,8 +133,8 @@ DeviceNttTables::DeviceNttTables(size_t n, const std::vector<uint64_t>& moduli, 
 DeviceNttTables::~DeviceNttTables() {
   for (uint64_t* p : {t_.modulus, t_.barrett, t_.tw, t_.tw_shoup, t_.itw, t_.itw_shoup, t_.n_inv, t_.n_inv_shoup})
     if (p) (void)hipFree(p);
-  for (void* p : {(void*)t_.modulus_f, (void*)t_.modulus_inv, (void*)t_.is_f64, (void*)t_.twf, (void*)t_.row_a,
-                  (void*)t_.row_b})
+  for (double* p : {t_.modulus_f, t_.modulus_inv, t_.col_fwd, t_.col_inv, t_.row_a_fwd, t_.row_b_fwd, t_.row_a_inv,
+                    t_.row_b_inv})
     if (p) (void)hipFree(p);
 }
 
