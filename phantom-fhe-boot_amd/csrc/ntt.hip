@@ -315,6 +315,14 @@ __device__ __forceinline__ LimbCtx limb_ctx(const KArgs& a, int row) {
   return c;
 }
 
+// Pass outputs use write-through stores (global_store_dwordx2 sc1): the lines leave the XCD's
+// L2 at once instead of sitting dirty until the end-of-kernel write-back.  Measured on the
+// column/row pass access patterns (tools/ubench_fused.hip, profiles/r01/ubench_fused.txt):
+// -2 us per pass at [44][65536].  Plain relaxed atomic stores carry no ordering.
+__device__ __forceinline__ void store_wt(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ double centered_f64(uint64_t w, uint64_t q) {
   return w > (q >> 1) ? -u52_to_f64(q - w) : u52_to_f64(w);
 }
@@ -375,7 +383,7 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) 
           ct_round_f64<S1_LOG, R, P::col_fwd.mask>(v, w, lc.qd, lc.qinv);
         });
 #pragma unroll
-        for (int j = 0; j < E; ++j) dst[(size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2] = as_bits(v[j]);
+        for (int j = 0; j < E; ++j) store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, as_bits(v[j]));
       } else {
         double c0 = tab[0], c1 = tab[1];
         if (a.scale) {
@@ -392,8 +400,7 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) 
         });
 #pragma unroll
         for (int j = 0; j < E; ++j)
-          __builtin_nontemporal_store(f64_to_canonical(v[j], lc.qd, lc.qinv),
-                                      dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2);
+          store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, f64_to_canonical(v[j], lc.qd, lc.qinv));
       }
     } else {
       const uint64_t* tw = a.tw + (size_t)__builtin_amdgcn_readfirstlane(row) * a.n;
@@ -413,7 +420,7 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) 
       });
       if constexpr (FWD) {
 #pragma unroll
-        for (int j = 0; j < E; ++j) dst[(size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2] = v[j];  // lazy [0, 4q)
+        for (int j = 0; j < E; ++j) store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, v[j]);  // lazy [0, 4q)
       } else {
         const uint64_t ni = a.n_inv[row], nis = a.n_inv_shoup[row];
         const bool scaled = a.scale != nullptr;
@@ -422,7 +429,7 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) 
         for (int j = 0; j < E; ++j) {
           uint64_t x = mul_shoup(v[j], ni, nis, lc.q);
           if (scaled) x = mul_shoup(x, sc, scs, lc.q);
-          dst[(size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2] = x;
+          store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, x);
         }
       }
     }
@@ -498,7 +505,7 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) 
         });
         if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
 #pragma unroll
-        for (int j = 0; j < E; ++j) __builtin_nontemporal_store(f64_to_canonical(v[j], lc.qd, lc.qinv), dst + j * T);
+        for (int j = 0; j < E; ++j) store_wt(dst + j * T, f64_to_canonical(v[j], lc.qd, lc.qinv));
       } else {
         if constexpr (RN > 1) relayout<S2_LOG, 0, RN - 1>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
         static_for<RN>([&](auto rc) {
@@ -509,7 +516,7 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) 
           gs_round_f64<S2_LOG, R, P::row_inv.mask, false>(v, w, lc.qd, lc.qinv, 0.0, 0.0);
         });
 #pragma unroll
-        for (int j = 0; j < E; ++j) dst[j * T] = as_bits(v[j]);  // exact-integer doubles for the column pass
+        for (int j = 0; j < E; ++j) store_wt(dst + j * T, as_bits(v[j]));  // exact-integer doubles for the column pass
       }
     } else {
       const uint32_t B = (1u << S1_LOG) + r;
@@ -530,7 +537,7 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) 
         if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, lrow, idx, sync, t);
         const uint64_t q2 = lc.q << 1;
 #pragma unroll
-        for (int j = 0; j < E; ++j) __builtin_nontemporal_store(csub(csub(v[j], q2), lc.q), dst + j * T);
+        for (int j = 0; j < E; ++j) store_wt(dst + j * T, csub(csub(v[j], q2), lc.q));
       } else {
         if constexpr (RN > 1) relayout<S2_LOG, 0, RN - 1>(v, lrow, idx, sync, t);
         static_for<RN>([&](auto rc) {
@@ -542,7 +549,7 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) 
           gs_round_int<S2_LOG, R>(v, w, ws, lc.q);
         });
 #pragma unroll
-        for (int j = 0; j < E; ++j) dst[j * T] = v[j];  // [0, 2q), column pass follows
+        for (int j = 0; j < E; ++j) store_wt(dst + j * T, v[j]);  // [0, 2q), column pass follows
       }
     }
   }
