@@ -41,7 +41,7 @@ constexpr int E = 1 << E_LOG;
 constexpr int COLS = 16;  // columns per column-pass tile
 constexpr int BLOCK = 256;
 #ifndef PHX_NTT_WAVES_PER_EU
-#define PHX_NTT_WAVES_PER_EU 4  // __launch_bounds__ occupancy target (waves per SIMD)
+#define PHX_NTT_WAVES_PER_EU 3  // __launch_bounds__ occupancy target (waves per SIMD) of one-tile grids
 #endif
 
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
@@ -333,13 +333,52 @@ __device__ __forceinline__ uint32_t rpad(uint32_t p) { return p + (p >> 4); }
 __device__ __forceinline__ uint32_t cidx(uint32_t p, uint32_t c) { return p * COLS + c + (p >> 4) * COLS; }
 
 // ---------------------------------------------------------------------------------------
+// Launch structure.  Default (PHX_NTT_PERSIST = 0): one tile per workgroup, the grid covers
+// every tile and all of it is resident at once (2.75 waves per SIMD at [44][65536]).  Every
+// twiddle load of a tile is issued right after its data loads, so no twiddle round trip sits
+// between two butterfly rounds.  PHX_NTT_PERSIST = P > 0 builds a persistent variant instead:
+// P workgroups per CU loop over tiles and issue the NEXT tile's loads before computing the
+// current one (twiddle loads first: vector-memory loads retire in order).  Measured on MI355X
+// (profiles/r01/ntt_variants.txt) the persistent forms are slower at this size (tile counts do
+// not divide evenly over the CUs), so they stay a tuning knob.
+// ---------------------------------------------------------------------------------------
+#ifndef PHX_NTT_PERSIST
+#define PHX_NTT_PERSIST 0  // workgroups per CU (0: one tile per workgroup, grid = all tiles)
+#endif
+constexpr int kWavesPerEU = PHX_NTT_PERSIST > 0 ? PHX_NTT_PERSIST : PHX_NTT_WAVES_PER_EU;
+constexpr bool kPrefetch = PHX_NTT_PERSIST > 0;
+
+struct TileRef {
+  int buf_limb, row;
+  size_t off;  // element offset of this lane's first element
+};
+
+// ---------------------------------------------------------------------------------------
 // Column pass: tile = COLS consecutive columns x S1 rows of one limb; 256-thread workgroup.
 // Any round layout is coalesced here (16 lanes cover one 128 B row segment), so the pass loads
 // in the layout of its first round and stores from its last: RN - 1 LDS transposes.
 // FWD: first log2(S1) CT stages.  INV: last log2(S1) GS stages (n^-1 and the optional scale).
 // ---------------------------------------------------------------------------------------
+template <int S2_LOG>
+__device__ __forceinline__ TileRef col_ref(const KArgs& a, int tile, uint32_t c) {
+  constexpr int CT = (1 << S2_LOG) / COLS;
+  TileRef r;
+  resolve_limb(a.map, tile / CT, r.buf_limb, r.row);
+  r.buf_limb = __builtin_amdgcn_readfirstlane(r.buf_limb);
+  r.row = __builtin_amdgcn_readfirstlane(r.row);
+  r.off = (size_t)r.buf_limb * a.n + (tile % CT) * COLS + c;
+  return r;
+}
+
+template <int S1_LOG, int S2_LOG, int RF>
+__device__ __forceinline__ void col_load(uint64_t (&x)[E], const uint64_t* src, uint32_t pf) {
+#pragma unroll
+  for (int j = 0; j < E; ++j)
+    x[j] = __builtin_nontemporal_load(src + (size_t)(pf | Round<S1_LOG, RF>::p_elem(j)) * (1 << S2_LOG));
+}
+
 template <int S1_LOG, int S2_LOG, bool FWD>
-__global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) {
+__global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_col(KArgs a) {
   using SB = Sub<S1_LOG>;
   using P = Plan<S1_LOG, S2_LOG>;
   constexpr int T = SB::T, S2 = 1 << S2_LOG, NT = COLS * T, CT = S2 / COLS, RN = SB::ROUNDS;
@@ -356,21 +395,27 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) 
   auto sync = [] { __syncthreads(); };
   const uint32_t pf = Round<S1_LOG, RF>::p_thread(t), pl = Round<S1_LOG, RL>::p_thread(t);
 
-  {  // one tile per workgroup (grid = ntiles)
-    const int tile = blockIdx.x;
-    if (tile >= ntiles) return;
-    int buf_limb, row;
-    resolve_limb(a.map, tile / CT, buf_limb, row);
-    buf_limb = __builtin_amdgcn_readfirstlane(buf_limb);
-    const LimbCtx lc = limb_ctx(a, row);
-    const size_t off = (size_t)buf_limb * a.n + (tile % CT) * COLS + c;
-    const uint64_t* src = a.in + off;
-    uint64_t* dst = a.out + off;
+  int tile = blockIdx.x;  // workgroup-uniform
+  if (tile >= ntiles) return;
+  uint64_t xn[E];
+  col_load<S1_LOG, S2_LOG, RF>(xn, a.in + col_ref<S2_LOG>(a, tile, c).off, pf);
+  for (;;) {
+    const TileRef tr = col_ref<S2_LOG>(a, tile, c);
+    const int next = tile + gridDim.x;
+    const bool more = kPrefetch && next < ntiles;
     uint64_t x[E];
 #pragma unroll
-    for (int j = 0; j < E; ++j) x[j] = __builtin_nontemporal_load(src + (size_t)(pf | Round<S1_LOG, RF>::p_elem(j)) * S2);
+    for (int j = 0; j < E; ++j) x[j] = xn[j];
+    const LimbCtx lc = limb_ctx(a, tr.row);
+    uint64_t* dst = a.out + tr.off;
     if (lc.f64) {
-      const double* tab = a.col + (size_t)__builtin_amdgcn_readfirstlane(row) * SB::S;
+      const double* tab = a.col + (size_t)tr.row * SB::S;
+      double w[RN][E];
+      static_for<RN>([&](auto rc) {
+        constexpr int R = decltype(rc)::value;
+        load_tw<S1_LOG, R>(w[R], tab, Round<S1_LOG, R>::p_thread(t), 1);
+      });
+      if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, a.in + col_ref<S2_LOG>(a, next, c).off, pf);
       double v[E];
 #pragma unroll
       for (int j = 0; j < E; ++j) v[j] = FWD ? u52_to_f64(x[j]) : as_f64(x[j]);
@@ -378,33 +423,32 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) 
         static_for<RN>([&](auto rc) {
           constexpr int R = decltype(rc)::value;
           if constexpr (R > 0) relayout<S1_LOG, R - 1, R>(v, reinterpret_cast<double*>(lds), idx, sync, t);
-          double w[E];
-          load_tw<S1_LOG, R>(w, tab, Round<S1_LOG, R>::p_thread(t), 1);
-          ct_round_f64<S1_LOG, R, P::col_fwd.mask>(v, w, lc.qd, lc.qinv);
+          ct_round_f64<S1_LOG, R, P::col_fwd.mask>(v, w[R], lc.qd, lc.qinv);
         });
 #pragma unroll
         for (int j = 0; j < E; ++j) store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, as_bits(v[j]));
       } else {
         double c0 = tab[0], c1 = tab[1];
         if (a.scale) {
-          const double sc = centered_f64(a.scale[buf_limb], lc.q);
+          const double sc = centered_f64(a.scale[tr.buf_limb], lc.q);
           c0 = fmodmul(c0, sc, lc.qd, lc.qinv);
           c1 = fmodmul(c1, sc, lc.qd, lc.qinv);
         }
         static_for<RN>([&](auto rc) {
           constexpr int R = RN - 1 - decltype(rc)::value;
           if constexpr (R < RN - 1) relayout<S1_LOG, R + 1, R>(v, reinterpret_cast<double*>(lds), idx, sync, t);
-          double w[E];
-          load_tw<S1_LOG, R>(w, tab, Round<S1_LOG, R>::p_thread(t), 1);
-          gs_round_f64<S1_LOG, R, P::col_inv.mask, true>(v, w, lc.qd, lc.qinv, c0, c1);
+          gs_round_f64<S1_LOG, R, P::col_inv.mask, true>(v, w[R], lc.qd, lc.qinv, c0, c1);
         });
 #pragma unroll
         for (int j = 0; j < E; ++j)
           store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, f64_to_canonical(v[j], lc.qd, lc.qinv));
       }
     } else {
-      const uint64_t* tw = a.tw + (size_t)__builtin_amdgcn_readfirstlane(row) * a.n;
-      const uint64_t* tws = a.tws + (size_t)__builtin_amdgcn_readfirstlane(row) * a.n;
+      const uint64_t* tw = a.tw + (size_t)tr.row * a.n;
+      const uint64_t* tws = a.tws + (size_t)tr.row * a.n;
+      // integer path (primes >= 2^50): twiddles and Shoup quotients per round, after the
+      // prefetch (fewer registers; such tiles wait for the prefetch)
+      if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, a.in + col_ref<S2_LOG>(a, next, c).off, pf);
       uint64_t(&v)[E] = x;
       static_for<RN>([&](auto rc) {
         constexpr int R = FWD ? decltype(rc)::value : RN - 1 - decltype(rc)::value;
@@ -422,17 +466,20 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) 
 #pragma unroll
         for (int j = 0; j < E; ++j) store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, v[j]);  // lazy [0, 4q)
       } else {
-        const uint64_t ni = a.n_inv[row], nis = a.n_inv_shoup[row];
+        const uint64_t ni = a.n_inv[tr.row], nis = a.n_inv_shoup[tr.row];
         const bool scaled = a.scale != nullptr;
-        const uint64_t sc = scaled ? a.scale[buf_limb] : 0, scs = scaled ? a.scale_shoup[buf_limb] : 0;
+        const uint64_t sc = scaled ? a.scale[tr.buf_limb] : 0, scs = scaled ? a.scale_shoup[tr.buf_limb] : 0;
 #pragma unroll
         for (int j = 0; j < E; ++j) {
-          uint64_t x = mul_shoup(v[j], ni, nis, lc.q);
-          if (scaled) x = mul_shoup(x, sc, scs, lc.q);
-          store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, x);
+          uint64_t y = mul_shoup(v[j], ni, nis, lc.q);
+          if (scaled) y = mul_shoup(y, sc, scs, lc.q);
+          store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, y);
         }
       }
     }
+    if (!more) break;
+    tile = next;
+    sync();  // the next tile's first LDS writes must not overtake this tile's last reads
   }
 }
 
@@ -441,15 +488,36 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) 
 // LDS transposes are wave-private and need no workgroup barrier.  Loads and stores use the
 // round-0 layout (p = t + 16 j: 16 lanes cover one 128 B segment).
 // FWD: last log2(S2) CT stages, canonical output.  INV: first log2(S2) GS stages.
+// FP64 twiddles: tw = A_g(row) * B_g(iloc), both factors loaded (before the prefetch) and
+// multiplied after it; round 0's 15 row-uniform twiddles are made once per row through LDS.
 // ---------------------------------------------------------------------------------------
+template <int S1_LOG, int S2_LOG>
+__device__ __forceinline__ TileRef row_ref(const KArgs& a, int item, uint32_t lr, uint32_t t, uint32_t& r) {
+  constexpr int S2 = 1 << S2_LOG, RW = cmin(64 / Sub<S2_LOG>::T, 1 << S1_LOG), GROUPS = (1 << S1_LOG) / RW;
+  TileRef tr;
+  resolve_limb(a.map, item / GROUPS, tr.buf_limb, tr.row);
+  tr.buf_limb = __builtin_amdgcn_readfirstlane(tr.buf_limb);
+  tr.row = __builtin_amdgcn_readfirstlane(tr.row);
+  r = (item % GROUPS) * RW + lr;
+  tr.off = (size_t)tr.buf_limb * a.n + (size_t)r * S2 + t;
+  return tr;
+}
+
+template <int S2_LOG>
+__device__ __forceinline__ void row_load(uint64_t (&x)[E], const uint64_t* src) {
+#pragma unroll
+  for (int j = 0; j < E; ++j) x[j] = __builtin_nontemporal_load(src + j * Sub<S2_LOG>::T);
+}
+
 template <int S1_LOG, int S2_LOG, bool FWD>
-__global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) {
+__global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
   using SB = Sub<S2_LOG>;
   using P = Plan<S1_LOG, S2_LOG>;
-  constexpr int S2 = SB::S, T = SB::T, RW = cmin(64 / T, 1 << S1_LOG), RSTR = S2 + S2 / 16, RN = SB::ROUNDS;
+  constexpr int S1 = 1 << S1_LOG, S2 = SB::S, T = SB::T, RW = cmin(64 / T, S1), RSTR = S2 + S2 / 16, RN = SB::ROUNDS;
   constexpr int WAVES = BLOCK / 64;
-  constexpr int GROUPS = (1 << S1_LOG) / RW;  // row groups per limb
-  constexpr int ER0 = Round<S2_LOG, 0>::er;   // stages of round 0 (its twiddles are row-uniform)
+  constexpr int GROUPS = S1 / RW;           // row groups per limb
+  constexpr int ER0 = Round<S2_LOG, 0>::er;  // stages of round 0 (its twiddles are row-uniform)
+  constexpr int K0 = ((1 << ER0) - 1 + T - 1) / T;  // round-0 twiddles made per lane
   static_assert(Round<S2_LOG, 0>::ex == 0, "round 0 must be a full radix-16 round");
   __shared__ uint64_t lds[WAVES * RW * RSTR];
   __shared__ double tw0[WAVES * RW * 16];
@@ -459,32 +527,64 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) 
   uint64_t* lrow = lds + (wave * RW + lr) * RSTR;
   double* trow = tw0 + (wave * RW + lr) * 16;
   const int nitems = a.limbs * GROUPS;
+  const int step = gridDim.x * WAVES;
   auto idx = [](uint32_t p) { return rpad(p); };
   auto sync = [] { __builtin_amdgcn_wave_barrier(); };
 
-  {  // one item (RW rows) per wavefront (grid = nitems / WAVES)
-    const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + wave);
-    if (item >= nitems) return;  // no workgroup barrier in this kernel
-    int buf_limb, row;
-    resolve_limb(a.map, item / GROUPS, buf_limb, row);
-    buf_limb = __builtin_amdgcn_readfirstlane(buf_limb);
-    row = __builtin_amdgcn_readfirstlane(row);
-    const LimbCtx lc = limb_ctx(a, row);
-    const uint32_t r = (item % GROUPS) * RW + lr;
-    const size_t off = (size_t)buf_limb * a.n + (size_t)r * S2 + t;
-    const uint64_t* src = a.in + off;
-    uint64_t* dst = a.out + off;
+  int item = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + wave);
+  if (item >= nitems) return;  // no workgroup barrier in this kernel
+  uint32_t r;
+  uint64_t xn[E];
+  row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, item, lr, t, r).off);
+  for (;;) {
+    const TileRef tr = row_ref<S1_LOG, S2_LOG>(a, item, lr, t, r);
+    const int next = item + step;
+    const bool more = kPrefetch && next < nitems;
+    uint64_t x[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) x[j] = xn[j];
+    const LimbCtx lc = limb_ctx(a, tr.row);
+    uint64_t* dst = a.out + tr.off;
+    uint32_t rn = 0;
     if (lc.f64) {
-      const double* A = a.row_a + ((size_t)row * (1u << S1_LOG) + r) * 16;
-      const double* Bt = a.row_b + (size_t)row * S2;
-      // round-0 twiddles of this row, computed once per row: trow[e] = A[log2 e] * B[e], e < 2^ER0
-      for (int e = t + 1; e < (1 << ER0); e += T) trow[e] = fmodmul(Bt[e], A[31 - __builtin_clz(e)], lc.qd, lc.qinv);
+      const double* A = a.row_a + ((size_t)tr.row * S1 + r) * 16;
+      const double* Bt = a.row_b + (size_t)tr.row * S2;
+      // raw factors: round 0 (e = t + 1 + T k < 2^ER0) and every later round's slots
+      double b0[K0], a0[K0];
+#pragma unroll
+      for (int k = 0; k < K0; ++k) {
+        const uint32_t e = t + 1 + T * k;
+        const bool ok = e < (1u << ER0);
+        b0[k] = ok ? Bt[e] : 0.0;
+        a0[k] = ok ? A[31 - __builtin_clz(e)] : 0.0;
+      }
+      double bw[RN][E], aw[RN][E_LOG];
+      static_for<RN>([&](auto rc) {
+        constexpr int R = decltype(rc)::value;
+        if constexpr (R > 0) {
+          using Rd = Round<S2_LOG, R>;
+          const uint32_t pt = Rd::p_thread(t);
+#pragma unroll
+          for (int gl = 0; gl < Rd::er; ++gl) {
+            const int g = Rd::g0 + gl;
+            aw[R][gl] = A[g];
+#pragma unroll
+            for (int key = 0; key < (1 << (gl + Rd::ex)); ++key) {
+              const uint32_t p = pt | Rd::p_elem(key_elem<Rd::ex>(gl, key));
+              bw[R][tw_slot<Rd::ex>(gl, key)] = Bt[(1u << g) + (p >> (S2_LOG - g))];
+            }
+          }
+        }
+      });
+      if (kPrefetch && more) row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, next, lr, t, rn).off);
+#pragma unroll
+      for (int k = 0; k < K0; ++k) {
+        const uint32_t e = t + 1 + T * k;
+        if (e < (1u << ER0)) trow[e] = fmodmul(b0[k], a0[k], lc.qd, lc.qinv);
+      }
       double v[E];
 #pragma unroll
-      for (int j = 0; j < E; ++j) {
-        const uint64_t x = src[j * T];
-        v[j] = FWD ? as_f64(x) : u52_to_f64(x);
-      }
+      for (int j = 0; j < E; ++j) v[j] = FWD ? as_f64(x[j]) : u52_to_f64(x[j]);
       sync();
       auto get_tw = [&](auto rc, double (&w)[E]) {
         constexpr int R = decltype(rc)::value;
@@ -492,7 +592,14 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) 
 #pragma unroll
           for (int s = 0; s < (1 << ER0) - 1; ++s) w[s] = trow[s + 1];
         } else {
-          gen_tw_row<S2_LOG, R>(w, A, Bt, Round<S2_LOG, R>::p_thread(t), lc.qd, lc.qinv);
+          using Rd = Round<S2_LOG, R>;
+#pragma unroll
+          for (int gl = 0; gl < Rd::er; ++gl)
+#pragma unroll
+            for (int key = 0; key < (1 << (gl + Rd::ex)); ++key) {
+              const int s = tw_slot<Rd::ex>(gl, key);
+              w[s] = fmodmul(bw[R][s], aw[R][gl], lc.qd, lc.qinv);
+            }
         }
       };
       if constexpr (FWD) {
@@ -520,18 +627,21 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) 
       }
     } else {
       const uint32_t B = (1u << S1_LOG) + r;
-      const uint64_t* tw = a.tw + (size_t)row * a.n;
-      const uint64_t* tws = a.tws + (size_t)row * a.n;
-      uint64_t v[E];
-#pragma unroll
-      for (int j = 0; j < E; ++j) v[j] = src[j * T];
+      const uint64_t* tw = a.tw + (size_t)tr.row * a.n;
+      const uint64_t* tws = a.tws + (size_t)tr.row * a.n;
+      if (kPrefetch && more) row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, next, lr, t, rn).off);
+      uint64_t(&v)[E] = x;
+      auto get_tw = [&](auto rc, uint64_t (&w)[E], uint64_t (&ws)[E]) {
+        constexpr int R = decltype(rc)::value;
+        load_tw<S2_LOG, R>(w, tw, Round<S2_LOG, R>::p_thread(t), B);
+        load_tw<S2_LOG, R>(ws, tws, Round<S2_LOG, R>::p_thread(t), B);
+      };
       if constexpr (FWD) {
         static_for<RN>([&](auto rc) {
           constexpr int R = decltype(rc)::value;
           if constexpr (R > 0) relayout<S2_LOG, R - 1, R>(v, lrow, idx, sync, t);
           uint64_t w[E], ws[E];
-          load_tw<S2_LOG, R>(w, tw, Round<S2_LOG, R>::p_thread(t), B);
-          load_tw<S2_LOG, R>(ws, tws, Round<S2_LOG, R>::p_thread(t), B);
+          get_tw(rc, w, ws);
           ct_round_int<S2_LOG, R>(v, w, ws, lc.q);
         });
         if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, lrow, idx, sync, t);
@@ -544,15 +654,29 @@ __global__ __launch_bounds__(BLOCK, PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) 
           constexpr int R = RN - 1 - decltype(rc)::value;
           if constexpr (R < RN - 1) relayout<S2_LOG, R + 1, R>(v, lrow, idx, sync, t);
           uint64_t w[E], ws[E];
-          load_tw<S2_LOG, R>(w, tw, Round<S2_LOG, R>::p_thread(t), B);
-          load_tw<S2_LOG, R>(ws, tws, Round<S2_LOG, R>::p_thread(t), B);
+          get_tw(std::integral_constant<int, R>{}, w, ws);
           gs_round_int<S2_LOG, R>(v, w, ws, lc.q);
         });
 #pragma unroll
         for (int j = 0; j < E; ++j) store_wt(dst + j * T, v[j]);  // [0, 2q), column pass follows
       }
     }
+    if (!more) break;
+    item = next;
+    sync();  // trow / lrow of the next item are rewritten
   }
+}
+// compute units of the current device (cached per device id)
+int num_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cache[dev] = v;
+  }
+  return cache[dev];
 }
 
 template <int S1_LOG, int S2_LOG>
@@ -575,7 +699,10 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   constexpr int RW = cmin(64 / Sub<S2_LOG>::T, S1);
   const int col_tiles = limbs * (S2 / COLS);
   const int row_items = limbs * (S1 / RW);
-  const dim3 grid_c(col_tiles), grid_r((row_items + BLOCK / 64 - 1) / (BLOCK / 64));
+  const int row_groups = (row_items + BLOCK / 64 - 1) / (BLOCK / 64);
+  // persistent grids: at most PHX_NTT_PERSIST workgroups per CU, each loops over tiles
+  const int cap = PHX_NTT_PERSIST > 0 ? num_cus() * PHX_NTT_PERSIST : 1 << 30;
+  const dim3 grid_c(std::min(col_tiles, cap)), grid_r(std::min(row_groups, cap));
   // column tiles of small transforms need fewer than BLOCK threads (rounded up to a wavefront)
   const dim3 block_c(std::max(64, COLS * Sub<S1_LOG>::T)), block_r(BLOCK);
   if (!inverse) {

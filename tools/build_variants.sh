@@ -9,9 +9,9 @@ build() {
   make -C $d -j8 INCDIR=$ROOT/include HIPFLAGS="-std=c++20 -O3 -fPIC -Wall -ffp-contract=off -I$ROOT/include --offload-arch=gfx950 $*" > $d/build.log 2>&1
   echo built $name
 }
-build base
-build w2 -DPHX_NTT_WAVES_PER_EU=2
-build w3 -DPHX_NTT_WAVES_PER_EU=3
-build w4_g4 -DPHX_NTT_GRID_MULT=4
-build w4_pf_g4 -DPHX_NTT_PREFETCH=1 -DPHX_NTT_GRID_MULT=4
-build w2_pf_g2 -DPHX_NTT_WAVES_PER_EU=2 -DPHX_NTT_PREFETCH=1 -DPHX_NTT_GRID_MULT=2
+rm -rf $ROOT/tools/variants
+for spec in "$@"; do
+  name=${spec%%:*}; flags=${spec#*:}
+  build $name $flags &
+done
+wait

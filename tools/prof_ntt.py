@@ -7,13 +7,13 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "phantom-fhe-boot_amd", "py"))
+sys.path.insert(0, sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "phantom-fhe-boot_amd", "py"))
 import torch  # noqa: E402
 import phantom_amd as PA  # noqa: E402
 
 N, L = 1 << 16, 44
 iters = int(os.environ.get("ITERS", "30"))
-inverse = os.environ.get("INV", "0") == "1"
+inverse = os.environ.get("INV", "1") == "1"
 lib = PA.load()
 mods = PA.coeff_modulus_create(N, [60] + [50] * 44 + [60] * 15)[:L]
 t = PA.NttTables(N, mods)
