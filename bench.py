@@ -58,12 +58,67 @@ def cpu_baseline(mods, seconds=12.0):
     }
 
 
+C3_BYTES = (4 * 45 + 3 * 2 * 60 + 2 * 44) * N * 8  # 329,252,864 B
+
+
+def c3_leg(PA, lib, torch, steps=20, warmup=3):
+    """Config C3: HE multiply + relinearize + rescale at N=2^16, Q = {60, 44x50},
+    P = 15x60 (dnum 3), ciphertexts at chain index 1 (45 limbs), uniform random ciphertexts and
+    key digits (parity of these ops is bit-exact, tests/test_gpu_ckks.py).  Per-op HIP-event time
+    on the stream the kernels run on, averaged over `steps`."""
+    mods = PA.coeff_modulus_create(N, C3_BITS)
+    ctx = PA.Context(N, mods, 15)
+    ql = mods[:45]
+    rng = np.random.default_rng(0xC3)
+
+    def rand_limbs(ms, polys=1):
+        a = np.concatenate([rng.integers(0, q, size=N, dtype=np.uint64) for _ in range(polys) for q in ms])
+        return torch.from_numpy(a.view(np.int64)).cuda()
+
+    ct1, ct2 = rand_limbs(ql, 2), rand_limbs(ql, 2)
+    keys = [rand_limbs(mods, 2) for _ in range(3)]
+    kp = PA.ptr_array([k.data_ptr() for k in keys])
+    prod = torch.empty(3 * 45 * N, dtype=torch.int64, device="cuda")
+    resc = torch.empty(2 * 44 * N, dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+    ops = {
+        "multiply": lambda: lib.phantom_multiply(ctx.handle, 1, ct1.data_ptr(), ct2.data_ptr(), prod.data_ptr(), sh),
+        "relinearize": lambda: lib.phantom_relinearize(ctx.handle, 1, prod.data_ptr(), kp, 3, sh),
+        "rescale": lambda: lib.phantom_rescale_to_next(ctx.handle, 1, prod.data_ptr(), resc.data_ptr(), 2, sh),
+    }
+    for _ in range(warmup):
+        for f in ops.values():
+            PA.check(f())
+    torch.cuda.synchronize()
+    ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+          for k in ops}
+    for i in range(steps):
+        for k, f in ops.items():
+            ev[k][i][0].record(stream)
+            PA.check(f())
+            ev[k][i][1].record(stream)
+    torch.cuda.synchronize()
+    ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
+    total = sum(ms.values())
+    ctx.close()
+    achieved = C3_BYTES / (total * 1e-3) / 1e9
+    return {
+        "workload": "C3: multiply + relinearize + rescale_to_next, N=65536, 45->44 limbs, P=15, dnum=3",
+        "ms": {k: round(v, 4) for k, v in ms.items()},
+        "total_ms": round(total, 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes": C3_BYTES},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 (mult+relin+rescale) leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -159,6 +214,8 @@ def main():
                 "traffic": None,
             },
         }
+        if not args.no_c3:
+            out["c3"] = c3_leg(PA, lib, torch)
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(mods)
         print(json.dumps(out), flush=True)

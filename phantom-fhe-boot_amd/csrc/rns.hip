@@ -130,76 +130,133 @@ __global__ __launch_bounds__(kBlock) void tensor_kernel(const uint64_t* ct1, con
 }
 
 // ---------------------------------------------------------------------------------------
-// fast base conversion: one thread per coefficient pair; the [ibase][obase] matrix and the
-// per-limb constants are wave-uniform (scalar loads).
+// fast base conversion.  2-D grid: x = coefficient pairs, y = groups of kBconvJ output limbs, so
+// a [15 -> 45] conversion at n = 2^16 runs 1,152 workgroups instead of 128 (one thread per
+// coefficient pair looping over all 45 outputs left the chip at half a wave per SIMD: 88 us ->
+// 25 us per conversion on MI355X, profiles/r01/c3_*).  Each output group re-reads its ibase
+// inputs (L2/MALL hits); J = 3..15 measured within 4% of each other (tools/c3_variants.sh).
 // ---------------------------------------------------------------------------------------
 constexpr int kMaxIbase = 64;
+#ifndef PHX_BCONV_J
+#define PHX_BCONV_J 5
+#endif
+constexpr int kBconvJ = PHX_BCONV_J;
 
-template <bool PRESCALE>
-__global__ __launch_bounds__(kBlock) void bconv_kernel(BconvArgs a, uint32_t n, uint32_t pairs_per_limb) {
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < pairs_per_limb; i += gridDim.x * kBlock) {
-    const uint32_t k = 2 * i;
-    uint64_t tx[kMaxIbase], ty[kMaxIbase];
-    const int ib = a.ibase_size;
+__device__ __forceinline__ void bconv_outputs(const BconvArgs& a, const uint64_t* tx, const uint64_t* ty, int ib,
+                                              uint32_t n, uint32_t k) {
+  const int j0 = blockIdx.y * kBconvJ, j1 = min(j0 + kBconvJ, a.obase_size);
+  for (int j = j0; j < j1; ++j) {
+    u128 accx{0, 0}, accy{0, 0};
+    const uint64_t p = a.obase[j], r0 = a.obase_barrett[2 * j], r1 = a.obase_barrett[2 * j + 1];
     for (int s = 0; s < ib; ++s) {
-      const u64x2 x = ld2(a.in + (size_t)s * n + k);
-      if constexpr (PRESCALE) {
-        const uint64_t q = a.ibase[s], w = a.qhat_inv[s], ws = a.qhat_inv_shoup[s];
-        tx[s] = mul_shoup(x.x, w, ws, q);
-        ty[s] = mul_shoup(x.y, w, ws, q);
-      } else {
-        tx[s] = x.x;
-        ty[s] = x.y;
+      const uint64_t c = a.qhat_mod_p[(size_t)s * a.obase_size + j];
+      add128(accx, mul_wide(tx[s], c));
+      add128(accy, mul_wide(ty[s], c));
+      if (s % 15 == 14 && s + 1 < ib) {  // keep the sum below p * 2^64 for the Barrett quotient
+        accx = u128{barrett_reduce_128(accx, p, r0, r1), 0};
+        accy = u128{barrett_reduce_128(accy, p, r0, r1), 0};
       }
     }
-    for (int j = 0; j < a.obase_size; ++j) {
-      u128 accx{0, 0}, accy{0, 0};
-      const uint64_t p = a.obase[j], r0 = a.obase_barrett[2 * j], r1 = a.obase_barrett[2 * j + 1];
-      for (int s = 0; s < ib; ++s) {
-        const uint64_t c = a.qhat_mod_p[(size_t)s * a.obase_size + j];
-        add128(accx, mul_wide(tx[s], c));
-        add128(accy, mul_wide(ty[s], c));
-        if (s % 15 == 14) {  // keep the sum below p * 2^64 for the Barrett quotient
-          accx = u128{barrett_reduce_128(accx, p, r0, r1), 0};
-          accy = u128{barrett_reduce_128(accy, p, r0, r1), 0};
-        }
-      }
-      const int oj = j < a.skip_at ? j : j + a.skip_len;
-      st2(a.out + (size_t)oj * n + k, barrett_reduce_128(accx, p, r0, r1), barrett_reduce_128(accy, p, r0, r1));
+    const int oj = j < a.skip_at ? j : j + a.skip_len;
+    st2(a.out + (size_t)oj * n + k, barrett_reduce_128(accx, p, r0, r1), barrett_reduce_128(accy, p, r0, r1));
+  }
+}
+
+__device__ __forceinline__ void bconv_inputs(const BconvArgs& a, uint64_t* tx, uint64_t* ty, int ib, uint32_t n,
+                                             uint32_t k, bool prescale) {
+  for (int s = 0; s < ib; ++s) {
+    const u64x2 x = ld2(a.in + (size_t)s * n + k);
+    if (prescale) {
+      const uint64_t q = a.ibase[s], w = a.qhat_inv[s], ws = a.qhat_inv_shoup[s];
+      tx[s] = mul_shoup(x.x, w, ws, q);
+      ty[s] = mul_shoup(x.y, w, ws, q);
+    } else {
+      tx[s] = x.x;
+      ty[s] = x.y;
     }
   }
 }
 
+__global__ __launch_bounds__(kBlock) void bconv_kernel(BconvArgs a, uint32_t n, uint32_t pairs, bool prescale) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= pairs) return;
+  uint64_t tx[kMaxIbase], ty[kMaxIbase];
+  bconv_inputs(a, tx, ty, a.ibase_size, n, 2 * i, prescale);
+  bconv_outputs(a, tx, ty, a.ibase_size, n, 2 * i);
+}
+
+// Fixed ibase <= 15: 30-bit limb splitting.  With t = th 2^30 + tl and c = ch 2^30 + cl (t, c <
+// 2^60), sum_s t_s c_s = HH 2^60 + (M1 + M2) 2^30 + LL where every partial sum of <= 15 products
+// of 30-bit halves stays below 2^64: 4 v_mad_u64_u32 per term and no carry chains (the 64x64
+// product + 128-bit accumulate form costs ~7 instructions per term plus register shuffles).
 template <int IB>
-__global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32_t n, uint32_t pairs_per_limb,
-                                                              bool prescale) {
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < pairs_per_limb; i += gridDim.x * kBlock) {
-    const uint32_t k = 2 * i;
-    uint64_t tx[IB], ty[IB];
+__global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32_t n, uint32_t pairs, bool prescale) {
+  static_assert(IB <= 15, "partial sums of 30-bit products must stay below 2^64");
+  constexpr uint64_t kM30 = (1ull << 30) - 1;
+  // this block's [IB][kBconvJ] slice of the matrix (split in 30-bit halves) and output moduli,
+  // staged once in LDS: the matrix may alias nothing the kernel writes, but the compiler cannot
+  // prove it, so direct reads would be vector loads inside the accumulation loop
+  __shared__ uint32_t mlo[IB][kBconvJ], mhi[IB][kBconvJ];
+  __shared__ uint64_t mp[kBconvJ][3];
+  const int j0 = blockIdx.y * kBconvJ;
+  for (int e = threadIdx.x; e < IB * kBconvJ; e += kBlock) {
+    const int sidx = e / kBconvJ, jj = e % kBconvJ;
+    const uint64_t c = j0 + jj < a.obase_size ? a.qhat_mod_p[(size_t)sidx * a.obase_size + j0 + jj] : 0;
+    mlo[sidx][jj] = static_cast<uint32_t>(c & kM30);
+    mhi[sidx][jj] = static_cast<uint32_t>(c >> 30);
+  }
+  if (threadIdx.x < kBconvJ && j0 + (int)threadIdx.x < a.obase_size) {
+    const int j = j0 + threadIdx.x;
+    mp[threadIdx.x][0] = a.obase[j];
+    mp[threadIdx.x][1] = a.obase_barrett[2 * j];
+    mp[threadIdx.x][2] = a.obase_barrett[2 * j + 1];
+  }
+  __syncthreads();
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= pairs) return;
+  uint32_t lo[2][IB], hi[2][IB];
+#pragma unroll
+  for (int s = 0; s < IB; ++s) {
+    const u64x2 x = ld2(a.in + (size_t)s * n + 2 * i);
+    uint64_t tx = x.x, ty = x.y;
+    if (prescale) {
+      const uint64_t q = a.ibase[s], w = a.qhat_inv[s], ws = a.qhat_inv_shoup[s];
+      tx = mul_shoup(tx, w, ws, q);
+      ty = mul_shoup(ty, w, ws, q);
+    }
+    lo[0][s] = static_cast<uint32_t>(tx & kM30);
+    hi[0][s] = static_cast<uint32_t>(tx >> 30);
+    lo[1][s] = static_cast<uint32_t>(ty & kM30);
+    hi[1][s] = static_cast<uint32_t>(ty >> 30);
+  }
+#pragma unroll
+  for (int jj = 0; jj < kBconvJ; ++jj) {
+    const int j = j0 + jj;
+    if (j >= a.obase_size) break;
+    uint64_t ll[2] = {0, 0}, m1[2] = {0, 0}, m2[2] = {0, 0}, hh[2] = {0, 0};
 #pragma unroll
     for (int s = 0; s < IB; ++s) {
-      const u64x2 x = ld2(a.in + (size_t)s * n + k);
-      if (prescale) {
-        const uint64_t q = a.ibase[s], w = a.qhat_inv[s], ws = a.qhat_inv_shoup[s];
-        tx[s] = mul_shoup(x.x, w, ws, q);
-        ty[s] = mul_shoup(x.y, w, ws, q);
-      } else {
-        tx[s] = x.x;
-        ty[s] = x.y;
-      }
-    }
-    for (int j = 0; j < a.obase_size; ++j) {
-      u128 accx{0, 0}, accy{0, 0};
+      const uint32_t cl = mlo[s][jj], ch = mhi[s][jj];
 #pragma unroll
-      for (int s = 0; s < IB; ++s) {
-        const uint64_t c = a.qhat_mod_p[(size_t)s * a.obase_size + j];
-        add128(accx, mul_wide(tx[s], c));
-        add128(accy, mul_wide(ty[s], c));
+      for (int e = 0; e < 2; ++e) {
+        ll[e] += static_cast<uint64_t>(lo[e][s]) * cl;
+        m1[e] += static_cast<uint64_t>(lo[e][s]) * ch;
+        m2[e] += static_cast<uint64_t>(hi[e][s]) * cl;
+        hh[e] += static_cast<uint64_t>(hi[e][s]) * ch;
       }
-      const uint64_t p = a.obase[j], r0 = a.obase_barrett[2 * j], r1 = a.obase_barrett[2 * j + 1];
-      const int oj = j < a.skip_at ? j : j + a.skip_len;
-      st2(a.out + (size_t)oj * n + k, barrett_reduce_128(accx, p, r0, r1), barrett_reduce_128(accy, p, r0, r1));
     }
+    const uint64_t p = mp[jj][0], r0 = mp[jj][1], r1 = mp[jj][2];
+    uint64_t out[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      u128 v{ll[e], 0};
+      add128(v, u128{m1[e] << 30, m1[e] >> 34});
+      add128(v, u128{m2[e] << 30, m2[e] >> 34});
+      add128(v, u128{hh[e] << 60, hh[e] >> 4});
+      out[e] = barrett_reduce_128(v, p, r0, r1);
+    }
+    const int oj = j < a.skip_at ? j : j + a.skip_len;
+    st2(a.out + (size_t)oj * n + 2 * i, out[0], out[1]);
   }
 }
 
@@ -374,7 +431,7 @@ hipError_t tensor_prod_2x2(const uint64_t* ct1, const uint64_t* ct2, uint64_t* o
 hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s) {
   if (a.ibase_size <= 0 || a.ibase_size > kMaxIbase || a.obase_size <= 0) return hipErrorInvalidValue;
   const uint32_t pairs = static_cast<uint32_t>(n / 2);
-  const int g = grid_for(pairs);
+  const dim3 g((pairs + kBlock - 1) / kBlock, (a.obase_size + kBconvJ - 1) / kBconvJ);
   const bool pre = a.qhat_inv != nullptr;
   switch (a.ibase_size) {
 #define PHX_BCONV_CASE(K) \
@@ -382,9 +439,7 @@ hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s) {
     PHX_BCONV_CASE(1) PHX_BCONV_CASE(2) PHX_BCONV_CASE(3) PHX_BCONV_CASE(4) PHX_BCONV_CASE(5)
     PHX_BCONV_CASE(6) PHX_BCONV_CASE(8) PHX_BCONV_CASE(10) PHX_BCONV_CASE(12) PHX_BCONV_CASE(15)
 #undef PHX_BCONV_CASE
-    default:
-      if (pre) bconv_kernel<true><<<g, kBlock, 0, s>>>(a, static_cast<uint32_t>(n), pairs);
-      else bconv_kernel<false><<<g, kBlock, 0, s>>>(a, static_cast<uint32_t>(n), pairs);
+    default: bconv_kernel<<<g, kBlock, 0, s>>>(a, static_cast<uint32_t>(n), pairs, pre);
   }
   return hipGetLastError();
 }

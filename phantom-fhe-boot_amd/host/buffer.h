@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
+#include <map>
+#include <mutex>
 #include <utility>
 #include <vector>
 
@@ -42,6 +44,13 @@ class DeviceBuffer {
     ptr_ = nullptr;
     count_ = 0;
   }
+  // free without touching the owning stream (which may no longer exist); the caller has
+  // synchronised the device
+  void release_sync() {
+    if (ptr_) (void)hipFree(ptr_);
+    ptr_ = nullptr;
+    count_ = 0;
+  }
   // setup-path upload: waits for the copy so the host source may be a temporary
   void upload(const T* host, size_t count, hipStream_t stream) {
     allocate(count, stream);
@@ -74,6 +83,33 @@ class DeviceBuffer {
   T* ptr_ = nullptr;
   size_t count_ = 0;
   hipStream_t stream_ = nullptr;
+};
+
+// Scratch buffers reused across calls, one set per stream (the reference allocates its
+// key-switch and rescale temporaries on every call, e.g. src/eval_key_switch.cu:150-160).
+// A buffer only grows; the old one is freed stream-ordered on the stream that used it.
+// Buffers of one stream are used in that stream's order, so reuse needs no synchronisation.
+class Workspace {
+ public:
+  Workspace() = default;
+  Workspace(const Workspace&) = delete;
+  Workspace& operator=(const Workspace&) = delete;
+  ~Workspace() {
+    (void)hipDeviceSynchronize();
+    for (auto& kv : bufs_)
+      for (auto& b : kv.second) b.release_sync();
+  }
+  enum Slot : int { kModupInv = 0, kModdownDelta, kRescaleLast, kRescaleTmp, kKsModup, kKsCx, kSlots };
+  uint64_t* get(hipStream_t s, Slot slot, size_t count) {
+    std::lock_guard<std::mutex> lk(mu_);
+    DeviceBuffer<uint64_t>& b = bufs_[s][slot];
+    if (b.size() < count) b.allocate(count, s);
+    return b.get();
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<hipStream_t, DeviceBuffer<uint64_t>[kSlots]> bufs_;
 };
 
 }  // namespace phantom

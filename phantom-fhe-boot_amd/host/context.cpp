@@ -27,6 +27,7 @@ PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t s
     (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &threshold);
   }
 
+  ws_ = std::make_unique<Workspace>();
   ntt_ = std::make_unique<DeviceNttTables>(n_, qp_, stream_);
   data_.push_back(std::make_unique<ContextData>(0, qp_));
   for (size_t c = 1; c <= size_Q_; ++c) {
@@ -52,7 +53,10 @@ PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t s
     for (auto& e : errs)
       if (e) std::rethrow_exception(e);
   }
-  for (size_t c = 1; c <= size_Q_; ++c) data_[c]->set_rns_tool(std::move(tools[c]));
+  for (size_t c = 1; c <= size_Q_; ++c) {
+    tools[c]->set_workspace(ws_.get());
+    data_[c]->set_rns_tool(std::move(tools[c]));
+  }
   PHX_CHECK(hipStreamSynchronize(stream_));
 }
 

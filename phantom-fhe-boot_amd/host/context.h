@@ -80,11 +80,13 @@ class PhantomContext {
   const phx::NttTables& gpu_rns_tables() const { return ntt_->get(); }
   phx::ModView mod_QP() const { return {ntt_->get().modulus, ntt_->get().barrett}; }
   hipStream_t stream() const { return stream_; }
+  Workspace& workspace() const { return *ws_; }
 
  private:
   EncryptionParameters params_;
   size_t n_ = 0, size_Q_ = 0, size_P_ = 0;
   std::vector<uint64_t> qp_;
+  std::unique_ptr<Workspace> ws_;  // declared before the tools that point into it
   std::unique_ptr<DeviceNttTables> ntt_;
   std::vector<std::unique_ptr<ContextData>> data_;
   hipStream_t stream_;

@@ -22,15 +22,14 @@ void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, 
   // levelsDropped = chain_index - 1 (src/eval_key_switch.cu:145-148)
   const RnsTool& rt = ctx.get_context_data(chain_index).gpu_rns_tool();
   const size_t size_Ql = rt.size_Ql(), size_QlP = size_Ql + ctx.size_P(), beta = rt.beta();
-  DeviceBuffer<uint64_t> t_mod_up(beta * size_QlP * n, s);
-  rt.modup(t_mod_up.get(), c2, ctx.gpu_rns_tables(), s);
-  DeviceBuffer<uint64_t> cx(2 * size_QlP * n, s);
-  hip_ok(phx::keyswitch_inner_prod(t_mod_up.get(), evk, cx.get(), ctx.mod_QP().q, ctx.mod_QP().barrett, n, size_Ql,
+  uint64_t* t_mod_up = rt.workspace().get(s, Workspace::kKsModup, beta * size_QlP * n);
+  rt.modup(t_mod_up, c2, ctx.gpu_rns_tables(), s);
+  uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * size_QlP * n);
+  hip_ok(phx::keyswitch_inner_prod(t_mod_up, evk, cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, size_Ql,
                                    ctx.size_Q(), ctx.size_P(), beta, s),
          "keyswitch inner product");
-  t_mod_up.release();
   for (size_t i = 0; i < 2; ++i)
-    rt.moddown_add(ct + i * size_Ql * n, cx.get() + i * size_QlP * n, true, ctx.gpu_rns_tables(), s);
+    rt.moddown_add(ct + i * size_Ql * n, cx + i * size_QlP * n, true, ctx.gpu_rns_tables(), s);
 }
 
 void keyswitch_inplace(const PhantomContext& ctx, PhantomCiphertext& ct, const uint64_t* c2,

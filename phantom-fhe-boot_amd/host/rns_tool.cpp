@@ -125,16 +125,16 @@ static void hip_ok(hipError_t e, const char* what) {
 
 void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables& ntt, hipStream_t s) const {
   const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_, alpha = size_P_;
-  DeviceBuffer<uint64_t> t_cks(size_Ql * n_, s);
+  uint64_t* t_cks = ws_->get(s, Workspace::kModupInv, size_Ql * n_);
   // INTT(c2) * partQlHatInv (nwt_2d_radix8_backward_scale)
-  hip_ok(phx::ntt_inverse(ntt, c2, t_cks.get(), phx::LimbMap::contiguous((int)size_Ql, 0), d_partQlHatInv_.get(),
+  hip_ok(phx::ntt_inverse(ntt, c2, t_cks, phx::LimbMap::contiguous((int)size_Ql, 0), d_partQlHatInv_.get(),
                           d_partQlHatInv_shoup_.get(), s),
          "modup INTT");
   hip_ok(phx::modup_copy_digits(c2, t_mod_up, n_, size_Ql, size_QlP, alpha, s), "modup copy");
   for (size_t b = 0; b < converters_.size(); ++b) {
     const size_t start = digit_start_[b], part = digit_size_[b];
     uint64_t* dst = t_mod_up + b * size_QlP * n_;
-    phx::BconvArgs a = converters_[b].args(t_cks.get() + start * n_, dst, false);
+    phx::BconvArgs a = converters_[b].args(t_cks + start * n_, dst, false);
     a.skip_at = (int)start;
     a.skip_len = (int)part;
     hip_ok(phx::bconv(a, n_, s), "modup bconv");
@@ -160,11 +160,10 @@ void RnsTool::moddown_add(uint64_t* ct_i, uint64_t* cx_i, bool accumulate, const
   pm.first_a = 0;
   pm.first_b = (int)size_Q_;
   hip_ok(phx::ntt_inverse(ntt, cp, cp, pm, nullptr, nullptr, s), "moddown INTT(P)");
-  DeviceBuffer<uint64_t> delta(size_Ql * n_, s);
-  hip_ok(phx::bconv(p_to_ql_.args(cp, delta.get(), true), n_, s), "moddown bconv");
-  hip_ok(phx::ntt_forward(ntt, delta.get(), delta.get(), phx::LimbMap::contiguous((int)size_Ql, 0), s),
-         "moddown NTT");
-  hip_ok(phx::moddown_finish(ct_i, cx_i, delta.get(), d_bigPInv_mod_q_.get(), d_bigPInv_mod_q_shoup_.get(),
+  uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, size_Ql * n_);
+  hip_ok(phx::bconv(p_to_ql_.args(cp, delta, true), n_, s), "moddown bconv");
+  hip_ok(phx::ntt_forward(ntt, delta, delta, phx::LimbMap::contiguous((int)size_Ql, 0), s), "moddown NTT");
+  hip_ok(phx::moddown_finish(ct_i, cx_i, delta, d_bigPInv_mod_q_.get(), d_bigPInv_mod_q_shoup_.get(),
                              d_Ql_.get(), n_, size_Ql, accumulate, s),
          "moddown finish");
 }
@@ -174,16 +173,17 @@ void RnsTool::rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const
   const size_t L = base_Ql_.size();
   if (L < 2) throw std::invalid_argument("end of modulus switching chain reached");
   const size_t Ln = L - 1;
-  DeviceBuffer<uint64_t> last(n_, s), tmp(Ln * n_, s);
+  uint64_t* last = ws_->get(s, Workspace::kRescaleLast, n_);
+  uint64_t* tmp = ws_->get(s, Workspace::kRescaleTmp, Ln * n_);
   for (size_t c = 0; c < polys; ++c) {
     const uint64_t* ci = in + c * L * n_;
     uint64_t* co = out + c * Ln * n_;
-    hip_ok(phx::ntt_inverse(ntt, ci + Ln * n_, last.get(), phx::LimbMap::contiguous(1, (int)Ln), nullptr, nullptr, s),
+    hip_ok(phx::ntt_inverse(ntt, ci + Ln * n_, last, phx::LimbMap::contiguous(1, (int)Ln), nullptr, nullptr, s),
            "rescale INTT(last)");
-    hip_ok(phx::rescale_spread_last(last.get(), tmp.get(), d_Ql_.get(), d_Ql_barrett_.get(), n_, Ln, s),
+    hip_ok(phx::rescale_spread_last(last, tmp, d_Ql_.get(), d_Ql_barrett_.get(), n_, Ln, s),
            "rescale spread");
-    hip_ok(phx::ntt_forward(ntt, tmp.get(), tmp.get(), phx::LimbMap::contiguous((int)Ln, 0), s), "rescale NTT");
-    hip_ok(phx::rescale_finish(ci, tmp.get(), co, d_inv_qlast_.get(), d_inv_qlast_shoup_.get(), d_Ql_.get(), n_, Ln,
+    hip_ok(phx::ntt_forward(ntt, tmp, tmp, phx::LimbMap::contiguous((int)Ln, 0), s), "rescale NTT");
+    hip_ok(phx::rescale_finish(ci, tmp, co, d_inv_qlast_.get(), d_inv_qlast_shoup_.get(), d_Ql_.get(), n_, Ln,
                                s),
            "rescale finish");
   }

@@ -49,6 +49,10 @@ class RnsTool {
   void rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const phx::NttTables& ntt,
                    hipStream_t s) const;
 
+  // scratch space shared by the drivers (owned by the PhantomContext)
+  void set_workspace(Workspace* ws) { ws_ = ws; }
+  Workspace& workspace() const { return *ws_; }
+
   // device views over Ql
   phx::ModView mod_Ql() const { return {d_Ql_.get(), d_Ql_barrett_.get()}; }
   const uint64_t* bigP_mod_q() const { return d_bigP_mod_q_.get(); }
@@ -56,6 +60,7 @@ class RnsTool {
 
  private:
   size_t n_, size_Q_, size_P_;
+  Workspace* ws_ = nullptr;
   std::vector<uint64_t> base_Ql_, base_P_;
   DeviceBuffer<uint64_t> d_Ql_, d_Ql_barrett_;
   // key switching

@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libphantom_amd.so")
+# PHANTOM_AMD_LIB: load another build of the same library (tools/build_variants.sh experiments)
+LIB_PATH = os.environ.get("PHANTOM_AMD_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libphantom_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "phantom_amd.h")
 
 u64p = ctypes.POINTER(ctypes.c_uint64)
