@@ -1,0 +1,488 @@
+#include "bootstrap.h"
+
+#include <algorithm>
+#include <cmath>
+#include <stdexcept>
+#include <thread>
+
+#include "../csrc/rns.h"
+#include "evaluate.h"
+#include "numth.h"
+
+namespace phantom {
+
+static void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw hip_error(e, what);
+}
+
+// ======================================================================================
+// host-side math
+// ======================================================================================
+namespace boot {
+
+static std::complex<double> root_of_unity(uint64_t e, uint64_t M) {
+  const double a = 2.0 * M_PI * static_cast<double>(e % M) / static_cast<double>(M);
+  return {std::cos(a), std::sin(a)};
+}
+
+DiagMap stage(size_t n, int s, bool inverse) {
+  const size_t m = size_t(1) << s, h = m / 2, M = 4 * n;
+  if (m > n) throw std::invalid_argument("stage out of range");
+  std::vector<uint64_t> pw(h);  // 5^j mod 4m
+  uint64_t p5 = 1;
+  for (size_t j = 0; j < h; ++j) {
+    pw[j] = p5;
+    p5 = p5 * 5 % (4 * m);
+  }
+  cvec d0(n), dp(n), dm(n);
+  for (size_t p = 0; p < n; ++p) {
+    const size_t j = p % m;
+    if (j < h) {
+      const std::complex<double> t = root_of_unity((n / m) * pw[j], M);
+      d0[p] = inverse ? 0.5 : 1.0;
+      dp[p] = inverse ? std::complex<double>(0.5) : t;
+    } else {
+      const std::complex<double> t = root_of_unity((n / m) * pw[j - h], M);
+      if (inverse) {
+        dm[p] = std::conj(t) * 0.5;
+        d0[p] = -std::conj(t) * 0.5;
+      } else {
+        d0[p] = -t;
+        dm[p] = 1.0;
+      }
+    }
+  }
+  DiagMap d;
+  auto add = [&](int a, const cvec& v) {
+    auto it = d.find(a);
+    if (it == d.end()) {
+      d.emplace(a, v);
+    } else {
+      for (size_t i = 0; i < n; ++i) it->second[i] += v[i];
+    }
+  };
+  add(0, d0);
+  add(static_cast<int>(h % n), dp);
+  add(static_cast<int>((n - h) % n), dm);
+  return d;
+}
+
+DiagMap compose(const DiagMap& A, const DiagMap& B, size_t n) {
+  DiagMap out;
+  for (const auto& [a, alpha] : A)
+    for (const auto& [b, beta] : B) {
+      const int key = static_cast<int>((static_cast<size_t>(a) + static_cast<size_t>(b)) % n);
+      cvec& dst = out[key];
+      if (dst.empty()) dst.assign(n, {0.0, 0.0});
+      for (size_t p = 0; p < n; ++p) dst[p] += alpha[p] * beta[(p + a) % n];
+    }
+  return out;
+}
+
+cvec apply(const DiagMap& T, const cvec& v) {
+  const size_t n = v.size();
+  cvec out(n, {0.0, 0.0});
+  for (const auto& [a, d] : T)
+    for (size_t p = 0; p < n; ++p) out[p] += d[p] * v[(p + a) % n];
+  return out;
+}
+
+std::vector<double> chebyshev_coefficients(double (*f)(double, const double*), const double* args, int degree) {
+  const int n = degree + 1;
+  std::vector<double> fx(n), c(n, 0.0);
+  for (int j = 0; j < n; ++j) fx[j] = f(std::cos(M_PI * (j + 0.5) / n), args);
+  for (int k = 0; k < n; ++k) {
+    double acc = 0.0;
+    for (int j = 0; j < n; ++j) acc += fx[j] * std::cos(M_PI * k * (j + 0.5) / n);
+    c[k] = 2.0 * acc / n;
+  }
+  c[0] *= 0.5;
+  return c;
+}
+
+double scaled_cosine(double y, const double* args) {
+  const double K = args[0], r = args[1], two_r = std::pow(2.0, r);
+  return std::pow(2.0 * M_PI, -1.0 / two_r) * std::cos(2.0 * M_PI * (K * y - 0.25) / two_r);
+}
+
+}  // namespace boot
+
+// ======================================================================================
+// Chebyshev evaluation: p = q T_m + r recursion down to degree < 16 leaves
+// ======================================================================================
+namespace {
+
+constexpr int kLeafDegree = 15;
+
+int ceil_log2(int x) {
+  int r = 0;
+  while ((1 << r) < x) ++r;
+  return r;
+}
+
+// depth (levels consumed) of evaluating a degree-d series with the recursion below
+int cheb_depth(int d) {
+  if (d <= kLeafDegree) return (d <= 1 ? 0 : ceil_log2(d)) + 1;
+  int m = 1;
+  while (2 * m <= d) m *= 2;
+  return std::max(std::max(cheb_depth(d - m), ceil_log2(m)) + 1, cheb_depth(m - 1));
+}
+
+struct ChebEvaluator {
+  const PhantomContext& cc;
+  const PhantomRelinKey& rlk;
+  const std::vector<double>& sf;
+  std::map<int, PhantomCiphertext> T;
+
+  const PhantomCiphertext& get(int i) {
+    auto it = T.find(i);
+    if (it != T.end()) return it->second;
+    PhantomCiphertext r;
+    int a = 1;
+    while (2 * a < i) a *= 2;  // a >= i / 2, a < i
+    if (2 * a == i) {
+      // T_2a = 2 T_a^2 - 1
+      const PhantomCiphertext& ta = get(a);
+      r = EvalMultRescale(cc, ta, ta, rlk, sf);
+      add_inplace(cc, r, r);
+      EvalAddConstInplace(cc, r, -1.0);
+    } else {
+      // T_i = 2 T_a T_(i-a) - T_(2a-i)
+      const PhantomCiphertext& ta = get(a);
+      const PhantomCiphertext& tb = get(i - a);
+      r = EvalMultRescale(cc, ta, tb, rlk, sf);
+      add_inplace(cc, r, r);
+      EvalSubAutoInplace(cc, r, get(2 * a - i), sf);
+    }
+    return T.emplace(i, std::move(r)).first->second;
+  }
+
+  // sum_i c_i T_i for deg < 16: every term lands on the deepest level with scale sf[l]^2 and
+  // one rescale finishes the linear combination
+  PhantomCiphertext leaf(const std::vector<double>& c) {
+    int d = static_cast<int>(c.size()) - 1;
+    while (d > 0 && c[d] == 0.0) --d;
+    size_t lvl = level_of(get(1));
+    for (int i = 1; i <= d; ++i) lvl = std::max(lvl, level_of(get(i)));
+    const double target = sf.at(lvl) * sf.at(lvl);
+    PhantomCiphertext acc;
+    bool have = false;
+    for (int i = 1; i <= d; ++i) {
+      if (c[i] == 0.0) continue;
+      PhantomCiphertext t = get(i);
+      if (level_of(t) < lvl) mod_switch_to_inplace(cc, t, lvl + 1);
+      mult_by_real_integer_inplace(cc, t, c[i] * target / t.scale());
+      t.set_scale(target);
+      t.SetNoiseScaleDeg(2);
+      if (!have) {
+        acc = std::move(t);
+        have = true;
+      } else {
+        add_inplace(cc, acc, t);
+      }
+    }
+    if (!have) throw std::invalid_argument("constant Chebyshev leaf");
+    EvalAddConstInplace(cc, acc, c[0]);
+    EvalModReduceInPlace(cc, acc, 1);
+    return acc;
+  }
+
+  PhantomCiphertext eval(const std::vector<double>& c) {
+    const int d = static_cast<int>(c.size()) - 1;
+    if (d <= kLeafDegree) return leaf(c);
+    int m = 1;
+    while (2 * m <= d) m *= 2;
+    // c_i T_i = c_i (2 T_m T_(i-m) - T_(2m-i)) for m < i <= d; i = m gives T_m T_0
+    std::vector<double> q(d - m + 1, 0.0), r(c.begin(), c.begin() + m);
+    q[0] = c[m];
+    for (int i = m + 1; i <= d; ++i) {
+      q[i - m] = 2.0 * c[i];
+      r[2 * m - i] -= c[i];
+    }
+    PhantomCiphertext qv = eval(q);
+    PhantomCiphertext res = EvalMultRescale(cc, qv, get(m), rlk, sf);
+    PhantomCiphertext rv = eval(r);
+    EvalAddAutoInplace(cc, res, rv, sf);
+    return res;
+  }
+};
+
+}  // namespace
+
+// ======================================================================================
+// FHECKKSRNS
+// ======================================================================================
+
+uint32_t FHECKKSRNS::GetBootstrapDepth(const std::vector<uint32_t>& levelBudget) {
+  return levelBudget.at(0) + levelBudget.at(1) + static_cast<uint32_t>(cheb_depth(kChebDegree)) + R_UNIFORM;
+}
+
+void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const std::vector<int>& sizes,
+                              double constant, size_t first_chain, std::vector<LTLevel>& out) const {
+  const size_t n = cc.poly_degree() / 2;
+  const int logslots = arith::log2_exact(n);
+  std::vector<int> order;
+  for (int s = 1; s <= logslots; ++s) order.push_back(s);
+  if (encode_dir) std::reverse(order.begin(), order.end());
+  out.clear();
+  size_t idx = 0;
+  for (size_t gi = 0; gi < sizes.size(); ++gi) {
+    boot::DiagMap T;
+    T.emplace(0, boot::cvec(n, {1.0, 0.0}));
+    int s_min = logslots;
+    for (int t = 0; t < sizes[gi]; ++t) {
+      const int s = order[idx++];
+      s_min = std::min(s_min, s);
+      T = boot::compose(boot::stage(n, s, encode_dir), T, n);
+    }
+    const bool scale_here = encode_dir ? gi == 0 : gi + 1 == sizes.size();
+    if (scale_here)
+      for (auto& kv : T)
+        for (auto& x : kv.second) x *= constant;
+    LTLevel lv;
+    lv.stride = 1 << (s_min - 1);
+    int kmin = 0, kmax = 0;
+    for (const auto& kv : T) {
+      int a = kv.first;
+      if (a > static_cast<int>(n / 2)) a -= static_cast<int>(n);
+      if (a % lv.stride) throw std::logic_error("diagonal offset not a multiple of the stride");
+      kmin = std::min(kmin, a / lv.stride);
+      kmax = std::max(kmax, a / lv.stride);
+    }
+    lv.center = -kmin;
+    lv.D = kmax - kmin + 1;
+    lv.g = 1;
+    while (lv.g * lv.g < lv.D) lv.g *= 2;
+    lv.b = (lv.D + lv.g - 1) / lv.g;
+    lv.chain = first_chain + gi;
+    const double scale = sf_.at(lv.chain - 1);
+    lv.pts.resize(lv.D);
+    for (int u = 0; u < lv.D; ++u) {
+      const long off = static_cast<long>(u - lv.center) * lv.stride;
+      const int key = static_cast<int>(((off % static_cast<long>(n)) + static_cast<long>(n)) % static_cast<long>(n));
+      auto it = T.find(key);
+      if (it == T.end()) continue;
+      // pre-rotate by -(g i stride) so the giant rotation can follow the inner sum
+      const size_t sh = static_cast<size_t>((u / lv.g) * lv.g) * lv.stride % n;
+      boot::cvec rot(n);
+      for (size_t p = 0; p < n; ++p) rot[p] = it->second[(p + n - sh) % n];
+      auto pt = std::make_unique<PhantomPlaintext>();
+      encoder_.encode_ext(cc, rot, scale, *pt, lv.chain);
+      lv.pts[u] = std::move(pt);
+    }
+    out.push_back(std::move(lv));
+  }
+}
+
+void FHECKKSRNS::EvalBootstrapSetup(const PhantomContext& cc, const std::vector<uint32_t>& levelBudget, double scale,
+                                    const std::vector<double>& sf, uint32_t correctionFactor) {
+  (void)scale;
+  sf_ = sf;
+  budget_ = levelBudget;
+  const size_t N = cc.poly_degree(), slots = N / 2;
+  const int logslots = arith::log2_exact(slots);
+  if (correctionFactor == 0) {
+    const double tmp = std::round(-0.265 * (2 * std::log2(static_cast<double>(N)) + std::log2(static_cast<double>(slots))) + 19.1);
+    correction_ = static_cast<uint32_t>(std::clamp(tmp, 7.0, 13.0));
+  } else {
+    correction_ = correctionFactor;
+  }
+  auto split = [&](uint32_t budget) {
+    budget = std::clamp<uint32_t>(budget, 1, static_cast<uint32_t>(logslots));
+    std::vector<int> sz(budget, logslots / static_cast<int>(budget));
+    for (int i = 0; i < logslots % static_cast<int>(budget); ++i) ++sz[i];
+    return sz;
+  };
+  const double q0 = static_cast<double>(cc.key_moduli()[0]);
+  const std::vector<int> enc_sizes = split(levelBudget.at(0));
+  std::vector<int> dec_sizes = split(levelBudget.at(1));
+  std::reverse(dec_sizes.begin(), dec_sizes.end());
+  const size_t depth_enc = enc_sizes.size(), depth_dec = dec_sizes.size();
+  const size_t depth_mod = static_cast<size_t>(cheb_depth(kChebDegree)) + R_UNIFORM;
+  if (1 + depth_enc + depth_mod + depth_dec > cc.size_Q())
+    throw std::invalid_argument("not enough levels in the modulus chain for bootstrapping");
+  // CoeffToSlot: slots become (t_lo + i t_hi) / (2 q0 K) (the conjugate split doubles them)
+  build_levels(cc, true, enc_sizes, sf_.at(0) / (2.0 * q0 * K_UNIFORM), 1, enc_);
+  // SlotToCoeff: from (t0_lo + i t0_hi) / q0 back to the message at the raise scale sf[0]
+  build_levels(cc, false, dec_sizes, q0 / sf_.at(0), 1 + depth_enc + depth_mod, dec_);
+  const double args[2] = {static_cast<double>(K_UNIFORM), static_cast<double>(R_UNIFORM)};
+  cheb_ = boot::chebyshev_coefficients(boot::scaled_cosine, args, kChebDegree);
+}
+
+std::vector<int> FHECKKSRNS::rotation_indices() const {
+  std::vector<int> r;
+  const int n = static_cast<int>(encoder_.slot_count());
+  auto add = [&](long x) {
+    const int v = static_cast<int>(((x % n) + n) % n);
+    if (v != 0 && std::find(r.begin(), r.end(), v) == r.end()) r.push_back(v);
+  };
+  for (const auto* lvs : {&enc_, &dec_})
+    for (const LTLevel& lv : *lvs) {
+      for (int j = 0; j < lv.g; ++j) add(static_cast<long>(j - lv.center) * lv.stride);
+      for (int i = 1; i < lv.b; ++i) add(static_cast<long>(lv.g) * i * lv.stride);
+    }
+  return r;
+}
+
+void FHECKKSRNS::EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext& cc) {
+  std::vector<uint32_t> elts;
+  for (int r : rotation_indices()) elts.push_back(FindAutomorphismIndex2nComplex(r, cc.poly_degree()));
+  elts.push_back(static_cast<uint32_t>(2 * cc.poly_degree() - 1));  // conjugation
+  galois_keys_ = sk.create_galois_keys_fused(cc, elts);
+}
+
+void FHECKKSRNS::EvalMultKeyGen(PhantomSecretKey& sk, const PhantomContext& cc) { mul_key_ = sk.gen_relinkey(cc); }
+
+// out (+)= a * b over Ql u P (extended-basis operands, `polys` polynomials of a, one of b)
+static void ext_mul_acc(const PhantomContext& cc, size_t Ql, const uint64_t* a, const uint64_t* b, uint64_t* out,
+                        bool accumulate) {
+  const size_t n = cc.poly_degree(), P = cc.size_P(), QlP = Ql + P;
+  hipStream_t s = cc.stream();
+  const phx::ModView mq = cc.mod_QP();
+  const phx::ModView mp{mq.q + cc.size_Q(), mq.barrett + 2 * cc.size_Q()};
+  for (size_t i = 0; i < 2; ++i) {
+    const uint64_t* x = a + i * QlP * n;
+    uint64_t* o = out + i * QlP * n;
+    if (accumulate) {
+      hip_ok(phx::poly_mul_add(x, b, o, o, mq, n, Ql, s), "lt mul-add Ql");
+      hip_ok(phx::poly_mul_add(x + Ql * n, b + Ql * n, o + Ql * n, o + Ql * n, mp, n, P, s), "lt mul-add P");
+    } else {
+      hip_ok(phx::poly_mul(x, b, o, mq, n, Ql, s), "lt mul Ql");
+      hip_ok(phx::poly_mul(x + Ql * n, b + Ql * n, o + Ql * n, mp, n, P, s), "lt mul P");
+    }
+  }
+}
+
+PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const PhantomCiphertext& in,
+                                          const LTLevel& lv) const {
+  PhantomCiphertext ct = in;
+  if (ct.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, ct, 1);
+  if (ct.chain_index() != lv.chain) AdjustToLevel(cc, ct, lv.chain - 1, sf_);
+  const size_t n = cc.poly_degree(), Ql = cc.get_context_data(ct.chain_index()).coeff_modulus_size();
+  const size_t QlP = Ql + cc.size_P();
+  hipStream_t s = cc.stream();
+  DeviceBuffer<uint64_t> digits = EvalFastRotationPrecompute(cc, ct);
+  std::vector<PhantomCiphertext> baby(lv.g);
+  for (int j = 0; j < lv.g; ++j) {
+    const long r = static_cast<long>(j - lv.center) * lv.stride;
+    const long nn = static_cast<long>(n / 2);
+    if (((r % nn) + nn) % nn == 0)
+      baby[j] = KeySwitchExt(cc, ct);
+    else
+      baby[j] = EvalFastRotationExt(cc, ct, galois_keys_, static_cast<int>(r), digits.get(), true);
+  }
+  digits.release();
+  PhantomCiphertext acc, inner;
+  bool have_acc = false;
+  for (int i = 0; i < lv.b; ++i) {
+    bool have_inner = false;
+    for (int j = 0; j < lv.g; ++j) {
+      const int u = lv.g * i + j;
+      if (u >= lv.D || !lv.pts[u]) continue;
+      if (!have_inner) {
+        inner.resize(2, QlP, n, s, false);
+        inner.set_chain_index(ct.chain_index());
+      }
+      ext_mul_acc(cc, Ql, baby[j].data(), lv.pts[u]->data(), inner.data(), have_inner);
+      have_inner = true;
+    }
+    if (!have_inner) continue;
+    inner.set_scale(ct.scale() * sf_.at(lv.chain - 1));
+    inner.SetNoiseScaleDeg(2);
+    if (i == 0) {
+      acc = std::move(inner);
+      have_acc = true;
+      continue;
+    }
+    PhantomCiphertext down = KeySwitchDown(cc, inner);
+    DeviceBuffer<uint64_t> d2 = EvalFastRotationPrecompute(cc, down);
+    PhantomCiphertext rot =
+        EvalFastRotationExt(cc, down, galois_keys_, static_cast<int>(static_cast<long>(lv.g) * i * lv.stride), d2.get(), true);
+    if (!have_acc) {
+      acc = std::move(rot);
+      have_acc = true;
+    } else {
+      EvalAddExtInPlace(cc, acc, rot);
+    }
+  }
+  PhantomCiphertext res = KeySwitchDown(cc, acc);
+  res.set_scale(ct.scale() * sf_.at(lv.chain - 1));
+  res.SetNoiseScaleDeg(2);
+  EvalModReduceInPlace(cc, res, 1);
+  return res;
+}
+
+PhantomCiphertext FHECKKSRNS::EvalCoeffsToSlots(const PhantomCiphertext& ct, const PhantomContext& cc) const {
+  PhantomCiphertext r = ct;
+  for (const LTLevel& lv : enc_) r = apply_level(cc, r, lv);
+  return r;
+}
+
+PhantomCiphertext FHECKKSRNS::EvalSlotsToCoeffs(const PhantomCiphertext& ct, const PhantomContext& cc) const {
+  PhantomCiphertext r = ct;
+  for (const LTLevel& lv : dec_) r = apply_level(cc, r, lv);
+  return r;
+}
+
+PhantomCiphertext FHECKKSRNS::EvalChebyshevSeries(const PhantomCiphertext& ct, const PhantomContext& cc,
+                                                  const std::vector<double>& coeffs) const {
+  ChebEvaluator ev{cc, mul_key_, sf_, {}};
+  PhantomCiphertext x = ct;
+  if (x.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, x, 1);
+  ev.T.emplace(1, std::move(x));
+  return ev.eval(coeffs);
+}
+
+void FHECKKSRNS::ApplyDoubleAngleIterations(PhantomCiphertext& ct, const PhantomContext& cc, uint32_t numIter) const {
+  const int r = static_cast<int>(numIter);
+  for (int j = 1; j <= r; ++j) {
+    ct = EvalMultRescale(cc, ct, ct, mul_key_, sf_);
+    add_inplace(cc, ct, ct);
+    EvalAddConstInplace(cc, ct, -1.0 / std::pow(2.0 * M_PI, std::pow(2.0, j - r)));
+  }
+}
+
+PhantomCiphertext FHECKKSRNS::eval_mod(const PhantomCiphertext& ct, const PhantomContext& cc) const {
+  PhantomCiphertext r = EvalChebyshevSeries(ct, cc, cheb_);
+  ApplyDoubleAngleIterations(r, cc, R_UNIFORM);
+  return r;
+}
+
+PhantomCiphertext FHECKKSRNS::RaiseWithCorrection(const PhantomCiphertext& in, const PhantomContext& cc) const {
+  PhantomCiphertext ct = in;
+  if (ct.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, ct, 1);
+  if (ct.coeff_modulus_size() < 2) throw std::invalid_argument("bootstrapping needs an input with at least two limbs");
+  // scale the message down by 2^-correction and land on scale sf[0] (AdjustCiphertext)
+  const double qdrop = static_cast<double>(cc.get_context_data(ct.chain_index()).moduli().back());
+  const double k = std::ldexp(1.0, -static_cast<int>(correction_)) * qdrop * sf_.at(0) / ct.scale();
+  mult_by_real_integer_inplace(cc, ct, k);
+  ct.SetNoiseScaleDeg(2);
+  EvalModReduceInPlace(cc, ct, 1);
+  ct.set_scale(sf_.at(0));
+  mod_switch_to_inplace(cc, ct, cc.size_Q());  // limb q0 only
+  return RaiseMod(cc, ct);
+}
+
+PhantomCiphertext FHECKKSRNS::EvalBootstrap(const PhantomCiphertext& in, const PhantomContext& cc) const {
+  if (enc_.empty()) throw std::invalid_argument("Precomputations were not generated: call EvalBootstrapSetup");
+  const uint32_t N = static_cast<uint32_t>(cc.poly_degree()), M = 2 * N;
+  PhantomCiphertext raised = RaiseWithCorrection(in, cc);
+  // CoeffToSlot, then split the real and imaginary parts with one conjugation
+  PhantomCiphertext enc = EvalCoeffsToSlots(raised, cc);
+  PhantomCiphertext conj = EvalConjFused(cc, enc, galois_keys_);
+  PhantomCiphertext enc_i = enc;
+  sub_inplace(cc, enc_i, conj);
+  add_inplace(cc, enc, conj);
+  MultByMonomialInPlace(cc, enc_i, 3 * M / 4);  // times -i
+  // approximate modular reduction of both halves
+  enc = eval_mod(enc, cc);
+  enc_i = eval_mod(enc_i, cc);
+  MultByMonomialInPlace(cc, enc_i, M / 4);  // times i
+  EvalAddAutoInplace(cc, enc, enc_i, sf_);
+  // SlotToCoeff and undo the correction scaling
+  PhantomCiphertext dec = EvalSlotsToCoeffs(enc, cc);
+  MultByIntegerInPlace(cc, dec, uint64_t(1) << correction_);
+  return dec;
+}
+
+}  // namespace phantom

@@ -1,0 +1,103 @@
+// bootstrap.h — CKKS bootstrapping (FHECKKSRNS, include/bootstrap.cuh + src/bootstrap.cu of the
+// reference): ModRaise -> CoeffToSlot -> conjugate split -> EvalMod (Chebyshev series of a scaled
+// cosine + double-angle iterations) -> SlotToCoeff, full packing (slots = N/2), FLEXIBLEAUTO
+// scaling, hoisted baby-step/giant-step linear transforms in the extended basis.
+//
+// The linear maps are this engine's own factorisation of the canonical-embedding matrix U
+// (U[j][k] = zeta^(5^j k), zeta = exp(2 pi i / 2N), k < N/2): a radix-2 decimation-in-time
+// recursion whose stage s (block size m = 2^s) is a slot-domain butterfly with twiddles
+// zeta_m^(5^j) and rotations by +-m/2.  CoeffToSlot applies the inverse stages top-down and
+// leaves the coefficients in bit-reversed slot order; SlotToCoeff applies the stages bottom-up
+// from that order, so no permutation is ever evaluated.  `levelBudget` groups the log2(N/2)
+// stages into that many levels (reference: bootstrap.cu:181-560, GetCollapsedFFTParams).
+#pragma once
+
+#include <complex>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <vector>
+
+#include "ciphertext.h"
+#include "ckks_eval.h"
+#include "context.h"
+#include "encoder.h"
+#include "keys.h"
+
+namespace phantom {
+
+namespace boot {
+using cvec = std::vector<std::complex<double>>;
+// a slot-domain linear map as diagonals: (T v)[p] = sum_a diag_a[p] v[p + a]  (a mod slots)
+using DiagMap = std::map<int, cvec>;
+
+// stage s (1 <= s <= log2 slots) of U's factorisation, or its inverse
+DiagMap stage(size_t slots, int s, bool inverse);
+// A * B (B applied first)
+DiagMap compose(const DiagMap& A, const DiagMap& B, size_t slots);
+// apply a DiagMap to a vector (tests)
+cvec apply(const DiagMap& T, const cvec& v);
+// Chebyshev interpolation coefficients of f on [-1, 1] (p(y) = sum_k c_k T_k(y), c_0 not halved)
+std::vector<double> chebyshev_coefficients(double (*f)(double, const double*), const double* args, int degree);
+// the EvalMod target before the double-angle iterations: (2 pi)^(-2^-r) cos(2 pi (K y - 1/4) / 2^r)
+double scaled_cosine(double y, const double* args /* {K, r} */);
+}  // namespace boot
+
+class FHECKKSRNS {
+ public:
+  explicit FHECKKSRNS(PhantomCKKSEncoder& encoder) : encoder_(encoder) {}
+
+  // EvalBootstrapSetup (bootstrap.cu:15-181): linear-transform plaintexts and EvalMod constants.
+  // `sf` are the FLEXIBLEAUTO scaling factors (precompute_scaling_factors).
+  void EvalBootstrapSetup(const PhantomContext& cc, const std::vector<uint32_t>& levelBudget, double scale,
+                          const std::vector<double>& sf, uint32_t correctionFactor = 0);
+  // EvalBootstrapKeyGen / EvalMultKeyGen (bootstrap.cu:566-841): fused rotation keys for the
+  // baby/giant steps and conjugation, and the relinearization key.
+  void EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext& cc);
+  void EvalMultKeyGen(PhantomSecretKey& sk, const PhantomContext& cc);
+  // EvalBootstrap (bootstrap.cu:843-1129); the input needs at least two limbs
+  PhantomCiphertext EvalBootstrap(const PhantomCiphertext& ct, const PhantomContext& cc) const;
+
+  // stages, exposed for tests and the benchmark
+  PhantomCiphertext EvalCoeffsToSlots(const PhantomCiphertext& ct, const PhantomContext& cc) const;
+  PhantomCiphertext EvalSlotsToCoeffs(const PhantomCiphertext& ct, const PhantomContext& cc) const;
+  PhantomCiphertext EvalChebyshevSeries(const PhantomCiphertext& ct, const PhantomContext& cc,
+                                        const std::vector<double>& coeffs) const;
+  void ApplyDoubleAngleIterations(PhantomCiphertext& ct, const PhantomContext& cc, uint32_t numIter) const;
+  // ModRaise input preparation (AdjustCiphertext, bootstrap.cu:1131-1155) + RaiseMod
+  PhantomCiphertext RaiseWithCorrection(const PhantomCiphertext& ct, const PhantomContext& cc) const;
+
+  static uint32_t GetBootstrapDepth(const std::vector<uint32_t>& levelBudget);
+  std::vector<int> rotation_indices() const;
+  uint32_t correction_factor() const { return correction_; }
+  const std::vector<double>& eval_mod_coefficients() const { return cheb_; }
+  const std::vector<double>& scaling_factors() const { return sf_; }
+
+  static constexpr uint32_t K_UNIFORM = 512;  // bound on |I| of the raised plaintext t = m + q0 I
+  static constexpr uint32_t R_UNIFORM = 6;    // double-angle iterations
+  static constexpr int kChebDegree = 88;      // bootstrap.cuh:232-255 (89 coefficients)
+
+ private:
+  // one level of a linear transform: diagonals (u - center) * stride, u < D, evaluated as
+  // baby steps j < g (hoisted rotations) and giant steps i < b
+  struct LTLevel {
+    int stride = 1, center = 0, D = 0, g = 1, b = 1;
+    size_t chain = 1;
+    std::vector<std::unique_ptr<PhantomPlaintext>> pts;  // [D], pre-rotated by -g i stride; null = zero
+  };
+  void build_levels(const PhantomContext& cc, bool encode_dir, const std::vector<int>& group_sizes, double constant,
+                    size_t first_chain, std::vector<LTLevel>& out) const;
+  PhantomCiphertext apply_level(const PhantomContext& cc, const PhantomCiphertext& ct, const LTLevel& lv) const;
+  PhantomCiphertext eval_mod(const PhantomCiphertext& ct, const PhantomContext& cc) const;
+
+  PhantomCKKSEncoder& encoder_;
+  std::vector<double> sf_;
+  std::vector<uint32_t> budget_;
+  uint32_t correction_ = 0;
+  std::vector<LTLevel> enc_, dec_;
+  std::vector<double> cheb_;
+  PhantomRelinKey mul_key_;
+  PhantomGaloisKey galois_keys_;  // fused keys
+};
+
+}  // namespace phantom

@@ -69,6 +69,13 @@ void PhantomPlaintext::resize(const PhantomContext& ctx, size_t chain_index, hip
   data_.allocate(L_ * n_, s);
 }
 
+void PhantomPlaintext::resize_ext(const PhantomContext& ctx, size_t chain_index, size_t limbs, hipStream_t s) {
+  chain_index_ = chain_index;
+  L_ = limbs;
+  n_ = ctx.poly_degree();
+  data_.allocate(L_ * n_, s);
+}
+
 void PhantomPlaintext::from_host(const PhantomContext& ctx, size_t chain_index, const std::vector<uint64_t>& v,
                                  hipStream_t s) {
   resize(ctx, chain_index, s);

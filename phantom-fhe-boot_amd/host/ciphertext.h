@@ -67,11 +67,16 @@ class PhantomPlaintext {
   double scale() const { return scale_; }
   bool is_ntt_form() const { return true; }
   void set_scale(double s) { scale_ = s; }
+  size_t GetNoiseScaleDeg() const { return noise_scale_deg_; }
+  void SetNoiseScaleDeg(size_t d) { noise_scale_deg_ = d; }
   void resize(const PhantomContext& ctx, size_t chain_index, hipStream_t s);
+  // `limbs` limbs tagged with `chain_index` (extended-basis plaintexts: Ql of the chain + P)
+  void resize_ext(const PhantomContext& ctx, size_t chain_index, size_t limbs, hipStream_t s);
   void from_host(const PhantomContext& ctx, size_t chain_index, const std::vector<uint64_t>& v, hipStream_t s);
 
  private:
   size_t chain_index_ = 0, n_ = 0, L_ = 0;
+  size_t noise_scale_deg_ = 1;
   double scale_ = 1.0;
   DeviceBuffer<uint64_t> data_;
 };

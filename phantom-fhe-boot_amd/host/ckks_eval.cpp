@@ -1,0 +1,374 @@
+#include "ckks_eval.h"
+
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+
+#include "../csrc/ckks.h"
+#include "../csrc/ntt.h"
+#include "../csrc/rns.h"
+#include "evaluate.h"
+#include "numth.h"
+
+namespace phantom {
+
+using namespace arith;
+
+static void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw hip_error(e, what);
+}
+
+// exact residue of round(x) mod q for any finite double
+static uint64_t residue_of_double(double x, uint64_t q) {
+  const double r = std::nearbyint(x);
+  const double a = std::fabs(r);
+  uint64_t v;
+  if (a < 9.2e18) {
+    v = static_cast<uint64_t>(a) % q;
+  } else {
+    int e = 0;
+    const double f = std::frexp(a, &e);
+    const uint64_t mant = static_cast<uint64_t>(std::ldexp(f, 53));
+    v = mul_mod(mant % q, pow_mod(2 % q, static_cast<uint64_t>(e - 53), q), q);
+  }
+  return (r < 0 && v) ? q - v : v;
+}
+
+// per-limb scalar and Shoup arrays on the device (setup-style upload; waits for the copy)
+struct Scalars {
+  DeviceBuffer<uint64_t> v, vs;
+};
+static Scalars upload_scalars(const std::vector<uint64_t>& vals, const std::vector<uint64_t>& mods, hipStream_t s) {
+  std::vector<uint64_t> sh(vals.size());
+  for (size_t i = 0; i < vals.size(); ++i) sh[i] = shoup(vals[i], mods[i]);
+  Scalars r;
+  r.v.upload(vals, s);
+  r.vs.upload(sh, s);
+  return r;
+}
+
+std::vector<double> precompute_scaling_factors(const PhantomContext& ctx, double scale) {
+  const size_t sizeQ = ctx.size_Q();
+  const auto& m = ctx.key_moduli();
+  std::vector<double> sf(sizeQ);
+  if (sizeQ == 1) {
+    sf[0] = scale;
+    return sf;
+  }
+  sf[0] = static_cast<double>(m[sizeQ - 1]);
+  for (size_t k = 1; k < sizeQ; ++k) {
+    sf[k] = sf[k - 1] * sf[k - 1] / static_cast<double>(m[sizeQ - k]);
+    const double ratio = sf[k] / sf[0];
+    if (ratio <= 0.5 || ratio >= 2.0)
+      throw std::invalid_argument("FLEXIBLEAUTO cannot support this number of levels in this parameter setting");
+  }
+  return sf;
+}
+
+void mult_by_real_integer_inplace(const PhantomContext& ctx, PhantomCiphertext& ct, double k) {
+  const auto& mods = ctx.get_context_data(ct.chain_index()).moduli();
+  const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size();
+  std::vector<uint64_t> r(L);
+  for (size_t l = 0; l < L; ++l) r[l] = residue_of_double(k, mods[l]);
+  Scalars sc = upload_scalars(r, mods, ctx.stream());
+  for (size_t i = 0; i < ct.size(); ++i)
+    hip_ok(phx::poly_mul_scalar(ct.data() + i * L * n, sc.v.get(), sc.vs.get(), ct.data() + i * L * n, ctx.mod_QP(), n, L,
+                                ctx.stream()),
+           "mult by integer");
+}
+
+void MultByIntegerInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, uint64_t k) {
+  mult_by_real_integer_inplace(ctx, ct, static_cast<double>(k));
+  if (static_cast<uint64_t>(static_cast<double>(k)) != k) throw std::invalid_argument("integer not exact in double");
+}
+
+void EvalMultConstInplace(const PhantomContext& ctx, PhantomCiphertext& ct, double c, const std::vector<double>& sf) {
+  const double f = sf.at(level_of(ct));
+  mult_by_real_integer_inplace(ctx, ct, c * f);
+  ct.SetNoiseScaleDeg(ct.GetNoiseScaleDeg() + 1);
+  ct.set_scale(ct.scale() * f);
+}
+
+void EvalAddConstInplace(const PhantomContext& ctx, PhantomCiphertext& ct, double c) {
+  const auto& mods = ctx.get_context_data(ct.chain_index()).moduli();
+  const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size();
+  std::vector<uint64_t> r(L);
+  for (size_t l = 0; l < L; ++l) r[l] = residue_of_double(c * ct.scale(), mods[l]);
+  Scalars sc = upload_scalars(r, mods, ctx.stream());
+  // NTT of a constant polynomial is that constant at every evaluation point
+  hip_ok(phx::poly_add_scalar(ct.data(), sc.v.get(), ct.data(), ctx.mod_QP(), n, L, ctx.stream()), "add const");
+}
+
+void MultByMonomialInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, uint32_t power) {
+  const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size();
+  hipStream_t s = ctx.stream();
+  // NTT(X^power) over the first L limbs, cached per (power mod 2n, L)
+  static std::mutex mu;
+  static auto& cache = *new std::map<std::tuple<const PhantomContext*, uint32_t, size_t>, DeviceBuffer<uint64_t>>();
+  const uint32_t pr = power % (2 * n);
+  const uint64_t* mono;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_tuple(&ctx, pr, L);
+    auto it = cache.find(key);
+    if (it == cache.end()) {
+      const auto& mods = ctx.key_moduli();
+      std::vector<uint64_t> h(L * n, 0);
+      for (size_t l = 0; l < L; ++l) h[l * n + pr % n] = pr < n ? 1 : mods[l] - 1;
+      DeviceBuffer<uint64_t> d;
+      d.upload(h, s);
+      hip_ok(phx::ntt_forward(ctx.gpu_rns_tables(), d.get(), d.get(), phx::LimbMap::contiguous((int)L, 0), s),
+             "monomial NTT");
+      it = cache.emplace(key, std::move(d)).first;
+    }
+    mono = it->second.get();
+  }
+  for (size_t i = 0; i < ct.size(); ++i)
+    hip_ok(phx::poly_mul(ct.data() + i * L * n, mono, ct.data() + i * L * n, ctx.mod_QP(), n, L, s), "monomial");
+}
+
+void EvalModReduceInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, size_t levels) {
+  for (size_t i = 0; i < levels; ++i) {
+    const size_t deg = ct.GetNoiseScaleDeg();
+    ct = rescale_to_next(ctx, ct);
+    ct.SetNoiseScaleDeg(deg > 1 ? deg - 1 : 1);
+  }
+}
+
+void AdjustToLevel(const PhantomContext& ctx, PhantomCiphertext& ct, size_t target, const std::vector<double>& sf) {
+  if (ct.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(ctx, ct, 1);
+  const size_t lvl = level_of(ct);
+  if (lvl > target) throw std::invalid_argument("cannot raise a ciphertext's level");
+  if (lvl == target) return;
+  // drop limbs without scaling down to target - 1, then one scaling multiply + rescale to
+  // land exactly on sf[target]
+  if (lvl + 1 < target) mod_switch_to_inplace(ctx, ct, target);  // chain index = level + 1
+  const size_t from = level_of(ct);
+  const double qdrop = static_cast<double>(ctx.get_context_data(ct.chain_index()).moduli().back());
+  const double k = sf.at(target) * qdrop / ct.scale();
+  mult_by_real_integer_inplace(ctx, ct, k);
+  ct.set_scale(ct.scale() * std::nearbyint(k));
+  ct.SetNoiseScaleDeg(2);
+  EvalModReduceInPlace(ctx, ct, 1);
+  (void)from;
+  ct.set_scale(sf.at(target));
+}
+
+static void align(const PhantomContext& ctx, PhantomCiphertext& a, PhantomCiphertext& b, const std::vector<double>& sf) {
+  if (a.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(ctx, a, 1);
+  if (b.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(ctx, b, 1);
+  if (level_of(a) < level_of(b)) AdjustToLevel(ctx, a, level_of(b), sf);
+  else if (level_of(b) < level_of(a)) AdjustToLevel(ctx, b, level_of(a), sf);
+}
+
+void EvalAddAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b,
+                        const std::vector<double>& sf) {
+  PhantomCiphertext bb = b;
+  align(ctx, a, bb, sf);
+  add_inplace(ctx, a, bb);
+}
+
+void EvalSubAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b,
+                        const std::vector<double>& sf) {
+  PhantomCiphertext bb = b;
+  align(ctx, a, bb, sf);
+  sub_inplace(ctx, a, bb);
+}
+
+PhantomCiphertext EvalMultRescale(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
+                                  const PhantomRelinKey& rlk, const std::vector<double>& sf) {
+  PhantomCiphertext x = a;
+  if (&a == &b) {
+    if (x.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(ctx, x, 1);
+    multiply_inplace(ctx, x, x);
+  } else {
+    PhantomCiphertext y = b;
+    align(ctx, x, y, sf);
+    multiply_inplace(ctx, x, y);
+  }
+  relinearize_inplace(ctx, x, rlk);
+  x.SetNoiseScaleDeg(2);
+  EvalModReduceInPlace(ctx, x, 1);
+  return x;
+}
+
+PhantomCiphertext RaiseMod(const PhantomContext& ctx, const PhantomCiphertext& ct) {
+  const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size(), Q = ctx.size_Q();
+  hipStream_t s = ctx.stream();
+  DeviceBuffer<uint64_t> c(n, s);
+  PhantomCiphertext out;
+  out.resize(ctx, 1, 2, s, false);
+  for (size_t i = 0; i < 2; ++i) {
+    // limb q0 to coefficient form
+    hip_ok(phx::ntt_inverse(ctx.gpu_rns_tables(), ct.data() + i * L * n, c.get(), phx::LimbMap::contiguous(1, 0),
+                            nullptr, nullptr, s),
+           "raise INTT");
+    uint64_t* o = out.data() + i * Q * n;
+    hip_ok(phx::switch_modulus_raise(c.get(), o, ctx.mod_QP().q, ctx.mod_QP().barrett, n, Q, s), "raise lift");
+    hip_ok(phx::ntt_forward(ctx.gpu_rns_tables(), o, o, phx::LimbMap::contiguous((int)Q, 0), s), "raise NTT");
+  }
+  out.set_scale(ct.scale());
+  out.set_ntt_form(true);
+  out.SetNoiseScaleDeg(ct.GetNoiseScaleDeg());
+  return out;
+}
+
+// ---- hoisted rotations -----------------------------------------------------------------
+
+uint32_t FindAutomorphismIndex2nComplex(int index, size_t n) {
+  const int64_t slots = static_cast<int64_t>(n / 2);
+  int64_t r = index % slots;
+  if (r < 0) r += slots;
+  if (r == 0) return 1;
+  uint64_t g = 1;
+  const uint64_t m = 2 * n;
+  uint64_t b = 5;
+  for (uint64_t e = static_cast<uint64_t>(r); e; e >>= 1, b = b * b % m)
+    if (e & 1) g = g * b % m;
+  return static_cast<uint32_t>(g);
+}
+
+static const uint32_t* perm_table(const PhantomContext& ctx, uint32_t elt) {
+  static std::mutex mu;
+  static auto& cache = *new std::map<std::pair<size_t, uint32_t>, DeviceBuffer<uint32_t>>();
+  const size_t n = ctx.poly_degree();
+  std::lock_guard<std::mutex> lk(mu);
+  auto key = std::make_pair(n, elt);
+  auto it = cache.find(key);
+  if (it == cache.end()) {
+    const int logn = log2_exact(n);
+    std::vector<uint32_t> perm(n);
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint64_t idx = ((2ull * j + 1) * elt) % (2ull * n);
+      perm[reverse_bits(j, logn)] = reverse_bits(static_cast<uint32_t>(idx >> 1), logn);
+    }
+    DeviceBuffer<uint32_t> d;
+    d.upload(perm, ctx.stream());
+    it = cache.emplace(key, std::move(d)).first;
+  }
+  return it->second.get();
+}
+
+DeviceBuffer<uint64_t> EvalFastRotationPrecompute(const PhantomContext& ctx, const PhantomCiphertext& ct) {
+  const RnsTool& rt = ctx.get_context_data(ct.chain_index()).gpu_rns_tool();
+  const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P();
+  DeviceBuffer<uint64_t> digits(rt.beta() * QlP * n, ctx.stream());
+  rt.modup(digits.get(), ct.data() + Ql * n, ctx.gpu_rns_tables(), ctx.stream());
+  return digits;
+}
+
+PhantomCiphertext EvalFastAutomorphismExt(const PhantomContext& ctx, const PhantomCiphertext& ct,
+                                          const PhantomGaloisKey& keys, uint32_t elt, const uint64_t* digits,
+                                          bool add_first) {
+  if (ct.size() != 2) throw std::invalid_argument("encrypted size must be 2");
+  const RnsTool& rt = ctx.get_context_data(ct.chain_index()).gpu_rns_tool();
+  const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P();
+  hipStream_t s = ctx.stream();
+  uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * QlP * n);
+  hip_ok(phx::keyswitch_inner_prod(digits, keys.get(elt).public_keys_ptr(), cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n,
+                                   Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s),
+         "fast rotation inner product");
+  if (add_first)
+    hip_ok(phx::mul_scalar_add(ct.data(), rt.bigP_mod_q(), rt.bigP_mod_q_shoup(), cx, cx, ctx.mod_QP().q, n, Ql, s),
+           "add P c0");
+  PhantomCiphertext out;
+  out.resize(2, QlP, n, s, false);
+  out.set_chain_index(ct.chain_index());
+  out.set_scale(ct.scale());
+  out.SetNoiseScaleDeg(ct.GetNoiseScaleDeg());
+  const uint32_t* perm = perm_table(ctx, elt);
+  hip_ok(phx::galois_ntt(cx, out.data(), perm, n, 2 * QlP, s), "fast rotation permute");
+  return out;
+}
+
+PhantomCiphertext EvalFastRotationExt(const PhantomContext& ctx, const PhantomCiphertext& ct,
+                                      const PhantomGaloisKey& keys, int index, const uint64_t* digits,
+                                      bool add_first) {
+  return EvalFastAutomorphismExt(ctx, ct, keys, FindAutomorphismIndex2nComplex(index, ctx.poly_degree()), digits,
+                                 add_first);
+}
+
+PhantomCiphertext KeySwitchExt(const PhantomContext& ctx, const PhantomCiphertext& ct) {
+  const RnsTool& rt = ctx.get_context_data(ct.chain_index()).gpu_rns_tool();
+  const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P();
+  hipStream_t s = ctx.stream();
+  PhantomCiphertext out;
+  out.resize(2, QlP, n, s, false);
+  out.set_chain_index(ct.chain_index());
+  out.set_scale(ct.scale());
+  out.SetNoiseScaleDeg(ct.GetNoiseScaleDeg());
+  PHX_CHECK(hipMemsetAsync(out.data(), 0, 2 * QlP * n * sizeof(uint64_t), s));
+  for (size_t i = 0; i < 2; ++i)
+    hip_ok(phx::mul_scalar_add(ct.data() + i * Ql * n, rt.bigP_mod_q(), rt.bigP_mod_q_shoup(), nullptr,
+                               out.data() + i * QlP * n, ctx.mod_QP().q, n, Ql, s),
+           "P c");
+  return out;
+}
+
+PhantomCiphertext KeySwitchDown(const PhantomContext& ctx, PhantomCiphertext& ext) {
+  const RnsTool& rt = ctx.get_context_data(ext.chain_index()).gpu_rns_tool();
+  const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P();
+  if (ext.coeff_modulus_size() != QlP) throw std::invalid_argument("not an extended-basis ciphertext");
+  hipStream_t s = ctx.stream();
+  PhantomCiphertext out;
+  out.resize(ctx, ext.chain_index(), 2, s, false);
+  for (size_t i = 0; i < 2; ++i)
+    rt.moddown_add(out.data() + i * Ql * n, ext.data() + i * QlP * n, false, ctx.gpu_rns_tables(), s);
+  out.set_scale(ext.scale());
+  out.SetNoiseScaleDeg(ext.GetNoiseScaleDeg());
+  out.set_ntt_form(true);
+  return out;
+}
+
+static void ext_binary(const PhantomContext& ctx, uint64_t* a, const uint64_t* b, size_t b_stride, size_t polys,
+                       size_t Ql, bool mul) {
+  const size_t n = ctx.poly_degree(), P = ctx.size_P(), QlP = Ql + P;
+  hipStream_t s = ctx.stream();
+  const phx::ModView mq = ctx.mod_QP();
+  const phx::ModView mp{mq.q + ctx.size_Q(), mq.barrett + 2 * ctx.size_Q()};
+  for (size_t i = 0; i < polys; ++i) {
+    uint64_t* x = a + i * QlP * n;
+    const uint64_t* y = b + i * b_stride;
+    if (mul) {
+      hip_ok(phx::poly_mul(x, y, x, mq, n, Ql, s), "ext mul Ql");
+      hip_ok(phx::poly_mul(x + Ql * n, y + Ql * n, x + Ql * n, mp, n, P, s), "ext mul P");
+    } else {
+      hip_ok(phx::poly_add(x, y, x, mq, n, Ql, s), "ext add Ql");
+      hip_ok(phx::poly_add(x + Ql * n, y + Ql * n, x + Ql * n, mp, n, P, s), "ext add P");
+    }
+  }
+}
+
+void EvalMultExtInPlace(const PhantomContext& ctx, PhantomCiphertext& ext, const PhantomPlaintext& pt) {
+  if (ext.chain_index() != pt.chain_index()) throw std::invalid_argument("Eval Mult Ext: chain index mismatch");
+  const size_t Ql = ctx.get_context_data(ext.chain_index()).coeff_modulus_size();
+  if (pt.coeff_modulus_size() != Ql + ctx.size_P() || ext.coeff_modulus_size() != Ql + ctx.size_P())
+    throw std::invalid_argument("Eval Mult Ext: operands are not in the extended basis");
+  ext_binary(ctx, ext.data(), pt.data(), 0, 2, Ql, true);
+  ext.set_scale(ext.scale() * pt.scale());
+  ext.SetNoiseScaleDeg(ext.GetNoiseScaleDeg() + pt.GetNoiseScaleDeg());
+}
+
+void EvalAddExtInPlace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b) {
+  if (a.chain_index() != b.chain_index() || a.GetNoiseScaleDeg() != b.GetNoiseScaleDeg())
+    throw std::invalid_argument("Eval Add Ext Failed.");
+  const size_t Ql = ctx.get_context_data(a.chain_index()).coeff_modulus_size();
+  ext_binary(ctx, a.data(), b.data(), (Ql + ctx.size_P()) * ctx.poly_degree(), 2, Ql, false);
+}
+
+PhantomCiphertext EvalRotateFused(const PhantomContext& ctx, const PhantomCiphertext& ct, const PhantomGaloisKey& keys,
+                                  int index) {
+  DeviceBuffer<uint64_t> d = EvalFastRotationPrecompute(ctx, ct);
+  PhantomCiphertext e = EvalFastRotationExt(ctx, ct, keys, index, d.get(), true);
+  return KeySwitchDown(ctx, e);
+}
+
+PhantomCiphertext EvalConjFused(const PhantomContext& ctx, const PhantomCiphertext& ct, const PhantomGaloisKey& keys) {
+  DeviceBuffer<uint64_t> d = EvalFastRotationPrecompute(ctx, ct);
+  PhantomCiphertext e =
+      EvalFastAutomorphismExt(ctx, ct, keys, static_cast<uint32_t>(2 * ctx.poly_degree() - 1), d.get(), true);
+  return KeySwitchDown(ctx, e);
+}
+
+}  // namespace phantom

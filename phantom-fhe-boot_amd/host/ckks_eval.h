@@ -1,0 +1,86 @@
+// ckks_eval.h — the CKKS evaluator pieces the bootstrap is built from (the helpers of
+// src/evaluate.cu:2284-2554 and :3631-3940 in the reference), with FLEXIBLEAUTO scale management
+// (PhantomCiphertext::PreComputeScale, include/ciphertext.h:320-367).
+//
+// Conventions: level(ct) = chain_index - 1 (the number of dropped primes).  A ciphertext at
+// level l with noise-scale degree 1 carries scale sf[l]; a product has degree 2 and scale
+// sf[l]^2, and a rescale divides by the dropped prime: sf[l]^2 / q = sf[l+1].
+//
+// Extended-basis ("Ext") ciphertexts are [2][size_Ql + size_P][n] NTT-form polynomials that
+// hold P * (c0, c1) (+ key-switch terms); KeySwitchDown divides by P and returns to Ql.
+#pragma once
+
+#include <complex>
+#include <cstdint>
+#include <vector>
+
+#include "ciphertext.h"
+#include "context.h"
+#include "keys.h"
+
+namespace phantom {
+
+inline size_t level_of(const PhantomCiphertext& ct) { return ct.chain_index() - 1; }
+
+// FLEXIBLEAUTO scaling factors per level (PreComputeScale): sf[0] = q_{L-1}, sf[k] = sf[k-1]^2 / q_{L-k}
+std::vector<double> precompute_scaling_factors(const PhantomContext& ctx, double scale);
+
+// multiply every polynomial by round(k) (exact residues of a double; scale metadata unchanged)
+void mult_by_real_integer_inplace(const PhantomContext& ctx, PhantomCiphertext& ct, double k);
+// MultByIntegerInPlace (src/evaluate.cu:3942-3970)
+void MultByIntegerInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, uint64_t k);
+// EvalMultConstInplace (src/evaluate.cu:2299-2412): times round(c * sf[level]), degree + 1
+void EvalMultConstInplace(const PhantomContext& ctx, PhantomCiphertext& ct, double c, const std::vector<double>& sf);
+// add the constant c to every slot (c * scale on the constant coefficient)
+void EvalAddConstInplace(const PhantomContext& ctx, PhantomCiphertext& ct, double c);
+// MultByMonomialInPlace (src/evaluate.cu:2505-2554): times X^power (slots times zeta^(power 5^j))
+void MultByMonomialInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, uint32_t power);
+// rescale once, degree - 1 (ModReduce / EvalModReduceInPlace, src/evaluate.cu:2284-2297)
+void EvalModReduceInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, size_t levels = 1);
+// bring a degree-1 (or 2) ciphertext to `target_level` with scale sf[target_level]: mod-switch,
+// then one scaling multiply + rescale (AdjustLevelsAndDepth of FLEXIBLEAUTO)
+void AdjustToLevel(const PhantomContext& ctx, PhantomCiphertext& ct, size_t target_level,
+                   const std::vector<double>& sf);
+// EvalAddAutoInplace / EvalSubAuto: level- and scale-aligned add / subtract
+void EvalAddAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b,
+                        const std::vector<double>& sf);
+void EvalSubAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b,
+                        const std::vector<double>& sf);
+// level-aligned multiply + relinearize + rescale (EvalMultAuto + ModReduce)
+PhantomCiphertext EvalMultRescale(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
+                                  const PhantomRelinKey& rlk, const std::vector<double>& sf);
+
+// RaiseMod (src/evaluate.cu:2459-2503): limb q0 of a ciphertext -> the full chain Q (chain 1),
+// centered lift; NTT form in and out.
+PhantomCiphertext RaiseMod(const PhantomContext& ctx, const PhantomCiphertext& ct);
+
+// ---- hoisted rotations (src/evaluate.cu:3631-3940) ------------------------------------
+// EvalFastRotationPrecompute: modup of c1, [beta][size_QlP][n]
+DeviceBuffer<uint64_t> EvalFastRotationPrecompute(const PhantomContext& ctx, const PhantomCiphertext& ct);
+// EvalFastRotationExt: rotation by `index` slots in the extended basis from shared digits, with
+// a fused key (PhantomSecretKey::create_galois_keys_fused); add_first adds P * c0.
+PhantomCiphertext EvalFastRotationExt(const PhantomContext& ctx, const PhantomCiphertext& ct,
+                                      const PhantomGaloisKey& fused_keys, int index, const uint64_t* digits,
+                                      bool add_first);
+// the same for an explicit Galois element (conjugation: 2N - 1)
+PhantomCiphertext EvalFastAutomorphismExt(const PhantomContext& ctx, const PhantomCiphertext& ct,
+                                          const PhantomGaloisKey& fused_keys, uint32_t galois_elt,
+                                          const uint64_t* digits, bool add_first);
+// KeySwitchExt: (c0, c1) -> P * (c0, c1) in the extended basis
+PhantomCiphertext KeySwitchExt(const PhantomContext& ctx, const PhantomCiphertext& ct);
+// KeySwitchDown: extended -> Ql (moddown of both polynomials); `ext` is consumed (its P limbs
+// are clobbered)
+PhantomCiphertext KeySwitchDown(const PhantomContext& ctx, PhantomCiphertext& ext);
+// EvalMultExtInPlace / EvalAddExtInPlace over Ql u P
+void EvalMultExtInPlace(const PhantomContext& ctx, PhantomCiphertext& ext, const PhantomPlaintext& pt_ext);
+void EvalAddExtInPlace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b);
+// rotation / conjugation through the hoisted path (one key switch)
+PhantomCiphertext EvalRotateFused(const PhantomContext& ctx, const PhantomCiphertext& ct,
+                                  const PhantomGaloisKey& fused_keys, int index);
+PhantomCiphertext EvalConjFused(const PhantomContext& ctx, const PhantomCiphertext& ct,
+                                const PhantomGaloisKey& fused_keys);
+
+// Galois element of a slot rotation (FindAutomorphismIndex2nComplex, src/util.cu:908-935)
+uint32_t FindAutomorphismIndex2nComplex(int index, size_t n);
+
+}  // namespace phantom

@@ -1,0 +1,62 @@
+// encoder.h — PhantomCKKSEncoder (include/ckks.h, src/ckks.cu): slots <-> NTT-form plaintexts.
+//
+// Slot j sits at the root zeta^(5^j) of X^N + 1 (zeta = exp(2 pi i / 2N)) and its conjugate at
+// zeta^(-5^j), the convention of the reference and of every 5^j rotation group.  The canonical
+// embedding and its inverse are evaluated on the host in double precision with one size-N
+// complex FFT each (the reference runs its special FFT on the GPU, src/fft.cu); coefficients
+// are rounded to integers, reduced into each RNS limb exactly and moved to NTT form on the GPU.
+#pragma once
+
+#include <complex>
+#include <cstdint>
+#include <vector>
+
+#include "ciphertext.h"
+#include "context.h"
+
+namespace phantom {
+
+class PhantomCKKSEncoder {
+ public:
+  explicit PhantomCKKSEncoder(const PhantomContext& ctx);
+  // host-only maps (slots_to_coeffs / coeffs_to_slots) for ring degree n, no device use
+  explicit PhantomCKKSEncoder(size_t n);
+
+  size_t slot_count() const { return n_ / 2; }
+
+  // encode(context, values, scale, plain[, chain_index]) (src/ckks.cu): plaintext in the Ql basis
+  // of `chain_index`, NTT form.  Fewer values than slots are zero-padded.
+  void encode(const PhantomContext& ctx, const std::vector<std::complex<double>>& values, double scale,
+              PhantomPlaintext& out, size_t chain_index = 1) const;
+  void encode(const PhantomContext& ctx, const std::vector<double>& values, double scale, PhantomPlaintext& out,
+              size_t chain_index = 1) const;
+  // encode_ext (the hoisted linear transforms' plaintexts): the Ql basis of `chain_index`
+  // followed by the special primes P, NTT form ([size_Ql + size_P][n]).
+  void encode_ext(const PhantomContext& ctx, const std::vector<std::complex<double>>& values, double scale,
+                  PhantomPlaintext& out, size_t chain_index) const;
+
+  // decode(context, plain, values) (src/ckks.cu): exact CRT composition of each coefficient,
+  // centered, divided by the plaintext's scale, then the canonical embedding.
+  void decode(const PhantomContext& ctx, const PhantomPlaintext& plain, std::vector<std::complex<double>>& out) const;
+  void decode(const PhantomContext& ctx, const PhantomPlaintext& plain, std::vector<double>& out) const;
+
+  // host-side maps, exposed for the bootstrap precomputation and tests
+  // slots -> real coefficients (inverse canonical embedding, coefficients not scaled)
+  std::vector<double> slots_to_coeffs(const std::vector<std::complex<double>>& values) const;
+  // real coefficients -> slots
+  std::vector<std::complex<double>> coeffs_to_slots(const std::vector<double>& coeffs) const;
+
+ private:
+  // rounds coeffs * scale and writes residues for `moduli` (limb-major) to `out` (host)
+  static void to_rns(const std::vector<double>& coeffs, double scale, const std::vector<uint64_t>& moduli,
+                     std::vector<uint64_t>& out);
+  void fft(std::vector<std::complex<double>>& a, bool inverse) const;
+
+  size_t n_ = 0;
+  int logn_ = 0;
+  std::vector<std::complex<double>> zeta_pows_;  // zeta^j, j < 2n
+  std::vector<uint32_t> slot_index_;             // (5^j mod 2n - 1) / 2 for j < n/2
+  std::vector<uint32_t> brev_;
+};
+
+}  // namespace phantom

@@ -4,6 +4,7 @@
 #include <random>
 #include <stdexcept>
 
+#include "../csrc/ckks.h"
 #include "../csrc/rns.h"
 #include "numth.h"
 
@@ -74,38 +75,24 @@ PhantomSecretKey::PhantomSecretKey(const PhantomContext& ctx, uint64_t seed) : s
   PHX_CHECK(hipStreamSynchronize(s));
 }
 
+// Randomness comes from device-side counter-based generators keyed by (seed, draw counter), so
+// key generation for hundreds of rotation keys stays on the GPU (the reference samples on the
+// GPU as well: src/prng.cu, sample_uniform_poly / sample_error_poly in src/secretkey.cu).
 void PhantomSecretKey::sample_uniform(const PhantomContext& ctx, uint64_t* dst, size_t L) {
-  const size_t n = ctx.poly_degree();
-  const auto& m = ctx.key_moduli();
-  std::vector<uint64_t> v(L * n);
-  for (size_t l = 0; l < L; ++l) {
-    const uint64_t q = m[l];
-    const uint64_t lim = UINT64_MAX - UINT64_MAX % q;
-    for (size_t k = 0; k < n; ++k) {
-      uint64_t x;
-      do x = next(); while (x >= lim);
-      v[l * n + k] = x % q;
-    }
-  }
-  PHX_CHECK(hipMemcpyAsync(dst, v.data(), v.size() * 8, hipMemcpyHostToDevice, ctx.stream()));
-  PHX_CHECK(hipStreamSynchronize(ctx.stream()));
+  hip_ok(phx::sample_uniform(dst, ctx.mod_QP().q, ctx.mod_QP().barrett, ctx.poly_degree(), L, seed_state_, draws_++,
+                             ctx.stream()),
+         "sample uniform");
 }
 
 void PhantomSecretKey::sample_error(const PhantomContext& ctx, uint64_t* dst, size_t L) {
-  // centered binomial, sigma ~ 3.2 (sample_error_poly uses a CBD as well)
-  const size_t n = ctx.poly_degree();
-  std::vector<int64_t> e(n);
-  for (size_t k = 0; k < n; ++k) {
-    const uint64_t r = next();
-    e[k] = __builtin_popcountll(r & 0x1FFFFF) - __builtin_popcountll((r >> 21) & 0x1FFFFF);
-  }
-  std::vector<uint64_t> v = signed_to_rns(e, std::vector<uint64_t>(ctx.key_moduli().begin(), ctx.key_moduli().begin() + L));
-  PHX_CHECK(hipMemcpyAsync(dst, v.data(), v.size() * 8, hipMemcpyHostToDevice, ctx.stream()));
-  PHX_CHECK(hipStreamSynchronize(ctx.stream()));
+  // centered binomial, sigma ~ 3.2 (sample_error_poly uses a CBD as well), then NTT
+  hip_ok(phx::sample_cbd(dst, ctx.mod_QP().q, ctx.poly_degree(), L, seed_state_, draws_++, ctx.stream()), "sample e");
   hip_ok(phx::ntt_forward(ctx.gpu_rns_tables(), dst, dst, phx::LimbMap::contiguous((int)L, 0), ctx.stream()), "e NTT");
 }
 
-PhantomKSwitchKey PhantomSecretKey::make_kswitch_key(const PhantomContext& ctx, const uint64_t* new_key) {
+PhantomKSwitchKey PhantomSecretKey::make_kswitch_key(const PhantomContext& ctx, const uint64_t* new_key,
+                                                    const uint64_t* enc_key) {
+  if (!enc_key) enc_key = s_.get();
   const size_t n = ctx.poly_degree(), QP = ctx.size_QP(), Q = ctx.size_Q(), alpha = ctx.size_P();
   hipStream_t s = ctx.stream();
   const size_t dnum = (Q + alpha - 1) / alpha;
@@ -119,7 +106,7 @@ PhantomKSwitchKey PhantomSecretKey::make_kswitch_key(const PhantomContext& ctx, 
     uint64_t* a = key.get() + QP * n;
     sample_uniform(ctx, a, QP);   // uniform in NTT form is uniform
     sample_error(ctx, e.get(), QP);
-    hip_ok(phx::poly_mul_add(a, s_.get(), e.get(), tmp.get(), mqp, n, QP, s), "a*s+e");
+    hip_ok(phx::poly_mul_add(a, enc_key, e.get(), tmp.get(), mqp, n, QP, s), "a*s+e");
     hip_ok(phx::poly_negate(tmp.get(), b, mqp, n, QP, s), "-(a*s+e)");
     // + P * new_key on this digit's primes (multiply_temp_mod_and_add_rns_poly)
     const size_t l0 = d * alpha, l1 = std::min(Q, l0 + alpha);
@@ -160,6 +147,30 @@ PhantomGaloisKey PhantomSecretKey::create_galois_keys(const PhantomContext& ctx,
     d_perm.upload(perm, s);
     hip_ok(phx::galois_ntt(s_.get(), rot.get(), d_perm.get(), n, QP, s), "rotate sk");
     gk.set(k, make_kswitch_key(ctx, rot.get()));
+  }
+  return gk;
+}
+
+PhantomGaloisKey PhantomSecretKey::create_galois_keys_fused(const PhantomContext& ctx,
+                                                           const std::vector<uint32_t>& elts) {
+  const size_t n = ctx.poly_degree(), QP = ctx.size_QP();
+  hipStream_t s = ctx.stream();
+  PhantomGaloisKey gk;
+  const int logn = arith::log2_exact(n);
+  const uint64_t m = 2 * n;
+  std::vector<uint32_t> perm(n);
+  DeviceBuffer<uint32_t> d_perm;
+  DeviceBuffer<uint64_t> rot(QP * n, s);
+  for (uint32_t k : elts) {
+    // encryption secret s(X^(k^-1)): the hoisted rotation applies X -> X^k after the key switch
+    const uint32_t kinv = static_cast<uint32_t>(arith::inv_mod(k, m));
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint64_t idx = ((2ull * j + 1) * kinv) % m;
+      perm[arith::reverse_bits(j, logn)] = arith::reverse_bits(static_cast<uint32_t>(idx >> 1), logn);
+    }
+    d_perm.upload(perm, s);
+    hip_ok(phx::galois_ntt(s_.get(), rot.get(), d_perm.get(), n, QP, s), "rotate sk");
+    gk.set(k, make_kswitch_key(ctx, s_.get(), rot.get()));
   }
   return gk;
 }

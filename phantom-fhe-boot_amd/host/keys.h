@@ -56,20 +56,26 @@ class PhantomSecretKey {
 
   PhantomRelinKey gen_relinkey(const PhantomContext& ctx);
   PhantomGaloisKey create_galois_keys(const PhantomContext& ctx, const std::vector<uint32_t>& galois_elts);
+  // keys for hoisted rotations (the reference's PhantomGaloisKeyFused): the key for element k
+  // switches from s to s(X^(k^-1)), so the automorphism can be applied after the inner product
+  // of the shared modup digits (EvalFastRotationExt, src/evaluate.cu:3656-3748)
+  PhantomGaloisKey create_galois_keys_fused(const PhantomContext& ctx, const std::vector<uint32_t>& galois_elts);
 
   // symmetric encryption of an NTT-form plaintext at `chain_index` (src/secretkey.cu:576-644)
   void encrypt_symmetric(const PhantomContext& ctx, const PhantomPlaintext& plain, PhantomCiphertext& out);
   // decryption c0 + c1 s (+ c2 s^2) in NTT form (ckks_decrypt, src/secretkey.cu:646-682)
   void decrypt(const PhantomContext& ctx, const PhantomCiphertext& ct, PhantomPlaintext& out);
 
-  // kswitch key for new_key (NTT form over QP) -> s (generate_one_kswitch_key)
-  PhantomKSwitchKey make_kswitch_key(const PhantomContext& ctx, const uint64_t* new_key);
+  // kswitch key for new_key (NTT form over QP) -> enc_key (default s) (generate_one_kswitch_key)
+  PhantomKSwitchKey make_kswitch_key(const PhantomContext& ctx, const uint64_t* new_key,
+                                     const uint64_t* enc_key = nullptr);
 
  private:
   void sample_uniform(const PhantomContext& ctx, uint64_t* dst, size_t L);
   void sample_error(const PhantomContext& ctx, uint64_t* dst, size_t L);  // NTT form
   uint64_t next();
   uint64_t seed_state_;
+  uint64_t draws_ = 0;  // counter of device sampling draws
   std::vector<int8_t> coeffs_;
   DeviceBuffer<uint64_t> s_, s2_;
 };
