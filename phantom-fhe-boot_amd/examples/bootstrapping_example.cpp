@@ -24,6 +24,8 @@
 #include "../host/evaluate.h"
 #include "../host/keys.h"
 #include "../host/modulus.h"
+#include "../csrc/rns.h"
+#include "../csrc/ntt.h"
 
 using namespace phantom;
 using namespace phantom::arith;
@@ -44,9 +46,15 @@ static double compute_bit_precision(const std::vector<double>& ref, const std::v
   return cnt ? sum / cnt : 0.0;
 }
 
+// NaN-propagating max |a - b|; also prints the first slots of a and b
 static double max_abs_err(const std::vector<std::complex<double>>& a, const std::vector<std::complex<double>>& b) {
   double m = 0;
-  for (size_t i = 0; i < a.size(); ++i) m = std::max(m, std::abs(a[i] - b[i]));
+  for (size_t i = 0; i < a.size(); ++i) {
+    const double e = std::abs(a[i] - b[i]);
+    if (!(e <= m)) m = e;  // NaN sticks
+  }
+  std::printf("{\"sample\": [[%.6f, %.6f], [%.6f, %.6f]], \"want\": [[%.6f, %.6f], [%.6f, %.6f]]}\n", a[0].real(),
+              a[0].imag(), a[1].real(), a[1].imag(), b[0].real(), b[0].imag(), b[1].real(), b[1].imag());
   return m;
 }
 
@@ -108,6 +116,100 @@ int main(int argc, char** argv) {
   PhantomCiphertext ct;
   sk.encrypt_symmetric(ctx, pt, ct);
   report("encrypt_decrypt", max_abs_err(decrypt_decode(ctx, sk, enc, ct), xz), 1e-6, ct.chain_index());
+
+  if (mode == "dbg") {
+    {  // rescale only
+      PhantomCiphertext r = ct;
+      EvalModReduceInPlace(ctx, r, 1);
+      report("dbg_rescale", max_abs_err(decrypt_decode(ctx, sk, enc, r), xz), 1e-6, r.chain_index());
+    }
+    {  // mod switch only
+      PhantomCiphertext r = mod_switch_to_next(ctx, ct);
+      report("dbg_modswitch", max_abs_err(decrypt_decode(ctx, sk, enc, r), xz), 1e-6, r.chain_index());
+    }
+    {  // const mult by 1 (degree 2, no rescale)
+      PhantomCiphertext r = ct;
+      EvalMultConstInplace(ctx, r, 1.0, sf);
+      report("dbg_constmult", max_abs_err(decrypt_decode(ctx, sk, enc, r), xz), 1e-6, r.chain_index());
+      EvalModReduceInPlace(ctx, r, 1);
+      report("dbg_constmult_rescale", max_abs_err(decrypt_decode(ctx, sk, enc, r), xz), 1e-6, r.chain_index());
+    }
+    {  // tensor only (3 components), decrypt with s^2
+      PhantomCiphertext r = ct;
+      multiply_inplace(ctx, r, r);
+      std::vector<std::complex<double>> want(slots);
+      for (size_t j = 0; j < slots; ++j) want[j] = x[j] * x[j];
+      report("dbg_tensor", max_abs_err(decrypt_decode(ctx, sk, enc, r), want), 1e-6, r.chain_index());
+      PhantomRelinKey rlk = sk.gen_relinkey(ctx);
+      relinearize_inplace(ctx, r, rlk);
+      report("dbg_relin", max_abs_err(decrypt_decode(ctx, sk, enc, r), want), 1e-6, r.chain_index());
+    }
+    {  // square via EvalMultRescale
+      PhantomRelinKey rlk = sk.gen_relinkey(ctx);
+      PhantomCiphertext r = EvalMultRescale(ctx, ct, ct, rlk, sf);
+      std::vector<std::complex<double>> want(slots);
+      for (size_t j = 0; j < slots; ++j) want[j] = x[j] * x[j];
+      report("dbg_square_rescale", max_abs_err(decrypt_decode(ctx, sk, enc, r), want), 1e-5, r.chain_index());
+    }
+    std::vector<std::complex<double>> want(slots);
+    for (size_t j = 0; j < slots; ++j) want[j] = xz[(j + 1) % slots];
+    {  // key residue check: b_i + a_i * enc must be small outside digit i's primes
+      auto check_key = [&](const PhantomKSwitchKey& k, const uint64_t* enc_key, const char* name) {
+        const size_t QP = ctx.size_QP();
+        DeviceBuffer<uint64_t> t(QP * N, nullptr);
+        for (size_t i = 0; i < k.dnum(); ++i) {
+          const uint64_t* b = k.digit(i);
+          const uint64_t* a = b + QP * N;
+          (void)phx::poly_mul_add(a, enc_key, b, t.get(), ctx.mod_QP(), N, QP, nullptr);
+          (void)phx::ntt_inverse(ctx.gpu_rns_tables(), t.get(), t.get(), phx::LimbMap::contiguous((int)QP, 0), nullptr,
+                                 nullptr, nullptr);
+          std::vector<uint64_t> h = t.download(nullptr);
+          uint64_t worst = 0;
+          size_t worst_l = 0;
+          for (size_t l = 0; l < QP; ++l) {
+            if (l >= i * ctx.size_P() && l < (i + 1) * ctx.size_P()) continue;
+            const uint64_t q = ctx.key_moduli()[l];
+            for (size_t c = 0; c < N; c += 97) {
+              const uint64_t v = h[l * N + c], m = std::min(v, q - v);
+              if (m > worst) { worst = m; worst_l = l; }
+            }
+          }
+          std::printf("{\"key\": \"%s\", \"digit\": %zu, \"worst_offdigit_residue\": %llu, \"limb\": %zu}\n", name, i,
+                      (unsigned long long)worst, worst_l);
+        }
+      };
+      PhantomRelinKey rk = sk.gen_relinkey(ctx);
+      check_key(rk, sk.secret_key_array(), "relin");
+      PhantomGaloisKey g = sk.create_galois_keys(ctx, {5});
+      check_key(g.get(5), sk.secret_key_array(), "galois5");
+      PhantomRelinKey rk2 = sk.gen_relinkey(ctx);
+      check_key(rk2, sk.secret_key_array(), "relin_again");
+    }
+    {  // standard Galois key rotation by 1
+      PhantomGaloisKey g = sk.create_galois_keys(ctx, {FindAutomorphismIndex2nComplex(1, N)});
+      PhantomCiphertext r = ct;
+      rotate_inplace(ctx, r, 1, g);
+      report("dbg_rotate_std", max_abs_err(decrypt_decode(ctx, sk, enc, r), want), 1e-6, r.chain_index());
+    }
+    {  // fused key rotation by 1, step by step
+      PhantomGaloisKey g = sk.create_galois_keys_fused(ctx, {FindAutomorphismIndex2nComplex(1, N)});
+      DeviceBuffer<uint64_t> d = EvalFastRotationPrecompute(ctx, ct);
+      PhantomCiphertext e0 = KeySwitchExt(ctx, ct);
+      PhantomCiphertext back = KeySwitchDown(ctx, e0);
+      report("dbg_ksext_down", max_abs_err(decrypt_decode(ctx, sk, enc, back), xz), 1e-6, back.chain_index());
+      PhantomCiphertext e = EvalFastRotationExt(ctx, ct, g, 1, d.get(), true);
+      PhantomCiphertext r = KeySwitchDown(ctx, e);
+      report("dbg_rotate_fused", max_abs_err(decrypt_decode(ctx, sk, enc, r), want), 1e-6, r.chain_index());
+    }
+    for (size_t lv = 0; lv + 2 < ctx.size_Q(); ++lv) {  // drain, every level
+      PhantomCiphertext& d = ct;
+      EvalMultConstInplace(ctx, d, 1.0, sf);
+      EvalModReduceInPlace(ctx, d, 1);
+      std::printf("{\"drain_level\": %zu, \"scale\": %.6e, \"sf\": %.6e}\n", level_of(d), d.scale(), sf[level_of(d)]);
+      report("dbg_drain", max_abs_err(decrypt_decode(ctx, sk, enc, d), xz), 1e-4, d.chain_index());
+    }
+    return g_ok ? 0 : 1;
+  }
 
   if (mode == "ops") {
     PhantomGaloisKey gk = sk.create_galois_keys_fused(

@@ -33,14 +33,25 @@ class DeviceBuffer {
     return *this;
   }
 
+  // Stream-ordered allocation only on a real stream: on the null stream it corrupted live
+  // buffers on ROCm 7.2 (a freed block handed out again while kernels still used it; reproduced
+  // by examples/bootstrapping_example dbg, gone with synchronous allocation).  Null-stream
+  // buffers therefore use plain hipMalloc / hipFree.
   void allocate(size_t count, hipStream_t stream) {
     release();
-    if (count) PHX_CHECK(hipMallocAsync(reinterpret_cast<void**>(&ptr_), count * sizeof(T), stream));
+    async_ = stream != nullptr;
+    if (count) {
+      if (async_) PHX_CHECK(hipMallocAsync(reinterpret_cast<void**>(&ptr_), count * sizeof(T), stream));
+      else PHX_CHECK(hipMalloc(reinterpret_cast<void**>(&ptr_), count * sizeof(T)));
+    }
     count_ = count;
     stream_ = stream;
   }
   void release() {
-    if (ptr_) (void)hipFreeAsync(ptr_, stream_);
+    if (ptr_) {
+      if (async_) (void)hipFreeAsync(ptr_, stream_);
+      else (void)hipFree(ptr_);
+    }
     ptr_ = nullptr;
     count_ = 0;
   }
@@ -79,10 +90,12 @@ class DeviceBuffer {
     std::swap(ptr_, o.ptr_);
     std::swap(count_, o.count_);
     std::swap(stream_, o.stream_);
+    std::swap(async_, o.async_);
   }
   T* ptr_ = nullptr;
   size_t count_ = 0;
   hipStream_t stream_ = nullptr;
+  bool async_ = false;
 };
 
 // Scratch buffers reused across calls, one set per stream (the reference allocates its

@@ -105,12 +105,12 @@ void MultByMonomialInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, uin
   hipStream_t s = ctx.stream();
   // NTT(X^power) over the first L limbs, cached per (power mod 2n, L)
   static std::mutex mu;
-  static auto& cache = *new std::map<std::tuple<const PhantomContext*, uint32_t, size_t>, DeviceBuffer<uint64_t>>();
+  static auto& cache = *new std::map<std::pair<uint32_t, std::vector<uint64_t>>, DeviceBuffer<uint64_t>>();
   const uint32_t pr = power % (2 * n);
   const uint64_t* mono;
   {
     std::lock_guard<std::mutex> lk(mu);
-    auto key = std::make_tuple(&ctx, pr, L);
+    auto key = std::make_pair(pr, std::vector<uint64_t>(ctx.key_moduli().begin(), ctx.key_moduli().begin() + L));
     auto it = cache.find(key);
     if (it == cache.end()) {
       const auto& mods = ctx.key_moduli();

@@ -7,8 +7,14 @@
 
 namespace phantom {
 
-PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t stream)
-    : params_(params), stream_(stream) {
+PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t stream) : params_(params) {
+  if (stream) {
+    stream_.s = stream;
+  } else {
+    PHX_CHECK(hipStreamCreateWithFlags(&stream_.s, hipStreamNonBlocking));
+    stream_.owned = true;
+  }
+  hipStream_t s = stream_.s;
   if (params.scheme() != scheme_type::ckks) throw std::invalid_argument("only CKKS is supported by this engine");
   const auto& mods = params.coeff_modulus();
   if (mods.size() < 2) throw std::invalid_argument("The coefficient modulus must be a vector of at least two primes");
@@ -28,7 +34,7 @@ PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t s
   }
 
   ws_ = std::make_unique<Workspace>();
-  ntt_ = std::make_unique<DeviceNttTables>(n_, qp_, stream_);
+  ntt_ = std::make_unique<DeviceNttTables>(n_, qp_, s);
   data_.push_back(std::make_unique<ContextData>(0, qp_));
   for (size_t c = 1; c <= size_Q_; ++c) {
     std::vector<uint64_t> ql(qp_.begin(), qp_.begin() + (size_Q_ - (c - 1)));
@@ -44,7 +50,7 @@ PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t s
       th.emplace_back([&, w] {
         try {
           for (size_t c = 1 + w; c <= size_Q_; c += nt)
-            tools[c] = std::make_unique<RnsTool>(n_, qp_, size_P_, size_Q_ - (c - 1), stream_);
+            tools[c] = std::make_unique<RnsTool>(n_, qp_, size_P_, size_Q_ - (c - 1), s);
         } catch (...) {
           errs[w] = std::current_exception();
         }
@@ -57,7 +63,7 @@ PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t s
     tools[c]->set_workspace(ws_.get());
     data_[c]->set_rns_tool(std::move(tools[c]));
   }
-  PHX_CHECK(hipStreamSynchronize(stream_));
+  PHX_CHECK(hipStreamSynchronize(s));
 }
 
 }  // namespace phantom

@@ -56,8 +56,26 @@ class ContextData {
   std::unique_ptr<RnsTool> rns_tool_;
 };
 
+// owns the context's default stream when none is supplied (the reference runs every op on
+// cudaStreamPerThread); destroyed last, after every buffer that frees on it
+struct OwnedStream {
+  hipStream_t s = nullptr;
+  bool owned = false;
+  OwnedStream() = default;
+  OwnedStream(const OwnedStream&) = delete;
+  OwnedStream& operator=(const OwnedStream&) = delete;
+  ~OwnedStream() {
+    if (owned && s) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+  }
+};
+
 class PhantomContext {
  public:
+  // stream: where setup work and the façade's operations run; nullptr = a stream owned by the
+  // context (never the null stream: see DeviceBuffer::allocate)
   explicit PhantomContext(const EncryptionParameters& params, hipStream_t stream = nullptr);
   PhantomContext(const PhantomContext&) = delete;
   PhantomContext& operator=(const PhantomContext&) = delete;
@@ -79,17 +97,17 @@ class PhantomContext {
   // NTT tables and per-modulus device constants over the whole Q u P chain
   const phx::NttTables& gpu_rns_tables() const { return ntt_->get(); }
   phx::ModView mod_QP() const { return {ntt_->get().modulus, ntt_->get().barrett}; }
-  hipStream_t stream() const { return stream_; }
+  hipStream_t stream() const { return stream_.s; }
   Workspace& workspace() const { return *ws_; }
 
  private:
+  OwnedStream stream_;  // first member: destroyed after everything that frees on it
   EncryptionParameters params_;
   size_t n_ = 0, size_Q_ = 0, size_P_ = 0;
   std::vector<uint64_t> qp_;
   std::unique_ptr<Workspace> ws_;  // declared before the tools that point into it
   std::unique_ptr<DeviceNttTables> ntt_;
   std::vector<std::unique_ptr<ContextData>> data_;
-  hipStream_t stream_;
 };
 
 }  // namespace phantom
