@@ -1,6 +1,8 @@
 #include "bootstrap.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <stdexcept>
 #include <thread>
@@ -463,24 +465,39 @@ PhantomCiphertext FHECKKSRNS::RaiseWithCorrection(const PhantomCiphertext& in, c
   return RaiseMod(cc, ct);
 }
 
+// PHX_BOOT_TRACE=1: synchronise and report after every bootstrap stage (debugging aid)
+static void trace(const PhantomContext& cc, const char* stage, const PhantomCiphertext& ct) {
+  static const bool on = std::getenv("PHX_BOOT_TRACE") != nullptr;
+  if (!on) return;
+  const hipError_t e = hipStreamSynchronize(cc.stream());
+  std::fprintf(stderr, "[boot] %-12s chain %zu limbs %zu scale %.6e deg %zu : %s\n", stage, ct.chain_index(),
+               ct.coeff_modulus_size(), ct.scale(), ct.GetNoiseScaleDeg(), hipGetErrorString(e));
+}
+
 PhantomCiphertext FHECKKSRNS::EvalBootstrap(const PhantomCiphertext& in, const PhantomContext& cc) const {
   if (enc_.empty()) throw std::invalid_argument("Precomputations were not generated: call EvalBootstrapSetup");
   const uint32_t N = static_cast<uint32_t>(cc.poly_degree()), M = 2 * N;
   PhantomCiphertext raised = RaiseWithCorrection(in, cc);
+  trace(cc, "raise", raised);
   // CoeffToSlot, then split the real and imaginary parts with one conjugation
   PhantomCiphertext enc = EvalCoeffsToSlots(raised, cc);
+  trace(cc, "cts", enc);
   PhantomCiphertext conj = EvalConjFused(cc, enc, galois_keys_);
   PhantomCiphertext enc_i = enc;
   sub_inplace(cc, enc_i, conj);
   add_inplace(cc, enc, conj);
   MultByMonomialInPlace(cc, enc_i, 3 * M / 4);  // times -i
+  trace(cc, "conj-split", enc_i);
   // approximate modular reduction of both halves
   enc = eval_mod(enc, cc);
+  trace(cc, "evalmod-re", enc);
   enc_i = eval_mod(enc_i, cc);
+  trace(cc, "evalmod-im", enc_i);
   MultByMonomialInPlace(cc, enc_i, M / 4);  // times i
   EvalAddAutoInplace(cc, enc, enc_i, sf_);
   // SlotToCoeff and undo the correction scaling
   PhantomCiphertext dec = EvalSlotsToCoeffs(enc, cc);
+  trace(cc, "stc", dec);
   MultByIntegerInPlace(cc, dec, uint64_t(1) << correction_);
   return dec;
 }

@@ -1,12 +1,13 @@
-// buffer.h — stream-ordered device buffers (the reference's cuda_auto_ptr,
-// include/cuda_wrapper.cuh:74-219), on hipMallocAsync / hipFreeAsync.  PhantomContext raises the
-// default pool's release threshold so freed blocks stay cached for reuse, as the reference
-// does for its CUDA pool (src/context.cu:127-131).
+// buffer.h — device buffers (the reference's cuda_auto_ptr, include/cuda_wrapper.cuh:74-219) on
+// a caching allocator (DevicePool): freed blocks stay cached for reuse, as the reference keeps
+// its CUDA pool's blocks (src/context.cu:127-131).
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -15,6 +16,35 @@
 #include "hip_check.h"
 
 namespace phantom {
+
+// Caching device allocator.  A freed block is kept with an event recorded on the stream that
+// freed it; it is handed out again to the same stream at once (stream order protects it) or
+// to another stream once that event has completed.  Blocks are never returned to the driver.
+// Replaces hipMallocAsync / hipFreeAsync: with ROCm 7.2's stream-ordered pool, reused blocks
+// were observed to still be in use (key-switching keys and ciphertexts corrupted; reproduced by
+// examples/bootstrapping_example ops, gone with synchronous allocation).
+class DevicePool {
+ public:
+  static DevicePool& instance();
+  void* alloc(size_t bytes, hipStream_t s);
+  // completed: the caller has synchronised the device (no event needed)
+  void free(void* p, size_t bytes, hipStream_t s, bool completed = false);
+  // size class of a request (blocks are reused only within a class)
+  static size_t size_class(size_t bytes);
+
+ private:
+  struct Block {
+    void* p;
+    hipStream_t stream;
+    hipEvent_t ev;  // null when known complete
+  };
+  std::mutex mu_;
+  std::map<std::pair<int, size_t>, std::vector<Block>> free_;  // (device, class) -> blocks
+  std::map<void*, size_t> live_;                               // handed-out blocks (double-free check)
+  std::vector<hipEvent_t> spare_;
+  hipEvent_t take_event();
+  void release_cached_locked();
+};
 
 template <typename T>
 class DeviceBuffer {
@@ -33,32 +63,50 @@ class DeviceBuffer {
     return *this;
   }
 
-  // Stream-ordered allocation only on a real stream: on the null stream it corrupted live
-  // buffers on ROCm 7.2 (a freed block handed out again while kernels still used it; reproduced
-  // by examples/bootstrapping_example dbg, gone with synchronous allocation).  Null-stream
-  // buffers therefore use plain hipMalloc / hipFree.
   void allocate(size_t count, hipStream_t stream) {
     release();
-    async_ = stream != nullptr;
     if (count) {
-      if (async_) PHX_CHECK(hipMallocAsync(reinterpret_cast<void**>(&ptr_), count * sizeof(T), stream));
-      else PHX_CHECK(hipMalloc(reinterpret_cast<void**>(&ptr_), count * sizeof(T)));
+      ptr_ = static_cast<T*>(DevicePool::instance().alloc(count * sizeof(T) + kGuardBytes, stream));
+#ifdef PHX_GUARD
+      PHX_CHECK(hipDeviceSynchronize());
+      PHX_CHECK(hipMemset(reinterpret_cast<char*>(ptr_) + count * sizeof(T), 0xA5, kGuardBytes));
+#endif
     }
     count_ = count;
     stream_ = stream;
   }
   void release() {
     if (ptr_) {
-      if (async_) (void)hipFreeAsync(ptr_, stream_);
-      else (void)hipFree(ptr_);
+#ifdef PHX_GUARD
+      check_guard();
+#endif
+      DevicePool::instance().free(ptr_, count_ * sizeof(T) + kGuardBytes, stream_);
     }
     ptr_ = nullptr;
     count_ = 0;
   }
+#ifdef PHX_GUARD
+  // debug builds: a 0xA5 guard region after every buffer, checked when the buffer is freed
+  static constexpr size_t kGuardBytes = size_t(1) << 20;
+  void check_guard() const {
+    (void)hipDeviceSynchronize();
+    std::vector<unsigned char> g(kGuardBytes);
+    (void)hipMemcpy(g.data(), reinterpret_cast<const char*>(ptr_) + count_ * sizeof(T), kGuardBytes,
+                    hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < kGuardBytes; ++i)
+      if (g[i] != 0xA5) {
+        std::fprintf(stderr, "GUARD VIOLATION: buffer of %zu bytes (%zu elements of %zu B), first bad guard byte +%zu\n",
+                     count_ * sizeof(T), count_, sizeof(T), i);
+        std::abort();
+      }
+  }
+#else
+  static constexpr size_t kGuardBytes = 0;
+#endif
   // free without touching the owning stream (which may no longer exist); the caller has
   // synchronised the device
   void release_sync() {
-    if (ptr_) (void)hipFree(ptr_);
+    if (ptr_) DevicePool::instance().free(ptr_, count_ * sizeof(T) + kGuardBytes, nullptr, true);
     ptr_ = nullptr;
     count_ = 0;
   }
@@ -90,12 +138,10 @@ class DeviceBuffer {
     std::swap(ptr_, o.ptr_);
     std::swap(count_, o.count_);
     std::swap(stream_, o.stream_);
-    std::swap(async_, o.async_);
   }
   T* ptr_ = nullptr;
   size_t count_ = 0;
   hipStream_t stream_ = nullptr;
-  bool async_ = false;
 };
 
 // Scratch buffers reused across calls, one set per stream (the reference allocates its
