@@ -16,9 +16,9 @@ void PhantomCiphertext::resize(size_t size, size_t L, size_t n, hipStream_t s, b
   const size_t old_count = size_ * L_ * n_, new_count = size * L * n;
   if (new_count == 0) {
     data_.release();
-  } else if (new_count != old_count) {
+  } else if (new_count != old_count || !data_) {  // a moved-from ciphertext keeps its sizes
     DeviceBuffer<uint64_t> fresh(new_count, s);
-    if (copy_old && data_) {
+    if (copy_old && data_ && old_count) {
       const size_t c = std::min(old_count, new_count);
       PHX_CHECK(hipMemcpyAsync(fresh.get(), data_.get(), c * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
     }

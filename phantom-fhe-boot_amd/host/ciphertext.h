@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <utility>
 #include <vector>
 
 #include "buffer.h"
@@ -14,8 +15,23 @@ namespace phantom {
 class PhantomCiphertext {
  public:
   PhantomCiphertext() = default;
-  PhantomCiphertext(PhantomCiphertext&&) = default;
-  PhantomCiphertext& operator=(PhantomCiphertext&&) = default;
+  PhantomCiphertext(PhantomCiphertext&& o) noexcept { *this = std::move(o); }
+  // moves leave the source empty (sizes zeroed with the buffer)
+  PhantomCiphertext& operator=(PhantomCiphertext&& o) noexcept {
+    if (this != &o) {
+      chain_index_ = o.chain_index_;
+      size_ = o.size_;
+      n_ = o.n_;
+      L_ = o.L_;
+      scale_ = o.scale_;
+      correction_factor_ = o.correction_factor_;
+      noise_scale_deg_ = o.noise_scale_deg_;
+      is_ntt_form_ = o.is_ntt_form_;
+      data_ = std::move(o.data_);
+      o.size_ = o.L_ = o.n_ = 0;
+    }
+    return *this;
+  }
   // deep device copy (the reference copies through cuda_auto_ptr, cuda_wrapper.cuh:94-104)
   PhantomCiphertext(const PhantomCiphertext& o) { copy_from(o); }
   PhantomCiphertext& operator=(const PhantomCiphertext& o) {
