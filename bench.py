@@ -112,6 +112,29 @@ def c3_leg(PA, lib, torch, steps=20, warmup=3):
     }
 
 
+def c4_leg(iters=3, timeout=240):
+    """Config C4: full CKKS bootstrap, N=2^16, Q = {60, 29x59}, P = 10x60,
+    levelBudget {2,2}, 2^15 reals in [1,5] (bootstrapping_example.cu:69-116), run by the C++
+    example binary in its own process; latency = median wall time of EvalBootstrap between device
+    synchronisations."""
+    import subprocess
+    exe = os.path.join(ROOT, "phantom-fhe-boot_amd", "bin", "bootstrapping_example")
+    out = subprocess.run([exe, "boot", "16", str(iters)], capture_output=True, text=True, timeout=timeout)
+    rows = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{") and '"sample"' not in l]
+    boot = [r for r in rows if r.get("stage") == "bootstrap"]
+    setup = [r for r in rows if r.get("stage") == "setup"]
+    if out.returncode != 0 or not boot:
+        return {"error": (out.stderr or out.stdout)[-300:]}
+    b = boot[0]
+    return {
+        "workload": "C4: EvalBootstrap, N=65536, Q={60,29x59}, P=10x60, levelBudget {2,2}, full packing",
+        "ms_median": b["ms_median"], "ms_min": b["ms_min"], "runs": b["runs"],
+        "avg_bits": b["avg_bits"], "levels_after": b["levels_after"],
+        "setup_ms": setup[0]["setup_ms"] if setup else None,
+        "keygen_ms": setup[0]["keygen_ms"] if setup else None,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,6 +142,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 (mult+relin+rescale) leg")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 (bootstrap latency) leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -216,6 +240,8 @@ def main():
         }
         if not args.no_c3:
             out["c3"] = c3_leg(PA, lib, torch)
+        if not args.no_c4 and world == 1:
+            out["c4"] = c4_leg()
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(mods)
         print(json.dumps(out), flush=True)

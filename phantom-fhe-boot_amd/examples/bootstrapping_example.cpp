@@ -312,7 +312,7 @@ int main(int argc, char** argv) {
               "\"max_abs_err\": %.3e, \"chain_in\": %zu, \"chain_out\": %zu, \"levels_after\": %zu}\n",
               times[times.size() / 2], times[0], times.size(), bits_avg, err, ct.chain_index(), out.chain_index(),
               levels_after);
-  g_ok &= bits_avg > 8.0;
+  g_ok &= bits_avg > 9.0;
   std::printf("{\"done\": \"boot\", \"ok\": %s}\n", g_ok ? "true" : "false");
   return g_ok ? 0 : 1;
 }
