@@ -24,3 +24,36 @@ hipError_t mul_scalar_add(const uint64_t* in, const uint64_t* c, const uint64_t*
                           uint64_t* out, const uint64_t* q, size_t n, size_t L, hipStream_t s);
 
 }  // namespace phx
+
+namespace phx {
+
+// ---- hoisted baby-step / giant-step linear transform (bootstrap CoeffToSlot / SlotToCoeff) ----
+// For every giant step i < b with out[i] != null:
+//   out[i][t] = sum_{j < g, u = g i + j < D, pts[u] != null} baby[j][t] * pts[u]   (t = 0, 1)
+// over the extended basis Ql u P ([2][Ql + P][n] ciphertexts, [Ql + P][n] plaintexts).  One
+// launch reads every baby and every plaintext once (the reference multiplies and adds one
+// (baby, plaintext) pair per launch: EvalMultExt + EvalAddExtInPlace, bootstrap.cu:1322-1332).
+constexpr int kLtMaxG = 32, kLtMaxB = 64;
+struct LtArgs {
+  const uint64_t* baby[kLtMaxG];
+  uint64_t* out[kLtMaxB];
+  const uint64_t* const* pts;  // device array [D]
+  const uint64_t* q;           // full QP chain
+  const uint64_t* barrett;     // [QP][2]
+  int g = 0, b = 0, D = 0, Ql = 0, P = 0, size_Q = 0;
+};
+hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s);
+
+// out[l] = in[l] * c[l] (+ acc[l]) with per-limb constants passed by value (no device upload);
+// L <= kMaxScalarLimbs
+constexpr int kMaxScalarLimbs = 64;
+struct LimbScalars {
+  uint64_t v[kMaxScalarLimbs];
+  uint64_t vs[kMaxScalarLimbs];  // Shoup quotients (mul) / unused (add)
+};
+hipError_t mul_scalar_v(const uint64_t* in, const LimbScalars& c, uint64_t* out, const uint64_t* q, size_t n,
+                        size_t L, hipStream_t s);
+hipError_t add_scalar_v(const uint64_t* in, const LimbScalars& c, uint64_t* out, const uint64_t* q, size_t n,
+                        size_t L, hipStream_t s);
+
+}  // namespace phx

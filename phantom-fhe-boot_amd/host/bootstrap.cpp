@@ -7,6 +7,7 @@
 #include <stdexcept>
 #include <thread>
 
+#include "../csrc/ckks.h"
 #include "../csrc/rns.h"
 #include "evaluate.h"
 #include "numth.h"
@@ -272,6 +273,11 @@ void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const s
       encoder_.encode_ext(cc, rot, scale, *pt, lv.chain);
       lv.pts[u] = std::move(pt);
     }
+    std::vector<const uint64_t*> ptrs(lv.D, nullptr);
+    for (int u = 0; u < lv.D; ++u)
+      if (lv.pts[u]) ptrs[u] = lv.pts[u]->data();
+    lv.d_pts.upload(ptrs, cc.stream());
+    if (lv.g > phx::kLtMaxG || lv.b > phx::kLtMaxB) throw std::invalid_argument("linear transform level too large");
     out.push_back(std::move(lv));
   }
 }
@@ -335,26 +341,6 @@ void FHECKKSRNS::EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext&
 
 void FHECKKSRNS::EvalMultKeyGen(PhantomSecretKey& sk, const PhantomContext& cc) { mul_key_ = sk.gen_relinkey(cc); }
 
-// out (+)= a * b over Ql u P (extended-basis operands, `polys` polynomials of a, one of b)
-static void ext_mul_acc(const PhantomContext& cc, size_t Ql, const uint64_t* a, const uint64_t* b, uint64_t* out,
-                        bool accumulate) {
-  const size_t n = cc.poly_degree(), P = cc.size_P(), QlP = Ql + P;
-  hipStream_t s = cc.stream();
-  const phx::ModView mq = cc.mod_QP();
-  const phx::ModView mp{mq.q + cc.size_Q(), mq.barrett + 2 * cc.size_Q()};
-  for (size_t i = 0; i < 2; ++i) {
-    const uint64_t* x = a + i * QlP * n;
-    uint64_t* o = out + i * QlP * n;
-    if (accumulate) {
-      hip_ok(phx::poly_mul_add(x, b, o, o, mq, n, Ql, s), "lt mul-add Ql");
-      hip_ok(phx::poly_mul_add(x + Ql * n, b + Ql * n, o + Ql * n, o + Ql * n, mp, n, P, s), "lt mul-add P");
-    } else {
-      hip_ok(phx::poly_mul(x, b, o, mq, n, Ql, s), "lt mul Ql");
-      hip_ok(phx::poly_mul(x + Ql * n, b + Ql * n, o + Ql * n, mp, n, P, s), "lt mul P");
-    }
-  }
-}
-
 PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const PhantomCiphertext& in,
                                           const LTLevel& lv) const {
   PhantomCiphertext ct = in;
@@ -374,29 +360,43 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
       baby[j] = EvalFastRotationExt(cc, ct, galois_keys_, static_cast<int>(r), digits.get(), true);
   }
   digits.release();
-  PhantomCiphertext acc, inner;
+  // every giant step's inner sum in one launch
+  std::vector<PhantomCiphertext> inner(lv.b);
+  phx::LtArgs la;
+  la.g = lv.g;
+  la.b = lv.b;
+  la.D = lv.D;
+  la.Ql = static_cast<int>(Ql);
+  la.P = static_cast<int>(cc.size_P());
+  la.size_Q = static_cast<int>(cc.size_Q());
+  la.pts = lv.d_pts.get();
+  la.q = cc.mod_QP().q;
+  la.barrett = cc.mod_QP().barrett;
+  for (int j = 0; j < lv.g; ++j) la.baby[j] = baby[j].data();
+  for (int i = 0; i < lv.b; ++i) {
+    bool any = false;
+    for (int j = 0; j < lv.g && lv.g * i + j < lv.D; ++j) any |= static_cast<bool>(lv.pts[lv.g * i + j]);
+    la.out[i] = nullptr;
+    if (!any) continue;
+    inner[i].resize(2, QlP, n, s, false);
+    inner[i].set_chain_index(ct.chain_index());
+    inner[i].set_scale(ct.scale() * sf_.at(lv.chain - 1));
+    inner[i].SetNoiseScaleDeg(2);
+    la.out[i] = inner[i].data();
+  }
+  hip_ok(phx::lt_bsgs(la, n, s), "linear transform inner products");
+  baby.clear();
+  PhantomCiphertext acc;
   bool have_acc = false;
   for (int i = 0; i < lv.b; ++i) {
-    bool have_inner = false;
-    for (int j = 0; j < lv.g; ++j) {
-      const int u = lv.g * i + j;
-      if (u >= lv.D || !lv.pts[u]) continue;
-      if (!have_inner) {
-        inner.resize(2, QlP, n, s, false);
-        inner.set_chain_index(ct.chain_index());
-      }
-      ext_mul_acc(cc, Ql, baby[j].data(), lv.pts[u]->data(), inner.data(), have_inner);
-      have_inner = true;
-    }
-    if (!have_inner) continue;
-    inner.set_scale(ct.scale() * sf_.at(lv.chain - 1));
-    inner.SetNoiseScaleDeg(2);
+    if (!la.out[i]) continue;
     if (i == 0) {
-      acc = std::move(inner);
+      acc = std::move(inner[0]);
       have_acc = true;
       continue;
     }
-    PhantomCiphertext down = KeySwitchDown(cc, inner);
+    PhantomCiphertext down = KeySwitchDown(cc, inner[i]);
+    inner[i] = PhantomCiphertext();
     DeviceBuffer<uint64_t> d2 = EvalFastRotationPrecompute(cc, down);
     PhantomCiphertext rot =
         EvalFastRotationExt(cc, down, galois_keys_, static_cast<int>(static_cast<long>(lv.g) * i * lv.stride), d2.get(), true);

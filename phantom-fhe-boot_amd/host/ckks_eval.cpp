@@ -71,6 +71,18 @@ void mult_by_real_integer_inplace(const PhantomContext& ctx, PhantomCiphertext& 
   const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size();
   std::vector<uint64_t> r(L);
   for (size_t l = 0; l < L; ++l) r[l] = residue_of_double(k, mods[l]);
+  if (L <= static_cast<size_t>(phx::kMaxScalarLimbs)) {
+    // constants travel in the kernel arguments: no upload, no stream synchronisation
+    phx::LimbScalars c;
+    for (size_t l = 0; l < L; ++l) {
+      c.v[l] = r[l];
+      c.vs[l] = shoup(r[l], mods[l]);
+    }
+    for (size_t i = 0; i < ct.size(); ++i)
+      hip_ok(phx::mul_scalar_v(ct.data() + i * L * n, c, ct.data() + i * L * n, ctx.mod_QP().q, n, L, ctx.stream()),
+             "mult by integer");
+    return;
+  }
   Scalars sc = upload_scalars(r, mods, ctx.stream());
   for (size_t i = 0; i < ct.size(); ++i)
     hip_ok(phx::poly_mul_scalar(ct.data() + i * L * n, sc.v.get(), sc.vs.get(), ct.data() + i * L * n, ctx.mod_QP(), n, L,
@@ -95,8 +107,14 @@ void EvalAddConstInplace(const PhantomContext& ctx, PhantomCiphertext& ct, doubl
   const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size();
   std::vector<uint64_t> r(L);
   for (size_t l = 0; l < L; ++l) r[l] = residue_of_double(c * ct.scale(), mods[l]);
-  Scalars sc = upload_scalars(r, mods, ctx.stream());
   // NTT of a constant polynomial is that constant at every evaluation point
+  if (L <= static_cast<size_t>(phx::kMaxScalarLimbs)) {
+    phx::LimbScalars v;
+    for (size_t l = 0; l < L; ++l) v.v[l] = r[l];
+    hip_ok(phx::add_scalar_v(ct.data(), v, ct.data(), ctx.mod_QP().q, n, L, ctx.stream()), "add const");
+    return;
+  }
+  Scalars sc = upload_scalars(r, mods, ctx.stream());
   hip_ok(phx::poly_add_scalar(ct.data(), sc.v.get(), ct.data(), ctx.mod_QP(), n, L, ctx.stream()), "add const");
 }
 
