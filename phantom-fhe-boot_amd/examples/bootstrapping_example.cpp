@@ -308,9 +308,11 @@ int main(int argc, char** argv) {
   const double err = max_abs_err(z, xz);
   std::sort(times.begin(), times.end());
   const size_t levels_after = ctx.size_Q() - out.chain_index();  // remaining levels (limbs - 1)
-  std::printf("{\"stage\": \"bootstrap\", \"ms_median\": %.2f, \"ms_min\": %.2f, \"runs\": %zu, \"avg_bits\": %.2f, "
+  double total = 0;
+  for (double t : times) total += t;
+  std::printf("{\"stage\": \"bootstrap\", \"ms_total\": %.2f, \"ms_median\": %.2f, \"ms_min\": %.2f, \"runs\": %zu, \"avg_bits\": %.2f, "
               "\"max_abs_err\": %.3e, \"chain_in\": %zu, \"chain_out\": %zu, \"levels_after\": %zu}\n",
-              times[times.size() / 2], times[0], times.size(), bits_avg, err, ct.chain_index(), out.chain_index(),
+              total, times[times.size() / 2], times[0], times.size(), bits_avg, err, ct.chain_index(), out.chain_index(),
               levels_after);
   g_ok &= bits_avg > 9.0;
   std::printf("{\"done\": \"boot\", \"ok\": %s}\n", g_ok ? "true" : "false");
