@@ -28,19 +28,21 @@ hipError_t mul_scalar_add(const uint64_t* in, const uint64_t* c, const uint64_t*
 namespace phx {
 
 // ---- hoisted baby-step / giant-step linear transform (bootstrap CoeffToSlot / SlotToCoeff) ----
-// For every giant step i < b with out[i] != null:
-//   out[i][t] = sum_{j < g, u = g i + j < D, pts[u] != null} baby[j][t] * pts[u]   (t = 0, 1)
+// For every giant step i < b:
+//   out[i][t] = sum_{j < g} baby[j][t] * pts[g i + j]   (t = 0, 1)
 // over the extended basis Ql u P ([2][Ql + P][n] ciphertexts, [Ql + P][n] plaintexts).  One
 // launch reads every baby and every plaintext once (the reference multiplies and adds one
 // (baby, plaintext) pair per launch: EvalMultExt + EvalAddExtInPlace, bootstrap.cu:1322-1332).
+// pts is a device array of b * g non-null pointers (absent diagonals point at a zero
+// plaintext); every out[i] is non-null.
 constexpr int kLtMaxG = 32, kLtMaxB = 64;
 struct LtArgs {
   const uint64_t* baby[kLtMaxG];
   uint64_t* out[kLtMaxB];
-  const uint64_t* const* pts;  // device array [D]
+  const uint64_t* const* pts;  // device array [b][g]
   const uint64_t* q;           // full QP chain
   const uint64_t* barrett;     // [QP][2]
-  int g = 0, b = 0, D = 0, Ql = 0, P = 0, size_Q = 0;
+  int g = 0, b = 0, Ql = 0, P = 0, size_Q = 0;
 };
 hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s);
 
@@ -51,8 +53,12 @@ struct LimbScalars {
   uint64_t v[kMaxScalarLimbs];
   uint64_t vs[kMaxScalarLimbs];  // Shoup quotients (mul) / unused (add)
 };
+// mul_scalar_v over `polys` polynomials with the same constants: input p at in + p * in_stride
+// (0: L n; a larger stride reads the first L limbs of longer polynomials, i.e. drops limbs),
+// out and acc contiguous [polys][L][n]: out = in * c (+ acc)
 hipError_t mul_scalar_v(const uint64_t* in, const LimbScalars& c, uint64_t* out, const uint64_t* q, size_t n,
-                        size_t L, hipStream_t s);
+                        size_t L, hipStream_t s, size_t polys = 1, size_t in_stride = 0,
+                        const uint64_t* acc = nullptr);
 hipError_t add_scalar_v(const uint64_t* in, const LimbScalars& c, uint64_t* out, const uint64_t* q, size_t n,
                         size_t L, hipStream_t s);
 

@@ -55,46 +55,87 @@ __global__ __launch_bounds__(kBlock) void mul_scalar_add_kernel(const uint64_t* 
   }
 }
 
+// One element (limb l, coefficient k) per thread and grid-stride step.  Babies are split into
+// 30-bit halves once; each giant step issues all G plaintext loads together (the pointer row
+// is one scalar block: no branches between the loads) and accumulates the 4 partial products
+// of every term in 64-bit sums — each is a sum of <= 16 products of 30-bit values, < 2^64 —
+// folded to 128 bits every 16 terms and Barrett-reduced once per output.
 template <int G>
-__global__ __launch_bounds__(kBlock) void lt_bsgs_kernel(LtArgs a, uint32_t log_n, size_t total) {
+__global__ __launch_bounds__(kBlock, 2) void lt_bsgs_kernel(LtArgs a, uint32_t log_n, size_t total) {
+  constexpr uint64_t kM30 = (1ull << 30) - 1;
+  constexpr int kChunk = 16;
+  // the [b][g] plaintext pointer table, staged in LDS once per workgroup (a global read of it
+  // per giant step would add a memory round trip before the plaintext loads can issue)
+  extern __shared__ const uint64_t* ptab[];
+  for (int k = threadIdx.x; k < a.b * G; k += kBlock) ptab[k] = a.pts[k];
+  __syncthreads();
   const size_t pstride = total;  // elements per polynomial ([Ql + P][n])
   for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
     const int l = static_cast<int>(e >> log_n);
     const int row = l < a.Ql ? l : a.size_Q + (l - a.Ql);
     const uint64_t q = a.q[row], r0 = a.barrett[2 * row], r1 = a.barrett[2 * row + 1];
-    uint64_t x0[G], x1[G];
+    uint32_t xl[2][G], xh[2][G];
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-      x0[j] = a.baby[j][e];
-      x1[j] = a.baby[j][pstride + e];
+      const uint64_t v0 = a.baby[j][e], v1 = a.baby[j][pstride + e];
+      xl[0][j] = static_cast<uint32_t>(v0 & kM30);
+      xh[0][j] = static_cast<uint32_t>(v0 >> 30);
+      xl[1][j] = static_cast<uint32_t>(v1 & kM30);
+      xh[1][j] = static_cast<uint32_t>(v1 >> 30);
     }
     for (int i = 0; i < a.b; ++i) {
-      uint64_t* o = a.out[i];
-      if (!o) continue;
-      u128 acc0{0, 0}, acc1{0, 0};
+      const uint64_t* const* prow = ptab + i * G;
+      uint64_t w[G];
+      // global (not flat) loads: they count in vmcnt only, so the LDS pointer reads between
+      // them do not wait for the plaintext data
 #pragma unroll
-      for (int j = 0; j < G; ++j) {
-        const int u = G * i + j;
-        if (u >= a.D) break;
-        const uint64_t* p = a.pts[u];
-        if (!p) continue;
-        const uint64_t w = p[e];
-        add128(acc0, mul_wide(x0[j], w));  // <= 32 products of 60-bit values: < 2^125
-        add128(acc1, mul_wide(x1[j], w));
+      for (int j = 0; j < G; ++j) w[j] = ((const __attribute__((address_space(1))) uint64_t*)prow[j])[e];
+      // keep the G loads together in flight: the scheduler would otherwise sink each load to
+      // its first use (one memory round trip per term)
+      __builtin_amdgcn_sched_barrier(0);
+      u128 acc[2] = {{0, 0}, {0, 0}};
+#pragma unroll
+      for (int c0 = 0; c0 < G; c0 += kChunk) {
+        uint64_t ll[2] = {0, 0}, m1[2] = {0, 0}, m2[2] = {0, 0}, hh[2] = {0, 0};
+#pragma unroll
+        for (int j = c0; j < c0 + kChunk && j < G; ++j) {
+          const uint32_t wl = static_cast<uint32_t>(w[j] & kM30), wh = static_cast<uint32_t>(w[j] >> 30);
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            ll[t] += static_cast<uint64_t>(xl[t][j]) * wl;
+            m1[t] += static_cast<uint64_t>(xl[t][j]) * wh;
+            m2[t] += static_cast<uint64_t>(xh[t][j]) * wl;
+            hh[t] += static_cast<uint64_t>(xh[t][j]) * wh;
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          add128(acc[t], u128{ll[t], 0});
+          add128(acc[t], u128{m1[t] << 30, m1[t] >> 34});
+          add128(acc[t], u128{m2[t] << 30, m2[t] >> 34});
+          add128(acc[t], u128{hh[t] << 60, hh[t] >> 4});
+        }
       }
-      o[e] = barrett_reduce_128(acc0, q, r0, r1);
-      o[pstride + e] = barrett_reduce_128(acc1, q, r0, r1);
+      uint64_t* o = a.out[i];
+      o[e] = barrett_reduce_128(acc[0], q, r0, r1);
+      o[pstride + e] = barrett_reduce_128(acc[1], q, r0, r1);
     }
   }
 }
 
-template <bool MUL>
-__global__ __launch_bounds__(kBlock) void scalar_v_kernel(const uint64_t* in, LimbScalars c, uint64_t* out,
-                                                          const uint64_t* q, uint32_t log_n, size_t total) {
+template <bool MUL, bool ACC>
+__global__ __launch_bounds__(kBlock) void scalar_v_kernel(const uint64_t* in, size_t in_stride, LimbScalars c,
+                                                          const uint64_t* acc, uint64_t* out, const uint64_t* q,
+                                                          uint32_t log_n, size_t total) {
+  in += blockIdx.y * in_stride;
+  out += blockIdx.y * total;
+  if constexpr (ACC) acc += blockIdx.y * total;
   for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
     const uint32_t l = static_cast<uint32_t>(e >> log_n);
     const uint64_t ql = q[l];
-    out[e] = MUL ? mul_shoup(in[e], c.v[l], c.vs[l], ql) : add_mod(in[e], c.v[l], ql);
+    uint64_t v = MUL ? mul_shoup(in[e], c.v[l], c.vs[l], ql) : add_mod(in[e], c.v[l], ql);
+    if constexpr (ACC) v = add_mod(v, acc[e], ql);
+    out[e] = v;
   }
 }
 
@@ -127,27 +168,35 @@ hipError_t mul_scalar_add(const uint64_t* in, const uint64_t* c, const uint64_t*
 }
 
 hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s) {
-  if (a.g < 1 || a.g > kLtMaxG || a.b < 1 || a.b > kLtMaxB || a.g * a.b < a.D) return hipErrorInvalidValue;
+  if (a.g < 1 || a.g > kLtMaxG || a.b < 1 || a.b > kLtMaxB || a.pts == nullptr) return hipErrorInvalidValue;
+  for (int i = 0; i < a.b; ++i)
+    if (!a.out[i]) return hipErrorInvalidValue;
   const size_t total = n * static_cast<size_t>(a.Ql + a.P);
   const uint32_t log_n = __builtin_ctzll(n);
   const int grid = grid_for(total);
+  const size_t lds = static_cast<size_t>(a.b) * a.g * sizeof(const uint64_t*);
   switch (a.g) {
-    case 1: lt_bsgs_kernel<1><<<grid, kBlock, 0, s>>>(a, log_n, total); break;
-    case 2: lt_bsgs_kernel<2><<<grid, kBlock, 0, s>>>(a, log_n, total); break;
-    case 4: lt_bsgs_kernel<4><<<grid, kBlock, 0, s>>>(a, log_n, total); break;
-    case 8: lt_bsgs_kernel<8><<<grid, kBlock, 0, s>>>(a, log_n, total); break;
-    case 16: lt_bsgs_kernel<16><<<grid, kBlock, 0, s>>>(a, log_n, total); break;
-    case 32: lt_bsgs_kernel<32><<<grid, kBlock, 0, s>>>(a, log_n, total); break;
+    case 1: lt_bsgs_kernel<1><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
+    case 2: lt_bsgs_kernel<2><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
+    case 4: lt_bsgs_kernel<4><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
+    case 8: lt_bsgs_kernel<8><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
+    case 16: lt_bsgs_kernel<16><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
+    case 32: lt_bsgs_kernel<32><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
 hipError_t mul_scalar_v(const uint64_t* in, const LimbScalars& c, uint64_t* out, const uint64_t* q, size_t n,
-                        size_t L, hipStream_t s) {
-  if (L > static_cast<size_t>(kMaxScalarLimbs)) return hipErrorInvalidValue;
+                        size_t L, hipStream_t s, size_t polys, size_t in_stride, const uint64_t* acc) {
+  if (L > static_cast<size_t>(kMaxScalarLimbs) || polys < 1) return hipErrorInvalidValue;
   const size_t total = n * L;
-  scalar_v_kernel<true><<<grid_for(total), kBlock, 0, s>>>(in, c, out, q, __builtin_ctzll(n), total);
+  const dim3 g(std::max<int>(1, grid_for(total * polys) / static_cast<int>(polys)), static_cast<unsigned>(polys));
+  const size_t is = in_stride ? in_stride : total;
+  if (acc)
+    scalar_v_kernel<true, true><<<g, kBlock, 0, s>>>(in, is, c, acc, out, q, __builtin_ctzll(n), total);
+  else
+    scalar_v_kernel<true, false><<<g, kBlock, 0, s>>>(in, is, c, nullptr, out, q, __builtin_ctzll(n), total);
   return hipGetLastError();
 }
 
@@ -155,7 +204,8 @@ hipError_t add_scalar_v(const uint64_t* in, const LimbScalars& c, uint64_t* out,
                         size_t L, hipStream_t s) {
   if (L > static_cast<size_t>(kMaxScalarLimbs)) return hipErrorInvalidValue;
   const size_t total = n * L;
-  scalar_v_kernel<false><<<grid_for(total), kBlock, 0, s>>>(in, c, out, q, __builtin_ctzll(n), total);
+  scalar_v_kernel<false, false><<<grid_for(total), kBlock, 0, s>>>(in, total, c, nullptr, out, q, __builtin_ctzll(n),
+                                                                    total);
   return hipGetLastError();
 }
 

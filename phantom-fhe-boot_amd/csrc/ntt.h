@@ -43,6 +43,10 @@ inline int ntt_split_log_s1(int log_n) { return log_n / 2; }
 // Which table row each buffer limb uses.  Buffer limb i (0 <= i < num_limbs) maps to
 // table row (i < split ? first_a + i : first_b + (i - split)); limbs in
 // [skip_begin, skip_end) are left untouched (the reference's exclude_range).
+//
+// Batching: `polys` polynomials of the same shape go through one launch.  Polynomial p starts
+// at in + p * in_stride / out + p * out_stride (elements; 0 = num_limbs * n, i.e. contiguous)
+// and skips [skip_begin + p * skip_step, skip_end + p * skip_step) — the modup digits.
 struct LimbMap {
   int num_limbs = 0;
   int split = 0;
@@ -50,9 +54,19 @@ struct LimbMap {
   int first_b = 0;
   int skip_begin = 0;
   int skip_end = 0;
+  int polys = 1;
+  int skip_step = 0;
+  size_t in_stride = 0;
+  size_t out_stride = 0;
   static LimbMap contiguous(int num_limbs, int first) {
     LimbMap m;
     m.num_limbs = num_limbs; m.split = num_limbs; m.first_a = first; m.first_b = 0;
+    return m;
+  }
+  // `polys` polynomials with the given element strides (0: contiguous)
+  LimbMap batched(int count, size_t in_s = 0, size_t out_s = 0) const {
+    LimbMap m = *this;
+    m.polys = count; m.in_stride = in_s; m.out_stride = out_s;
     return m;
   }
 };

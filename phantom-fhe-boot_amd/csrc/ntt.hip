@@ -289,12 +289,16 @@ struct KArgs {
   const uint64_t* scale_shoup;
   LimbMap map;
   int n;
-  int limbs;                  // number of processed limbs (excluding skipped)
+  int limbs;                  // number of processed limbs over all polynomials (excluding skipped)
+  int limbs_per_poly;
 };
 
-__device__ __forceinline__ void resolve_limb(const LimbMap& m, int y, int& buf_limb, int& row) {
-  int i = y;
-  if (i >= m.skip_begin) i += (m.skip_end - m.skip_begin);
+// y: processed-limb index over the batch -> polynomial, buffer limb within it, table row
+__device__ __forceinline__ void resolve_limb(const KArgs& a, int y, int& poly, int& buf_limb, int& row) {
+  const LimbMap& m = a.map;
+  poly = m.polys > 1 ? y / a.limbs_per_poly : 0;
+  int i = y - poly * a.limbs_per_poly;
+  if (i >= m.skip_begin + poly * m.skip_step) i += (m.skip_end - m.skip_begin);
   buf_limb = i;
   row = i < m.split ? m.first_a + i : m.first_b + (i - m.split);
 }
@@ -350,7 +354,8 @@ constexpr bool kPrefetch = PHX_NTT_PERSIST > 0;
 
 struct TileRef {
   int buf_limb, row;
-  size_t off;  // element offset of this lane's first element
+  size_t off;     // element offset of this lane's first element in the output
+  size_t in_off;  // ... and in the input
 };
 
 // ---------------------------------------------------------------------------------------
@@ -363,10 +368,14 @@ template <int S2_LOG>
 __device__ __forceinline__ TileRef col_ref(const KArgs& a, int tile, uint32_t c) {
   constexpr int CT = (1 << S2_LOG) / COLS;
   TileRef r;
-  resolve_limb(a.map, tile / CT, r.buf_limb, r.row);
+  int poly;
+  resolve_limb(a, tile / CT, poly, r.buf_limb, r.row);
+  poly = __builtin_amdgcn_readfirstlane(poly);
   r.buf_limb = __builtin_amdgcn_readfirstlane(r.buf_limb);
   r.row = __builtin_amdgcn_readfirstlane(r.row);
-  r.off = (size_t)r.buf_limb * a.n + (tile % CT) * COLS + c;
+  const size_t e = (size_t)r.buf_limb * a.n + (tile % CT) * COLS + c;
+  r.off = poly * a.map.out_stride + e;
+  r.in_off = poly * a.map.in_stride + e;
   return r;
 }
 
@@ -398,7 +407,7 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_col(KArgs a) {
   int tile = blockIdx.x;  // workgroup-uniform
   if (tile >= ntiles) return;
   uint64_t xn[E];
-  col_load<S1_LOG, S2_LOG, RF>(xn, a.in + col_ref<S2_LOG>(a, tile, c).off, pf);
+  col_load<S1_LOG, S2_LOG, RF>(xn, a.in + col_ref<S2_LOG>(a, tile, c).in_off, pf);
   for (;;) {
     const TileRef tr = col_ref<S2_LOG>(a, tile, c);
     const int next = tile + gridDim.x;
@@ -415,7 +424,7 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_col(KArgs a) {
         constexpr int R = decltype(rc)::value;
         load_tw<S1_LOG, R>(w[R], tab, Round<S1_LOG, R>::p_thread(t), 1);
       });
-      if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, a.in + col_ref<S2_LOG>(a, next, c).off, pf);
+      if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, a.in + col_ref<S2_LOG>(a, next, c).in_off, pf);
       double v[E];
 #pragma unroll
       for (int j = 0; j < E; ++j) v[j] = FWD ? u52_to_f64(x[j]) : as_f64(x[j]);
@@ -448,7 +457,7 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_col(KArgs a) {
       const uint64_t* tws = a.tws + (size_t)tr.row * a.n;
       // integer path (primes >= 2^50): twiddles and Shoup quotients per round, after the
       // prefetch (fewer registers; such tiles wait for the prefetch)
-      if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, a.in + col_ref<S2_LOG>(a, next, c).off, pf);
+      if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, a.in + col_ref<S2_LOG>(a, next, c).in_off, pf);
       uint64_t(&v)[E] = x;
       static_for<RN>([&](auto rc) {
         constexpr int R = FWD ? decltype(rc)::value : RN - 1 - decltype(rc)::value;
@@ -495,11 +504,15 @@ template <int S1_LOG, int S2_LOG>
 __device__ __forceinline__ TileRef row_ref(const KArgs& a, int item, uint32_t lr, uint32_t t, uint32_t& r) {
   constexpr int S2 = 1 << S2_LOG, RW = cmin(64 / Sub<S2_LOG>::T, 1 << S1_LOG), GROUPS = (1 << S1_LOG) / RW;
   TileRef tr;
-  resolve_limb(a.map, item / GROUPS, tr.buf_limb, tr.row);
+  int poly;
+  resolve_limb(a, item / GROUPS, poly, tr.buf_limb, tr.row);
+  poly = __builtin_amdgcn_readfirstlane(poly);
   tr.buf_limb = __builtin_amdgcn_readfirstlane(tr.buf_limb);
   tr.row = __builtin_amdgcn_readfirstlane(tr.row);
   r = (item % GROUPS) * RW + lr;
-  tr.off = (size_t)tr.buf_limb * a.n + (size_t)r * S2 + t;
+  const size_t e = (size_t)tr.buf_limb * a.n + (size_t)r * S2 + t;
+  tr.off = poly * a.map.out_stride + e;
+  tr.in_off = poly * a.map.in_stride + e;
   return tr;
 }
 
@@ -535,7 +548,7 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
   if (item >= nitems) return;  // no workgroup barrier in this kernel
   uint32_t r;
   uint64_t xn[E];
-  row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, item, lr, t, r).off);
+  row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, item, lr, t, r).in_off);
   for (;;) {
     const TileRef tr = row_ref<S1_LOG, S2_LOG>(a, item, lr, t, r);
     const int next = item + step;
@@ -576,7 +589,7 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
           }
         }
       });
-      if (kPrefetch && more) row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, next, lr, t, rn).off);
+      if (kPrefetch && more) row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, next, lr, t, rn).in_off);
 #pragma unroll
       for (int k = 0; k < K0; ++k) {
         const uint32_t e = t + 1 + T * k;
@@ -629,7 +642,7 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
       const uint32_t B = (1u << S1_LOG) + r;
       const uint64_t* tw = a.tw + (size_t)tr.row * a.n;
       const uint64_t* tws = a.tws + (size_t)tr.row * a.n;
-      if (kPrefetch && more) row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, next, lr, t, rn).off);
+      if (kPrefetch && more) row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, next, lr, t, rn).in_off);
       uint64_t(&v)[E] = x;
       auto get_tw = [&](auto rc, uint64_t (&w)[E], uint64_t (&ws)[E]) {
         constexpr int R = decltype(rc)::value;
@@ -682,8 +695,9 @@ int num_cus() {
 template <int S1_LOG, int S2_LOG>
 hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const LimbMap& map, bool inverse,
                   const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream) {
-  const int limbs = map.num_limbs - (map.skip_end - map.skip_begin);
-  if (limbs <= 0) return hipSuccess;
+  const int per_poly = map.num_limbs - (map.skip_end - map.skip_begin);
+  if (per_poly <= 0 || map.polys <= 0) return hipSuccess;
+  const int limbs = per_poly * map.polys;
   KArgs a;
   a.in = in; a.out = out; a.modulus = tb.modulus;
   a.modulus_f = tb.modulus_f; a.modulus_inv = tb.modulus_inv;
@@ -694,7 +708,9 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   a.row_b = inverse ? tb.row_b_inv : tb.row_b_fwd;
   a.n_inv = tb.n_inv; a.n_inv_shoup = tb.n_inv_shoup;
   a.scale = scale; a.scale_shoup = scale_shoup;
-  a.map = map; a.n = (int)tb.n; a.limbs = limbs;
+  a.map = map; a.n = (int)tb.n; a.limbs = limbs; a.limbs_per_poly = per_poly;
+  if (a.map.in_stride == 0) a.map.in_stride = (size_t)map.num_limbs * tb.n;
+  if (a.map.out_stride == 0) a.map.out_stride = (size_t)map.num_limbs * tb.n;
   constexpr int S1 = 1 << S1_LOG, S2 = 1 << S2_LOG;
   constexpr int RW = cmin(64 / Sub<S2_LOG>::T, S1);
   const int col_tiles = limbs * (S2 / COLS);
@@ -708,10 +724,12 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   if (!inverse) {
     hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true>), grid_c, block_c, 0, stream, a);
     a.in = out;
+    a.map.in_stride = a.map.out_stride;
     hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true>), grid_r, block_r, 0, stream, a);
   } else {
     hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false>), grid_r, block_r, 0, stream, a);
     a.in = out;
+    a.map.in_stride = a.map.out_stride;
     hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false>), grid_c, block_c, 0, stream, a);
   }
   return hipGetLastError();

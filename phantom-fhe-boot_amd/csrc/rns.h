@@ -20,19 +20,23 @@ struct ModView {
 };
 
 // ---- elementwise, all [L][n] limb-major, one modulus per limb -------------------------
+// `polys` polynomials per launch: a and out contiguous [polys][L][n]; b at b + p * b_stride
+// (kContiguous: [polys][L][n] too; 0: the same b for every polynomial, e.g. a plaintext)
+constexpr size_t kContiguous = ~size_t(0);
 hipError_t poly_add(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
-                    hipStream_t s);
+                    hipStream_t s, size_t polys = 1, size_t b_stride = kContiguous);
 hipError_t poly_sub(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
-                    hipStream_t s);
-hipError_t poly_negate(const uint64_t* a, uint64_t* out, ModView m, size_t n, size_t L, hipStream_t s);
+                    hipStream_t s, size_t polys = 1, size_t b_stride = kContiguous);
+hipError_t poly_negate(const uint64_t* a, uint64_t* out, ModView m, size_t n, size_t L, hipStream_t s,
+                       size_t polys = 1);
 hipError_t poly_mul(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
-                    hipStream_t s);
+                    hipStream_t s, size_t polys = 1, size_t b_stride = kContiguous);
 // out = a * b + c
 hipError_t poly_mul_add(const uint64_t* a, const uint64_t* b, const uint64_t* c, uint64_t* out, ModView m,
                         size_t n, size_t L, hipStream_t s);
 // out[l] = a[l] * scalar[l] (scalar, scalar_shoup: device arrays of L)
 hipError_t poly_mul_scalar(const uint64_t* a, const uint64_t* scalar, const uint64_t* scalar_shoup, uint64_t* out,
-                           ModView m, size_t n, size_t L, hipStream_t s);
+                           ModView m, size_t n, size_t L, hipStream_t s, size_t polys = 1);
 // out[l] = a[l] + scalar[l]
 hipError_t poly_add_scalar(const uint64_t* a, const uint64_t* scalar, uint64_t* out, ModView m, size_t n,
                            size_t L, hipStream_t s);
@@ -59,6 +63,10 @@ struct BconvArgs {
   int obase_size = 0;
   int skip_at = 1 << 30;
   int skip_len = 0;
+  // batch: `polys` inputs at in + p * in_stride, outputs at out + p * out_stride (elements)
+  int polys = 1;
+  size_t in_stride = 0;
+  size_t out_stride = 0;
 };
 hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s);
 
@@ -75,22 +83,47 @@ hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const*
 // moddown tail + add_to_ct (src/ntt/ntt_moddown.cu:199-214, src/rns_bconv.cu:763-789):
 //   ct[j] = ct[j] + (cx[j] - delta[j]) * Pinv[j] mod q_j   (accumulate = true)
 //   ct[j] =         (cx[j] - delta[j]) * Pinv[j] mod q_j   (accumulate = false)
+// for `polys` polynomials: ct and delta contiguous [polys][size_ql][n], cx at cx + p * cx_stride
 hipError_t moddown_finish(uint64_t* ct, const uint64_t* cx, const uint64_t* delta, const uint64_t* pinv,
                           const uint64_t* pinv_shoup, const uint64_t* q, size_t n, size_t size_ql, bool accumulate,
-                          hipStream_t s);
+                          hipStream_t s, size_t polys = 1, size_t cx_stride = 0);
 
 // ---- rescale --------------------------------------------------------------------------
 // divide_and_round_reduce_q_last_kernel (src/rns.cu:1128-1139): tmp[j] = c_last mod q_j, j < L-1
+// for `polys` polynomials: c_last [polys][n], tmp [polys][L_next][n]
 hipError_t rescale_spread_last(const uint64_t* c_last, uint64_t* tmp, const uint64_t* q, const uint64_t* barrett,
-                               size_t n, size_t L_next, hipStream_t s);
+                               size_t n, size_t L_next, hipStream_t s, size_t polys = 1);
 // divide_and_round_ntt_inv_scalar_kernel (src/rns.cu:1141-1158): out[j] = (c[j] - tmp[j]) * qlast_inv[j]
+// for `polys` polynomials: c at c + p * c_stride (0: (L_next + 1) n), tmp and out contiguous
 hipError_t rescale_finish(const uint64_t* c, const uint64_t* tmp, uint64_t* out, const uint64_t* inv,
-                          const uint64_t* inv_shoup, const uint64_t* q, size_t n, size_t L_next, hipStream_t s);
+                          const uint64_t* inv_shoup, const uint64_t* q, size_t n, size_t L_next, hipStream_t s,
+                          size_t polys = 1, size_t c_stride = 0);
 
 // ---- automorphism ---------------------------------------------------------------------
 // apply_galois_ntt_permutation_direct (src/galois.cu:104-119): out[l][j] = in[l][perm[j]]
 hipError_t galois_ntt(const uint64_t* in, uint64_t* out, const uint32_t* perm, size_t n, size_t L,
                       hipStream_t s);
+
+// Hoisted-rotation epilogue (EvalFastRotationExt, src/evaluate.cu:3770-3860: add P c0, then
+// the NTT-domain automorphism), fused with the giant-step accumulation of the linear
+// transforms.  cx [2][qlp][n] is the key-switch output before the permutation:
+//   mode 0: x = cx
+//   mode 1: x = cx + (P c0 on the first ql limbs of polynomial 0)   c0 [ql][n], pmod per limb
+//   mode 2: x = cx + (c0 on every limb of polynomial 0)             c0 [qlp][n]
+//   out[t][l][j] = (accumulate ? out[t][l][j] : 0) + x[t][l][perm[j]]
+// q: the extended-basis moduli in buffer order.  out must not alias cx or c0.
+struct GaloisFinishArgs {
+  const uint64_t* cx;
+  const uint64_t* c0;
+  const uint64_t* pmod;
+  const uint64_t* pmod_shoup;
+  uint64_t* out;
+  const uint32_t* perm;
+  const uint64_t* q;
+  uint32_t ql = 0, qlp = 0;
+  bool accumulate = false;
+};
+hipError_t galois_finish(const GaloisFinishArgs& a, int mode, size_t n, hipStream_t s);
 
 // ---- bootstrap helpers ----------------------------------------------------------------
 // switchModulusKernel (src/evaluate.cu:2414-2457): lift limb-0 coefficients (mod q0) to L limbs

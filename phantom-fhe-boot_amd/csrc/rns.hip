@@ -24,6 +24,13 @@ int grid_for(size_t work_items) {
   return static_cast<int>(std::max<size_t>(1, std::min<size_t>(blocks, static_cast<size_t>(cus) * 8)));
 }
 
+// grid of a per-polynomial kernel: x covers one polynomial's work, y = polynomial
+dim3 poly_grid(size_t work_items, size_t polys) {
+  const int total = grid_for(work_items * polys);
+  const int x = std::max(1, (total + static_cast<int>(polys) - 1) / static_cast<int>(polys));
+  return dim3(static_cast<unsigned>(x), static_cast<unsigned>(polys));
+}
+
 using u64x2 = ulonglong2;
 
 __device__ __forceinline__ u64x2 ld2(const uint64_t* p) { return *reinterpret_cast<const u64x2*>(p); }
@@ -32,9 +39,14 @@ __device__ __forceinline__ void st2(uint64_t* p, uint64_t a, uint64_t b) {
 }
 
 // generic binary elementwise over [L][n] with per-limb modulus
+// blockIdx.y: polynomial (a and out contiguous [polys][L][n], b at b + y * b_stride)
 template <typename Op>
 __global__ __launch_bounds__(kBlock) void ew2_kernel(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b,
-                                                     uint64_t* out, ModView m, uint32_t log_n, size_t pairs, Op op) {
+                                                     uint64_t* out, ModView m, uint32_t log_n, size_t pairs, Op op,
+                                                     size_t b_stride) {
+  a += blockIdx.y * 2 * pairs;
+  out += blockIdx.y * 2 * pairs;
+  b += blockIdx.y * b_stride;
   for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
     const size_t e = 2 * i;
     const uint32_t l = static_cast<uint32_t>(e >> log_n);
@@ -63,6 +75,8 @@ struct MulOp {
 
 __global__ __launch_bounds__(kBlock) void negate_kernel(const uint64_t* __restrict__ a, uint64_t* out, ModView m,
                                                         uint32_t log_n, size_t pairs) {
+  a += blockIdx.y * 2 * pairs;  // blockIdx.y: polynomial
+  out += blockIdx.y * 2 * pairs;
   for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
     const size_t e = 2 * i;
     const uint64_t q = m.q[e >> log_n];
@@ -89,6 +103,8 @@ __global__ __launch_bounds__(kBlock) void mul_add_kernel(const uint64_t* __restr
 __global__ __launch_bounds__(kBlock) void mul_scalar_kernel(const uint64_t* __restrict__ a, const uint64_t* sc,
                                                             const uint64_t* scs, uint64_t* out, ModView m,
                                                             uint32_t log_n, size_t pairs) {
+  a += blockIdx.y * 2 * pairs;  // blockIdx.y: polynomial
+  out += blockIdx.y * 2 * pairs;
   for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
     const size_t e = 2 * i;
     const uint32_t l = static_cast<uint32_t>(e >> log_n);
@@ -178,6 +194,8 @@ __device__ __forceinline__ void bconv_inputs(const BconvArgs& a, uint64_t* tx, u
 }
 
 __global__ __launch_bounds__(kBlock) void bconv_kernel(BconvArgs a, uint32_t n, uint32_t pairs, bool prescale) {
+  a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial
+  a.out += blockIdx.z * a.out_stride;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= pairs) return;
   uint64_t tx[kMaxIbase], ty[kMaxIbase];
@@ -214,6 +232,8 @@ __global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32
   __syncthreads();
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= pairs) return;
+  a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial
+  a.out += blockIdx.z * a.out_stride;
   uint32_t lo[2][IB], hi[2][IB];
 #pragma unroll
   for (int s = 0; s < IB; ++s) {
@@ -299,7 +319,12 @@ __global__ __launch_bounds__(kBlock) void ks_inner_kernel(const uint64_t* __rest
 template <bool ACC>
 __global__ __launch_bounds__(kBlock) void moddown_finish_kernel(uint64_t* ct, const uint64_t* cx, const uint64_t* delta,
                                                                 const uint64_t* pinv, const uint64_t* pinvs,
-                                                                const uint64_t* q, uint32_t log_n, size_t pairs) {
+                                                                const uint64_t* q, uint32_t log_n, size_t pairs,
+                                                                size_t cx_stride) {
+  // blockIdx.y: polynomial (ct and delta contiguous [polys][Ql][n], cx strided)
+  ct += blockIdx.y * 2 * pairs;
+  delta += blockIdx.y * 2 * pairs;
+  cx += blockIdx.y * cx_stride;
   for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
     const size_t e = 2 * i;
     const uint32_t l = static_cast<uint32_t>(e >> log_n);
@@ -319,6 +344,8 @@ __global__ __launch_bounds__(kBlock) void moddown_finish_kernel(uint64_t* ct, co
 __global__ __launch_bounds__(kBlock) void rescale_spread_kernel(const uint64_t* c_last, uint64_t* tmp,
                                                                 const uint64_t* q, const uint64_t* qb, uint32_t log_n,
                                                                 size_t pairs) {
+  c_last += (size_t)blockIdx.y << log_n;  // blockIdx.y: polynomial
+  tmp += blockIdx.y * 2 * pairs;
   for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
     const size_t e = 2 * i;
     const uint32_t l = static_cast<uint32_t>(e >> log_n);
@@ -331,13 +358,40 @@ __global__ __launch_bounds__(kBlock) void rescale_spread_kernel(const uint64_t* 
 
 __global__ __launch_bounds__(kBlock) void rescale_finish_kernel(const uint64_t* c, const uint64_t* tmp, uint64_t* out,
                                                                 const uint64_t* inv, const uint64_t* invs,
-                                                                const uint64_t* q, uint32_t log_n, size_t pairs) {
+                                                                const uint64_t* q, uint32_t log_n, size_t pairs,
+                                                                size_t c_stride) {
+  c += blockIdx.y * c_stride;  // blockIdx.y: polynomial
+  tmp += blockIdx.y * 2 * pairs;
+  out += blockIdx.y * 2 * pairs;
   for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
     const size_t e = 2 * i;
     const uint32_t l = static_cast<uint32_t>(e >> log_n);
     const uint64_t m = q[l], w = inv[l], ws = invs[l];
     const u64x2 x = ld2(c + e), t = ld2(tmp + e);
     st2(out + e, mul_shoup(sub_mod(x.x, t.x, m), w, ws, m), mul_shoup(sub_mod(x.y, t.y, m), w, ws, m));
+  }
+}
+
+// hoisted-rotation epilogue: out[t][l][j] (+)= x[t][l][perm j] with x = cx + (t == 0 ? c0 term : 0)
+// (MODE 0: none, 1: P c0 on the Ql limbs, 2: an extended-basis c0 on every limb)
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void galois_finish_kernel(GaloisFinishArgs a, uint32_t log_n, size_t total) {
+  const size_t nmask = (size_t(1) << log_n) - 1;
+  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
+    const uint32_t row = static_cast<uint32_t>(e >> log_n);  // t * QlP + l
+    const uint32_t t = row >= a.qlp ? 1 : 0, l = row - t * a.qlp;
+    const size_t src = (e & ~nmask) | a.perm[e & nmask];
+    const uint64_t q = a.q[l];
+    uint64_t v = a.cx[src];
+    if (t == 0) {
+      if constexpr (MODE == 1) {
+        if (l < a.ql) v = add_mod(v, mul_shoup(a.c0[src], a.pmod[l], a.pmod_shoup[l], q), q);
+      } else if constexpr (MODE == 2) {
+        v = add_mod(v, a.c0[src], q);
+      }
+    }
+    if (a.accumulate) v = add_mod(v, a.out[e], q);
+    a.out[e] = v;
   }
 }
 
@@ -374,29 +428,33 @@ __global__ __launch_bounds__(kBlock) void raise_kernel(const uint64_t* in_q0, ui
 }  // namespace
 
 hipError_t poly_add(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
-                    hipStream_t s) {
+                    hipStream_t s, size_t polys, size_t b_stride) {
   const size_t pairs = n * L / 2;
-  ew2_kernel<<<grid_for(pairs), kBlock, 0, s>>>(a, b, out, m, __builtin_ctzll(n), pairs, AddOp{});
+  ew2_kernel<<<poly_grid(pairs, polys), kBlock, 0, s>>>(a, b, out, m, __builtin_ctzll(n), pairs, AddOp{},
+                                                        b_stride == kContiguous ? n * L : b_stride);
   return hipGetLastError();
 }
 
 hipError_t poly_sub(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
-                    hipStream_t s) {
+                    hipStream_t s, size_t polys, size_t b_stride) {
   const size_t pairs = n * L / 2;
-  ew2_kernel<<<grid_for(pairs), kBlock, 0, s>>>(a, b, out, m, __builtin_ctzll(n), pairs, SubOp{});
+  ew2_kernel<<<poly_grid(pairs, polys), kBlock, 0, s>>>(a, b, out, m, __builtin_ctzll(n), pairs, SubOp{},
+                                                        b_stride == kContiguous ? n * L : b_stride);
   return hipGetLastError();
 }
 
 hipError_t poly_mul(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
-                    hipStream_t s) {
+                    hipStream_t s, size_t polys, size_t b_stride) {
   const size_t pairs = n * L / 2;
-  ew2_kernel<<<grid_for(pairs), kBlock, 0, s>>>(a, b, out, m, __builtin_ctzll(n), pairs, MulOp{});
+  ew2_kernel<<<poly_grid(pairs, polys), kBlock, 0, s>>>(a, b, out, m, __builtin_ctzll(n), pairs, MulOp{},
+                                                        b_stride == kContiguous ? n * L : b_stride);
   return hipGetLastError();
 }
 
-hipError_t poly_negate(const uint64_t* a, uint64_t* out, ModView m, size_t n, size_t L, hipStream_t s) {
+hipError_t poly_negate(const uint64_t* a, uint64_t* out, ModView m, size_t n, size_t L, hipStream_t s,
+                       size_t polys) {
   const size_t pairs = n * L / 2;
-  negate_kernel<<<grid_for(pairs), kBlock, 0, s>>>(a, out, m, __builtin_ctzll(n), pairs);
+  negate_kernel<<<poly_grid(pairs, polys), kBlock, 0, s>>>(a, out, m, __builtin_ctzll(n), pairs);
   return hipGetLastError();
 }
 
@@ -408,9 +466,9 @@ hipError_t poly_mul_add(const uint64_t* a, const uint64_t* b, const uint64_t* c,
 }
 
 hipError_t poly_mul_scalar(const uint64_t* a, const uint64_t* scalar, const uint64_t* scalar_shoup, uint64_t* out,
-                           ModView m, size_t n, size_t L, hipStream_t s) {
+                           ModView m, size_t n, size_t L, hipStream_t s, size_t polys) {
   const size_t pairs = n * L / 2;
-  mul_scalar_kernel<<<grid_for(pairs), kBlock, 0, s>>>(a, scalar, scalar_shoup, out, m, __builtin_ctzll(n), pairs);
+  mul_scalar_kernel<<<poly_grid(pairs, polys), kBlock, 0, s>>>(a, scalar, scalar_shoup, out, m, __builtin_ctzll(n), pairs);
   return hipGetLastError();
 }
 
@@ -431,7 +489,8 @@ hipError_t tensor_prod_2x2(const uint64_t* ct1, const uint64_t* ct2, uint64_t* o
 hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s) {
   if (a.ibase_size <= 0 || a.ibase_size > kMaxIbase || a.obase_size <= 0) return hipErrorInvalidValue;
   const uint32_t pairs = static_cast<uint32_t>(n / 2);
-  const dim3 g((pairs + kBlock - 1) / kBlock, (a.obase_size + kBconvJ - 1) / kBconvJ);
+  if (a.polys < 1) return hipErrorInvalidValue;
+  const dim3 g((pairs + kBlock - 1) / kBlock, (a.obase_size + kBconvJ - 1) / kBconvJ, a.polys);
   const bool pre = a.qhat_inv != nullptr;
   switch (a.ibase_size) {
 #define PHX_BCONV_CASE(K) \
@@ -465,29 +524,45 @@ hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const*
 
 hipError_t moddown_finish(uint64_t* ct, const uint64_t* cx, const uint64_t* delta, const uint64_t* pinv,
                           const uint64_t* pinv_shoup, const uint64_t* q, size_t n, size_t size_ql, bool accumulate,
-                          hipStream_t s) {
+                          hipStream_t s, size_t polys, size_t cx_stride) {
   const size_t pairs = n * size_ql / 2;
+  const dim3 g = poly_grid(pairs, polys);
   if (accumulate)
-    moddown_finish_kernel<true><<<grid_for(pairs), kBlock, 0, s>>>(ct, cx, delta, pinv, pinv_shoup, q,
-                                                                   __builtin_ctzll(n), pairs);
+    moddown_finish_kernel<true><<<g, kBlock, 0, s>>>(ct, cx, delta, pinv, pinv_shoup, q, __builtin_ctzll(n), pairs,
+                                                     cx_stride);
   else
-    moddown_finish_kernel<false><<<grid_for(pairs), kBlock, 0, s>>>(ct, cx, delta, pinv, pinv_shoup, q,
-                                                                    __builtin_ctzll(n), pairs);
+    moddown_finish_kernel<false><<<g, kBlock, 0, s>>>(ct, cx, delta, pinv, pinv_shoup, q, __builtin_ctzll(n), pairs,
+                                                      cx_stride);
   return hipGetLastError();
 }
 
 hipError_t rescale_spread_last(const uint64_t* c_last, uint64_t* tmp, const uint64_t* q, const uint64_t* barrett,
-                               size_t n, size_t L_next, hipStream_t s) {
+                               size_t n, size_t L_next, hipStream_t s, size_t polys) {
   const size_t pairs = n * L_next / 2;
-  rescale_spread_kernel<<<grid_for(pairs), kBlock, 0, s>>>(c_last, tmp, q, barrett, __builtin_ctzll(n), pairs);
+  const dim3 g = poly_grid(pairs, polys);
+  rescale_spread_kernel<<<g, kBlock, 0, s>>>(c_last, tmp, q, barrett, __builtin_ctzll(n), pairs);
   return hipGetLastError();
 }
 
 hipError_t rescale_finish(const uint64_t* c, const uint64_t* tmp, uint64_t* out, const uint64_t* inv,
-                          const uint64_t* inv_shoup, const uint64_t* q, size_t n, size_t L_next, hipStream_t s) {
+                          const uint64_t* inv_shoup, const uint64_t* q, size_t n, size_t L_next, hipStream_t s,
+                          size_t polys, size_t c_stride) {
   const size_t pairs = n * L_next / 2;
-  rescale_finish_kernel<<<grid_for(pairs), kBlock, 0, s>>>(c, tmp, out, inv, inv_shoup, q, __builtin_ctzll(n),
-                                                           pairs);
+  const dim3 g = poly_grid(pairs, polys);
+  rescale_finish_kernel<<<g, kBlock, 0, s>>>(c, tmp, out, inv, inv_shoup, q, __builtin_ctzll(n), pairs,
+                                             c_stride ? c_stride : n * (L_next + 1));
+  return hipGetLastError();
+}
+
+hipError_t galois_finish(const GaloisFinishArgs& a, int mode, size_t n, hipStream_t s) {
+  const size_t total = 2 * n * a.qlp;
+  const uint32_t log_n = __builtin_ctzll(n);
+  switch (mode) {
+    case 0: galois_finish_kernel<0><<<grid_for(total), kBlock, 0, s>>>(a, log_n, total); break;
+    case 1: galois_finish_kernel<1><<<grid_for(total), kBlock, 0, s>>>(a, log_n, total); break;
+    case 2: galois_finish_kernel<2><<<grid_for(total), kBlock, 0, s>>>(a, log_n, total); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -168,23 +168,23 @@ struct ChebEvaluator {
     size_t lvl = level_of(get(1));
     for (int i = 1; i <= d; ++i) lvl = std::max(lvl, level_of(get(i)));
     const double target = sf.at(lvl) * sf.at(lvl);
+    // one kernel per term: acc (+)= round(c_i target / scale_i) * T_i, T_i's extra limbs dropped
     PhantomCiphertext acc;
     bool have = false;
     for (int i = 1; i <= d; ++i) {
       if (c[i] == 0.0) continue;
-      PhantomCiphertext t = get(i);
-      if (level_of(t) < lvl) mod_switch_to_inplace(cc, t, lvl + 1);
-      mult_by_real_integer_inplace(cc, t, c[i] * target / t.scale());
-      t.set_scale(target);
-      t.SetNoiseScaleDeg(2);
+      const PhantomCiphertext& t = get(i);
+      const double k = c[i] * target / t.scale();
       if (!have) {
-        acc = std::move(t);
+        acc = ScaledModSwitch(cc, t, lvl + 1, k);
         have = true;
       } else {
-        add_inplace(cc, acc, t);
+        AccumulateScaled(cc, acc, t, k);
       }
     }
     if (!have) throw std::invalid_argument("constant Chebyshev leaf");
+    acc.set_scale(target);
+    acc.SetNoiseScaleDeg(2);
     EvalAddConstInplace(cc, acc, c[0]);
     EvalModReduceInPlace(cc, acc, 1);
     return acc;
@@ -273,9 +273,20 @@ void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const s
       encoder_.encode_ext(cc, rot, scale, *pt, lv.chain);
       lv.pts[u] = std::move(pt);
     }
-    std::vector<const uint64_t*> ptrs(lv.D, nullptr);
-    for (int u = 0; u < lv.D; ++u)
-      if (lv.pts[u]) ptrs[u] = lv.pts[u]->data();
+    // pointer table [b][g] for the kernel; absent diagonals read a zero plaintext
+    std::vector<const uint64_t*> ptrs(static_cast<size_t>(lv.b) * lv.g, nullptr);
+    for (size_t u = 0; u < ptrs.size(); ++u) {
+      if (u < static_cast<size_t>(lv.D) && lv.pts[u]) {
+        ptrs[u] = lv.pts[u]->data();
+        continue;
+      }
+      if (!lv.zero) {
+        const size_t limbs = cc.get_context_data(lv.chain).coeff_modulus_size() + cc.size_P();
+        lv.zero.allocate(limbs * cc.poly_degree(), cc.stream());
+        PHX_CHECK(hipMemsetAsync(lv.zero.get(), 0, limbs * cc.poly_degree() * sizeof(uint64_t), cc.stream()));
+      }
+      ptrs[u] = lv.zero.get();
+    }
     lv.d_pts.upload(ptrs, cc.stream());
     if (lv.g > phx::kLtMaxG || lv.b > phx::kLtMaxB) throw std::invalid_argument("linear transform level too large");
     out.push_back(std::move(lv));
@@ -343,9 +354,8 @@ void FHECKKSRNS::EvalMultKeyGen(PhantomSecretKey& sk, const PhantomContext& cc) 
 
 PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const PhantomCiphertext& in,
                                           const LTLevel& lv) const {
-  PhantomCiphertext ct = in;
-  if (ct.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, ct, 1);
-  if (ct.chain_index() != lv.chain) AdjustToLevel(cc, ct, lv.chain - 1, sf_);
+  PhantomCiphertext tmp;
+  const PhantomCiphertext& ct = AtLevel(cc, in, lv.chain - 1, sf_, tmp);
   const size_t n = cc.poly_degree(), Ql = cc.get_context_data(ct.chain_index()).coeff_modulus_size();
   const size_t QlP = Ql + cc.size_P();
   hipStream_t s = cc.stream();
@@ -365,7 +375,6 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
   phx::LtArgs la;
   la.g = lv.g;
   la.b = lv.b;
-  la.D = lv.D;
   la.Ql = static_cast<int>(Ql);
   la.P = static_cast<int>(cc.size_P());
   la.size_Q = static_cast<int>(cc.size_Q());
@@ -374,10 +383,6 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
   la.barrett = cc.mod_QP().barrett;
   for (int j = 0; j < lv.g; ++j) la.baby[j] = baby[j].data();
   for (int i = 0; i < lv.b; ++i) {
-    bool any = false;
-    for (int j = 0; j < lv.g && lv.g * i + j < lv.D; ++j) any |= static_cast<bool>(lv.pts[lv.g * i + j]);
-    la.out[i] = nullptr;
-    if (!any) continue;
     inner[i].resize(2, QlP, n, s, false);
     inner[i].set_chain_index(ct.chain_index());
     inner[i].set_scale(ct.scale() * sf_.at(lv.chain - 1));
@@ -386,26 +391,18 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
   }
   hip_ok(phx::lt_bsgs(la, n, s), "linear transform inner products");
   baby.clear();
+  // giant steps accumulate in the extended basis; one moddown at the end
   PhantomCiphertext acc;
   bool have_acc = false;
-  for (int i = 0; i < lv.b; ++i) {
-    if (!la.out[i]) continue;
-    if (i == 0) {
-      acc = std::move(inner[0]);
-      have_acc = true;
-      continue;
-    }
-    PhantomCiphertext down = KeySwitchDown(cc, inner[i]);
+  if (la.out[0]) {
+    acc = std::move(inner[0]);
+    have_acc = true;
+  }
+  for (int i = 1; i < lv.b; ++i) {
+    EvalRotateExtAccumulate(cc, inner[i], galois_keys_, static_cast<int>(static_cast<long>(lv.g) * i * lv.stride), acc,
+                            have_acc);
+    have_acc = true;
     inner[i] = PhantomCiphertext();
-    DeviceBuffer<uint64_t> d2 = EvalFastRotationPrecompute(cc, down);
-    PhantomCiphertext rot =
-        EvalFastRotationExt(cc, down, galois_keys_, static_cast<int>(static_cast<long>(lv.g) * i * lv.stride), d2.get(), true);
-    if (!have_acc) {
-      acc = std::move(rot);
-      have_acc = true;
-    } else {
-      EvalAddExtInPlace(cc, acc, rot);
-    }
   }
   PhantomCiphertext res = KeySwitchDown(cc, acc);
   res.set_scale(ct.scale() * sf_.at(lv.chain - 1));
@@ -415,14 +412,14 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
 }
 
 PhantomCiphertext FHECKKSRNS::EvalCoeffsToSlots(const PhantomCiphertext& ct, const PhantomContext& cc) const {
-  PhantomCiphertext r = ct;
-  for (const LTLevel& lv : enc_) r = apply_level(cc, r, lv);
+  PhantomCiphertext r = apply_level(cc, ct, enc_.at(0));
+  for (size_t i = 1; i < enc_.size(); ++i) r = apply_level(cc, r, enc_[i]);
   return r;
 }
 
 PhantomCiphertext FHECKKSRNS::EvalSlotsToCoeffs(const PhantomCiphertext& ct, const PhantomContext& cc) const {
-  PhantomCiphertext r = ct;
-  for (const LTLevel& lv : dec_) r = apply_level(cc, r, lv);
+  PhantomCiphertext r = apply_level(cc, ct, dec_.at(0));
+  for (size_t i = 1; i < dec_.size(); ++i) r = apply_level(cc, r, dec_[i]);
   return r;
 }
 

@@ -84,7 +84,8 @@ class FHECKKSRNS {
     int stride = 1, center = 0, D = 0, g = 1, b = 1;
     size_t chain = 1;
     std::vector<std::unique_ptr<PhantomPlaintext>> pts;  // [D], pre-rotated by -g i stride; null = zero
-    DeviceBuffer<const uint64_t*> d_pts;                // device copy of the pts pointers
+    DeviceBuffer<const uint64_t*> d_pts;                // [b][g] device pointer table (zero-padded)
+    DeviceBuffer<uint64_t> zero;                        // the zero plaintext absent diagonals point at
   };
   void build_levels(const PhantomContext& cc, bool encode_dir, const std::vector<int>& group_sizes, double constant,
                     size_t first_chain, std::vector<LTLevel>& out) const;

@@ -16,6 +16,8 @@ void PhantomCiphertext::resize(size_t size, size_t L, size_t n, hipStream_t s, b
   const size_t old_count = size_ * L_ * n_, new_count = size * L * n;
   if (new_count == 0) {
     data_.release();
+  } else if (data_ && new_count <= data_.size()) {
+    // fits the current buffer: the leading data stays where it is (relinearize's 3 -> 2)
   } else if (new_count != old_count || !data_) {  // a moved-from ciphertext keeps its sizes
     DeviceBuffer<uint64_t> fresh(new_count, s);
     if (copy_old && data_ && old_count) {

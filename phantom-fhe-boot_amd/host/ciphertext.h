@@ -39,7 +39,8 @@ class PhantomCiphertext {
     return *this;
   }
 
-  // ciphertext.h:50-80: reallocate for (chain_index, size); keeps the leading old data.
+  // ciphertext.h:50-80: reallocate for (chain_index, size); keeps the leading old data.  A
+  // shrink that fits the current buffer keeps it (no copy).
   void resize(const PhantomContext& ctx, size_t chain_index, size_t size, hipStream_t s, bool copy_old = true);
   void resize(size_t size, size_t coeff_modulus_size, size_t n, hipStream_t s, bool copy_old = true);
 

@@ -78,16 +78,14 @@ void mult_by_real_integer_inplace(const PhantomContext& ctx, PhantomCiphertext& 
       c.v[l] = r[l];
       c.vs[l] = shoup(r[l], mods[l]);
     }
-    for (size_t i = 0; i < ct.size(); ++i)
-      hip_ok(phx::mul_scalar_v(ct.data() + i * L * n, c, ct.data() + i * L * n, ctx.mod_QP().q, n, L, ctx.stream()),
-             "mult by integer");
+    hip_ok(phx::mul_scalar_v(ct.data(), c, ct.data(), ctx.mod_QP().q, n, L, ctx.stream(), ct.size()),
+           "mult by integer");
     return;
   }
   Scalars sc = upload_scalars(r, mods, ctx.stream());
-  for (size_t i = 0; i < ct.size(); ++i)
-    hip_ok(phx::poly_mul_scalar(ct.data() + i * L * n, sc.v.get(), sc.vs.get(), ct.data() + i * L * n, ctx.mod_QP(), n, L,
-                                ctx.stream()),
-           "mult by integer");
+  hip_ok(phx::poly_mul_scalar(ct.data(), sc.v.get(), sc.vs.get(), ct.data(), ctx.mod_QP(), n, L, ctx.stream(),
+                              ct.size()),
+         "mult by integer");
 }
 
 void MultByIntegerInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, uint64_t k) {
@@ -142,8 +140,7 @@ void MultByMonomialInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, uin
     }
     mono = it->second.get();
   }
-  for (size_t i = 0; i < ct.size(); ++i)
-    hip_ok(phx::poly_mul(ct.data() + i * L * n, mono, ct.data() + i * L * n, ctx.mod_QP(), n, L, s), "monomial");
+  hip_ok(phx::poly_mul(ct.data(), mono, ct.data(), ctx.mod_QP(), n, L, s, ct.size(), 0), "monomial");
 }
 
 void EvalModReduceInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, size_t levels) {
@@ -154,61 +151,125 @@ void EvalModReduceInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, size
   }
 }
 
+// exact residues of round(k) at `chain` as kernel-argument constants (L <= kMaxScalarLimbs)
+static phx::LimbScalars limb_scalars(const PhantomContext& ctx, size_t chain, double k) {
+  const auto& mods = ctx.get_context_data(chain).moduli();
+  if (mods.size() > static_cast<size_t>(phx::kMaxScalarLimbs)) throw std::invalid_argument("too many limbs");
+  phx::LimbScalars c;
+  for (size_t l = 0; l < mods.size(); ++l) {
+    c.v[l] = residue_of_double(k, mods[l]);
+    c.vs[l] = shoup(c.v[l], mods[l]);
+  }
+  return c;
+}
+
+PhantomCiphertext ScaledModSwitch(const PhantomContext& ctx, const PhantomCiphertext& ct, size_t chain, double k) {
+  if (chain < ct.chain_index()) throw std::invalid_argument("cannot switch to higher level modulus");
+  const size_t n = ctx.poly_degree();
+  PhantomCiphertext out;
+  out.resize(ctx, chain, ct.size(), ctx.stream(), false);
+  const size_t L = out.coeff_modulus_size();
+  if (L > static_cast<size_t>(phx::kMaxScalarLimbs)) {
+    out = mod_switch_to(ctx, ct, chain);
+    mult_by_real_integer_inplace(ctx, out, k);
+    return out;
+  }
+  hip_ok(phx::mul_scalar_v(ct.data(), limb_scalars(ctx, chain, k), out.data(), ctx.mod_QP().q, n, L, ctx.stream(),
+                           ct.size(), ct.coeff_modulus_size() * n),
+         "scaled mod switch");
+  out.set_scale(ct.scale());
+  out.set_ntt_form(ct.is_ntt_form());
+  out.set_correction_factor(ct.correction_factor());
+  out.SetNoiseScaleDeg(ct.GetNoiseScaleDeg());
+  return out;
+}
+
+void AccumulateScaled(const PhantomContext& ctx, PhantomCiphertext& acc, const PhantomCiphertext& ct, double k) {
+  if (acc.chain_index() < ct.chain_index() || acc.size() != ct.size())
+    throw std::invalid_argument("accumulate: operand below the accumulator's level");
+  const size_t n = ctx.poly_degree(), L = acc.coeff_modulus_size();
+  hip_ok(phx::mul_scalar_v(ct.data(), limb_scalars(ctx, acc.chain_index(), k), acc.data(), ctx.mod_QP().q, n, L,
+                           ctx.stream(), ct.size(), ct.coeff_modulus_size() * n, acc.data()),
+         "accumulate scaled");
+}
+
+// degree-1 `ct` (level < target) -> level `target` at scale sf[target]: drop to level target - 1
+// and multiply by the integer that makes the next rescale land on sf[target], in one kernel,
+// then rescale
+static PhantomCiphertext adjusted(const PhantomContext& ctx, const PhantomCiphertext& ct, size_t target,
+                                  const std::vector<double>& sf) {
+  const size_t chain_mid = target;  // chain index = level + 1
+  const double qdrop = static_cast<double>(ctx.get_context_data(chain_mid).moduli().back());
+  const double k = sf.at(target) * qdrop / ct.scale();
+  PhantomCiphertext t = ScaledModSwitch(ctx, ct, chain_mid, k);
+  t.set_scale(ct.scale() * std::nearbyint(k));
+  t.SetNoiseScaleDeg(2);
+  PhantomCiphertext r = rescale_to_next(ctx, t);
+  r.SetNoiseScaleDeg(1);
+  r.set_scale(sf.at(target));
+  return r;
+}
+
+static size_t level_after_reduce(const PhantomCiphertext& ct) {
+  return level_of(ct) + (ct.GetNoiseScaleDeg() > 1 ? 1 : 0);
+}
+
+// `ct` at degree 1 and level `target` (>= its level after reduction): ct itself when it already
+// is, otherwise a new ciphertext held in `tmp`
+const PhantomCiphertext& AtLevel(const PhantomContext& ctx, const PhantomCiphertext& ct, size_t target,
+                                 const std::vector<double>& sf, PhantomCiphertext& tmp) {
+  if (ct.GetNoiseScaleDeg() <= 1 && level_of(ct) == target) return ct;
+  if (level_after_reduce(ct) > target) throw std::invalid_argument("cannot raise a ciphertext's level");
+  const PhantomCiphertext* src = &ct;
+  PhantomCiphertext reduced;
+  if (ct.GetNoiseScaleDeg() > 1) {
+    reduced = rescale_to_next(ctx, ct);
+    reduced.SetNoiseScaleDeg(ct.GetNoiseScaleDeg() - 1);
+    src = &reduced;
+  }
+  if (level_of(*src) == target) {
+    tmp = std::move(reduced);
+  } else {
+    tmp = adjusted(ctx, *src, target, sf);
+  }
+  return tmp;
+}
+
 void AdjustToLevel(const PhantomContext& ctx, PhantomCiphertext& ct, size_t target, const std::vector<double>& sf) {
   if (ct.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(ctx, ct, 1);
   const size_t lvl = level_of(ct);
   if (lvl > target) throw std::invalid_argument("cannot raise a ciphertext's level");
   if (lvl == target) return;
-  // drop limbs without scaling down to target - 1, then one scaling multiply + rescale to
-  // land exactly on sf[target]
-  if (lvl + 1 < target) mod_switch_to_inplace(ctx, ct, target);  // chain index = level + 1
-  const size_t from = level_of(ct);
-  const double qdrop = static_cast<double>(ctx.get_context_data(ct.chain_index()).moduli().back());
-  const double k = sf.at(target) * qdrop / ct.scale();
-  mult_by_real_integer_inplace(ctx, ct, k);
-  ct.set_scale(ct.scale() * std::nearbyint(k));
-  ct.SetNoiseScaleDeg(2);
-  EvalModReduceInPlace(ctx, ct, 1);
-  (void)from;
-  ct.set_scale(sf.at(target));
-}
-
-static void align(const PhantomContext& ctx, PhantomCiphertext& a, PhantomCiphertext& b, const std::vector<double>& sf) {
-  if (a.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(ctx, a, 1);
-  if (b.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(ctx, b, 1);
-  if (level_of(a) < level_of(b)) AdjustToLevel(ctx, a, level_of(b), sf);
-  else if (level_of(b) < level_of(a)) AdjustToLevel(ctx, b, level_of(a), sf);
+  ct = adjusted(ctx, ct, target, sf);
 }
 
 void EvalAddAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b,
                         const std::vector<double>& sf) {
-  PhantomCiphertext bb = b;
-  align(ctx, a, bb, sf);
-  add_inplace(ctx, a, bb);
+  const size_t target = std::max(level_after_reduce(a), level_after_reduce(b));
+  AdjustToLevel(ctx, a, target, sf);
+  PhantomCiphertext tmp;
+  add_inplace(ctx, a, AtLevel(ctx, b, target, sf, tmp));
 }
 
 void EvalSubAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b,
                         const std::vector<double>& sf) {
-  PhantomCiphertext bb = b;
-  align(ctx, a, bb, sf);
-  sub_inplace(ctx, a, bb);
+  const size_t target = std::max(level_after_reduce(a), level_after_reduce(b));
+  AdjustToLevel(ctx, a, target, sf);
+  PhantomCiphertext tmp;
+  sub_inplace(ctx, a, AtLevel(ctx, b, target, sf, tmp));
 }
 
 PhantomCiphertext EvalMultRescale(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
                                   const PhantomRelinKey& rlk, const std::vector<double>& sf) {
-  PhantomCiphertext x = a;
-  if (&a == &b) {
-    if (x.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(ctx, x, 1);
-    multiply_inplace(ctx, x, x);
-  } else {
-    PhantomCiphertext y = b;
-    align(ctx, x, y, sf);
-    multiply_inplace(ctx, x, y);
-  }
-  relinearize_inplace(ctx, x, rlk);
-  x.SetNoiseScaleDeg(2);
-  EvalModReduceInPlace(ctx, x, 1);
-  return x;
+  const size_t target = std::max(level_after_reduce(a), level_after_reduce(b));
+  PhantomCiphertext ta, tb;
+  const PhantomCiphertext& x = AtLevel(ctx, a, target, sf, ta);
+  const PhantomCiphertext& y = &a == &b ? x : AtLevel(ctx, b, target, sf, tb);
+  PhantomCiphertext d = multiply(ctx, x, y);
+  relinearize_inplace(ctx, d, rlk);
+  d.SetNoiseScaleDeg(2);
+  EvalModReduceInPlace(ctx, d, 1);
+  return d;
 }
 
 PhantomCiphertext RaiseMod(const PhantomContext& ctx, const PhantomCiphertext& ct) {
@@ -287,17 +348,59 @@ PhantomCiphertext EvalFastAutomorphismExt(const PhantomContext& ctx, const Phant
   hip_ok(phx::keyswitch_inner_prod(digits, keys.get(elt).public_keys_ptr(), cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n,
                                    Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s),
          "fast rotation inner product");
-  if (add_first)
-    hip_ok(phx::mul_scalar_add(ct.data(), rt.bigP_mod_q(), rt.bigP_mod_q_shoup(), cx, cx, ctx.mod_QP().q, n, Ql, s),
-           "add P c0");
   PhantomCiphertext out;
   out.resize(2, QlP, n, s, false);
   out.set_chain_index(ct.chain_index());
   out.set_scale(ct.scale());
   out.SetNoiseScaleDeg(ct.GetNoiseScaleDeg());
-  const uint32_t* perm = perm_table(ctx, elt);
-  hip_ok(phx::galois_ntt(cx, out.data(), perm, n, 2 * QlP, s), "fast rotation permute");
+  // + P c0, then the permutation, in one pass
+  phx::GaloisFinishArgs g;
+  g.cx = cx;
+  g.c0 = ct.data();
+  g.pmod = rt.bigP_mod_q();
+  g.pmod_shoup = rt.bigP_mod_q_shoup();
+  g.out = out.data();
+  g.perm = perm_table(ctx, elt);
+  g.q = rt.mod_QlP().q;
+  g.ql = static_cast<uint32_t>(Ql);
+  g.qlp = static_cast<uint32_t>(QlP);
+  hip_ok(phx::galois_finish(g, add_first ? 1 : 0, n, s), "fast rotation permute");
   return out;
+}
+
+void EvalRotateExtAccumulate(const PhantomContext& ctx, PhantomCiphertext& ext, const PhantomGaloisKey& keys,
+                             int index, PhantomCiphertext& acc, bool accumulate) {
+  const RnsTool& rt = ctx.get_context_data(ext.chain_index()).gpu_rns_tool();
+  const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P();
+  if (ext.size() != 2 || ext.coeff_modulus_size() != QlP) throw std::invalid_argument("not an extended-basis ciphertext");
+  hipStream_t s = ctx.stream();
+  const uint32_t elt = FindAutomorphismIndex2nComplex(index, n);
+  // only c1 comes down to Ql: it is what the key switch consumes; c0 stays P-scaled in QlP
+  DeviceBuffer<uint64_t> c1(Ql * n, s);
+  rt.moddown_add(c1.get(), ext.data() + QlP * n, false, ctx.gpu_rns_tables(), s, 1);
+  DeviceBuffer<uint64_t> digits(rt.beta() * QlP * n, s);
+  rt.modup(digits.get(), c1.get(), ctx.gpu_rns_tables(), s);
+  uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * QlP * n);
+  hip_ok(phx::keyswitch_inner_prod(digits.get(), keys.get(elt).public_keys_ptr(), cx, ctx.mod_QP().q,
+                                   ctx.mod_QP().barrett, n, Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s),
+         "giant step inner product");
+  if (!accumulate) {
+    acc.resize(2, QlP, n, s, false);
+    acc.set_chain_index(ext.chain_index());
+    acc.set_scale(ext.scale());
+    acc.SetNoiseScaleDeg(ext.GetNoiseScaleDeg());
+    acc.set_ntt_form(true);
+  }
+  phx::GaloisFinishArgs g;
+  g.cx = cx;
+  g.c0 = ext.data();
+  g.out = acc.data();
+  g.perm = perm_table(ctx, elt);
+  g.q = rt.mod_QlP().q;
+  g.ql = static_cast<uint32_t>(Ql);
+  g.qlp = static_cast<uint32_t>(QlP);
+  g.accumulate = accumulate;
+  hip_ok(phx::galois_finish(g, 2, n, s), "giant step permute + accumulate");
 }
 
 PhantomCiphertext EvalFastRotationExt(const PhantomContext& ctx, const PhantomCiphertext& ct,
@@ -326,36 +429,25 @@ PhantomCiphertext KeySwitchExt(const PhantomContext& ctx, const PhantomCiphertex
 
 PhantomCiphertext KeySwitchDown(const PhantomContext& ctx, PhantomCiphertext& ext) {
   const RnsTool& rt = ctx.get_context_data(ext.chain_index()).gpu_rns_tool();
-  const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P();
+  const size_t Ql = rt.size_Ql(), QlP = Ql + ctx.size_P();
   if (ext.coeff_modulus_size() != QlP) throw std::invalid_argument("not an extended-basis ciphertext");
   hipStream_t s = ctx.stream();
   PhantomCiphertext out;
   out.resize(ctx, ext.chain_index(), 2, s, false);
-  for (size_t i = 0; i < 2; ++i)
-    rt.moddown_add(out.data() + i * Ql * n, ext.data() + i * QlP * n, false, ctx.gpu_rns_tables(), s);
+  rt.moddown_add(out.data(), ext.data(), false, ctx.gpu_rns_tables(), s, 2);
   out.set_scale(ext.scale());
   out.SetNoiseScaleDeg(ext.GetNoiseScaleDeg());
   out.set_ntt_form(true);
   return out;
 }
 
-static void ext_binary(const PhantomContext& ctx, uint64_t* a, const uint64_t* b, size_t b_stride, size_t polys,
-                       size_t Ql, bool mul) {
-  const size_t n = ctx.poly_degree(), P = ctx.size_P(), QlP = Ql + P;
-  hipStream_t s = ctx.stream();
-  const phx::ModView mq = ctx.mod_QP();
-  const phx::ModView mp{mq.q + ctx.size_Q(), mq.barrett + 2 * ctx.size_Q()};
-  for (size_t i = 0; i < polys; ++i) {
-    uint64_t* x = a + i * QlP * n;
-    const uint64_t* y = b + i * b_stride;
-    if (mul) {
-      hip_ok(phx::poly_mul(x, y, x, mq, n, Ql, s), "ext mul Ql");
-      hip_ok(phx::poly_mul(x + Ql * n, y + Ql * n, x + Ql * n, mp, n, P, s), "ext mul P");
-    } else {
-      hip_ok(phx::poly_add(x, y, x, mq, n, Ql, s), "ext add Ql");
-      hip_ok(phx::poly_add(x + Ql * n, y + Ql * n, x + Ql * n, mp, n, P, s), "ext add P");
-    }
-  }
+// one launch over both polynomials of an extended-basis ciphertext (moduli Ql u P)
+static void ext_binary(const PhantomContext& ctx, size_t chain, uint64_t* a, const uint64_t* b, size_t b_stride,
+                       size_t polys, bool mul) {
+  const RnsTool& rt = ctx.get_context_data(chain).gpu_rns_tool();
+  const size_t n = ctx.poly_degree(), QlP = rt.size_Ql() + ctx.size_P();
+  if (mul) hip_ok(phx::poly_mul(a, b, a, rt.mod_QlP(), n, QlP, ctx.stream(), polys, b_stride), "ext mul");
+  else hip_ok(phx::poly_add(a, b, a, rt.mod_QlP(), n, QlP, ctx.stream(), polys, b_stride), "ext add");
 }
 
 void EvalMultExtInPlace(const PhantomContext& ctx, PhantomCiphertext& ext, const PhantomPlaintext& pt) {
@@ -363,7 +455,7 @@ void EvalMultExtInPlace(const PhantomContext& ctx, PhantomCiphertext& ext, const
   const size_t Ql = ctx.get_context_data(ext.chain_index()).coeff_modulus_size();
   if (pt.coeff_modulus_size() != Ql + ctx.size_P() || ext.coeff_modulus_size() != Ql + ctx.size_P())
     throw std::invalid_argument("Eval Mult Ext: operands are not in the extended basis");
-  ext_binary(ctx, ext.data(), pt.data(), 0, 2, Ql, true);
+  ext_binary(ctx, ext.chain_index(), ext.data(), pt.data(), 0, 2, true);
   ext.set_scale(ext.scale() * pt.scale());
   ext.SetNoiseScaleDeg(ext.GetNoiseScaleDeg() + pt.GetNoiseScaleDeg());
 }
@@ -372,7 +464,7 @@ void EvalAddExtInPlace(const PhantomContext& ctx, PhantomCiphertext& a, const Ph
   if (a.chain_index() != b.chain_index() || a.GetNoiseScaleDeg() != b.GetNoiseScaleDeg())
     throw std::invalid_argument("Eval Add Ext Failed.");
   const size_t Ql = ctx.get_context_data(a.chain_index()).coeff_modulus_size();
-  ext_binary(ctx, a.data(), b.data(), (Ql + ctx.size_P()) * ctx.poly_degree(), 2, Ql, false);
+  ext_binary(ctx, a.chain_index(), a.data(), b.data(), (Ql + ctx.size_P()) * ctx.poly_degree(), 2, false);
 }
 
 PhantomCiphertext EvalRotateFused(const PhantomContext& ctx, const PhantomCiphertext& ct, const PhantomGaloisKey& keys,

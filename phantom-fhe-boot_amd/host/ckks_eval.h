@@ -41,6 +41,15 @@ void EvalModReduceInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, size
 // then one scaling multiply + rescale (AdjustLevelsAndDepth of FLEXIBLEAUTO)
 void AdjustToLevel(const PhantomContext& ctx, PhantomCiphertext& ct, size_t target_level,
                    const std::vector<double>& sf);
+// round(k) * (the leading limbs of ct at `chain`) as a new ciphertext, one kernel (metadata of
+// ct; the caller sets the scale)
+PhantomCiphertext ScaledModSwitch(const PhantomContext& ctx, const PhantomCiphertext& ct, size_t chain, double k);
+// acc += round(k) * ct, ct at acc's level or above (its extra limbs are ignored); one kernel
+void AccumulateScaled(const PhantomContext& ctx, PhantomCiphertext& acc, const PhantomCiphertext& ct, double k);
+// `ct` at noise degree 1 and level `target` (>= its level after one rescale): ct itself when it
+// already is, else a new ciphertext stored in `tmp` (no copy when nothing is to be done)
+const PhantomCiphertext& AtLevel(const PhantomContext& ctx, const PhantomCiphertext& ct, size_t target,
+                                 const std::vector<double>& sf, PhantomCiphertext& tmp);
 // EvalAddAutoInplace / EvalSubAuto: level- and scale-aligned add / subtract
 void EvalAddAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b,
                         const std::vector<double>& sf);
@@ -66,6 +75,13 @@ PhantomCiphertext EvalFastRotationExt(const PhantomContext& ctx, const PhantomCi
 PhantomCiphertext EvalFastAutomorphismExt(const PhantomContext& ctx, const PhantomCiphertext& ct,
                                           const PhantomGaloisKey& fused_keys, uint32_t galois_elt,
                                           const uint64_t* digits, bool add_first);
+// Giant step of a hoisted linear transform: acc (+)= rotation by `index` of the extended-basis
+// ciphertext `ext` (P-scaled, as EvalFastRotationExt outputs and their plaintext products are).
+// Only c1 is brought down to Ql, key switched and permuted; c0 is added in the extended basis
+// (one moddown instead of two, and no rounding of c0).  `ext`'s c1 P limbs are clobbered;
+// accumulate = false initialises acc.
+void EvalRotateExtAccumulate(const PhantomContext& ctx, PhantomCiphertext& ext, const PhantomGaloisKey& fused_keys,
+                             int index, PhantomCiphertext& acc, bool accumulate);
 // KeySwitchExt: (c0, c1) -> P * (c0, c1) in the extended basis
 PhantomCiphertext KeySwitchExt(const PhantomContext& ctx, const PhantomCiphertext& ct);
 // KeySwitchDown: extended -> Ql (moddown of both polynomials); `ext` is consumed (its P limbs

@@ -28,8 +28,7 @@ void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, 
   hip_ok(phx::keyswitch_inner_prod(t_mod_up, evk, cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, size_Ql,
                                    ctx.size_Q(), ctx.size_P(), beta, s),
          "keyswitch inner product");
-  for (size_t i = 0; i < 2; ++i)
-    rt.moddown_add(ct + i * size_Ql * n, cx + i * size_QlP * n, true, ctx.gpu_rns_tables(), s);
+  rt.moddown_add(ct, cx, true, ctx.gpu_rns_tables(), s, 2);
 }
 
 void keyswitch_inplace(const PhantomContext& ctx, PhantomCiphertext& ct, const uint64_t* c2,
@@ -46,27 +45,22 @@ void add_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomC
   check_same(a, b);
   if (a.size() != b.size()) throw std::invalid_argument("poly number mismatch");
   const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
-  for (size_t i = 0; i < a.size(); ++i)
-    hip_ok(phx::poly_add(a.data() + i * L * n, b.data() + i * L * n, a.data() + i * L * n, ctx.mod_QP(), n, L,
-                         ctx.stream()),
-           "add");
+  hip_ok(phx::poly_add(a.data(), b.data(), a.data(), ctx.mod_QP(), n, L, ctx.stream(), a.size()), "add");
 }
 
 void sub_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b, bool negate) {
   check_same(a, b);
+  if (a.size() != b.size()) throw std::invalid_argument("poly number mismatch");
   const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
-  for (size_t i = 0; i < a.size(); ++i) {
-    uint64_t* x = a.data() + i * L * n;
-    const uint64_t* y = b.data() + i * L * n;
-    if (negate) hip_ok(phx::poly_sub(y, x, x, ctx.mod_QP(), n, L, ctx.stream()), "sub");
-    else hip_ok(phx::poly_sub(x, y, x, ctx.mod_QP(), n, L, ctx.stream()), "sub");
-  }
+  uint64_t* x = a.data();
+  const uint64_t* y = b.data();
+  if (negate) hip_ok(phx::poly_sub(y, x, x, ctx.mod_QP(), n, L, ctx.stream(), a.size()), "sub");
+  else hip_ok(phx::poly_sub(x, y, x, ctx.mod_QP(), n, L, ctx.stream(), a.size()), "sub");
 }
 
 void negate_inplace(const PhantomContext& ctx, PhantomCiphertext& a) {
   const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
-  for (size_t i = 0; i < a.size(); ++i)
-    hip_ok(phx::poly_negate(a.data() + i * L * n, a.data() + i * L * n, ctx.mod_QP(), n, L, ctx.stream()), "negate");
+  hip_ok(phx::poly_negate(a.data(), a.data(), ctx.mod_QP(), n, L, ctx.stream(), a.size()), "negate");
 }
 
 void add_plain_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomPlaintext& p) {
@@ -79,23 +73,30 @@ void add_plain_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const Ph
 void multiply_plain_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomPlaintext& p) {
   if (a.chain_index() != p.chain_index()) throw std::invalid_argument("encrypted and plain parameter mismatch");
   const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
-  for (size_t i = 0; i < a.size(); ++i)
-    hip_ok(phx::poly_mul(a.data() + i * L * n, p.data(), a.data() + i * L * n, ctx.mod_QP(), n, L, ctx.stream()),
-           "multiply_plain");
+  hip_ok(phx::poly_mul(a.data(), p.data(), a.data(), ctx.mod_QP(), n, L, ctx.stream(), a.size(), 0),
+         "multiply_plain");
   a.set_scale(a.scale() * p.scale());
 }
 
-void multiply_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b) {
+PhantomCiphertext multiply(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b) {
   check_same(a, b);
   if (!a.is_ntt_form()) throw std::invalid_argument("encrypted1 and encrypted2 must be in NTT form");
   if (a.size() != 2 || b.size() != 2) throw std::invalid_argument("only size-2 ciphertexts are supported");
   const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
   hipStream_t s = ctx.stream();
-  a.resize(ctx, a.chain_index(), 3, s);
-  // tensor_prod_2x2 reads (a0, a1) and writes (d0, d1, d2) in place: every element is read
-  // before the same thread writes it, so aliasing out with ct1 is safe.
-  hip_ok(phx::tensor_prod_2x2(a.data(), &a == &b ? a.data() : b.data(), a.data(), ctx.mod_QP(), n, L, s), "tensor");
-  a.set_scale(a.scale() * b.scale());
+  // the tensor product goes straight into a fresh 3-polynomial buffer: no copy of a
+  PhantomCiphertext d;
+  d.resize(ctx, a.chain_index(), 3, s, false);
+  hip_ok(phx::tensor_prod_2x2(a.data(), b.data(), d.data(), ctx.mod_QP(), n, L, s), "tensor");
+  d.set_ntt_form(true);
+  d.set_scale(a.scale() * b.scale());
+  d.set_correction_factor(a.correction_factor());
+  d.SetNoiseScaleDeg(a.GetNoiseScaleDeg());
+  return d;
+}
+
+void multiply_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b) {
+  a = multiply(ctx, a, b);
 }
 
 void relinearize_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomRelinKey& rlk) {
@@ -118,23 +119,30 @@ PhantomCiphertext rescale_to_next(const PhantomContext& ctx, const PhantomCipher
   return d;
 }
 
-PhantomCiphertext mod_switch_to_next(const PhantomContext& ctx, const PhantomCiphertext& a) {
-  if (a.chain_index() + 1 >= ctx.total_parm_size()) throw std::invalid_argument("end of modulus switching chain reached");
+PhantomCiphertext mod_switch_to(const PhantomContext& ctx, const PhantomCiphertext& a, size_t chain_index) {
+  if (chain_index >= ctx.total_parm_size()) throw std::invalid_argument("end of modulus switching chain reached");
+  if (chain_index < a.chain_index()) throw std::invalid_argument("cannot switch to higher level modulus");
   const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
   PhantomCiphertext d;
-  d.resize(ctx, a.chain_index() + 1, a.size(), ctx.stream(), false);
-  for (size_t i = 0; i < a.size(); ++i)
-    PHX_CHECK(hipMemcpyAsync(d.data() + i * (L - 1) * n, a.data() + i * L * n, (L - 1) * n * sizeof(uint64_t),
-                             hipMemcpyDeviceToDevice, ctx.stream()));
+  d.resize(ctx, chain_index, a.size(), ctx.stream(), false);
+  const size_t Ld = d.coeff_modulus_size();
+  // every polynomial's leading Ld limbs in one strided copy
+  PHX_CHECK(hipMemcpy2DAsync(d.data(), Ld * n * sizeof(uint64_t), a.data(), L * n * sizeof(uint64_t),
+                             Ld * n * sizeof(uint64_t), a.size(), hipMemcpyDeviceToDevice, ctx.stream()));
   d.set_scale(a.scale());
   d.set_ntt_form(a.is_ntt_form());
+  d.set_correction_factor(a.correction_factor());
   d.SetNoiseScaleDeg(a.GetNoiseScaleDeg());
   return d;
 }
 
+PhantomCiphertext mod_switch_to_next(const PhantomContext& ctx, const PhantomCiphertext& a) {
+  return mod_switch_to(ctx, a, a.chain_index() + 1);
+}
+
 void mod_switch_to_inplace(const PhantomContext& ctx, PhantomCiphertext& a, size_t chain_index) {
   if (chain_index < a.chain_index()) throw std::invalid_argument("cannot switch to higher level modulus");
-  while (a.chain_index() < chain_index) a = mod_switch_to_next(ctx, a);
+  if (chain_index > a.chain_index()) a = mod_switch_to(ctx, a, chain_index);
 }
 
 // NTT-domain permutation tables per Galois element (PrecomputeAutoMapKernel, src/util.cu:941-958),

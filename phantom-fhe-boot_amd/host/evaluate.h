@@ -25,11 +25,7 @@ void multiply_plain_inplace(const PhantomContext& ctx, PhantomCiphertext& a, con
 
 // multiply_inplace (src/evaluate.cu:1183-1216 -> bgv_ckks_multiply :415-473)
 void multiply_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b);
-inline PhantomCiphertext multiply(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b) {
-  PhantomCiphertext d = a;
-  multiply_inplace(ctx, d, b);
-  return d;
-}
+PhantomCiphertext multiply(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b);
 
 // relinearize_inplace (src/evaluate.cu:1552-1589)
 void relinearize_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomRelinKey& rlk);
@@ -49,6 +45,8 @@ inline void mod_switch_to_next_inplace(const PhantomContext& ctx, PhantomCiphert
   a = mod_switch_to_next(ctx, a);
 }
 void mod_switch_to_inplace(const PhantomContext& ctx, PhantomCiphertext& a, size_t chain_index);
+// a copy of `a` at `chain_index` (its leading limbs), one strided device copy
+PhantomCiphertext mod_switch_to(const PhantomContext& ctx, const PhantomCiphertext& a, size_t chain_index);
 
 // apply_galois_inplace / rotate_inplace (src/evaluate.cu:1830-1900, NTT-domain path)
 void apply_galois_inplace(const PhantomContext& ctx, PhantomCiphertext& a, uint32_t galois_elt,

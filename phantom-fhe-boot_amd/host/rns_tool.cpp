@@ -93,6 +93,10 @@ RnsTool::RnsTool(size_t n, const std::vector<uint64_t>& qp, size_t size_P, size_
 
   std::vector<uint64_t> qlp(base_Ql_);
   qlp.insert(qlp.end(), base_P_.begin(), base_P_.end());
+  std::vector<uint64_t> qlpb(2 * qlp.size());
+  for (size_t i = 0; i < qlp.size(); ++i) barrett_ratio(qlp[i], &qlpb[2 * i]);
+  d_QlP_.upload(qlp, s);
+  d_QlP_barrett_.upload(qlpb, s);
   const size_t beta = static_cast<size_t>(std::ceil(static_cast<double>(size_Ql) / static_cast<double>(alpha)));
   std::vector<uint64_t> hatinv(size_Ql), hatinvs(size_Ql);
   converters_.resize(beta);
@@ -138,33 +142,51 @@ void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables
     a.skip_at = (int)start;
     a.skip_len = (int)part;
     hip_ok(phx::bconv(a, n_, s), "modup bconv");
-    // NTT of every limb but the digit's own (include_special_mod_exclude_range)
+  }
+  // NTT of every limb but the digit's own (include_special_mod_exclude_range): the full
+  // digits in one launch (digit b skips [b alpha, (b + 1) alpha)), a short last digit apart
+  const size_t beta = converters_.size();
+  const size_t full = digit_size_.back() == alpha ? beta : beta - 1;
+  auto run = [&](size_t b0, size_t cnt) {
+    const size_t part = digit_size_[b0];
     phx::LimbMap m;
     m.num_limbs = (int)size_QlP;
     m.split = (int)size_Ql;
     m.first_a = 0;
     m.first_b = (int)size_Q_;
-    m.skip_begin = (int)start;
-    m.skip_end = (int)(start + part);
-    hip_ok(phx::ntt_forward(ntt, dst, dst, m, s), "modup NTT");
-  }
+    m.skip_begin = (int)digit_start_[b0];
+    m.skip_end = (int)(digit_start_[b0] + part);
+    m.skip_step = (int)alpha;
+    uint64_t* dst = t_mod_up + b0 * size_QlP * n_;
+    hip_ok(phx::ntt_forward(ntt, dst, dst, m.batched((int)cnt), s), "modup NTT");
+  };
+  if (full > 0) run(0, full);
+  if (full < beta) run(full, 1);
 }
 
-void RnsTool::moddown_add(uint64_t* ct_i, uint64_t* cx_i, bool accumulate, const phx::NttTables& ntt,
-                          hipStream_t s) const {
-  const size_t size_Ql = base_Ql_.size();
-  uint64_t* cp = cx_i + size_Ql * n_;
+void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx::NttTables& ntt, hipStream_t s,
+                          size_t polys) const {
+  // every stage runs once over all `polys` polynomials (ct [polys][Ql][n], cx [polys][QlP][n])
+  const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_;
+  const int np = static_cast<int>(polys);
+  uint64_t* cp = cx + size_Ql * n_;
   phx::LimbMap pm;
   pm.num_limbs = (int)size_P_;
   pm.split = 0;
   pm.first_a = 0;
   pm.first_b = (int)size_Q_;
-  hip_ok(phx::ntt_inverse(ntt, cp, cp, pm, nullptr, nullptr, s), "moddown INTT(P)");
-  uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, size_Ql * n_);
-  hip_ok(phx::bconv(p_to_ql_.args(cp, delta, true), n_, s), "moddown bconv");
-  hip_ok(phx::ntt_forward(ntt, delta, delta, phx::LimbMap::contiguous((int)size_Ql, 0), s), "moddown NTT");
-  hip_ok(phx::moddown_finish(ct_i, cx_i, delta, d_bigPInv_mod_q_.get(), d_bigPInv_mod_q_shoup_.get(),
-                             d_Ql_.get(), n_, size_Ql, accumulate, s),
+  hip_ok(phx::ntt_inverse(ntt, cp, cp, pm.batched(np, size_QlP * n_, size_QlP * n_), nullptr, nullptr, s),
+         "moddown INTT(P)");
+  uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, polys * size_Ql * n_);
+  phx::BconvArgs ba = p_to_ql_.args(cp, delta, true);
+  ba.polys = np;
+  ba.in_stride = size_QlP * n_;
+  ba.out_stride = size_Ql * n_;
+  hip_ok(phx::bconv(ba, n_, s), "moddown bconv");
+  hip_ok(phx::ntt_forward(ntt, delta, delta, phx::LimbMap::contiguous((int)size_Ql, 0).batched(np), s),
+         "moddown NTT");
+  hip_ok(phx::moddown_finish(ct, cx, delta, d_bigPInv_mod_q_.get(), d_bigPInv_mod_q_shoup_.get(), d_Ql_.get(), n_,
+                             size_Ql, accumulate, s, polys, size_QlP * n_),
          "moddown finish");
 }
 
@@ -173,20 +195,18 @@ void RnsTool::rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const
   const size_t L = base_Ql_.size();
   if (L < 2) throw std::invalid_argument("end of modulus switching chain reached");
   const size_t Ln = L - 1;
-  uint64_t* last = ws_->get(s, Workspace::kRescaleLast, n_);
-  uint64_t* tmp = ws_->get(s, Workspace::kRescaleTmp, Ln * n_);
-  for (size_t c = 0; c < polys; ++c) {
-    const uint64_t* ci = in + c * L * n_;
-    uint64_t* co = out + c * Ln * n_;
-    hip_ok(phx::ntt_inverse(ntt, ci + Ln * n_, last, phx::LimbMap::contiguous(1, (int)Ln), nullptr, nullptr, s),
-           "rescale INTT(last)");
-    hip_ok(phx::rescale_spread_last(last, tmp, d_Ql_.get(), d_Ql_barrett_.get(), n_, Ln, s),
-           "rescale spread");
-    hip_ok(phx::ntt_forward(ntt, tmp, tmp, phx::LimbMap::contiguous((int)Ln, 0), s), "rescale NTT");
-    hip_ok(phx::rescale_finish(ci, tmp, co, d_inv_qlast_.get(), d_inv_qlast_shoup_.get(), d_Ql_.get(), n_, Ln,
-                               s),
-           "rescale finish");
-  }
+  const int np = static_cast<int>(polys);
+  uint64_t* last = ws_->get(s, Workspace::kRescaleLast, polys * n_);
+  uint64_t* tmp = ws_->get(s, Workspace::kRescaleTmp, polys * Ln * n_);
+  // all polynomials in one launch per stage
+  hip_ok(phx::ntt_inverse(ntt, in + Ln * n_, last, phx::LimbMap::contiguous(1, (int)Ln).batched(np, L * n_, n_),
+                          nullptr, nullptr, s),
+         "rescale INTT(last)");
+  hip_ok(phx::rescale_spread_last(last, tmp, d_Ql_.get(), d_Ql_barrett_.get(), n_, Ln, s, polys), "rescale spread");
+  hip_ok(phx::ntt_forward(ntt, tmp, tmp, phx::LimbMap::contiguous((int)Ln, 0).batched(np), s), "rescale NTT");
+  hip_ok(phx::rescale_finish(in, tmp, out, d_inv_qlast_.get(), d_inv_qlast_shoup_.get(), d_Ql_.get(), n_, Ln, s,
+                             polys, L * n_),
+         "rescale finish");
 }
 
 }  // namespace phantom

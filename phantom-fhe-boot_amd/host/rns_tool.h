@@ -40,10 +40,11 @@ class RnsTool {
 
   // modup (src/rns_bconv.cu:530-628): c2 [size_Ql][n] NTT form -> t_mod_up [beta][size_QlP][n]
   void modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables& ntt, hipStream_t s) const;
-  // moddown_from_NTT (src/rns_bconv.cu:791-843) fused with add_to_ct_kernel: cx_i is
-  // [size_QlP][n] NTT form (its P limbs are clobbered); ct_i (+)= moddown(cx_i).
-  void moddown_add(uint64_t* ct_i, uint64_t* cx_i, bool accumulate, const phx::NttTables& ntt,
-                   hipStream_t s) const;
+  // moddown_from_NTT (src/rns_bconv.cu:791-843) fused with add_to_ct_kernel, for `polys`
+  // polynomials at once: cx is [polys][size_QlP][n] NTT form (its P limbs are clobbered);
+  // ct [polys][size_Ql][n] (+)= moddown(cx).
+  void moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx::NttTables& ntt, hipStream_t s,
+                   size_t polys = 1) const;
   // divide_and_round_q_last_ntt (src/rns.cu:1160-1184): in [polys][size_Ql][n] -> out
   // [polys][size_Ql-1][n], NTT form.  `in` is not modified.
   void rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const phx::NttTables& ntt,
@@ -55,6 +56,8 @@ class RnsTool {
 
   // device views over Ql
   phx::ModView mod_Ql() const { return {d_Ql_.get(), d_Ql_barrett_.get()}; }
+  // the extended basis Ql u P in buffer order (limb i < size_Ql: q_i, then p_0 ..)
+  phx::ModView mod_QlP() const { return {d_QlP_.get(), d_QlP_barrett_.get()}; }
   const uint64_t* bigP_mod_q() const { return d_bigP_mod_q_.get(); }
   const uint64_t* bigP_mod_q_shoup() const { return d_bigP_mod_q_shoup_.get(); }
 
@@ -62,7 +65,7 @@ class RnsTool {
   size_t n_, size_Q_, size_P_;
   Workspace* ws_ = nullptr;
   std::vector<uint64_t> base_Ql_, base_P_;
-  DeviceBuffer<uint64_t> d_Ql_, d_Ql_barrett_;
+  DeviceBuffer<uint64_t> d_Ql_, d_Ql_barrett_, d_QlP_, d_QlP_barrett_;
   // key switching
   DeviceBuffer<uint64_t> d_partQlHatInv_, d_partQlHatInv_shoup_;
   std::vector<DeviceBaseConverter> converters_;  // digit beta: part -> complement of QlP
