@@ -77,9 +77,17 @@ hipError_t modup_copy_digits(const uint64_t* c2, uint64_t* t_mod_up, size_t n, s
                              size_t alpha, hipStream_t s);
 // key_switch_inner_prod_c2_and_evk (src/eval_key_switch.cu:26-85).  evk: device array of
 // beta pointers to [2][size_QP][n] key digits; modulus/barrett over the full QP chain.
+// Optional addend: cx[t][l] += P c[t][l] for the Ql limbs (c [2][size_ql][n], P mod q_l with
+// Shoup quotients), i.e. the P-scaled extended form of (c0, c1) + KeySwitch(c2).
+struct KsAddend {
+  const uint64_t* c = nullptr;
+  const uint64_t* pmod = nullptr;
+  const uint64_t* pmod_shoup = nullptr;
+};
 hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const* evk, uint64_t* cx,
                                 const uint64_t* qp_mod, const uint64_t* qp_barrett, size_t n, size_t size_ql,
-                                size_t size_q, size_t size_p, size_t beta, hipStream_t s);
+                                size_t size_q, size_t size_p, size_t beta, hipStream_t s,
+                                const KsAddend& add = KsAddend{});
 // moddown tail + add_to_ct (src/ntt/ntt_moddown.cu:199-214, src/rns_bconv.cu:763-789):
 //   ct[j] = ct[j] + (cx[j] - delta[j]) * Pinv[j] mod q_j   (accumulate = true)
 //   ct[j] =         (cx[j] - delta[j]) * Pinv[j] mod q_j   (accumulate = false)

@@ -293,7 +293,8 @@ __global__ __launch_bounds__(kBlock) void ks_inner_kernel(const uint64_t* __rest
                                                           const uint64_t* const* __restrict__ evk, uint64_t* cx,
                                                           const uint64_t* qp, const uint64_t* qpb, uint32_t log_n,
                                                           size_t pairs, uint32_t size_ql, uint32_t size_q,
-                                                          size_t size_qlp_n, size_t size_qp_n, uint32_t beta) {
+                                                          size_t size_qlp_n, size_t size_qp_n, uint32_t beta,
+                                                          KsAddend add) {
   for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
     const size_t e = 2 * i;
     const uint32_t nid = static_cast<uint32_t>(e >> log_n);
@@ -311,8 +312,19 @@ __global__ __launch_bounds__(kBlock) void ks_inner_kernel(const uint64_t* __rest
       add128(a1y, mul_wide(c.y, k1.y));
     }
     const uint64_t q = qp[twr], r0 = qpb[2 * twr], r1 = qpb[2 * twr + 1];
-    st2(cx + e, barrett_reduce_128(a0x, q, r0, r1), barrett_reduce_128(a0y, q, r0, r1));
-    st2(cx + size_qlp_n + e, barrett_reduce_128(a1x, q, r0, r1), barrett_reduce_128(a1y, q, r0, r1));
+    uint64_t o0x = barrett_reduce_128(a0x, q, r0, r1), o0y = barrett_reduce_128(a0y, q, r0, r1);
+    uint64_t o1x = barrett_reduce_128(a1x, q, r0, r1), o1y = barrett_reduce_128(a1y, q, r0, r1);
+    if (add.c && nid < size_ql) {  // + P (c0, c1): the key switch result stays P-scaled in QlP
+      const uint64_t w = add.pmod[nid], ws = add.pmod_shoup[nid];
+      const size_t ql_n = (size_t)size_ql << log_n;
+      const u64x2 c0 = ld2(add.c + e), c1 = ld2(add.c + ql_n + e);
+      o0x = add_mod(o0x, mul_shoup(c0.x, w, ws, q), q);
+      o0y = add_mod(o0y, mul_shoup(c0.y, w, ws, q), q);
+      o1x = add_mod(o1x, mul_shoup(c1.x, w, ws, q), q);
+      o1y = add_mod(o1y, mul_shoup(c1.y, w, ws, q), q);
+    }
+    st2(cx + e, o0x, o0y);
+    st2(cx + size_qlp_n + e, o1x, o1y);
   }
 }
 
@@ -496,7 +508,8 @@ hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s) {
 #define PHX_BCONV_CASE(K) \
   case K: bconv_fixed_kernel<K><<<g, kBlock, 0, s>>>(a, static_cast<uint32_t>(n), pairs, pre); break;
     PHX_BCONV_CASE(1) PHX_BCONV_CASE(2) PHX_BCONV_CASE(3) PHX_BCONV_CASE(4) PHX_BCONV_CASE(5)
-    PHX_BCONV_CASE(6) PHX_BCONV_CASE(8) PHX_BCONV_CASE(10) PHX_BCONV_CASE(12) PHX_BCONV_CASE(15)
+    PHX_BCONV_CASE(6) PHX_BCONV_CASE(7) PHX_BCONV_CASE(8) PHX_BCONV_CASE(9) PHX_BCONV_CASE(10)
+    PHX_BCONV_CASE(11) PHX_BCONV_CASE(12) PHX_BCONV_CASE(13) PHX_BCONV_CASE(14) PHX_BCONV_CASE(15)
 #undef PHX_BCONV_CASE
     default: bconv_kernel<<<g, kBlock, 0, s>>>(a, static_cast<uint32_t>(n), pairs, pre);
   }
@@ -513,12 +526,12 @@ hipError_t modup_copy_digits(const uint64_t* c2, uint64_t* t_mod_up, size_t n, s
 
 hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const* evk, uint64_t* cx,
                                 const uint64_t* qp_mod, const uint64_t* qp_barrett, size_t n, size_t size_ql,
-                                size_t size_q, size_t size_p, size_t beta, hipStream_t s) {
+                                size_t size_q, size_t size_p, size_t beta, hipStream_t s, const KsAddend& add) {
   const size_t size_qlp = size_ql + size_p;
   const size_t pairs = n * size_qlp / 2;
   ks_inner_kernel<<<grid_for(pairs), kBlock, 0, s>>>(t_mod_up, evk, cx, qp_mod, qp_barrett, __builtin_ctzll(n), pairs,
                                                      (uint32_t)size_ql, (uint32_t)size_q, size_qlp * n,
-                                                     (size_q + size_p) * n, (uint32_t)beta);
+                                                     (size_q + size_p) * n, (uint32_t)beta, add);
   return hipGetLastError();
 }
 

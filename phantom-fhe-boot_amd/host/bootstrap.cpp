@@ -1,9 +1,11 @@
 #include "bootstrap.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
+#include <exception>
 #include <stdexcept>
 #include <thread>
 
@@ -213,6 +215,48 @@ struct ChebEvaluator {
 }  // namespace
 
 // ======================================================================================
+// two concurrent chains: `main` on the context's stream (this thread), `aux` on its second
+// stream from a worker thread (StreamScope).  The aux stream starts after everything already
+// enqueued on the main stream; the main stream continues after both.  Buffers allocated on one
+// stream and used on the other must stay alive until this returns.
+// ======================================================================================
+template <typename Main, typename Aux>
+static void run_concurrently(const PhantomContext& cc, Main&& main, Aux&& aux) {
+  const hipStream_t s0 = cc.stream(), s1 = cc.aux_stream();
+  hipEvent_t fork, join;
+  PHX_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+  PHX_CHECK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  PHX_CHECK(hipEventRecord(fork, s0));
+  PHX_CHECK(hipStreamWaitEvent(s1, fork, 0));
+  std::exception_ptr err_aux, err_main;
+  std::thread worker([&] {
+    try {
+      StreamScope scope(s1);
+      aux();
+    } catch (...) {
+      err_aux = std::current_exception();
+    }
+  });
+  try {
+    main();
+  } catch (...) {
+    err_main = std::current_exception();
+  }
+  worker.join();
+  const hipError_t e = hipEventRecord(join, s1);
+  if (e == hipSuccess) (void)hipStreamWaitEvent(s0, join, 0);
+  if (err_main || err_aux || e != hipSuccess) {
+    (void)hipStreamSynchronize(s1);
+    (void)hipStreamSynchronize(s0);
+  }
+  (void)hipEventDestroy(fork);
+  (void)hipEventDestroy(join);
+  if (err_main) std::rethrow_exception(err_main);
+  if (err_aux) std::rethrow_exception(err_aux);
+  PHX_CHECK(e);
+}
+
+// ======================================================================================
 // FHECKKSRNS
 // ======================================================================================
 
@@ -391,24 +435,23 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
   }
   hip_ok(phx::lt_bsgs(la, n, s), "linear transform inner products");
   baby.clear();
-  // giant steps accumulate in the extended basis; one moddown at the end
-  PhantomCiphertext acc;
-  bool have_acc = false;
-  if (la.out[0]) {
-    acc = std::move(inner[0]);
-    have_acc = true;
-  }
-  for (int i = 1; i < lv.b; ++i) {
-    EvalRotateExtAccumulate(cc, inner[i], galois_keys_, static_cast<int>(static_cast<long>(lv.g) * i * lv.stride), acc,
-                            have_acc);
-    have_acc = true;
-    inner[i] = PhantomCiphertext();
-  }
-  PhantomCiphertext res = KeySwitchDown(cc, acc);
-  res.set_scale(ct.scale() * sf_.at(lv.chain - 1));
-  res.SetNoiseScaleDeg(2);
-  EvalModReduceInPlace(cc, res, 1);
-  return res;
+  // giant steps accumulate in the extended basis (one moddown at the end), the odd ones on
+  // the context's second stream; inner[] (main-stream buffers) lives until both have joined
+  PhantomCiphertext acc = std::move(inner[0]), acc_aux;
+  auto giants = [&](int first, PhantomCiphertext& a, bool have) {
+    for (int i = first; i < lv.b; i += 2) {
+      EvalRotateExtAccumulate(cc, inner[i], galois_keys_, static_cast<int>(static_cast<long>(lv.g) * i * lv.stride), a,
+                              have);
+      have = true;
+    }
+  };
+  run_concurrently(
+      cc, [&] { giants(2, acc, true); }, [&] { giants(1, acc_aux, false); });
+  if (lv.b > 1) EvalAddExtInPlace(cc, acc, acc_aux);
+  inner.clear();
+  acc.set_scale(ct.scale() * sf_.at(lv.chain - 1));
+  acc.SetNoiseScaleDeg(2);
+  return KeySwitchDownRescale(cc, acc);
 }
 
 PhantomCiphertext FHECKKSRNS::EvalCoeffsToSlots(const PhantomCiphertext& ct, const PhantomContext& cc) const {
@@ -466,14 +509,19 @@ PhantomCiphertext FHECKKSRNS::RaiseWithCorrection(const PhantomCiphertext& in, c
 static void trace(const PhantomContext& cc, const char* stage, const PhantomCiphertext& ct) {
   static const bool on = std::getenv("PHX_BOOT_TRACE") != nullptr;
   if (!on) return;
+  static auto last = std::chrono::steady_clock::now();
   const hipError_t e = hipStreamSynchronize(cc.stream());
-  std::fprintf(stderr, "[boot] %-12s chain %zu limbs %zu scale %.6e deg %zu : %s\n", stage, ct.chain_index(),
-               ct.coeff_modulus_size(), ct.scale(), ct.GetNoiseScaleDeg(), hipGetErrorString(e));
+  const auto now = std::chrono::steady_clock::now();
+  const double ms = std::chrono::duration<double, std::milli>(now - last).count();
+  last = now;
+  std::fprintf(stderr, "[boot] %-12s %8.3f ms  chain %zu limbs %zu scale %.6e deg %zu : %s\n", stage, ms,
+               ct.chain_index(), ct.coeff_modulus_size(), ct.scale(), ct.GetNoiseScaleDeg(), hipGetErrorString(e));
 }
 
 PhantomCiphertext FHECKKSRNS::EvalBootstrap(const PhantomCiphertext& in, const PhantomContext& cc) const {
   if (enc_.empty()) throw std::invalid_argument("Precomputations were not generated: call EvalBootstrapSetup");
   const uint32_t N = static_cast<uint32_t>(cc.poly_degree()), M = 2 * N;
+  trace(cc, "start", in);
   PhantomCiphertext raised = RaiseWithCorrection(in, cc);
   trace(cc, "raise", raised);
   // CoeffToSlot, then split the real and imaginary parts with one conjugation
@@ -485,13 +533,19 @@ PhantomCiphertext FHECKKSRNS::EvalBootstrap(const PhantomCiphertext& in, const P
   add_inplace(cc, enc, conj);
   MultByMonomialInPlace(cc, enc_i, 3 * M / 4);  // times -i
   trace(cc, "conj-split", enc_i);
-  // approximate modular reduction of both halves
-  enc = eval_mod(enc, cc);
-  trace(cc, "evalmod-re", enc);
-  enc_i = eval_mod(enc_i, cc);
-  trace(cc, "evalmod-im", enc_i);
-  MultByMonomialInPlace(cc, enc_i, M / 4);  // times i
-  EvalAddAutoInplace(cc, enc, enc_i, sf_);
+  // approximate modular reduction of both halves, concurrently: the imaginary half runs on the
+  // context's second stream from a second host thread (both are chains of small, dependent
+  // launches that leave most of the GPU idle on their own)
+  // enc_i (allocated on the main stream) stays alive until the main stream has joined
+  PhantomCiphertext im;
+  run_concurrently(
+      cc, [&] { enc = eval_mod(enc, cc); },
+      [&] {
+        im = eval_mod(enc_i, cc);
+        MultByMonomialInPlace(cc, im, M / 4);  // times i
+      });
+  trace(cc, "evalmod", enc);
+  EvalAddAutoInplace(cc, enc, im, sf_);
   // SlotToCoeff and undo the correction scaling
   PhantomCiphertext dec = EvalSlotsToCoeffs(enc, cc);
   trace(cc, "stc", dec);

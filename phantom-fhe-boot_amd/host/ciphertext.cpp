@@ -41,7 +41,8 @@ void PhantomCiphertext::copy_from(const PhantomCiphertext& o) {
   noise_scale_deg_ = o.noise_scale_deg_;
   is_ntt_form_ = o.is_ntt_form_;
   const size_t count = size_ * L_ * n_;
-  hipStream_t s = o.data_.stream();
+  // the copy runs on this thread's stream (a StreamScope's), else on the source's stream
+  hipStream_t s = StreamScope::current() ? StreamScope::current() : o.data_.stream();
   data_.allocate(count, s);
   if (count) PHX_CHECK(hipMemcpyAsync(data_.get(), o.data_.get(), count * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
 }

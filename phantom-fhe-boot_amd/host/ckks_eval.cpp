@@ -259,6 +259,47 @@ void EvalSubAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const P
   sub_inplace(ctx, a, AtLevel(ctx, b, target, sf, tmp));
 }
 
+PhantomCiphertext RelinearizeRescale(const PhantomContext& ctx, const PhantomCiphertext& d, const PhantomRelinKey& rlk) {
+  if (d.size() != 3) throw std::invalid_argument("destination_size must be 3");
+  const RnsTool& rt = ctx.get_context_data(d.chain_index()).gpu_rns_tool();
+  const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P(), beta = rt.beta();
+  if (d.chain_index() + 1 >= ctx.total_parm_size()) throw std::invalid_argument("end of modulus switching chain reached");
+  hipStream_t s = ctx.stream();
+  uint64_t* t_mod_up = rt.workspace().get(s, Workspace::kKsModup, beta * QlP * n);
+  rt.modup(t_mod_up, d.data() + 2 * Ql * n, ctx.gpu_rns_tables(), s);
+  uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * QlP * n);
+  phx::KsAddend add;
+  add.c = d.data();
+  add.pmod = rt.bigP_mod_q();
+  add.pmod_shoup = rt.bigP_mod_q_shoup();
+  hip_ok(phx::keyswitch_inner_prod(t_mod_up, rlk.public_keys_ptr(), cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, Ql,
+                                   ctx.size_Q(), ctx.size_P(), beta, s, add),
+         "relinearize inner product");
+  PhantomCiphertext out;
+  out.resize(ctx, d.chain_index() + 1, 2, s, false);
+  rt.moddown_rescale(out.data(), cx, ctx.gpu_rns_tables(), s, 2);
+  out.set_ntt_form(true);
+  out.set_scale(d.scale() / static_cast<double>(rt.base_Ql().back()));
+  out.set_correction_factor(d.correction_factor());
+  out.SetNoiseScaleDeg(d.GetNoiseScaleDeg() > 1 ? d.GetNoiseScaleDeg() - 1 : 1);
+  return out;
+}
+
+PhantomCiphertext KeySwitchDownRescale(const PhantomContext& ctx, PhantomCiphertext& ext) {
+  const RnsTool& rt = ctx.get_context_data(ext.chain_index()).gpu_rns_tool();
+  const size_t QlP = rt.size_Ql() + ctx.size_P();
+  if (ext.size() != 2 || ext.coeff_modulus_size() != QlP) throw std::invalid_argument("not an extended-basis ciphertext");
+  if (ext.chain_index() + 1 >= ctx.total_parm_size()) throw std::invalid_argument("end of modulus switching chain reached");
+  hipStream_t s = ctx.stream();
+  PhantomCiphertext out;
+  out.resize(ctx, ext.chain_index() + 1, 2, s, false);
+  rt.moddown_rescale(out.data(), ext.data(), ctx.gpu_rns_tables(), s, 2);
+  out.set_ntt_form(true);
+  out.set_scale(ext.scale() / static_cast<double>(rt.base_Ql().back()));
+  out.SetNoiseScaleDeg(ext.GetNoiseScaleDeg() > 1 ? ext.GetNoiseScaleDeg() - 1 : 1);
+  return out;
+}
+
 PhantomCiphertext EvalMultRescale(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
                                   const PhantomRelinKey& rlk, const std::vector<double>& sf) {
   const size_t target = std::max(level_after_reduce(a), level_after_reduce(b));
@@ -266,10 +307,8 @@ PhantomCiphertext EvalMultRescale(const PhantomContext& ctx, const PhantomCipher
   const PhantomCiphertext& x = AtLevel(ctx, a, target, sf, ta);
   const PhantomCiphertext& y = &a == &b ? x : AtLevel(ctx, b, target, sf, tb);
   PhantomCiphertext d = multiply(ctx, x, y);
-  relinearize_inplace(ctx, d, rlk);
   d.SetNoiseScaleDeg(2);
-  EvalModReduceInPlace(ctx, d, 1);
-  return d;
+  return RelinearizeRescale(ctx, d, rlk);
 }
 
 PhantomCiphertext RaiseMod(const PhantomContext& ctx, const PhantomCiphertext& ct) {

@@ -55,6 +55,11 @@ void EvalAddAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const P
                         const std::vector<double>& sf);
 void EvalSubAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b,
                         const std::vector<double>& sf);
+// relinearize a 3-polynomial product and rescale it in one key-switch: (c0, c1) + KS(c2) is formed
+// P-scaled in the extended basis and divided by P q_last at once (RnsTool::moddown_rescale)
+PhantomCiphertext RelinearizeRescale(const PhantomContext& ctx, const PhantomCiphertext& d3, const PhantomRelinKey& rlk);
+// KeySwitchDown followed by a rescale, as one division by P q_last
+PhantomCiphertext KeySwitchDownRescale(const PhantomContext& ctx, PhantomCiphertext& ext);
 // level-aligned multiply + relinearize + rescale (EvalMultAuto + ModReduce)
 PhantomCiphertext EvalMultRescale(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
                                   const PhantomRelinKey& rlk, const std::vector<double>& sf);

@@ -72,6 +72,24 @@ struct OwnedStream {
   }
 };
 
+// Thread-local stream override: while a StreamScope lives, every PhantomContext operation
+// issued by this thread runs on `s` instead of the context's stream (each stream has its own
+// key-switch workspace).  Used to run independent chains of a bootstrap concurrently.
+class StreamScope {
+ public:
+  explicit StreamScope(hipStream_t s) : prev_(current()) { current() = s; }
+  ~StreamScope() { current() = prev_; }
+  StreamScope(const StreamScope&) = delete;
+  StreamScope& operator=(const StreamScope&) = delete;
+  static hipStream_t& current() {
+    static thread_local hipStream_t s = nullptr;
+    return s;
+  }
+
+ private:
+  hipStream_t prev_;
+};
+
 class PhantomContext {
  public:
   // stream: where setup work and the façade's operations run; nullptr = a stream owned by the
@@ -97,11 +115,17 @@ class PhantomContext {
   // NTT tables and per-modulus device constants over the whole Q u P chain
   const phx::NttTables& gpu_rns_tables() const { return ntt_->get(); }
   phx::ModView mod_QP() const { return {ntt_->get().modulus, ntt_->get().barrett}; }
-  hipStream_t stream() const { return stream_.s; }
+  hipStream_t stream() const {
+    const hipStream_t o = StreamScope::current();
+    return o ? o : stream_.s;
+  }
+  // a second stream owned by the context, for work that runs beside stream()
+  hipStream_t aux_stream() const { return aux_.s; }
   Workspace& workspace() const { return *ws_; }
 
  private:
-  OwnedStream stream_;  // first member: destroyed after everything that frees on it
+  OwnedStream stream_;  // first members: destroyed after everything that frees on them
+  OwnedStream aux_;
   EncryptionParameters params_;
   size_t n_ = 0, size_Q_ = 0, size_P_ = 0;
   std::vector<uint64_t> qp_;

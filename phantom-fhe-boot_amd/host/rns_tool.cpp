@@ -121,6 +121,20 @@ RnsTool::RnsTool(size_t n, const std::vector<uint64_t>& qp, size_t size_P, size_
   d_partQlHatInv_.upload(hatinv, s);
   d_partQlHatInv_shoup_.upload(hatinvs, s);
   p_to_ql_.init(base_P_, base_Ql_, s);
+  if (size_Ql >= 2) {
+    std::vector<uint64_t> ib{base_Ql_.back()};
+    ib.insert(ib.end(), base_P_.begin(), base_P_.end());
+    const std::vector<uint64_t> ob(base_Ql_.begin(), base_Ql_.end() - 1);
+    pq_to_ql1_.init(ib, ob, s);
+    std::vector<uint64_t> inv(ob.size()), invs(ob.size());
+    for (size_t j = 0; j < ob.size(); ++j) {
+      const uint64_t q = ob[j];
+      inv[j] = mul_mod(pim[j], inv_mod(base_Ql_.back() % q, q), q);
+      invs[j] = shoup(inv[j], q);
+    }
+    d_PQinv_.upload(inv, s);
+    d_PQinv_shoup_.upload(invs, s);
+  }
 }
 
 static void hip_ok(hipError_t e, const char* what) {
@@ -188,6 +202,34 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
   hip_ok(phx::moddown_finish(ct, cx, delta, d_bigPInv_mod_q_.get(), d_bigPInv_mod_q_shoup_.get(), d_Ql_.get(), n_,
                              size_Ql, accumulate, s, polys, size_QlP * n_),
          "moddown finish");
+}
+
+void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables& ntt, hipStream_t s,
+                              size_t polys) const {
+  const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_;
+  if (size_Ql < 2 || size_P_ == 0) throw std::invalid_argument("end of modulus switching chain reached");
+  const size_t Ln = size_Ql - 1;
+  const int np = static_cast<int>(polys);
+  // the dropped limbs q_last, p_0 .. p_{P-1} are contiguous in the extended buffer
+  uint64_t* dropped = cx + Ln * n_;
+  phx::LimbMap dm;
+  dm.num_limbs = (int)(1 + size_P_);
+  dm.split = 1;
+  dm.first_a = (int)Ln;
+  dm.first_b = (int)size_Q_;
+  hip_ok(phx::ntt_inverse(ntt, dropped, dropped, dm.batched(np, size_QlP * n_, size_QlP * n_), nullptr, nullptr, s),
+         "moddown-rescale INTT");
+  uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, polys * Ln * n_);
+  phx::BconvArgs ba = pq_to_ql1_.args(dropped, delta, true);
+  ba.polys = np;
+  ba.in_stride = size_QlP * n_;
+  ba.out_stride = Ln * n_;
+  hip_ok(phx::bconv(ba, n_, s), "moddown-rescale bconv");
+  hip_ok(phx::ntt_forward(ntt, delta, delta, phx::LimbMap::contiguous((int)Ln, 0).batched(np), s),
+         "moddown-rescale NTT");
+  hip_ok(phx::moddown_finish(out, cx, delta, d_PQinv_.get(), d_PQinv_shoup_.get(), d_Ql_.get(), n_, Ln, false, s,
+                             polys, size_QlP * n_),
+         "moddown-rescale finish");
 }
 
 void RnsTool::rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const phx::NttTables& ntt,

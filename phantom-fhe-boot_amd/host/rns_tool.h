@@ -45,6 +45,13 @@ class RnsTool {
   // ct [polys][size_Ql][n] (+)= moddown(cx).
   void moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx::NttTables& ntt, hipStream_t s,
                    size_t polys = 1) const;
+  // moddown fused with the following rescale: cx [polys][size_QlP][n] NTT form holds P x (a
+  // ciphertext at this level, scale S); out [polys][size_Ql - 1][n] = round(cx / (P q_last)),
+  // the ciphertext rescaled to the next level (scale S / q_last).  One INTT over the 1 + size_P
+  // dropped limbs, one base conversion, one NTT and one finish instead of a moddown (INTT P,
+  // NTT Ql) followed by a rescale (INTT 1, NTT Ql - 1).  cx's dropped limbs are clobbered.
+  void moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables& ntt, hipStream_t s,
+                       size_t polys = 1) const;
   // divide_and_round_q_last_ntt (src/rns.cu:1160-1184): in [polys][size_Ql][n] -> out
   // [polys][size_Ql-1][n], NTT form.  `in` is not modified.
   void rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const phx::NttTables& ntt,
@@ -71,6 +78,9 @@ class RnsTool {
   std::vector<DeviceBaseConverter> converters_;  // digit beta: part -> complement of QlP
   std::vector<size_t> digit_start_, digit_size_;
   DeviceBaseConverter p_to_ql_;
+  // fused moddown + rescale: {q_last} u P -> Q_{l-1}, and (P q_last)^-1 mod q_j
+  DeviceBaseConverter pq_to_ql1_;
+  DeviceBuffer<uint64_t> d_PQinv_, d_PQinv_shoup_;
   DeviceBuffer<uint64_t> d_bigP_mod_q_, d_bigP_mod_q_shoup_, d_bigPInv_mod_q_, d_bigPInv_mod_q_shoup_;
   // rescale
   DeviceBuffer<uint64_t> d_inv_qlast_, d_inv_qlast_shoup_;
