@@ -135,6 +135,29 @@ def c4_leg(iters=3, timeout=240):
     }
 
 
+def max_over_ranks(dist, values, device):
+    """MAX all-reduce of per-rank timings: the slowest rank defines the job's time."""
+    import torch
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t]
+
+
+def all_ranks_ok(dist, ok, device):
+    """True only if every rank reports success (MIN all-reduce of a flag)."""
+    import torch
+    t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=device)
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item() > 0.5)
+
+
+def job_throughput(units_per_rank, world, max_seconds):
+    """Whole-job throughput: the units every rank processed over the max-over-ranks time."""
+    return units_per_rank * world / max_seconds
+
+
 def c5_leg(dist, torch, world, rank, local_rank, batch=8, timeout=600):
     """Config C5: a batch of independent bootstraps sharded over the ranks, one
     process per GPU, replicas only (no collective on the data path: every rank holds its own
@@ -149,21 +172,30 @@ def c5_leg(dist, torch, world, rank, local_rank, batch=8, timeout=600):
     boot = [r for r in rows if r.get("stage") == "bootstrap"]
     ok = out.returncode == 0 and bool(boot)
     total_ms = boot[0]["ms_total"] if ok else float("inf")
-    t = torch.tensor([total_ms, 1.0 if ok else 0.0], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        okc = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device="cuda")
-        dist.all_reduce(okc, op=dist.ReduceOp.MIN)
-        ok = bool(okc.item())
-    if not ok:
+    max_ms = max_over_ranks(dist, [total_ms], "cuda")[0]
+    if not all_ranks_ok(dist, ok, "cuda"):
         return {"error": (out.stderr or out.stdout)[-300:]}
-    max_ms = float(t[0])
     return {
         "workload": "C5: independent bootstraps (C4 parameters) sharded over ranks, replicas only",
         "bootstraps_per_rank": batch, "ranks": world,
-        "bootstraps_per_s": round(batch * world / (max_ms / 1e3), 3),
+        "bootstraps_per_s": round(job_throughput(batch, world, max_ms / 1e3), 3),
         "max_rank_ms": round(max_ms, 2), "scaling": "weak",
     }
+
+
+# HBM bytes per forward-NTT launch (column + row pass) from PMC counters: FETCH_SIZE and
+# WRITE_SIZE collected in separate rocprofv3 --pmc passes over the same NTT shape
+# (tools/gpu_pmc_traffic.sh), gfx950 FETCH_SIZE correction applied (tools/pmc_traffic.py).
+PMC_TRAFFIC_FILE = "profiles/r01/ntt_pmc_traffic.json"
+
+
+def pmc_traffic():
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), PMC_TRAFFIC_FILE)
+    try:
+        with open(path) as f:
+            return json.load(f).get("forward_ntt_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
 
 
 def main():
@@ -227,18 +259,14 @@ def main():
     elapsed = time.perf_counter() - t0
 
     fwd_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
-    if world > 1:
-        t = torch.tensor([elapsed, fwd_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, fwd_ms = float(t[0]), float(t[1])
+    elapsed, fwd_ms = max_over_ranks(dist if world > 1 else None, [elapsed, fwd_ms], "cuda")
 
     c5 = None
     if world > 1 and not args.no_c5:
         c5 = c5_leg(dist, torch, world, rank, local_rank)
 
     # parity spot-check of the last buffer state is done by tests/; here just sanity
-    total_bytes = 2 * BYTES_PER_TRANSFORM * args.steps * world
-    value = total_bytes / elapsed / 1e9
+    value = job_throughput(2 * BYTES_PER_TRANSFORM * args.steps, world, elapsed) / 1e9
     achieved = BYTES_PER_TRANSFORM / (fwd_ms * 1e-3) / 1e9
 
     if rank == 0:
@@ -271,7 +299,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "fwd_ms": round(fwd_ms, 5),
-                "traffic": None,
+                "traffic": pmc_traffic(),
+                "traffic_source": PMC_TRAFFIC_FILE,
             },
         }
         if not args.no_c3:

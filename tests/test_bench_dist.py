@@ -1,0 +1,61 @@
+"""The N > 1 path of bench.py on CPU: two `gloo` ranks (one process each, as torchrun launches
+them) aggregate per-rank timings with a MAX all-reduce, agree on success with a MIN all-reduce,
+and report whole-job throughput = units of every rank / max-over-ranks time.  The C5 leg is
+replicas only (no collective on the data path), so these reductions are its only communication.
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, q):
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # rank r took (1 + r) s for its steps and (2 - r) ms per forward transform
+        elapsed, fwd = bench.max_over_ranks(dist, [1.0 + rank, 2.0 - rank], "cpu")
+        ok_all = bench.all_ranks_ok(dist, True, "cpu")
+        ok_one_failed = bench.all_ranks_ok(dist, rank == 0, "cpu")
+        thr = bench.job_throughput(100, world, elapsed)
+        q.put((rank, elapsed, fwd, ok_all, ok_one_failed, thr))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_aggregation():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, elapsed, fwd, ok_all, ok_one_failed, thr in res:
+        assert elapsed == 2.0 and fwd == 2.0  # the slowest rank's numbers, on every rank
+        assert ok_all is True and ok_one_failed is False
+        assert thr == pytest.approx(100 * 2 / 2.0)
+
+
+def test_single_process_helpers_without_a_group():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.max_over_ranks(None, [3.0, 4.0], "cpu") == [3.0, 4.0]
+    assert bench.all_ranks_ok(None, False, "cpu") is False
+    assert bench.job_throughput(10, 1, 2.0) == 5.0
