@@ -59,6 +59,10 @@ struct LimbScalars {
 hipError_t mul_scalar_v(const uint64_t* in, const LimbScalars& c, uint64_t* out, const uint64_t* q, size_t n,
                         size_t L, hipStream_t s, size_t polys = 1, size_t in_stride = 0,
                         const uint64_t* acc = nullptr);
+// d[p] = d[p] * ca (ca may be null: unscaled) + (p < t_polys ? t[p] * cb : 0) for p < d_polys;
+// d contiguous [d_polys][L][n], t[p] at t + p * t_stride (its first L limbs)
+hipError_t lin_comb_v(uint64_t* d, size_t d_polys, const LimbScalars* ca, const uint64_t* t, size_t t_polys,
+                      size_t t_stride, const LimbScalars& cb, const uint64_t* q, size_t n, size_t L, hipStream_t s);
 hipError_t add_scalar_v(const uint64_t* in, const LimbScalars& c, uint64_t* out, const uint64_t* q, size_t n,
                         size_t L, hipStream_t s);
 

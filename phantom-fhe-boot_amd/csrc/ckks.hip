@@ -139,6 +139,26 @@ __global__ __launch_bounds__(kBlock) void scalar_v_kernel(const uint64_t* in, si
   }
 }
 
+// blockIdx.y: polynomial p < d_polys of d ([d_polys][L][n]):
+//   d[p] = d[p] * ca (if SCALE) + (p < t_polys ? t[p] * cb : 0),  t[p] at t + p * t_stride
+template <bool SCALE>
+__global__ __launch_bounds__(kBlock) void lin_comb_kernel(uint64_t* d, LimbScalars ca, const uint64_t* t,
+                                                          uint32_t t_polys, size_t t_stride, LimbScalars cb,
+                                                          const uint64_t* q, uint32_t log_n, size_t total) {
+  d += blockIdx.y * total;
+  const bool with_t = t != nullptr && blockIdx.y < t_polys;
+  if (with_t) t += blockIdx.y * t_stride;
+  if (!SCALE && !with_t) return;
+  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const uint64_t ql = q[l];
+    uint64_t v = d[e];
+    if constexpr (SCALE) v = mul_shoup(v, ca.v[l], ca.vs[l], ql);
+    if (with_t) v = add_mod(v, mul_shoup(t[e], cb.v[l], cb.vs[l], ql), ql);
+    d[e] = v;
+  }
+}
+
 int grid_for(size_t items) {
   const size_t b = (items + kBlock - 1) / kBlock;
   return static_cast<int>(std::max<size_t>(1, std::min<size_t>(b, 2048)));
@@ -184,6 +204,20 @@ hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s) {
     case 32: lt_bsgs_kernel<32><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t lin_comb_v(uint64_t* d, size_t d_polys, const LimbScalars* ca, const uint64_t* t, size_t t_polys,
+                      size_t t_stride, const LimbScalars& cb, const uint64_t* q, size_t n, size_t L, hipStream_t s) {
+  if (L > static_cast<size_t>(kMaxScalarLimbs) || d_polys < 1 || t_polys > d_polys) return hipErrorInvalidValue;
+  const size_t total = n * L;
+  const dim3 g(std::max<int>(1, grid_for(total * d_polys) / static_cast<int>(d_polys)), static_cast<unsigned>(d_polys));
+  const uint32_t log_n = __builtin_ctzll(n);
+  if (ca)
+    lin_comb_kernel<true><<<g, kBlock, 0, s>>>(d, *ca, t, static_cast<uint32_t>(t_polys), t_stride, cb, q, log_n, total);
+  else
+    lin_comb_kernel<false><<<g, kBlock, 0, s>>>(d, LimbScalars{}, t, static_cast<uint32_t>(t_polys), t_stride, cb, q,
+                                                log_n, total);
   return hipGetLastError();
 }
 

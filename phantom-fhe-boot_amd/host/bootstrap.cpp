@@ -138,6 +138,20 @@ struct ChebEvaluator {
   const PhantomRelinKey& rlk;
   const std::vector<double>& sf;
   std::map<int, PhantomCiphertext> T;
+  std::map<std::pair<int, size_t>, PhantomCiphertext> aligned_;  // T_i brought to a deeper level
+
+  // T_i at level `lvl` (>= its own), cached: the power ladder re-uses T_1, T_2, .. at the level
+  // of every larger factor
+  const PhantomCiphertext& aligned(int i, size_t lvl) {
+    const PhantomCiphertext& t = get(i);
+    if (level_of(t) == lvl) return t;
+    auto key = std::make_pair(i, lvl);
+    auto it = aligned_.find(key);
+    if (it != aligned_.end()) return it->second;
+    PhantomCiphertext tmp;
+    const PhantomCiphertext& r = AtLevel(cc, t, lvl, sf, tmp);
+    return aligned_.emplace(key, &r == &t ? PhantomCiphertext(t) : std::move(tmp)).first->second;
+  }
 
   const PhantomCiphertext& get(int i) {
     auto it = T.find(i);
@@ -146,18 +160,21 @@ struct ChebEvaluator {
     int a = 1;
     while (2 * a < i) a *= 2;  // a >= i / 2, a < i
     if (2 * a == i) {
-      // T_2a = 2 T_a^2 - 1
+      // T_2a = 2 T_a^2 - 1, the doubling and the constant folded in before the one key switch
       const PhantomCiphertext& ta = get(a);
-      r = EvalMultRescale(cc, ta, ta, rlk, sf);
-      add_inplace(cc, r, r);
-      EvalAddConstInplace(cc, r, -1.0);
+      r = MulAddRescale(cc, ta, ta, rlk, 2, {}, -1.0);
     } else {
-      // T_i = 2 T_a T_(i-a) - T_(2a-i)
-      const PhantomCiphertext& ta = get(a);
-      const PhantomCiphertext& tb = get(i - a);
-      r = EvalMultRescale(cc, ta, tb, rlk, sf);
-      add_inplace(cc, r, r);
-      EvalSubAutoInplace(cc, r, get(2 * a - i), sf);
+      // T_i = 2 T_a T_(i-a) - T_(2a-i); T_(2a-i) joins the product before its rescale
+      const size_t lvl = std::max(level_of(get(a)), level_of(get(i - a)));
+      const PhantomCiphertext& x = aligned(a, lvl);
+      const PhantomCiphertext& y = aligned(i - a, lvl);
+      const PhantomCiphertext& z = get(2 * a - i);
+      if (level_of(z) <= lvl) {
+        r = MulAddRescale(cc, x, y, rlk, 2, {{&z, -1.0}}, 0.0);
+      } else {
+        r = MulAddRescale(cc, x, y, rlk, 2, {}, 0.0);
+        EvalSubAutoInplace(cc, r, z, sf);
+      }
     }
     return T.emplace(i, std::move(r)).first->second;
   }
@@ -205,8 +222,14 @@ struct ChebEvaluator {
       r[2 * m - i] -= c[i];
     }
     PhantomCiphertext qv = eval(q);
-    PhantomCiphertext res = EvalMultRescale(cc, qv, get(m), rlk, sf);
     PhantomCiphertext rv = eval(r);
+    // q T_m + r: r joins the product before its rescale when it is not deeper than it
+    const size_t lvl = std::max(level_of(qv), level_of(get(m)));
+    PhantomCiphertext tmp;
+    const PhantomCiphertext& x = AtLevel(cc, qv, lvl, sf, tmp);
+    const PhantomCiphertext& y = aligned(m, lvl);
+    if (level_of(rv) <= lvl) return MulAddRescale(cc, x, y, rlk, 1, {{&rv, 1.0}}, 0.0);
+    PhantomCiphertext res = MulAddRescale(cc, x, y, rlk, 1, {}, 0.0);
     EvalAddAutoInplace(cc, res, rv, sf);
     return res;
   }
@@ -215,50 +238,68 @@ struct ChebEvaluator {
 }  // namespace
 
 // ======================================================================================
-// two concurrent chains: `main` on the context's stream (this thread), `aux` on its second
-// stream from a worker thread (StreamScope).  The aux stream starts after everything already
-// enqueued on the main stream; the main stream continues after both.  Buffers allocated on one
-// stream and used on the other must stay alive until this returns.
+// concurrent chains: task(0) on the context's stream (this thread), task(i) on the context's
+// aux stream i - 1 from worker thread i (StreamScope).  Every aux stream starts after everything
+// already enqueued on the main stream; the main stream continues after all of them.  Buffers
+// allocated on one stream and used on another must stay alive until this returns.  Called from
+// a thread that already runs under a StreamScope (a nested use), the tasks run in order there.
 // ======================================================================================
-template <typename Main, typename Aux>
-static void run_concurrently(const PhantomContext& cc, Main&& main, Aux&& aux) {
-  const hipStream_t s0 = cc.stream(), s1 = cc.aux_stream();
-  hipEvent_t fork, join;
-  PHX_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-  PHX_CHECK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
-  PHX_CHECK(hipEventRecord(fork, s0));
-  PHX_CHECK(hipStreamWaitEvent(s1, fork, 0));
-  std::exception_ptr err_aux, err_main;
-  std::thread worker([&] {
-    try {
-      StreamScope scope(s1);
-      aux();
-    } catch (...) {
-      err_aux = std::current_exception();
-    }
-  });
-  try {
-    main();
-  } catch (...) {
-    err_main = std::current_exception();
+template <typename Task>
+static void run_parallel(const PhantomContext& cc, int k, Task&& task) {
+  k = std::min(k, 1 + PhantomContext::kAuxStreams);
+  if (k <= 1 || StreamScope::current()) {
+    for (int i = 0; i < k; ++i) task(i);
+    return;
   }
-  worker.join();
-  const hipError_t e = hipEventRecord(join, s1);
-  if (e == hipSuccess) (void)hipStreamWaitEvent(s0, join, 0);
-  if (err_main || err_aux || e != hipSuccess) {
-    (void)hipStreamSynchronize(s1);
+  const hipStream_t s0 = cc.stream();
+  hipEvent_t fork;
+  std::vector<hipEvent_t> join(k - 1);
+  PHX_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+  for (auto& e : join) PHX_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  PHX_CHECK(hipEventRecord(fork, s0));
+  for (int i = 1; i < k; ++i) PHX_CHECK(hipStreamWaitEvent(cc.aux_stream(i - 1), fork, 0));
+  std::vector<std::exception_ptr> err(k);
+  std::vector<std::thread> workers;
+  for (int i = 1; i < k; ++i)
+    workers.emplace_back([&, i] {
+      try {
+        StreamScope scope(cc.aux_stream(i - 1));
+        task(i);
+      } catch (...) {
+        err[i] = std::current_exception();
+      }
+    });
+  try {
+    task(0);
+  } catch (...) {
+    err[0] = std::current_exception();
+  }
+  for (auto& w : workers) w.join();
+  hipError_t e = hipSuccess;
+  for (int i = 1; i < k; ++i) {
+    if (e == hipSuccess) e = hipEventRecord(join[i - 1], cc.aux_stream(i - 1));
+    if (e == hipSuccess) e = hipStreamWaitEvent(s0, join[i - 1], 0);
+  }
+  bool failed = e != hipSuccess;
+  for (auto& x : err) failed |= static_cast<bool>(x);
+  if (failed) {
+    for (int i = 1; i < k; ++i) (void)hipStreamSynchronize(cc.aux_stream(i - 1));
     (void)hipStreamSynchronize(s0);
   }
   (void)hipEventDestroy(fork);
-  (void)hipEventDestroy(join);
-  if (err_main) std::rethrow_exception(err_main);
-  if (err_aux) std::rethrow_exception(err_aux);
+  for (auto& j : join) (void)hipEventDestroy(j);
+  for (auto& x : err)
+    if (x) std::rethrow_exception(x);
   PHX_CHECK(e);
 }
 
 // ======================================================================================
 // FHECKKSRNS
 // ======================================================================================
+
+FHECKKSRNS::FHECKKSRNS(PhantomCKKSEncoder& encoder) : encoder_(encoder) {
+  if (const char* e = std::getenv("PHX_BOOT_GIANT_STREAMS")) giant_streams_ = std::max(1, std::atoi(e));
+}
 
 uint32_t FHECKKSRNS::GetBootstrapDepth(const std::vector<uint32_t>& levelBudget) {
   return levelBudget.at(0) + levelBudget.at(1) + static_cast<uint32_t>(cheb_depth(kChebDegree)) + R_UNIFORM;
@@ -435,19 +476,23 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
   }
   hip_ok(phx::lt_bsgs(la, n, s), "linear transform inner products");
   baby.clear();
-  // giant steps accumulate in the extended basis (one moddown at the end), the odd ones on
-  // the context's second stream; inner[] (main-stream buffers) lives until both have joined
-  PhantomCiphertext acc = std::move(inner[0]), acc_aux;
-  auto giants = [&](int first, PhantomCiphertext& a, bool have) {
-    for (int i = first; i < lv.b; i += 2) {
-      EvalRotateExtAccumulate(cc, inner[i], galois_keys_, static_cast<int>(static_cast<long>(lv.g) * i * lv.stride), a,
-                              have);
+  // giant steps accumulate in the extended basis (one moddown at the end), spread over the
+  // context's streams (giant i on chain i mod k); inner[] (main-stream buffers) lives until all
+  // chains have joined
+  const int k = std::max(1, std::min(giant_streams_, lv.b));
+  std::vector<PhantomCiphertext> part(k);
+  part[0] = std::move(inner[0]);
+  run_parallel(cc, k, [&](int t) {
+    bool have = t == 0;
+    for (int i = t == 0 ? k : t; i < lv.b; i += k) {
+      EvalRotateExtAccumulate(cc, inner[i], galois_keys_, static_cast<int>(static_cast<long>(lv.g) * i * lv.stride),
+                              part[t], have);
       have = true;
     }
-  };
-  run_concurrently(
-      cc, [&] { giants(2, acc, true); }, [&] { giants(1, acc_aux, false); });
-  if (lv.b > 1) EvalAddExtInPlace(cc, acc, acc_aux);
+  });
+  PhantomCiphertext acc = std::move(part[0]);
+  for (int t = 1; t < k; ++t)
+    if (part[t].size()) EvalAddExtInPlace(cc, acc, part[t]);
   inner.clear();
   acc.set_scale(ct.scale() * sf_.at(lv.chain - 1));
   acc.SetNoiseScaleDeg(2);
@@ -478,9 +523,9 @@ PhantomCiphertext FHECKKSRNS::EvalChebyshevSeries(const PhantomCiphertext& ct, c
 void FHECKKSRNS::ApplyDoubleAngleIterations(PhantomCiphertext& ct, const PhantomContext& cc, uint32_t numIter) const {
   const int r = static_cast<int>(numIter);
   for (int j = 1; j <= r; ++j) {
-    ct = EvalMultRescale(cc, ct, ct, mul_key_, sf_);
-    add_inplace(cc, ct, ct);
-    EvalAddConstInplace(cc, ct, -1.0 / std::pow(2.0 * M_PI, std::pow(2.0, j - r)));
+    // 2 ct^2 - (2 pi)^(-2^(j - r)): doubling and constant folded in before the key switch
+    if (ct.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, ct, 1);
+    ct = MulAddRescale(cc, ct, ct, mul_key_, 2, {}, -1.0 / std::pow(2.0 * M_PI, std::pow(2.0, j - r)));
   }
 }
 
@@ -538,12 +583,14 @@ PhantomCiphertext FHECKKSRNS::EvalBootstrap(const PhantomCiphertext& in, const P
   // launches that leave most of the GPU idle on their own)
   // enc_i (allocated on the main stream) stays alive until the main stream has joined
   PhantomCiphertext im;
-  run_concurrently(
-      cc, [&] { enc = eval_mod(enc, cc); },
-      [&] {
-        im = eval_mod(enc_i, cc);
-        MultByMonomialInPlace(cc, im, M / 4);  // times i
-      });
+  run_parallel(cc, 2, [&](int t) {
+    if (t == 0) {
+      enc = eval_mod(enc, cc);
+    } else {
+      im = eval_mod(enc_i, cc);
+      MultByMonomialInPlace(cc, im, M / 4);  // times i
+    }
+  });
   trace(cc, "evalmod", enc);
   EvalAddAutoInplace(cc, enc, im, sf_);
   // SlotToCoeff and undo the correction scaling

@@ -45,7 +45,7 @@ double scaled_cosine(double y, const double* args /* {K, r} */);
 
 class FHECKKSRNS {
  public:
-  explicit FHECKKSRNS(PhantomCKKSEncoder& encoder) : encoder_(encoder) {}
+  explicit FHECKKSRNS(PhantomCKKSEncoder& encoder);
 
   // EvalBootstrapSetup (bootstrap.cu:15-181): linear-transform plaintexts and EvalMod constants.
   // `sf` are the FLEXIBLEAUTO scaling factors (precompute_scaling_factors).
@@ -98,6 +98,7 @@ class FHECKKSRNS {
   uint32_t correction_ = 0;
   std::vector<LTLevel> enc_, dec_;
   std::vector<double> cheb_;
+  int giant_streams_ = 2;  // PHX_BOOT_GIANT_STREAMS: concurrent giant-step chains per level
   PhantomRelinKey mul_key_;
   PhantomGaloisKey galois_keys_;  // fused keys
 };

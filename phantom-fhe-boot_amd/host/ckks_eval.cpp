@@ -300,6 +300,35 @@ PhantomCiphertext KeySwitchDownRescale(const PhantomContext& ctx, PhantomCiphert
   return out;
 }
 
+PhantomCiphertext MulAddRescale(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
+                                const PhantomRelinKey& rlk, int factor, const std::vector<ScaledTerm>& terms,
+                                double constant) {
+  if (a.chain_index() != b.chain_index() || a.GetNoiseScaleDeg() > 1 || b.GetNoiseScaleDeg() > 1)
+    throw std::invalid_argument("MulAddRescale: operands must be level-aligned and of degree 1");
+  const size_t n = ctx.poly_degree();
+  PhantomCiphertext d = multiply(ctx, a, b);
+  const size_t L = d.coeff_modulus_size(), chain = d.chain_index();
+  const double S = d.scale();
+  const uint64_t* q = ctx.mod_QP().q;
+  hipStream_t s = ctx.stream();
+  const phx::LimbScalars ca = limb_scalars(ctx, chain, static_cast<double>(factor));
+  bool scaled = factor == 1;
+  for (const ScaledTerm& t : terms) {
+    if (t.ct->chain_index() > chain || t.ct->GetNoiseScaleDeg() > 1 || t.ct->size() != 2)
+      throw std::invalid_argument("MulAddRescale: a term is below the product's level");
+    // round(c S / scale_t) t carries c m_t at the product's scale S
+    const phx::LimbScalars cb = limb_scalars(ctx, chain, t.coeff * S / t.ct->scale());
+    hip_ok(phx::lin_comb_v(d.data(), scaled ? 2 : 3, scaled ? nullptr : &ca, t.ct->data(), 2,
+                           t.ct->coeff_modulus_size() * n, cb, q, n, L, s),
+           "mul-add term");
+    scaled = true;
+  }
+  if (!scaled) hip_ok(phx::lin_comb_v(d.data(), 3, &ca, nullptr, 0, 0, ca, q, n, L, s), "mul-add factor");
+  if (constant != 0.0) EvalAddConstInplace(ctx, d, constant);
+  d.SetNoiseScaleDeg(2);
+  return RelinearizeRescale(ctx, d, rlk);
+}
+
 PhantomCiphertext EvalMultRescale(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
                                   const PhantomRelinKey& rlk, const std::vector<double>& sf) {
   const size_t target = std::max(level_after_reduce(a), level_after_reduce(b));

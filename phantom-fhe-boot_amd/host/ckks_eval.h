@@ -60,6 +60,17 @@ void EvalSubAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const P
 PhantomCiphertext RelinearizeRescale(const PhantomContext& ctx, const PhantomCiphertext& d3, const PhantomRelinKey& rlk);
 // KeySwitchDown followed by a rescale, as one division by P q_last
 PhantomCiphertext KeySwitchDownRescale(const PhantomContext& ctx, PhantomCiphertext& ext);
+// rescale(relinearize(factor a b + sum_t coeff_t t + constant)) with one key switch: every term
+// t (degree 1, at the product's level or above, i.e. with at least its limbs) is brought to the
+// product's scale by an integer multiply before the rescale, so it costs no rescale of its own
+// (the FLEXIBLEAUTO alignment would rescale it: AdjustToLevel).  a and b: degree 1, same level.
+struct ScaledTerm {
+  const PhantomCiphertext* ct;
+  double coeff;
+};
+PhantomCiphertext MulAddRescale(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
+                                const PhantomRelinKey& rlk, int factor, const std::vector<ScaledTerm>& terms,
+                                double constant);
 // level-aligned multiply + relinearize + rescale (EvalMultAuto + ModReduce)
 PhantomCiphertext EvalMultRescale(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
                                   const PhantomRelinKey& rlk, const std::vector<double>& sf);

@@ -14,9 +14,9 @@ PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t s
     PHX_CHECK(hipStreamCreateWithFlags(&stream_.s, hipStreamNonBlocking));
     stream_.owned = true;
   }
-  {
-    PHX_CHECK(hipStreamCreateWithFlags(&aux_.s, hipStreamNonBlocking));
-    aux_.owned = true;
+  for (auto& a : aux_) {
+    PHX_CHECK(hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking));
+    a.owned = true;
   }
   hipStream_t s = stream_.s;
   if (params.scheme() != scheme_type::ckks) throw std::invalid_argument("only CKKS is supported by this engine");

@@ -119,13 +119,14 @@ class PhantomContext {
     const hipStream_t o = StreamScope::current();
     return o ? o : stream_.s;
   }
-  // a second stream owned by the context, for work that runs beside stream()
-  hipStream_t aux_stream() const { return aux_.s; }
+  // further streams owned by the context, for work that runs beside stream()
+  static constexpr int kAuxStreams = 3;
+  hipStream_t aux_stream(int i = 0) const { return aux_[i].s; }
   Workspace& workspace() const { return *ws_; }
 
  private:
   OwnedStream stream_;  // first members: destroyed after everything that frees on them
-  OwnedStream aux_;
+  OwnedStream aux_[kAuxStreams];
   EncryptionParameters params_;
   size_t n_ = 0, size_Q_ = 0, size_P_ = 0;
   std::vector<uint64_t> qp_;

@@ -28,7 +28,14 @@ def run(fn, iters=60):
     return ts[len(ts) // 2]
 fwd = run(lib.phantom_nwt_forward_inplace)
 inv = run(lib.phantom_nwt_backward_inplace)
-print("RESULT", fwd, inv)
+def b2b(fn, iters=150):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for i in range(10): PA.check(fn(ring[i % 15].data_ptr(), t.handle, L, 0, s.cuda_stream))
+    a.record(s)
+    for i in range(iters): PA.check(fn(ring[i % 15].data_ptr(), t.handle, L, 0, s.cuda_stream))
+    b.record(s); torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1e3 / iters
+print("RESULT", fwd, inv, b2b(lib.phantom_nwt_forward_inplace), b2b(lib.phantom_nwt_backward_inplace))
 '''
 res = {}
 for name in sorted(os.listdir(os.path.join(ROOT, "tools", "variants"))):
@@ -36,8 +43,8 @@ for name in sorted(os.listdir(os.path.join(ROOT, "tools", "variants"))):
     out = subprocess.run([sys.executable, "-c", CODE, py], capture_output=True, text=True, timeout=300)
     line = [l for l in out.stdout.splitlines() if l.startswith("RESULT")]
     if line:
-        f, i = map(float, line[0].split()[1:])
-        res[name] = {"fwd_us": round(f, 2), "inv_us": round(i, 2)}
+        f, i, fb, ib = map(float, line[0].split()[1:])
+        res[name] = {"fwd_us": round(f, 2), "inv_us": round(i, 2), "fwd_b2b_us": round(fb, 2), "inv_b2b_us": round(ib, 2)}
     else:
         res[name] = {"error": out.stderr[-500:]}
     print(name, res[name], flush=True)
