@@ -46,6 +46,24 @@ struct LtArgs {
 };
 hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s);
 
+// ---- Chebyshev leaves: M linear combinations of the same K ciphertexts in one pass ----------
+//   out[m][t][l] = sum_k in[k][t][l] * coef[m][k][l] + (t == 0 ? cadd[m][l] : 0)   (mod q_l)
+// in[k]: [2][*][n] ciphertexts with at least L limbs (polynomial stride in_stride[k] elements),
+// out[m]: [2][L][n]; coef: device [2][M][K][L] (values, then Shoup quotients), cadd: [M][L].
+// Every input is read once for all M outputs (the reference evaluates each leaf by separate
+// EvalMult/EvalAdd passes: bootstrap.cu EvalChebyshevSeriesPS).
+constexpr int kLeafMaxK = 16, kLeafMaxM = 8;
+struct LeafArgs {
+  const uint64_t* in[kLeafMaxK];
+  size_t in_stride[kLeafMaxK];
+  uint64_t* out[kLeafMaxM];
+  const uint64_t* coef;
+  const uint64_t* cadd;
+  const uint64_t* q;
+  int K = 0, M = 0, L = 0;
+};
+hipError_t leaf_combine(const LeafArgs& a, size_t n, hipStream_t s);
+
 // out[l] = in[l] * c[l] (+ acc[l]) with per-limb constants passed by value (no device upload);
 // L <= kMaxScalarLimbs
 constexpr int kMaxScalarLimbs = 64;

@@ -159,6 +159,31 @@ __global__ __launch_bounds__(kBlock) void lin_comb_kernel(uint64_t* d, LimbScala
   }
 }
 
+// one element (t, l, k) per thread and step; inputs read once, M accumulators
+template <int K>
+__global__ __launch_bounds__(kBlock) void leaf_combine_kernel(LeafArgs a, uint32_t log_n, size_t total) {
+  const size_t ln = static_cast<size_t>(a.L) << log_n;  // elements per output polynomial
+  const size_t mkl = static_cast<size_t>(a.M) * K * a.L;
+  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
+    const uint32_t t = e >= ln ? 1 : 0;
+    const size_t el = e - t * ln;                          // offset inside the polynomial
+    const uint32_t l = static_cast<uint32_t>(el >> log_n);
+    const uint64_t ql = a.q[l];
+    uint64_t x[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) x[k] = a.in[k][t * a.in_stride[k] + el];
+    for (int m = 0; m < a.M; ++m) {
+      const uint64_t* cv = a.coef + static_cast<size_t>(m) * K * a.L + l;
+      uint64_t acc = t == 0 ? a.cadd[static_cast<size_t>(m) * a.L + l] : 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        acc = add_mod(acc, mul_shoup(x[k], cv[static_cast<size_t>(k) * a.L], cv[mkl + static_cast<size_t>(k) * a.L], ql),
+                      ql);
+      a.out[m][e] = acc;
+    }
+  }
+}
+
 int grid_for(size_t items) {
   const size_t b = (items + kBlock - 1) / kBlock;
   return static_cast<int>(std::max<size_t>(1, std::min<size_t>(b, 2048)));
@@ -202,6 +227,24 @@ hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s) {
     case 8: lt_bsgs_kernel<8><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
     case 16: lt_bsgs_kernel<16><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
     case 32: lt_bsgs_kernel<32><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t leaf_combine(const LeafArgs& a, size_t n, hipStream_t s) {
+  if (a.K < 1 || a.K > kLeafMaxK || a.M < 1 || a.M > kLeafMaxM || a.L < 1 || !a.coef || !a.cadd)
+    return hipErrorInvalidValue;
+  const size_t total = 2 * n * static_cast<size_t>(a.L);
+  const uint32_t log_n = __builtin_ctzll(n);
+  const int grid = grid_for(total);
+  switch (a.K) {
+#define PHX_LEAF_CASE(K) \
+  case K: leaf_combine_kernel<K><<<grid, kBlock, 0, s>>>(a, log_n, total); break;
+    PHX_LEAF_CASE(1) PHX_LEAF_CASE(2) PHX_LEAF_CASE(3) PHX_LEAF_CASE(4) PHX_LEAF_CASE(5) PHX_LEAF_CASE(6)
+    PHX_LEAF_CASE(7) PHX_LEAF_CASE(8) PHX_LEAF_CASE(9) PHX_LEAF_CASE(10) PHX_LEAF_CASE(11) PHX_LEAF_CASE(12)
+    PHX_LEAF_CASE(13) PHX_LEAF_CASE(14) PHX_LEAF_CASE(15) PHX_LEAF_CASE(16)
+#undef PHX_LEAF_CASE
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

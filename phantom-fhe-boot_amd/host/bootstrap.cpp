@@ -118,6 +118,7 @@ double scaled_cosine(double y, const double* args) {
 namespace {
 
 constexpr int kLeafDegree = 15;
+static_assert(kLeafDegree <= phx::kLeafMaxK, "leaf degree above the leaf kernel's input count");
 
 int ceil_log2(int x) {
   int r = 0;
@@ -137,6 +138,7 @@ struct ChebEvaluator {
   const PhantomContext& cc;
   const PhantomRelinKey& rlk;
   const std::vector<double>& sf;
+  LeafTableCache& tables;
   std::map<int, PhantomCiphertext> T;
   std::map<std::pair<int, size_t>, PhantomCiphertext> aligned_;  // T_i brought to a deeper level
 
@@ -179,39 +181,23 @@ struct ChebEvaluator {
     return T.emplace(i, std::move(r)).first->second;
   }
 
-  // sum_i c_i T_i for deg < 16: every term lands on the deepest level with scale sf[l]^2 and
-  // one rescale finishes the linear combination
-  PhantomCiphertext leaf(const std::vector<double>& c) {
-    int d = static_cast<int>(c.size()) - 1;
-    while (d > 0 && c[d] == 0.0) --d;
-    size_t lvl = level_of(get(1));
-    for (int i = 1; i <= d; ++i) lvl = std::max(lvl, level_of(get(i)));
-    const double target = sf.at(lvl) * sf.at(lvl);
-    // one kernel per term: acc (+)= round(c_i target / scale_i) * T_i, T_i's extra limbs dropped
-    PhantomCiphertext acc;
-    bool have = false;
-    for (int i = 1; i <= d; ++i) {
-      if (c[i] == 0.0) continue;
-      const PhantomCiphertext& t = get(i);
-      const double k = c[i] * target / t.scale();
-      if (!have) {
-        acc = ScaledModSwitch(cc, t, lvl + 1, k);
-        have = true;
-      } else {
-        AccumulateScaled(cc, acc, t, k);
-      }
-    }
-    if (!have) throw std::invalid_argument("constant Chebyshev leaf");
-    acc.set_scale(target);
-    acc.SetNoiseScaleDeg(2);
-    EvalAddConstInplace(cc, acc, c[0]);
-    EvalModReduceInPlace(cc, acc, 1);
-    return acc;
-  }
+  // ---- the series as a tree: p = q T_m + r down to degree <= kLeafDegree leaves ----------
+  struct Node {
+    std::vector<double> c;  // leaf coefficients
+    int m = 0;              // inner node: q T_m + r
+    std::unique_ptr<Node> q, r;
+    PhantomCiphertext v;    // a leaf's value
+  };
 
-  PhantomCiphertext eval(const std::vector<double>& c) {
-    const int d = static_cast<int>(c.size()) - 1;
-    if (d <= kLeafDegree) return leaf(c);
+  static std::unique_ptr<Node> plan(const std::vector<double>& c) {
+    auto node = std::make_unique<Node>();
+    int d = static_cast<int>(c.size()) - 1;
+    if (d <= kLeafDegree) {
+      node->c = c;
+      while (d > 0 && node->c[d] == 0.0) --d;
+      node->c.resize(d + 1);
+      return node;
+    }
     int m = 1;
     while (2 * m <= d) m *= 2;
     // c_i T_i = c_i (2 T_m T_(i-m) - T_(2m-i)) for m < i <= d; i = m gives T_m T_0
@@ -221,17 +207,100 @@ struct ChebEvaluator {
       q[i - m] = 2.0 * c[i];
       r[2 * m - i] -= c[i];
     }
-    PhantomCiphertext qv = eval(q);
-    PhantomCiphertext rv = eval(r);
+    node->m = m;
+    node->q = plan(q);
+    node->r = plan(r);
+    return node;
+  }
+
+  static void collect(Node* n, std::vector<Node*>& out) {
+    if (!n->m) {
+      out.push_back(n);
+      return;
+    }
+    collect(n->q.get(), out);
+    collect(n->r.get(), out);
+  }
+
+  // every leaf sum_i c_i T_i lands on the deepest level of its T_1..T_d with scale sf[l]^2;
+  // the leaves of one level are evaluated together by one kernel that reads each T_i once
+  // (FHECKKSRNS::leaf_tables caches the constant tables), then each is rescaled
+  void eval_leaves(std::vector<Node*>& leaves) {
+    std::map<size_t, std::vector<Node*>> by_level;
+    for (Node* lf : leaves) {
+      const int d = static_cast<int>(lf->c.size()) - 1;
+      if (d < 1) throw std::invalid_argument("constant Chebyshev leaf");
+      size_t lvl = 0;
+      for (int i = 1; i <= d; ++i) lvl = std::max(lvl, level_of(get(i)));
+      by_level[lvl].push_back(lf);
+    }
+    const size_t n = cc.poly_degree();
+    for (auto& [lvl, group] : by_level) {
+      for (size_t g0 = 0; g0 < group.size(); g0 += phx::kLeafMaxM) {
+        const int M = static_cast<int>(std::min<size_t>(phx::kLeafMaxM, group.size() - g0));
+        int K = 0;
+        for (int m = 0; m < M; ++m) K = std::max(K, static_cast<int>(group[g0 + m]->c.size()) - 1);
+        const size_t chain = lvl + 1, L = cc.get_context_data(chain).coeff_modulus_size();
+        const double target = sf.at(lvl) * sf.at(lvl);
+        std::vector<uint64_t> tab(2 * static_cast<size_t>(M) * K * L + static_cast<size_t>(M) * L, 0);
+        uint64_t* cv = tab.data();
+        uint64_t* cs = cv + static_cast<size_t>(M) * K * L;
+        uint64_t* ca = cs + static_cast<size_t>(M) * K * L;
+        for (int m = 0; m < M; ++m) {
+          const std::vector<double>& c = group[g0 + m]->c;
+          for (int k = 0; k < K; ++k) {
+            const double coeff = k + 1 < static_cast<int>(c.size()) ? c[k + 1] : 0.0;
+            const size_t off = (static_cast<size_t>(m) * K + k) * L;
+            ScalarResidues(cc, chain, coeff * target / get(k + 1).scale(), cv + off, cs + off);
+          }
+          ScalarResidues(cc, chain, c[0] * target, ca + static_cast<size_t>(m) * L, nullptr);
+        }
+        phx::LeafArgs la;
+        la.K = K;
+        la.M = M;
+        la.L = static_cast<int>(L);
+        la.q = cc.mod_QP().q;
+        la.coef = tables.get(tab, cc.stream());
+        la.cadd = la.coef + 2 * static_cast<size_t>(M) * K * L;
+        for (int k = 0; k < K; ++k) {
+          la.in[k] = get(k + 1).data();
+          la.in_stride[k] = get(k + 1).coeff_modulus_size() * n;
+        }
+        for (int m = 0; m < M; ++m) {
+          PhantomCiphertext& v = group[g0 + m]->v;
+          v.resize(cc, chain, 2, cc.stream(), false);
+          v.set_ntt_form(true);
+          v.set_scale(target);
+          v.SetNoiseScaleDeg(2);
+          la.out[m] = v.data();
+        }
+        hip_ok(phx::leaf_combine(la, n, cc.stream()), "Chebyshev leaves");
+        for (int m = 0; m < M; ++m) EvalModReduceInPlace(cc, group[g0 + m]->v, 1);
+      }
+    }
+  }
+
+  PhantomCiphertext combine(Node* node) {
+    if (!node->m) return std::move(node->v);
+    PhantomCiphertext qv = combine(node->q.get());
+    PhantomCiphertext rv = combine(node->r.get());
     // q T_m + r: r joins the product before its rescale when it is not deeper than it
-    const size_t lvl = std::max(level_of(qv), level_of(get(m)));
+    const size_t lvl = std::max(level_of(qv), level_of(get(node->m)));
     PhantomCiphertext tmp;
     const PhantomCiphertext& x = AtLevel(cc, qv, lvl, sf, tmp);
-    const PhantomCiphertext& y = aligned(m, lvl);
+    const PhantomCiphertext& y = aligned(node->m, lvl);
     if (level_of(rv) <= lvl) return MulAddRescale(cc, x, y, rlk, 1, {{&rv, 1.0}}, 0.0);
     PhantomCiphertext res = MulAddRescale(cc, x, y, rlk, 1, {}, 0.0);
     EvalAddAutoInplace(cc, res, rv, sf);
     return res;
+  }
+
+  PhantomCiphertext eval(const std::vector<double>& c) {
+    std::unique_ptr<Node> root = plan(c);
+    std::vector<Node*> leaves;
+    collect(root.get(), leaves);
+    eval_leaves(leaves);
+    return combine(root.get());
   }
 };
 
@@ -296,6 +365,17 @@ static void run_parallel(const PhantomContext& cc, int k, Task&& task) {
 // ======================================================================================
 // FHECKKSRNS
 // ======================================================================================
+
+const uint64_t* LeafTableCache::get(const std::vector<uint64_t>& table, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = tables_.find(table);
+  if (it == tables_.end()) {
+    DeviceBuffer<uint64_t> d;
+    d.upload(table, s);  // once per distinct table: the same constants recur every bootstrap
+    it = tables_.emplace(table, std::move(d)).first;
+  }
+  return it->second.get();
+}
 
 FHECKKSRNS::FHECKKSRNS(PhantomCKKSEncoder& encoder) : encoder_(encoder) {
   if (const char* e = std::getenv("PHX_BOOT_GIANT_STREAMS")) giant_streams_ = std::max(1, std::atoi(e));
@@ -513,7 +593,7 @@ PhantomCiphertext FHECKKSRNS::EvalSlotsToCoeffs(const PhantomCiphertext& ct, con
 
 PhantomCiphertext FHECKKSRNS::EvalChebyshevSeries(const PhantomCiphertext& ct, const PhantomContext& cc,
                                                   const std::vector<double>& coeffs) const {
-  ChebEvaluator ev{cc, mul_key_, sf_, {}};
+  ChebEvaluator ev{cc, mul_key_, sf_, leaf_tables_, {}, {}};
   PhantomCiphertext x = ct;
   if (x.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, x, 1);
   ev.T.emplace(1, std::move(x));

@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "ciphertext.h"
@@ -42,6 +43,17 @@ std::vector<double> chebyshev_coefficients(double (*f)(double, const double*), c
 // the EvalMod target before the double-angle iterations: (2 pi)^(-2^-r) cos(2 pi (K y - 1/4) / 2^r)
 double scaled_cosine(double y, const double* args /* {K, r} */);
 }  // namespace boot
+
+// device copies of the Chebyshev leaf constant tables, keyed by content (they depend only on
+// the levels and scales the evaluation reaches, the same for every bootstrap)
+class LeafTableCache {
+ public:
+  const uint64_t* get(const std::vector<uint64_t>& table, hipStream_t s);
+
+ private:
+  std::mutex mu_;
+  std::map<std::vector<uint64_t>, DeviceBuffer<uint64_t>> tables_;
+};
 
 class FHECKKSRNS {
  public:
@@ -99,6 +111,7 @@ class FHECKKSRNS {
   std::vector<LTLevel> enc_, dec_;
   std::vector<double> cheb_;
   int giant_streams_ = 2;  // PHX_BOOT_GIANT_STREAMS: concurrent giant-step chains per level
+  mutable LeafTableCache leaf_tables_;
   PhantomRelinKey mul_key_;
   PhantomGaloisKey galois_keys_;  // fused keys
 };

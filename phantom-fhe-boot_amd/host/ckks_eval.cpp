@@ -151,6 +151,14 @@ void EvalModReduceInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, size
   }
 }
 
+void ScalarResidues(const PhantomContext& ctx, size_t chain, double k, uint64_t* v, uint64_t* vs) {
+  const auto& mods = ctx.get_context_data(chain).moduli();
+  for (size_t l = 0; l < mods.size(); ++l) {
+    v[l] = residue_of_double(k, mods[l]);
+    if (vs) vs[l] = shoup(v[l], mods[l]);
+  }
+}
+
 // exact residues of round(k) at `chain` as kernel-argument constants (L <= kMaxScalarLimbs)
 static phx::LimbScalars limb_scalars(const PhantomContext& ctx, size_t chain, double k) {
   const auto& mods = ctx.get_context_data(chain).moduli();

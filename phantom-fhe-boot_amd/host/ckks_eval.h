@@ -25,6 +25,8 @@ inline size_t level_of(const PhantomCiphertext& ct) { return ct.chain_index() - 
 // FLEXIBLEAUTO scaling factors per level (PreComputeScale): sf[0] = q_{L-1}, sf[k] = sf[k-1]^2 / q_{L-k}
 std::vector<double> precompute_scaling_factors(const PhantomContext& ctx, double scale);
 
+// residues of round(k) modulo every prime of `chain` (v), with Shoup quotients (vs, optional)
+void ScalarResidues(const PhantomContext& ctx, size_t chain, double k, uint64_t* v, uint64_t* vs);
 // multiply every polynomial by round(k) (exact residues of a double; scale metadata unchanged)
 void mult_by_real_integer_inplace(const PhantomContext& ctx, PhantomCiphertext& ct, double k);
 // MultByIntegerInPlace (src/evaluate.cu:3942-3970)
