@@ -112,6 +112,18 @@ int phantom_keyswitch_inner_prod(const phantom_context *ctx, size_t chain_index,
  * -> out [L][n] = (cx_i - NTT(bconv(INTT(cx_i|P)))) * P^-1 */
 int phantom_moddown_from_ntt(const phantom_context *ctx, size_t chain_index, uint64_t *cx_i, uint64_t *out,
                              hipStream_t stream);
+/* Fused forms used by the bootstrap (no single reference function; each replaces a pair):
+ * phantom_moddown_modup: moddown_from_NTT of one extended-basis polynomial followed by the modup of
+ * its result (KeySwitchDown + EvalFastRotationPrecompute in EvalLinearTransform's giant steps,
+ * src/bootstrap.cu:1335-1348) = modup(moddown(cx_i)) bit for bit.  cx_i [QlP][n] is clobbered;
+ * t_mod_up [beta][QlP][n].
+ * phantom_moddown_rescale: moddown_from_NTT followed by rescale_to_next as one division by
+ * P q_last (the same algorithm with {q_last} u P as the dropped basis): cx [polys][QlP][n] at
+ * chain_index (clobbered) -> out [polys][Ql-1][n]. */
+int phantom_moddown_modup(const phantom_context *ctx, size_t chain_index, uint64_t *cx_i, uint64_t *t_mod_up,
+                          hipStream_t stream);
+int phantom_moddown_rescale(const phantom_context *ctx, size_t chain_index, uint64_t *cx, uint64_t *out,
+                            size_t polys, hipStream_t stream);
 /* rescale_to_next (src/evaluate.cu:1779-1801) -> divide_and_round_q_last_ntt (src/rns.cu:1160-1184):
  * in [polys][L][n] at chain_index -> out [polys][L-1][n] */
 int phantom_rescale_to_next(const phantom_context *ctx, size_t chain_index, const uint64_t *in, uint64_t *out,

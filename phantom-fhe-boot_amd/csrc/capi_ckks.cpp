@@ -130,6 +130,24 @@ int phantom_moddown_from_ntt(const phantom_context* ctx, size_t chain_index, uin
   });
 }
 
+int phantom_moddown_modup(const phantom_context* ctx, size_t chain_index, uint64_t* cx_i, uint64_t* t_mod_up,
+                          hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    tool(ctx, chain_index).moddown_modup(t_mod_up, cx_i, ctx->ctx->gpu_rns_tables(), stream);
+    return from_hip(hipGetLastError());
+  });
+}
+
+int phantom_moddown_rescale(const phantom_context* ctx, size_t chain_index, uint64_t* cx, uint64_t* out, size_t polys,
+                            hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& rt = tool(ctx, chain_index);
+    if (rt.size_Ql() < 2) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "end of modulus switching chain reached");
+    rt.moddown_rescale(out, cx, ctx->ctx->gpu_rns_tables(), stream, polys);
+    return from_hip(hipGetLastError());
+  });
+}
+
 int phantom_rescale_to_next(const phantom_context* ctx, size_t chain_index, const uint64_t* in, uint64_t* out,
                             size_t polys, hipStream_t stream) {
   PHX_CAPI_GUARD({

@@ -96,6 +96,21 @@ hipError_t moddown_finish(uint64_t* ct, const uint64_t* cx, const uint64_t* delt
                           const uint64_t* pinv_shoup, const uint64_t* q, size_t n, size_t size_ql, bool accumulate,
                           hipStream_t s, size_t polys = 1, size_t cx_stride = 0);
 
+// Coefficient-domain moddown whose result goes straight into a modup (a giant-step rotation of
+// an extended-basis ciphertext): c1 and delta [size_ql][n] coefficient form,
+//   y = (c1 - delta) P^-1 mod q_l -> t_mod_up[l / alpha][l]  (the digit's own limb)
+//   t_cks[l] = y partQlHatInv_l                                (the digits' base-conversion input)
+struct ModdownModupConsts {
+  const uint64_t* q;  // Ql
+  const uint64_t* pinv;
+  const uint64_t* pinv_shoup;
+  const uint64_t* hatinv;
+  const uint64_t* hatinv_shoup;
+};
+hipError_t moddown_modup_finish(const uint64_t* c1, const uint64_t* delta, const ModdownModupConsts& k,
+                                uint64_t* t_cks, uint64_t* t_mod_up, size_t n, size_t size_ql, size_t size_qlp,
+                                size_t alpha, hipStream_t s);
+
 // ---- rescale --------------------------------------------------------------------------
 // divide_and_round_reduce_q_last_kernel (src/rns.cu:1128-1139): tmp[j] = c_last mod q_j, j < L-1
 // for `polys` polynomials: c_last [polys][n], tmp [polys][L_next][n]

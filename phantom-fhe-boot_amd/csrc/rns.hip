@@ -328,6 +328,24 @@ __global__ __launch_bounds__(kBlock) void ks_inner_kernel(const uint64_t* __rest
   }
 }
 
+// coefficient-domain moddown tail feeding a modup: y = (c1 - delta) P^-1 (mod q_l) goes to the
+// digit's own slot of t_mod_up and, times partQlHatInv, to the base-conversion input t_cks
+__global__ __launch_bounds__(kBlock) void moddown_modup_finish_kernel(const uint64_t* c1, const uint64_t* delta,
+                                                                      ModdownModupConsts k, uint64_t* t_cks,
+                                                                      uint64_t* t_mod_up, uint32_t log_n, size_t pairs,
+                                                                      uint32_t alpha, size_t qlp_n) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const uint64_t m = k.q[l];
+    const u64x2 c = ld2(c1 + e), d = ld2(delta + e);
+    const uint64_t yx = mul_shoup(sub_mod(c.x, d.x, m), k.pinv[l], k.pinv_shoup[l], m);
+    const uint64_t yy = mul_shoup(sub_mod(c.y, d.y, m), k.pinv[l], k.pinv_shoup[l], m);
+    st2(t_mod_up + (l / alpha) * qlp_n + e, yx, yy);
+    st2(t_cks + e, mul_shoup(yx, k.hatinv[l], k.hatinv_shoup[l], m), mul_shoup(yy, k.hatinv[l], k.hatinv_shoup[l], m));
+  }
+}
+
 template <bool ACC>
 __global__ __launch_bounds__(kBlock) void moddown_finish_kernel(uint64_t* ct, const uint64_t* cx, const uint64_t* delta,
                                                                 const uint64_t* pinv, const uint64_t* pinvs,
@@ -546,6 +564,15 @@ hipError_t moddown_finish(uint64_t* ct, const uint64_t* cx, const uint64_t* delt
   else
     moddown_finish_kernel<false><<<g, kBlock, 0, s>>>(ct, cx, delta, pinv, pinv_shoup, q, __builtin_ctzll(n), pairs,
                                                       cx_stride);
+  return hipGetLastError();
+}
+
+hipError_t moddown_modup_finish(const uint64_t* c1, const uint64_t* delta, const ModdownModupConsts& k,
+                                uint64_t* t_cks, uint64_t* t_mod_up, size_t n, size_t size_ql, size_t size_qlp,
+                                size_t alpha, hipStream_t s) {
+  const size_t pairs = n * size_ql / 2;
+  moddown_modup_finish_kernel<<<grid_for(pairs), kBlock, 0, s>>>(c1, delta, k, t_cks, t_mod_up, __builtin_ctzll(n),
+                                                                 pairs, static_cast<uint32_t>(alpha), size_qlp * n);
   return hipGetLastError();
 }
 

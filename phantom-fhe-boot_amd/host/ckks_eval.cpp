@@ -451,11 +451,10 @@ void EvalRotateExtAccumulate(const PhantomContext& ctx, PhantomCiphertext& ext, 
   if (ext.size() != 2 || ext.coeff_modulus_size() != QlP) throw std::invalid_argument("not an extended-basis ciphertext");
   hipStream_t s = ctx.stream();
   const uint32_t elt = FindAutomorphismIndex2nComplex(index, n);
-  // only c1 comes down to Ql: it is what the key switch consumes; c0 stays P-scaled in QlP
-  DeviceBuffer<uint64_t> c1(Ql * n, s);
-  rt.moddown_add(c1.get(), ext.data() + QlP * n, false, ctx.gpu_rns_tables(), s, 1);
+  // only c1 comes down to Ql (it is what the key switch consumes), straight into its digits;
+  // c0 stays P-scaled in QlP
   DeviceBuffer<uint64_t> digits(rt.beta() * QlP * n, s);
-  rt.modup(digits.get(), c1.get(), ctx.gpu_rns_tables(), s);
+  rt.moddown_modup(digits.get(), ext.data() + QlP * n, ctx.gpu_rns_tables(), s);
   uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * QlP * n);
   hip_ok(phx::keyswitch_inner_prod(digits.get(), keys.get(elt).public_keys_ptr(), cx, ctx.mod_QP().q,
                                    ctx.mod_QP().barrett, n, Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s),

@@ -204,6 +204,32 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
          "moddown finish");
 }
 
+void RnsTool::moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTables& ntt, hipStream_t s) const {
+  const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_, alpha = size_P_;
+  if (size_P_ == 0) throw std::invalid_argument("no special primes");
+  phx::LimbMap all;
+  all.num_limbs = (int)size_QlP;
+  all.split = (int)size_Ql;
+  all.first_a = 0;
+  all.first_b = (int)size_Q_;
+  hip_ok(phx::ntt_inverse(ntt, c1, c1, all, nullptr, nullptr, s), "moddown-modup INTT");
+  uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, size_Ql * n_);
+  hip_ok(phx::bconv(p_to_ql_.args(c1 + size_Ql * n_, delta, true), n_, s), "moddown-modup bconv P");
+  uint64_t* t_cks = ws_->get(s, Workspace::kModupInv, size_Ql * n_);
+  phx::ModdownModupConsts k{d_Ql_.get(), d_bigPInv_mod_q_.get(), d_bigPInv_mod_q_shoup_.get(), d_partQlHatInv_.get(),
+                            d_partQlHatInv_shoup_.get()};
+  hip_ok(phx::moddown_modup_finish(c1, delta, k, t_cks, t_mod_up, n_, size_Ql, size_QlP, alpha, s),
+         "moddown-modup finish");
+  for (size_t b = 0; b < converters_.size(); ++b) {
+    const size_t start = digit_start_[b], part = digit_size_[b];
+    phx::BconvArgs a = converters_[b].args(t_cks + start * n_, t_mod_up + b * size_QlP * n_, false);
+    a.skip_at = (int)start;
+    a.skip_len = (int)part;
+    hip_ok(phx::bconv(a, n_, s), "moddown-modup bconv digits");
+  }
+  hip_ok(phx::ntt_forward(ntt, t_mod_up, t_mod_up, all.batched((int)converters_.size()), s), "moddown-modup NTT");
+}
+
 void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables& ntt, hipStream_t s,
                               size_t polys) const {
   const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_;

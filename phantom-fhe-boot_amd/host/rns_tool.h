@@ -45,6 +45,12 @@ class RnsTool {
   // ct [polys][size_Ql][n] (+)= moddown(cx).
   void moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx::NttTables& ntt, hipStream_t s,
                    size_t polys = 1) const;
+  // moddown of an extended-basis polynomial fused with the modup of its result (giant-step
+  // rotations): c1 [size_QlP][n] NTT form holding P x (a polynomial over Ql) -> t_mod_up
+  // [beta][size_QlP][n] = modup(round(c1 / P)).  The subtraction happens in the coefficient
+  // domain: one INTT over Ql u P and one NTT over every digit replace moddown's INTT(P) + NTT(Ql)
+  // and modup's INTT(Ql) + NTT(digits).  c1 is clobbered.
+  void moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTables& ntt, hipStream_t s) const;
   // moddown fused with the following rescale: cx [polys][size_QlP][n] NTT form holds P x (a
   // ciphertext at this level, scale S); out [polys][size_Ql - 1][n] = round(cx / (P q_last)),
   // the ciphertext rescaled to the next level (scale S / q_last).  One INTT over the 1 + size_P

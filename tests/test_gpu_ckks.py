@@ -114,6 +114,43 @@ def test_moddown(request, rng, fixture, chain):
     assert np.array_equal(to_host(dout), want)
 
 
+@pytest.mark.parametrize("fixture,chain", [("c3", 1), ("c3", 30), ("small", 1), ("small", 2), ("small", 5)])
+def test_moddown_modup_fused(request, rng, fixture, chain):
+    """The giant-step fusion equals modup(moddown(cx)) bit for bit."""
+    ctx = request.getfixturevalue(fixture)
+    ql, p = ctx.ql(chain), ctx.moduli[ctx.size_Q:]
+    beta = -(-len(ql) // ctx.size_P)
+    cx = O.random_limbs(rng, ctx.n, ql + p)
+    d = to_dev(cx)
+    dout = to_dev(np.zeros(beta * (len(ql) + len(p)) * ctx.n, dtype=np.uint64))
+    PA.check(_lib().phantom_moddown_modup(ctx.handle, chain, ptr(d), ptr(dout), stream()))
+    down = np.zeros(len(ql) * ctx.n, dtype=np.uint64)
+    O.lib().or_moddown_from_ntt(O.P(cx.copy()), O.P(down), ctx.n, O.P(O.arr(ql)), len(ql), O.P(O.arr(p)), len(p))
+    want = np.zeros(beta * (len(ql) + len(p)) * ctx.n, dtype=np.uint64)
+    O.lib().or_modup(O.P(down), O.P(want), ctx.n, O.P(O.arr(ql)), len(ql), O.P(O.arr(p)), len(p))
+    assert np.array_equal(to_host(dout), want)
+
+
+@pytest.mark.parametrize("fixture,chain", [("c3", 1), ("c3", 30), ("small", 1), ("small", 5)])
+def test_moddown_rescale_fused(request, rng, fixture, chain):
+    """moddown + rescale as one division by P q_last = moddown_from_NTT with {q_last} u P as the
+    special basis (the buffer layout [Ql-1][q_last][P] is exactly that split)."""
+    ctx = request.getfixturevalue(fixture)
+    ql, p = ctx.ql(chain), ctx.moduli[ctx.size_Q:]
+    polys = 2
+    cxs = [O.random_limbs(rng, ctx.n, ql + p) for _ in range(polys)]
+    d = to_dev(np.concatenate(cxs))
+    dout = to_dev(np.zeros(polys * (len(ql) - 1) * ctx.n, dtype=np.uint64))
+    PA.check(_lib().phantom_moddown_rescale(ctx.handle, chain, ptr(d), ptr(dout), polys, stream()))
+    want = []
+    for cx in cxs:
+        w = np.zeros((len(ql) - 1) * ctx.n, dtype=np.uint64)
+        O.lib().or_moddown_from_ntt(O.P(cx.copy()), O.P(w), ctx.n, O.P(O.arr(ql[:-1])), len(ql) - 1,
+                                    O.P(O.arr([ql[-1]] + list(p))), len(p) + 1)
+        want.append(w)
+    assert np.array_equal(to_host(dout), np.concatenate(want))
+
+
 @pytest.mark.parametrize("fixture,chain", [("c3", 1), ("small", 1), ("small", 4), ("small", 7)])
 def test_relinearize(request, rng, fixture, chain):
     ctx = request.getfixturevalue(fixture)
