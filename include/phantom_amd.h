@@ -124,6 +124,24 @@ int phantom_moddown_modup(const phantom_context *ctx, size_t chain_index, uint64
                           hipStream_t stream);
 int phantom_moddown_rescale(const phantom_context *ctx, size_t chain_index, uint64_t *cx, uint64_t *out,
                             size_t polys, hipStream_t stream);
+/* ---- serialization (host memory; no GPU involved) ------------------------------------
+ * The byte format of PhantomCiphertext::save / load (include/ciphertext.h:184-225): the header
+ * fields one by one (4 x size_t, double, uint64_t, size_t, bool, bool = 58 bytes) followed by
+ * size * coeff_modulus_size * poly_modulus_degree uint64_t words. */
+typedef struct phantom_ct_header {
+  uint64_t chain_index, size, poly_modulus_degree, coeff_modulus_size;
+  double scale;
+  uint64_t correction_factor, noise_scale_deg;
+  int is_ntt_form, is_asymmetric;
+} phantom_ct_header;
+/* writes the header and data (host) to out[capacity]; *written = bytes (needed size when too small) */
+int phantom_ciphertext_serialize(const phantom_ct_header *h, const uint64_t *host_data, uint8_t *out,
+                                 size_t capacity, size_t *written);
+/* parses in[len]; copies the words to host_data[capacity_words] (may be null: header only);
+ * *words = the ciphertext's word count */
+int phantom_ciphertext_deserialize(const uint8_t *in, size_t len, phantom_ct_header *h, uint64_t *host_data,
+                                   size_t capacity_words, size_t *words);
+
 /* rescale_to_next (src/evaluate.cu:1779-1801) -> divide_and_round_q_last_ntt (src/rns.cu:1160-1184):
  * in [polys][L][n] at chain_index -> out [polys][L-1][n] */
 int phantom_rescale_to_next(const phantom_context *ctx, size_t chain_index, const uint64_t *in, uint64_t *out,

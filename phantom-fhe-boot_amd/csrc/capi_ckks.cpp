@@ -1,8 +1,11 @@
 // capi_ckks.cpp — C-ABI entry points for context-level CKKS evaluation on raw device buffers
 // (declared in include/phantom_amd.h).  Thin wrappers over the C++ façade in host/.
+#include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <sstream>
+#include <string>
 #include <vector>
 
 #include "../host/buffer.h"
@@ -10,6 +13,7 @@
 #include "../host/context.h"
 #include "../host/evaluate.h"
 #include "../host/numth.h"
+#include "../host/serialize.h"
 #include "phantom_amd.h"
 #include "rns.h"
 
@@ -145,6 +149,62 @@ int phantom_moddown_rescale(const phantom_context* ctx, size_t chain_index, uint
     if (rt.size_Ql() < 2) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "end of modulus switching chain reached");
     rt.moddown_rescale(out, cx, ctx->ctx->gpu_rns_tables(), stream, polys);
     return from_hip(hipGetLastError());
+  });
+}
+
+int phantom_ciphertext_serialize(const phantom_ct_header* h, const uint64_t* host_data, uint8_t* out, size_t capacity,
+                                 size_t* written) {
+  PHX_CAPI_GUARD({
+    if (!h || !written) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    phantom::ser::CiphertextHeader c;
+    c.chain_index = h->chain_index;
+    c.size = h->size;
+    c.poly_modulus_degree = h->poly_modulus_degree;
+    c.coeff_modulus_size = h->coeff_modulus_size;
+    c.scale = h->scale;
+    c.correction_factor = h->correction_factor;
+    c.noise_scale_deg = h->noise_scale_deg;
+    c.is_ntt_form = h->is_ntt_form != 0;
+    c.is_asymmetric = h->is_asymmetric != 0;
+    const size_t need = phantom::ser::kCiphertextHeaderBytes + c.words() * sizeof(uint64_t);
+    *written = need;
+    if (!out || capacity < need) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "output buffer too small");
+    if (c.words() && !host_data) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null data");
+    std::ostringstream os;
+    phantom::ser::write_ciphertext(os, c, host_data);
+    const std::string b = os.str();
+    std::memcpy(out, b.data(), b.size());
+    return PHANTOM_OK;
+  });
+}
+
+int phantom_ciphertext_deserialize(const uint8_t* in, size_t len, phantom_ct_header* h, uint64_t* host_data,
+                                   size_t capacity_words, size_t* words) {
+  PHX_CAPI_GUARD({
+    if (!in || !h || !words) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    std::istringstream is(std::string(reinterpret_cast<const char*>(in), len));
+    phantom::ser::CiphertextHeader c;
+    std::vector<uint64_t> v;
+    try {
+      phantom::ser::read_ciphertext(is, c, v);
+    } catch (const std::runtime_error& e) {
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, e.what());
+    }
+    h->chain_index = c.chain_index;
+    h->size = c.size;
+    h->poly_modulus_degree = c.poly_modulus_degree;
+    h->coeff_modulus_size = c.coeff_modulus_size;
+    h->scale = c.scale;
+    h->correction_factor = c.correction_factor;
+    h->noise_scale_deg = c.noise_scale_deg;
+    h->is_ntt_form = c.is_ntt_form;
+    h->is_asymmetric = c.is_asymmetric;
+    *words = v.size();
+    if (host_data) {
+      if (capacity_words < v.size()) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "output buffer too small");
+      std::memcpy(host_data, v.data(), v.size() * sizeof(uint64_t));
+    }
+    return PHANTOM_OK;
   });
 }
 

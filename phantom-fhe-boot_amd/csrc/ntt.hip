@@ -38,8 +38,12 @@ namespace {
 
 constexpr int E_LOG = 4;  // elements per thread per round = 16 (radix-16 rounds)
 constexpr int E = 1 << E_LOG;
-constexpr int COLS = 16;  // columns per column-pass tile
+#ifndef PHX_NTT_COLS
+#define PHX_NTT_COLS 16
+#endif
+constexpr int COLS = PHX_NTT_COLS;  // columns per column-pass tile
 constexpr int BLOCK = 256;
+constexpr int CBLOCK = COLS * 16 > BLOCK ? COLS * 16 : BLOCK;  // column-pass workgroup bound
 #ifndef PHX_NTT_WAVES_PER_EU
 #define PHX_NTT_WAVES_PER_EU 3  // __launch_bounds__ occupancy target (waves per SIMD) of one-tile grids
 #endif
@@ -387,13 +391,13 @@ __device__ __forceinline__ void col_load(uint64_t (&x)[E], const uint64_t* src, 
 }
 
 template <int S1_LOG, int S2_LOG, bool FWD>
-__global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_col(KArgs a) {
+__global__ __launch_bounds__(CBLOCK, kWavesPerEU) void ntt_col(KArgs a) {
   using SB = Sub<S1_LOG>;
   using P = Plan<S1_LOG, S2_LOG>;
   constexpr int T = SB::T, S2 = 1 << S2_LOG, NT = COLS * T, CT = S2 / COLS, RN = SB::ROUNDS;
   constexpr int RF = FWD ? 0 : RN - 1;  // first round executed
   constexpr int RL = FWD ? RN - 1 : 0;  // last round executed
-  static_assert(NT <= BLOCK, "column tile too large");
+  static_assert(NT <= CBLOCK, "column tile too large");
   __shared__ uint64_t lds[(SB::S + SB::S / 16) * COLS];
 
   const uint32_t tid = threadIdx.x;

@@ -207,8 +207,8 @@ __global__ __launch_bounds__(kBlock) void bconv_kernel(BconvArgs a, uint32_t n, 
 // 2^60), sum_s t_s c_s = HH 2^60 + (M1 + M2) 2^30 + LL where every partial sum of <= 15 products
 // of 30-bit halves stays below 2^64: 4 v_mad_u64_u32 per term and no carry chains (the 64x64
 // product + 128-bit accumulate form costs ~7 instructions per term plus register shuffles).
-template <int IB>
-__global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32_t n, uint32_t pairs, bool prescale) {
+template <int IB, bool PRE>
+__global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32_t n, uint32_t pairs) {
   static_assert(IB <= 15, "partial sums of 30-bit products must stay below 2^64");
   constexpr uint64_t kM30 = (1ull << 30) - 1;
   // this block's [IB][kBconvJ] slice of the matrix (split in 30-bit halves) and output moduli,
@@ -235,11 +235,16 @@ __global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32
   a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial
   a.out += blockIdx.z * a.out_stride;
   uint32_t lo[2][IB], hi[2][IB];
+  // every input load issued before any use (a branch between them would serialise them)
+  u64x2 xin[IB];
+#pragma unroll
+  for (int s = 0; s < IB; ++s) xin[s] = ld2(a.in + (size_t)s * n + 2 * i);
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int s = 0; s < IB; ++s) {
-    const u64x2 x = ld2(a.in + (size_t)s * n + 2 * i);
+    const u64x2 x = xin[s];
     uint64_t tx = x.x, ty = x.y;
-    if (prescale) {
+    if constexpr (PRE) {
       const uint64_t q = a.ibase[s], w = a.qhat_inv[s], ws = a.qhat_inv_shoup[s];
       tx = mul_shoup(tx, w, ws, q);
       ty = mul_shoup(ty, w, ws, q);
@@ -523,8 +528,11 @@ hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s) {
   const dim3 g((pairs + kBlock - 1) / kBlock, (a.obase_size + kBconvJ - 1) / kBconvJ, a.polys);
   const bool pre = a.qhat_inv != nullptr;
   switch (a.ibase_size) {
-#define PHX_BCONV_CASE(K) \
-  case K: bconv_fixed_kernel<K><<<g, kBlock, 0, s>>>(a, static_cast<uint32_t>(n), pairs, pre); break;
+#define PHX_BCONV_CASE(K)                                                                      \
+  case K:                                                                                      \
+    if (pre) bconv_fixed_kernel<K, true><<<g, kBlock, 0, s>>>(a, static_cast<uint32_t>(n), pairs); \
+    else bconv_fixed_kernel<K, false><<<g, kBlock, 0, s>>>(a, static_cast<uint32_t>(n), pairs);    \
+    break;
     PHX_BCONV_CASE(1) PHX_BCONV_CASE(2) PHX_BCONV_CASE(3) PHX_BCONV_CASE(4) PHX_BCONV_CASE(5)
     PHX_BCONV_CASE(6) PHX_BCONV_CASE(7) PHX_BCONV_CASE(8) PHX_BCONV_CASE(9) PHX_BCONV_CASE(10)
     PHX_BCONV_CASE(11) PHX_BCONV_CASE(12) PHX_BCONV_CASE(13) PHX_BCONV_CASE(14) PHX_BCONV_CASE(15)

@@ -13,6 +13,7 @@
 #include <cmath>
 #include <complex>
 #include <cstdio>
+#include <sstream>
 #include <cstring>
 #include <random>
 #include <string>
@@ -264,6 +265,37 @@ int main(int argc, char** argv) {
         EvalModReduceInPlace(ctx, d, 1);
       }
       report("drain_const_mult", max_abs_err(decrypt_decode(ctx, sk, enc, d), xz), 1e-4, d.chain_index());
+    }
+    // save / load in the reference's byte formats: a ciphertext and the keys round-trip bit
+    // for bit, and a rotation with the reloaded key and secret key still decrypts
+    {
+      std::stringstream cs, ks, gs, ss;
+      ct.save(cs);
+      PhantomCiphertext c2;
+      c2.load(ctx, cs);
+      const bool same_ct = c2.to_host(ctx.stream()) == ct.to_host(ctx.stream()) && c2.scale() == ct.scale() &&
+                           c2.chain_index() == ct.chain_index();
+      rlk.save(ctx, ks);
+      PhantomRelinKey rlk2;
+      rlk2.load(ctx, ks);
+      bool same_key = rlk2.dnum() == rlk.dnum();
+      for (size_t i = 0; same_key && i < rlk.dnum(); ++i) {
+        std::vector<uint64_t> ha(2 * ctx.size_QP() * N), hb(ha.size());
+        PHX_CHECK(hipMemcpy(ha.data(), rlk.digit(i), ha.size() * 8, hipMemcpyDeviceToHost));
+        PHX_CHECK(hipMemcpy(hb.data(), rlk2.digit(i), hb.size() * 8, hipMemcpyDeviceToHost));
+        same_key = ha == hb;
+      }
+      gk.save(ctx, gs);
+      PhantomGaloisKey gk2;
+      gk2.load(ctx, gs);
+      sk.save(ctx, ss);
+      PhantomSecretKey sk2 = PhantomSecretKey::load(ctx, ss, 99);
+      PhantomCiphertext rc = EvalRotateFused(ctx, c2, gk2, 1);
+      std::vector<std::complex<double>> want(slots);
+      for (size_t j = 0; j < slots; ++j) want[j] = xz[(j + 1) % slots];
+      const double err = max_abs_err(decrypt_decode(ctx, sk2, enc, rc), want);
+      report("save_load", (same_ct && same_key && sk2.coefficients() == sk.coefficients()) ? err : 1.0, 1e-6,
+             rc.chain_index());
     }
     std::printf("{\"done\": \"ops\", \"ok\": %s}\n", g_ok ? "true" : "false");
     return g_ok ? 0 : 1;

@@ -3,6 +3,8 @@
 #include <algorithm>
 #include <stdexcept>
 
+#include "serialize.h"
+
 namespace phantom {
 
 void PhantomCiphertext::resize(const PhantomContext& ctx, size_t chain_index, size_t size, hipStream_t s,
@@ -31,6 +33,70 @@ void PhantomCiphertext::resize(size_t size, size_t L, size_t n, hipStream_t s, b
   n_ = n;
 }
 
+void PhantomCiphertext::save(std::ostream& os) const {
+  ser::CiphertextHeader h;
+  h.chain_index = chain_index_;
+  h.size = size_;
+  h.poly_modulus_degree = n_;
+  h.coeff_modulus_size = L_;
+  h.scale = scale_;
+  h.correction_factor = correction_factor_;
+  h.noise_scale_deg = noise_scale_deg_;
+  h.is_ntt_form = is_ntt_form_;
+  h.is_asymmetric = is_asymmetric_;
+  const hipStream_t s = StreamScope::current() ? StreamScope::current() : data_.stream();
+  const std::vector<uint64_t> v = to_host(s);
+  ser::write_ciphertext(os, h, v.data());
+}
+
+void PhantomCiphertext::load(const PhantomContext& ctx, std::istream& is) {
+  ser::CiphertextHeader h;
+  std::vector<uint64_t> v;
+  ser::read_ciphertext(is, h, v);
+  if (h.poly_modulus_degree != ctx.poly_degree()) throw std::invalid_argument("ciphertext degree mismatch");
+  resize(h.size, h.coeff_modulus_size, h.poly_modulus_degree, ctx.stream(), false);
+  if (!v.empty()) {
+    PHX_CHECK(hipMemcpyAsync(data_.get(), v.data(), v.size() * sizeof(uint64_t), hipMemcpyHostToDevice, ctx.stream()));
+    PHX_CHECK(hipStreamSynchronize(ctx.stream()));
+  }
+  chain_index_ = h.chain_index;
+  scale_ = h.scale;
+  correction_factor_ = h.correction_factor;
+  noise_scale_deg_ = h.noise_scale_deg;
+  is_ntt_form_ = h.is_ntt_form;
+  is_asymmetric_ = h.is_asymmetric;
+}
+
+void PhantomPlaintext::save(std::ostream& os, hipStream_t s) const {
+  ser::PlaintextHeader h;
+  h.chain_index = chain_index_;
+  h.poly_modulus_degree = n_;
+  h.coeff_modulus_size = L_;
+  h.scale = scale_;
+  std::vector<uint64_t> v(h.words());
+  if (!v.empty()) {
+    PHX_CHECK(hipMemcpyAsync(v.data(), data_.get(), v.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    PHX_CHECK(hipStreamSynchronize(s));
+  }
+  ser::write_plaintext(os, h, v.data());
+}
+
+void PhantomPlaintext::load(const PhantomContext& ctx, std::istream& is) {
+  ser::PlaintextHeader h;
+  std::vector<uint64_t> v;
+  ser::read_plaintext(is, h, v);
+  if (h.poly_modulus_degree != ctx.poly_degree()) throw std::invalid_argument("plaintext degree mismatch");
+  chain_index_ = h.chain_index;
+  n_ = h.poly_modulus_degree;
+  L_ = h.coeff_modulus_size;
+  scale_ = h.scale;
+  data_.allocate(v.size(), ctx.stream());
+  if (!v.empty()) {
+    PHX_CHECK(hipMemcpyAsync(data_.get(), v.data(), v.size() * sizeof(uint64_t), hipMemcpyHostToDevice, ctx.stream()));
+    PHX_CHECK(hipStreamSynchronize(ctx.stream()));
+  }
+}
+
 void PhantomCiphertext::copy_from(const PhantomCiphertext& o) {
   chain_index_ = o.chain_index_;
   size_ = o.size_;
@@ -40,6 +106,7 @@ void PhantomCiphertext::copy_from(const PhantomCiphertext& o) {
   correction_factor_ = o.correction_factor_;
   noise_scale_deg_ = o.noise_scale_deg_;
   is_ntt_form_ = o.is_ntt_form_;
+  is_asymmetric_ = o.is_asymmetric_;
   const size_t count = size_ * L_ * n_;
   // the copy runs on this thread's stream (a StreamScope's), else on the source's stream
   hipStream_t s = StreamScope::current() ? StreamScope::current() : o.data_.stream();

@@ -4,6 +4,8 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <istream>
+#include <ostream>
 #include <utility>
 #include <vector>
 
@@ -27,6 +29,7 @@ class PhantomCiphertext {
       correction_factor_ = o.correction_factor_;
       noise_scale_deg_ = o.noise_scale_deg_;
       is_ntt_form_ = o.is_ntt_form_;
+      is_asymmetric_ = o.is_asymmetric_;
       data_ = std::move(o.data_);
       o.size_ = o.L_ = o.n_ = 0;
     }
@@ -60,6 +63,14 @@ class PhantomCiphertext {
   void SetNoiseScaleDeg(size_t d) { noise_scale_deg_ = d; }
   void set_correction_factor(uint64_t c) { correction_factor_ = c; }
 
+  // save / load in the reference's byte format (include/ciphertext.h:184-225, host/serialize.h).
+  // load takes the context for the stream it allocates on (the reference uses
+  // cudaStreamPerThread); the loaded ciphertext keeps the saved chain index and sizes.
+  void save(std::ostream& os) const;
+  void load(const PhantomContext& ctx, std::istream& is);
+  bool is_asymmetric() const { return is_asymmetric_; }
+  void set_asymmetric(bool b) { is_asymmetric_ = b; }
+
   // host transfer helpers (the reference's save/load staging, ciphertext.h:184-225)
   std::vector<uint64_t> to_host(hipStream_t s) const;
   void from_host(const PhantomContext& ctx, size_t chain_index, size_t size, const std::vector<uint64_t>& v,
@@ -72,6 +83,7 @@ class PhantomCiphertext {
   uint64_t correction_factor_ = 1;
   size_t noise_scale_deg_ = 1;
   bool is_ntt_form_ = true;
+  bool is_asymmetric_ = false;
   DeviceBuffer<uint64_t> data_;
 };
 
@@ -90,6 +102,9 @@ class PhantomPlaintext {
   // `limbs` limbs tagged with `chain_index` (extended-basis plaintexts: Ql of the chain + P)
   void resize_ext(const PhantomContext& ctx, size_t chain_index, size_t limbs, hipStream_t s);
   void from_host(const PhantomContext& ctx, size_t chain_index, const std::vector<uint64_t>& v, hipStream_t s);
+  // save / load in the reference's byte format (include/plaintext.h:90-122)
+  void save(std::ostream& os, hipStream_t s) const;
+  void load(const PhantomContext& ctx, std::istream& is);
 
  private:
   size_t chain_index_ = 0, n_ = 0, L_ = 0;

@@ -5,8 +5,10 @@
 #include <stdexcept>
 
 #include "../csrc/ckks.h"
+#include "../csrc/ntt.h"
 #include "../csrc/rns.h"
 #include "numth.h"
+#include "serialize.h"
 
 namespace phantom {
 
@@ -19,6 +21,98 @@ void PhantomKSwitchKey::adopt(std::vector<DeviceBuffer<uint64_t>>&& digits, hipS
   std::vector<uint64_t*> p;
   for (auto& d : digits_) p.push_back(d.get());
   ptrs_.upload(p, s);
+}
+
+void PhantomKSwitchKey::save(const PhantomContext& ctx, std::ostream& os) const {
+  const uint64_t dnum = digits_.size(), n = ctx.poly_degree(), QP = ctx.size_QP();
+  os.write(reinterpret_cast<const char*>(&dnum), sizeof(dnum));
+  std::vector<uint64_t> h(2 * QP * n);
+  for (const auto& d : digits_) {
+    PHX_CHECK(hipMemcpyAsync(h.data(), d.get(), h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx.stream()));
+    PHX_CHECK(hipStreamSynchronize(ctx.stream()));
+    ser::CiphertextHeader hd;
+    hd.chain_index = 0;
+    hd.size = 2;
+    hd.poly_modulus_degree = n;
+    hd.coeff_modulus_size = QP;
+    ser::write_ciphertext(os, hd, h.data());
+  }
+}
+
+void PhantomKSwitchKey::load(const PhantomContext& ctx, std::istream& is) {
+  uint64_t dnum = 0;
+  is.read(reinterpret_cast<char*>(&dnum), sizeof(dnum));
+  if (!is || dnum > 64) throw std::runtime_error("bad key-switching key stream");
+  const uint64_t n = ctx.poly_degree(), QP = ctx.size_QP();
+  std::vector<DeviceBuffer<uint64_t>> digits;
+  for (uint64_t i = 0; i < dnum; ++i) {
+    ser::CiphertextHeader hd;
+    std::vector<uint64_t> v;
+    ser::read_ciphertext(is, hd, v);
+    if (hd.size != 2 || hd.poly_modulus_degree != n || hd.coeff_modulus_size != QP)
+      throw std::invalid_argument("key-switching key does not match the context");
+    DeviceBuffer<uint64_t> d;
+    d.upload(v, ctx.stream());
+    digits.push_back(std::move(d));
+  }
+  adopt(std::move(digits), ctx.stream());
+}
+
+void PhantomGaloisKey::save(const PhantomContext& ctx, std::ostream& os) const {
+  const uint64_t count = keys_.size();
+  os.write(reinterpret_cast<const char*>(&count), sizeof(count));
+  for (const auto& kv : keys_) kv.second.save(ctx, os);
+  for (const auto& kv : keys_) os.write(reinterpret_cast<const char*>(&kv.first), sizeof(uint32_t));
+}
+
+void PhantomGaloisKey::load(const PhantomContext& ctx, std::istream& is) {
+  uint64_t count = 0;
+  is.read(reinterpret_cast<char*>(&count), sizeof(count));
+  if (!is || count > (uint64_t(1) << 20)) throw std::runtime_error("bad Galois key stream");
+  std::vector<PhantomKSwitchKey> ks(count);
+  for (auto& k : ks) k.load(ctx, is);
+  keys_.clear();
+  for (auto& k : ks) {
+    uint32_t elt = 0;
+    is.read(reinterpret_cast<char*>(&elt), sizeof(elt));
+    if (!is) throw std::runtime_error("Galois key stream truncated");
+    keys_[elt] = std::move(k);
+  }
+}
+
+void PhantomSecretKey::save(const PhantomContext& ctx, std::ostream& os) const {
+  const uint64_t n = ctx.poly_degree(), QP = ctx.size_QP();
+  std::vector<uint64_t> h(QP * n);
+  PHX_CHECK(hipMemcpyAsync(h.data(), s_.get(), h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx.stream()));
+  PHX_CHECK(hipStreamSynchronize(ctx.stream()));
+  ser::write_secret_key(os, 1, n, QP, h.data());
+}
+
+PhantomSecretKey PhantomSecretKey::load(const PhantomContext& ctx, std::istream& is, uint64_t seed) {
+  uint64_t power = 0, n = 0, limbs = 0;
+  std::vector<uint64_t> v;
+  ser::read_secret_key(is, power, n, limbs, v);
+  if (power < 1 || n != ctx.poly_degree() || limbs != ctx.size_QP())
+    throw std::invalid_argument("secret key does not match the context");
+  v.resize(n * limbs);  // s itself; higher powers are recomputed
+  PhantomSecretKey k;
+  k.seed_state_ = seed;
+  hipStream_t s = ctx.stream();
+  k.s_.upload(v, s);
+  k.s2_.allocate(limbs * n, s);
+  hip_ok(phx::poly_mul(k.s_.get(), k.s_.get(), k.s2_.get(), ctx.mod_QP(), n, limbs, s), "sk^2");
+  // ternary coefficients from limb 0 in coefficient form
+  DeviceBuffer<uint64_t> c(n, s);
+  hip_ok(phx::ntt_inverse(ctx.gpu_rns_tables(), k.s_.get(), c.get(), phx::LimbMap::contiguous(1, 0), nullptr, nullptr, s),
+         "sk INTT");
+  const std::vector<uint64_t> h = c.download(s);
+  const uint64_t q0 = ctx.key_moduli()[0];
+  k.coeffs_.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (h[i] > 1 && h[i] != q0 - 1) throw std::invalid_argument("loaded secret key is not ternary");
+    k.coeffs_[i] = h[i] == 0 ? 0 : (h[i] == 1 ? 1 : -1);
+  }
+  return k;
 }
 
 const PhantomKSwitchKey& PhantomGaloisKey::get(uint32_t elt) const {

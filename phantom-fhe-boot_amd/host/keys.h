@@ -10,8 +10,10 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <istream>
 #include <map>
 #include <memory>
+#include <ostream>
 #include <vector>
 
 #include "buffer.h"
@@ -29,6 +31,10 @@ class PhantomKSwitchKey {
   const uint64_t* const* public_keys_ptr() const { return ptrs_.get(); }
   const uint64_t* digit(size_t i) const { return digits_.at(i).get(); }
   void adopt(std::vector<DeviceBuffer<uint64_t>>&& digits, hipStream_t s);
+  // PhantomRelinKey::save / load (include/secretkey.h:130-157): dnum, then every digit as a
+  // 2-polynomial key-level ciphertext (chain index 0, size_QP limbs, NTT form)
+  void save(const PhantomContext& ctx, std::ostream& os) const;
+  void load(const PhantomContext& ctx, std::istream& is);
 
  private:
   std::vector<DeviceBuffer<uint64_t>> digits_;
@@ -42,6 +48,12 @@ class PhantomGaloisKey {
   const PhantomKSwitchKey& get(uint32_t galois_elt) const;
   bool has(uint32_t galois_elt) const { return keys_.count(galois_elt) != 0; }
   void set(uint32_t galois_elt, PhantomKSwitchKey&& k) { keys_[galois_elt] = std::move(k); }
+  // PhantomGaloisKey::save / load (include/secretkey.h:195-220): the number of keys, then each
+  // as a relin key.  The reference indexes keys by position in its galois_elts list; here the
+  // element itself is the key, so the count is followed by the elements (uint32_t each, in
+  // ascending order) after the keys
+  void save(const PhantomContext& ctx, std::ostream& os) const;
+  void load(const PhantomContext& ctx, std::istream& is);
 
  private:
   std::map<uint32_t, PhantomKSwitchKey> keys_;
@@ -50,6 +62,10 @@ class PhantomGaloisKey {
 class PhantomSecretKey {
  public:
   PhantomSecretKey(const PhantomContext& ctx, uint64_t seed);
+  // save / load (include/secretkey.h:405-440): sk_max_power (1), n, size_QP, then s in NTT
+  // form.  A loaded key samples its later randomness from `seed`.
+  void save(const PhantomContext& ctx, std::ostream& os) const;
+  static PhantomSecretKey load(const PhantomContext& ctx, std::istream& is, uint64_t seed);
   // s in NTT form over the full Q u P chain, [size_QP][n]
   const uint64_t* secret_key_array() const { return s_.get(); }
   const std::vector<int8_t>& coefficients() const { return coeffs_; }
@@ -71,10 +87,11 @@ class PhantomSecretKey {
                                      const uint64_t* enc_key = nullptr);
 
  private:
+  PhantomSecretKey() = default;
   void sample_uniform(const PhantomContext& ctx, uint64_t* dst, size_t L);
   void sample_error(const PhantomContext& ctx, uint64_t* dst, size_t L);  // NTT form
   uint64_t next();
-  uint64_t seed_state_;
+  uint64_t seed_state_ = 0;
   uint64_t draws_ = 0;  // counter of device sampling draws
   std::vector<int8_t> coeffs_;
   DeviceBuffer<uint64_t> s_, s2_;

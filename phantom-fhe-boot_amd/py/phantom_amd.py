@@ -39,6 +39,8 @@ _SIGS = {
     "phantom_keyswitch_inner_prod": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, vp, vp]),
     "phantom_moddown_from_ntt": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_moddown_modup": (ctypes.c_int, [vp, sz, vp, vp, vp]),
+    "phantom_ciphertext_serialize": (ctypes.c_int, [vp, vp, vp, sz, vp]),
+    "phantom_ciphertext_deserialize": (ctypes.c_int, [vp, sz, vp, vp, sz, vp]),
     "phantom_moddown_rescale": (ctypes.c_int, [vp, sz, vp, vp, sz, vp]),
     "phantom_rescale_to_next": (ctypes.c_int, [vp, sz, vp, vp, sz, vp]),
     "phantom_apply_galois_ntt": (ctypes.c_int, [vp, ctypes.c_uint32, vp, vp, sz, vp]),

@@ -35,6 +35,12 @@ def b2b(fn, iters=150):
     for i in range(iters): PA.check(fn(ring[i % 15].data_ptr(), t.handle, L, 0, s.cuda_stream))
     b.record(s); torch.cuda.synchronize()
     return a.elapsed_time(b) * 1e3 / iters
+chk = torch.from_numpy(base.view(np.int64)).cuda()
+PA.check(lib.phantom_nwt_forward_inplace(chk.data_ptr(), t.handle, L, 0, s.cuda_stream))
+torch.cuda.synchronize()
+h = chk.cpu().numpy().view(np.uint64)
+csum = int(np.bitwise_xor.reduce(h * np.arange(1, len(h) + 1, dtype=np.uint64)))
+print("CHECK", csum)
 print("RESULT", fwd, inv, b2b(lib.phantom_nwt_forward_inplace), b2b(lib.phantom_nwt_backward_inplace))
 '''
 res = {}
@@ -45,6 +51,8 @@ for name in sorted(os.listdir(os.path.join(ROOT, "tools", "variants"))):
     if line:
         f, i, fb, ib = map(float, line[0].split()[1:])
         res[name] = {"fwd_us": round(f, 2), "inv_us": round(i, 2), "fwd_b2b_us": round(fb, 2), "inv_b2b_us": round(ib, 2)}
+        chk = [l for l in out.stdout.splitlines() if l.startswith("CHECK")]
+        res[name]["check"] = chk[0].split()[1][-8:] if chk else None
     else:
         res[name] = {"error": out.stderr[-500:]}
     print(name, res[name], flush=True)
