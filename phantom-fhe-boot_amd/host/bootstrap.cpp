@@ -525,15 +525,19 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
   const size_t QlP = Ql + cc.size_P();
   hipStream_t s = cc.stream();
   DeviceBuffer<uint64_t> digits = EvalFastRotationPrecompute(cc, ct);
+  // baby steps from the shared digits, alternating between two streams (ct and the digits,
+  // main-stream buffers, live until both have joined)
   std::vector<PhantomCiphertext> baby(lv.g);
-  for (int j = 0; j < lv.g; ++j) {
-    const long r = static_cast<long>(j - lv.center) * lv.stride;
-    const long nn = static_cast<long>(n / 2);
-    if (((r % nn) + nn) % nn == 0)
-      baby[j] = KeySwitchExt(cc, ct);
-    else
-      baby[j] = EvalFastRotationExt(cc, ct, galois_keys_, static_cast<int>(r), digits.get(), true);
-  }
+  run_parallel(cc, std::min(2, lv.g), [&](int t) {
+    for (int j = t; j < lv.g; j += 2) {
+      const long r = static_cast<long>(j - lv.center) * lv.stride;
+      const long nn = static_cast<long>(n / 2);
+      if (((r % nn) + nn) % nn == 0)
+        baby[j] = KeySwitchExt(cc, ct);
+      else
+        baby[j] = EvalFastRotationExt(cc, ct, galois_keys_, static_cast<int>(r), digits.get(), true);
+    }
+  });
   digits.release();
   // every giant step's inner sum in one launch
   std::vector<PhantomCiphertext> inner(lv.b);
