@@ -141,6 +141,7 @@ struct ChebEvaluator {
   LeafTableCache& tables;
   std::map<int, PhantomCiphertext> T;
   std::map<std::pair<int, size_t>, PhantomCiphertext> aligned_;  // T_i brought to a deeper level
+  std::mutex mu;  // the maps, when the power ladder runs a generation on two streams
 
   // T_i at level `lvl` (>= its own), cached: the power ladder re-uses T_1, T_2, .. at the level
   // of every larger factor
@@ -148,16 +149,35 @@ struct ChebEvaluator {
     const PhantomCiphertext& t = get(i);
     if (level_of(t) == lvl) return t;
     auto key = std::make_pair(i, lvl);
-    auto it = aligned_.find(key);
-    if (it != aligned_.end()) return it->second;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto it = aligned_.find(key);
+      if (it != aligned_.end()) return it->second;
+    }
     PhantomCiphertext tmp;
     const PhantomCiphertext& r = AtLevel(cc, t, lvl, sf, tmp);
-    return aligned_.emplace(key, &r == &t ? PhantomCiphertext(t) : std::move(tmp)).first->second;
+    PhantomCiphertext v = &r == &t ? PhantomCiphertext(t) : std::move(tmp);
+    std::lock_guard<std::mutex> lk(mu);
+    return aligned_.emplace(key, std::move(v)).first->second;
+  }
+
+  // the operands T_a, T_(i-a) of T_i at their common level (computed ahead of a parallel
+  // generation, so that no stream uses an aligned copy another stream is still writing)
+  void prepare(int i) {
+    int a = 1;
+    while (2 * a < i) a *= 2;
+    if (2 * a == i) return;
+    const size_t lvl = std::max(level_of(get(a)), level_of(get(i - a)));
+    aligned(a, lvl);
+    aligned(i - a, lvl);
   }
 
   const PhantomCiphertext& get(int i) {
-    auto it = T.find(i);
-    if (it != T.end()) return it->second;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto it = T.find(i);
+      if (it != T.end()) return it->second;
+    }
     PhantomCiphertext r;
     int a = 1;
     while (2 * a < i) a *= 2;  // a >= i / 2, a < i
@@ -178,6 +198,7 @@ struct ChebEvaluator {
         EvalSubAutoInplace(cc, r, z, sf);
       }
     }
+    std::lock_guard<std::mutex> lk(mu);
     return T.emplace(i, std::move(r)).first->second;
   }
 
@@ -307,52 +328,81 @@ struct ChebEvaluator {
 }  // namespace
 
 // ======================================================================================
-// concurrent chains: task(0) on the context's stream (this thread), task(i) on the context's
-// aux stream i - 1 from worker thread i (StreamScope).  Every aux stream starts after everything
-// already enqueued on the main stream; the main stream continues after all of them.  Buffers
-// allocated on one stream and used on another must stay alive until this returns.  Called from
-// a thread that already runs under a StreamScope (a nested use), the tasks run in order there.
+// concurrent chains: task(0) on this thread's stream, task(i) from worker thread i on stream i
+// of a pool (StreamScope): at top level the pool is the context's aux streams; inside a task
+// it is the task's spare stream, so two levels of nesting can each run two chains.  Every
+// pool stream starts after everything already enqueued on this thread's stream, which
+// continues after all of them.  Buffers allocated on one stream and used on another must stay
+// alive until this returns.
 // ======================================================================================
+// true on every thread while it runs a task of run_parallel (the main thread included)
+static bool& in_parallel_section() {
+  static thread_local bool b = false;
+  return b;
+}
+
 template <typename Task>
 static void run_parallel(const PhantomContext& cc, int k, Task&& task) {
-  k = std::min(k, 1 + PhantomContext::kAuxStreams);
-  if (k <= 1 || StreamScope::current()) {
-    for (int i = 0; i < k; ++i) task(i);
+  std::vector<hipStream_t> pool;
+  if (!in_parallel_section() && !StreamScope::current()) {
+    for (int i = 0; i < PhantomContext::kAuxStreams; ++i) pool.push_back(cc.aux_stream(i));
+  } else if (StreamScope::spare()) {
+    pool.push_back(StreamScope::spare());
+  }
+  k = std::min<int>(k, 1 + static_cast<int>(pool.size()));
+  if (k <= 1) {
+    for (int i = 0; i < std::max(k, 1); ++i) task(i);
     return;
   }
+  // pool[0 .. k-2] run the workers; the rest become the tasks' spare streams
+  auto spare_of = [&](int t) -> hipStream_t {
+    const size_t i = static_cast<size_t>(k - 1 + t);
+    return i < pool.size() ? pool[i] : nullptr;
+  };
   const hipStream_t s0 = cc.stream();
   hipEvent_t fork;
   std::vector<hipEvent_t> join(k - 1);
   PHX_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
   for (auto& e : join) PHX_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   PHX_CHECK(hipEventRecord(fork, s0));
-  for (int i = 1; i < k; ++i) PHX_CHECK(hipStreamWaitEvent(cc.aux_stream(i - 1), fork, 0));
+  for (int i = 1; i < k; ++i) PHX_CHECK(hipStreamWaitEvent(pool[i - 1], fork, 0));
   std::vector<std::exception_ptr> err(k);
   std::vector<std::thread> workers;
   for (int i = 1; i < k; ++i)
     workers.emplace_back([&, i] {
+      in_parallel_section() = true;
       try {
-        StreamScope scope(cc.aux_stream(i - 1));
+        StreamScope scope(pool[i - 1]);
+        StreamScope::spare() = spare_of(i);
         task(i);
+        StreamScope::spare() = nullptr;
       } catch (...) {
+        StreamScope::spare() = nullptr;
         err[i] = std::current_exception();
       }
+      in_parallel_section() = false;
     });
+  const hipStream_t own_spare = StreamScope::spare();
+  const bool own_flag = in_parallel_section();
+  in_parallel_section() = true;
   try {
+    StreamScope::spare() = spare_of(0);
     task(0);
   } catch (...) {
     err[0] = std::current_exception();
   }
+  StreamScope::spare() = own_spare;
+  in_parallel_section() = own_flag;
   for (auto& w : workers) w.join();
   hipError_t e = hipSuccess;
   for (int i = 1; i < k; ++i) {
-    if (e == hipSuccess) e = hipEventRecord(join[i - 1], cc.aux_stream(i - 1));
+    if (e == hipSuccess) e = hipEventRecord(join[i - 1], pool[i - 1]);
     if (e == hipSuccess) e = hipStreamWaitEvent(s0, join[i - 1], 0);
   }
   bool failed = e != hipSuccess;
   for (auto& x : err) failed |= static_cast<bool>(x);
   if (failed) {
-    for (int i = 1; i < k; ++i) (void)hipStreamSynchronize(cc.aux_stream(i - 1));
+    for (int i = 1; i < k; ++i) (void)hipStreamSynchronize(pool[i - 1]);
     (void)hipStreamSynchronize(s0);
   }
   (void)hipEventDestroy(fork);
@@ -597,10 +647,22 @@ PhantomCiphertext FHECKKSRNS::EvalSlotsToCoeffs(const PhantomCiphertext& ct, con
 
 PhantomCiphertext FHECKKSRNS::EvalChebyshevSeries(const PhantomCiphertext& ct, const PhantomContext& cc,
                                                   const std::vector<double>& coeffs) const {
-  ChebEvaluator ev{cc, mul_key_, sf_, leaf_tables_, {}, {}};
+  ChebEvaluator ev{cc, mul_key_, sf_, leaf_tables_, {}, {}, {}};
   PhantomCiphertext x = ct;
   if (x.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, x, 1);
   ev.T.emplace(1, std::move(x));
+  // the power ladder T_2 .. T_15 generation by generation (T_(2^(g-1)+1) .. T_(2^g) depend only
+  // on earlier generations), each generation's members alternating between two streams
+  const int top = std::min<int>(kLeafDegree, static_cast<int>(coeffs.size()) - 1);
+  for (int lo = 2, hi = 2; lo <= top; lo = hi + 1, hi = std::min(2 * hi, top)) {
+    std::vector<int> members;
+    for (int i = lo; i <= hi; ++i) members.push_back(i);
+    for (int i : members) ev.prepare(i);
+    const int k = std::min<int>(2, static_cast<int>(members.size()));
+    run_parallel(cc, k, [&](int t) {
+      for (size_t m = t; m < members.size(); m += k) ev.get(members[m]);
+    });
+  }
   return ev.eval(coeffs);
 }
 

@@ -85,6 +85,11 @@ class StreamScope {
     static thread_local hipStream_t s = nullptr;
     return s;
   }
+  // a further stream this thread may hand to a nested concurrent section (run_parallel)
+  static hipStream_t& spare() {
+    static thread_local hipStream_t s = nullptr;
+    return s;
+  }
 
  private:
   hipStream_t prev_;
