@@ -60,6 +60,7 @@ struct LeafArgs {
   const uint64_t* coef;
   const uint64_t* cadd;
   const uint64_t* q;
+  const uint64_t* barrett;  // [L][2]
   int K = 0, M = 0, L = 0;
 };
 hipError_t leaf_combine(const LeafArgs& a, size_t n, hipStream_t s);
@@ -77,6 +78,23 @@ struct LimbScalars {
 hipError_t mul_scalar_v(const uint64_t* in, const LimbScalars& c, uint64_t* out, const uint64_t* q, size_t n,
                         size_t L, hipStream_t s, size_t polys = 1, size_t in_stride = 0,
                         const uint64_t* acc = nullptr);
+// Tensor product of two [2][L][n] ciphertexts into out [3][L][n] with MulAddRescale's linear
+// epilogue fused: d = f (ct1 x ct2) (if scale) and, for t, d[p] += t[p] c for p < 2
+// (t[p] at t + p * t_stride, its first L limbs).  out must not alias the inputs.
+struct TensorLinArgs {
+  const uint64_t* ct1;
+  const uint64_t* ct2;
+  uint64_t* out;
+  const uint64_t* t = nullptr;
+  size_t t_stride = 0;
+  const uint64_t* q;
+  const uint64_t* barrett;
+  bool scale = false;
+  LimbScalars f;
+  LimbScalars c;
+};
+hipError_t tensor_lin(const TensorLinArgs& a, size_t n, size_t L, hipStream_t s);
+
 // d[p] = d[p] * ca (ca may be null: unscaled) + (p < t_polys ? t[p] * cb : 0) for p < d_polys;
 // d contiguous [d_polys][L][n], t[p] at t + p * t_stride (its first L limbs)
 hipError_t lin_comb_v(uint64_t* d, size_t d_polys, const LimbScalars* ca, const uint64_t* t, size_t t_polys,

@@ -159,28 +159,80 @@ __global__ __launch_bounds__(kBlock) void lin_comb_kernel(uint64_t* d, LimbScala
   }
 }
 
-// one element (t, l, k) per thread and step; inputs read once, M accumulators
+// blockIdx.y = limb l, blockIdx.x strides over the 2 n elements (t, k) of that limb.  The
+// limb's coefficients sit in LDS split into 30-bit halves; every output is sum_k x_k c_mk as
+// four 64-bit partial sums of 30-bit products (<= 16 terms: no overflow), one Barrett per output.
 template <int K>
-__global__ __launch_bounds__(kBlock) void leaf_combine_kernel(LeafArgs a, uint32_t log_n, size_t total) {
-  const size_t ln = static_cast<size_t>(a.L) << log_n;  // elements per output polynomial
-  const size_t mkl = static_cast<size_t>(a.M) * K * a.L;
-  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
-    const uint32_t t = e >= ln ? 1 : 0;
-    const size_t el = e - t * ln;                          // offset inside the polynomial
-    const uint32_t l = static_cast<uint32_t>(el >> log_n);
-    const uint64_t ql = a.q[l];
-    uint64_t x[K];
+__global__ __launch_bounds__(kBlock) void leaf_combine_kernel(LeafArgs a, uint32_t log_n) {
+  constexpr uint64_t kM30 = (1ull << 30) - 1;
+  __shared__ uint32_t clo[kLeafMaxM][K], chi[kLeafMaxM][K];
+  __shared__ uint64_t cadd[kLeafMaxM];
+  const int l = blockIdx.y;
+  const size_t n = size_t(1) << log_n;
+  for (int e = threadIdx.x; e < a.M * K; e += kBlock) {
+    const int m = e / K, k = e % K;
+    const uint64_t c = a.coef[(static_cast<size_t>(m) * K + k) * a.L + l];
+    clo[m][k] = static_cast<uint32_t>(c & kM30);
+    chi[m][k] = static_cast<uint32_t>(c >> 30);
+  }
+  if (threadIdx.x < a.M) cadd[threadIdx.x] = a.cadd[static_cast<size_t>(threadIdx.x) * a.L + l];
+  __syncthreads();
+  const uint64_t q = a.q[l], r0 = a.barrett[2 * l], r1 = a.barrett[2 * l + 1];
+  const size_t ln = static_cast<size_t>(a.L) << log_n;
+  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < 2 * n; e += (size_t)gridDim.x * kBlock) {
+    const uint32_t t = e >= n ? 1 : 0;
+    const size_t el = (static_cast<size_t>(l) << log_n) + (e - t * n);  // offset inside the polynomial
+    uint32_t xl[K], xh[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) x[k] = a.in[k][t * a.in_stride[k] + el];
-    for (int m = 0; m < a.M; ++m) {
-      const uint64_t* cv = a.coef + static_cast<size_t>(m) * K * a.L + l;
-      uint64_t acc = t == 0 ? a.cadd[static_cast<size_t>(m) * a.L + l] : 0;
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-        acc = add_mod(acc, mul_shoup(x[k], cv[static_cast<size_t>(k) * a.L], cv[mkl + static_cast<size_t>(k) * a.L], ql),
-                      ql);
-      a.out[m][e] = acc;
+    for (int k = 0; k < K; ++k) {
+      const uint64_t v = a.in[k][t * a.in_stride[k] + el];
+      xl[k] = static_cast<uint32_t>(v & kM30);
+      xh[k] = static_cast<uint32_t>(v >> 30);
     }
+    for (int m = 0; m < a.M; ++m) {
+      uint64_t ll = 0, m1 = 0, m2 = 0, hh = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint32_t cl = clo[m][k], ch = chi[m][k];
+        ll += static_cast<uint64_t>(xl[k]) * cl;
+        m1 += static_cast<uint64_t>(xl[k]) * ch;
+        m2 += static_cast<uint64_t>(xh[k]) * cl;
+        hh += static_cast<uint64_t>(xh[k]) * ch;
+      }
+      u128 acc{ll, 0};
+      add128(acc, u128{m1 << 30, m1 >> 34});
+      add128(acc, u128{m2 << 30, m2 >> 34});
+      add128(acc, u128{hh << 60, hh >> 4});
+      uint64_t v = barrett_reduce_128(acc, q, r0, r1);
+      if (t == 0) v = add_mod(v, cadd[m], q);
+      a.out[m][t * ln + el] = v;
+    }
+  }
+}
+
+// tensor product with the fused linear epilogue of MulAddRescale (see ckks.h)
+template <bool SCALE, bool TERM>
+__global__ __launch_bounds__(kBlock) void tensor_lin_kernel(TensorLinArgs a, uint32_t log_n, size_t total) {
+  const size_t stride = total;  // elements per polynomial
+  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const uint64_t q = a.q[l], r0 = a.barrett[2 * l], r1 = a.barrett[2 * l + 1];
+    const uint64_t a0 = a.ct1[e], a1 = a.ct1[stride + e], b0 = a.ct2[e], b1 = a.ct2[stride + e];
+    u128 c1 = mul_wide(a0, b1);
+    add128(c1, mul_wide(a1, b0));
+    uint64_t d0 = mul_mod(a0, b0, q, r0, r1), d1 = barrett_reduce_128(c1, q, r0, r1), d2 = mul_mod(a1, b1, q, r0, r1);
+    if constexpr (SCALE) {
+      d0 = mul_shoup(d0, a.f.v[l], a.f.vs[l], q);
+      d1 = mul_shoup(d1, a.f.v[l], a.f.vs[l], q);
+      d2 = mul_shoup(d2, a.f.v[l], a.f.vs[l], q);
+    }
+    if constexpr (TERM) {
+      d0 = add_mod(d0, mul_shoup(a.t[e], a.c.v[l], a.c.vs[l], q), q);
+      d1 = add_mod(d1, mul_shoup(a.t[a.t_stride + e], a.c.v[l], a.c.vs[l], q), q);
+    }
+    a.out[e] = d0;
+    a.out[stride + e] = d1;
+    a.out[2 * stride + e] = d2;
   }
 }
 
@@ -232,15 +284,28 @@ hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t leaf_combine(const LeafArgs& a, size_t n, hipStream_t s) {
-  if (a.K < 1 || a.K > kLeafMaxK || a.M < 1 || a.M > kLeafMaxM || a.L < 1 || !a.coef || !a.cadd)
-    return hipErrorInvalidValue;
-  const size_t total = 2 * n * static_cast<size_t>(a.L);
+hipError_t tensor_lin(const TensorLinArgs& a, size_t n, size_t L, hipStream_t s) {
+  if (L > static_cast<size_t>(kMaxScalarLimbs)) return hipErrorInvalidValue;
+  const size_t total = n * L;
   const uint32_t log_n = __builtin_ctzll(n);
   const int grid = grid_for(total);
+  if (a.scale && a.t) tensor_lin_kernel<true, true><<<grid, kBlock, 0, s>>>(a, log_n, total);
+  else if (a.scale) tensor_lin_kernel<true, false><<<grid, kBlock, 0, s>>>(a, log_n, total);
+  else if (a.t) tensor_lin_kernel<false, true><<<grid, kBlock, 0, s>>>(a, log_n, total);
+  else tensor_lin_kernel<false, false><<<grid, kBlock, 0, s>>>(a, log_n, total);
+  return hipGetLastError();
+}
+
+hipError_t leaf_combine(const LeafArgs& a, size_t n, hipStream_t s) {
+  if (a.K < 1 || a.K > kLeafMaxK || a.M < 1 || a.M > kLeafMaxM || a.L < 1 || !a.coef || !a.cadd || !a.barrett)
+    return hipErrorInvalidValue;
+  const uint32_t log_n = __builtin_ctzll(n);
+  // x: enough workgroups per limb to fill the chip, y: limb
+  const unsigned gx = static_cast<unsigned>(std::max<int>(1, std::min<int>(2 * n / kBlock, grid_for(2 * n * a.L) / a.L)));
+  const dim3 grid(gx, static_cast<unsigned>(a.L));
   switch (a.K) {
 #define PHX_LEAF_CASE(K) \
-  case K: leaf_combine_kernel<K><<<grid, kBlock, 0, s>>>(a, log_n, total); break;
+  case K: leaf_combine_kernel<K><<<grid, kBlock, 0, s>>>(a, log_n); break;
     PHX_LEAF_CASE(1) PHX_LEAF_CASE(2) PHX_LEAF_CASE(3) PHX_LEAF_CASE(4) PHX_LEAF_CASE(5) PHX_LEAF_CASE(6)
     PHX_LEAF_CASE(7) PHX_LEAF_CASE(8) PHX_LEAF_CASE(9) PHX_LEAF_CASE(10) PHX_LEAF_CASE(11) PHX_LEAF_CASE(12)
     PHX_LEAF_CASE(13) PHX_LEAF_CASE(14) PHX_LEAF_CASE(15) PHX_LEAF_CASE(16)

@@ -281,6 +281,7 @@ struct ChebEvaluator {
         la.M = M;
         la.L = static_cast<int>(L);
         la.q = cc.mod_QP().q;
+        la.barrett = cc.mod_QP().barrett;
         la.coef = tables.get(tab, cc.stream());
         la.cadd = la.coef + 2 * static_cast<size_t>(M) * K * L;
         for (int k = 0; k < K; ++k) {

@@ -313,25 +313,41 @@ PhantomCiphertext MulAddRescale(const PhantomContext& ctx, const PhantomCipherte
                                 double constant) {
   if (a.chain_index() != b.chain_index() || a.GetNoiseScaleDeg() > 1 || b.GetNoiseScaleDeg() > 1)
     throw std::invalid_argument("MulAddRescale: operands must be level-aligned and of degree 1");
-  const size_t n = ctx.poly_degree();
-  PhantomCiphertext d = multiply(ctx, a, b);
-  const size_t L = d.coeff_modulus_size(), chain = d.chain_index();
-  const double S = d.scale();
-  const uint64_t* q = ctx.mod_QP().q;
+  const size_t n = ctx.poly_degree(), chain = a.chain_index();
+  const size_t L = a.coeff_modulus_size();
   hipStream_t s = ctx.stream();
-  const phx::LimbScalars ca = limb_scalars(ctx, chain, static_cast<double>(factor));
-  bool scaled = factor == 1;
-  for (const ScaledTerm& t : terms) {
+  const uint64_t* q = ctx.mod_QP().q;
+  for (const ScaledTerm& t : terms)
     if (t.ct->chain_index() > chain || t.ct->GetNoiseScaleDeg() > 1 || t.ct->size() != 2)
       throw std::invalid_argument("MulAddRescale: a term is below the product's level");
+  // tensor product with the factor and the first term fused into one pass
+  PhantomCiphertext d;
+  d.resize(ctx, chain, 3, s, false);
+  d.set_ntt_form(true);
+  d.set_correction_factor(a.correction_factor());
+  d.set_scale(a.scale() * b.scale());
+  const double S = d.scale();
+  phx::TensorLinArgs ta;
+  ta.ct1 = a.data();
+  ta.ct2 = b.data();
+  ta.out = d.data();
+  ta.q = q;
+  ta.barrett = ctx.mod_QP().barrett;
+  ta.scale = factor != 1;
+  if (ta.scale) ta.f = limb_scalars(ctx, chain, static_cast<double>(factor));
+  if (!terms.empty()) {
     // round(c S / scale_t) t carries c m_t at the product's scale S
-    const phx::LimbScalars cb = limb_scalars(ctx, chain, t.coeff * S / t.ct->scale());
-    hip_ok(phx::lin_comb_v(d.data(), scaled ? 2 : 3, scaled ? nullptr : &ca, t.ct->data(), 2,
-                           t.ct->coeff_modulus_size() * n, cb, q, n, L, s),
-           "mul-add term");
-    scaled = true;
+    ta.t = terms[0].ct->data();
+    ta.t_stride = terms[0].ct->coeff_modulus_size() * n;
+    ta.c = limb_scalars(ctx, chain, terms[0].coeff * S / terms[0].ct->scale());
   }
-  if (!scaled) hip_ok(phx::lin_comb_v(d.data(), 3, &ca, nullptr, 0, 0, ca, q, n, L, s), "mul-add factor");
+  hip_ok(phx::tensor_lin(ta, n, L, s), "tensor + linear epilogue");
+  for (size_t i = 1; i < terms.size(); ++i) {
+    const ScaledTerm& t = terms[i];
+    const phx::LimbScalars cb = limb_scalars(ctx, chain, t.coeff * S / t.ct->scale());
+    hip_ok(phx::lin_comb_v(d.data(), 2, nullptr, t.ct->data(), 2, t.ct->coeff_modulus_size() * n, cb, q, n, L, s),
+           "mul-add term");
+  }
   if (constant != 0.0) EvalAddConstInplace(ctx, d, constant);
   d.SetNoiseScaleDeg(2);
   return RelinearizeRescale(ctx, d, rlk);
