@@ -158,18 +158,19 @@ def job_throughput(units_per_rank, world, max_seconds):
     return units_per_rank * world / max_seconds
 
 
-def c5_leg(dist, torch, world, rank, local_rank, batch=8, timeout=600):
+def c5_leg(dist, torch, world, rank, local_rank, batch=16, lanes=4, timeout=600):
     """Config C5: a batch of independent bootstraps sharded over the ranks, one
     process per GPU, replicas only (no collective on the data path: every rank holds its own
     context and keys and bootstraps its own ciphertexts).  Each rank runs `batch` bootstraps in
-    the example binary on its GPU; throughput = all bootstraps / max-over-ranks wall time of the
-    timed loops."""
+    the example binary on its GPU, `lanes` side by side (FHECKKSRNS::EvalBootstrapBatch);
+    throughput = all bootstraps / max-over-ranks wall time of the timed batches."""
     import subprocess
     exe = os.path.join(ROOT, "phantom-fhe-boot_amd", "bin", "bootstrapping_example")
     env = dict(os.environ, HIP_VISIBLE_DEVICES=str(local_rank))
-    out = subprocess.run([exe, "boot", "16", str(batch)], capture_output=True, text=True, timeout=timeout, env=env)
+    out = subprocess.run([exe, "batch", "16", str(batch), str(lanes)], capture_output=True, text=True,
+                         timeout=timeout, env=env)
     rows = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{") and '"sample"' not in l]
-    boot = [r for r in rows if r.get("stage") == "bootstrap"]
+    boot = [r for r in rows if r.get("stage") == "batch"]
     ok = out.returncode == 0 and bool(boot)
     total_ms = boot[0]["ms_total"] if ok else float("inf")
     max_ms = max_over_ranks(dist, [total_ms], "cuda")[0]
@@ -177,7 +178,8 @@ def c5_leg(dist, torch, world, rank, local_rank, batch=8, timeout=600):
         return {"error": (out.stderr or out.stdout)[-300:]}
     return {
         "workload": "C5: independent bootstraps (C4 parameters) sharded over ranks, replicas only",
-        "bootstraps_per_rank": batch, "ranks": world,
+        "bootstraps_per_rank": batch, "lanes_per_rank": lanes, "ranks": world,
+        "min_avg_bits": boot[0]["min_avg_bits"],
         "bootstraps_per_s": round(job_throughput(batch, world, max_ms / 1e3), 3),
         "max_rank_ms": round(max_ms, 2), "scaling": "weak",
     }
@@ -206,7 +208,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 (mult+relin+rescale) leg")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (bootstrap latency) leg")
-    ap.add_argument("--no-c5", action="store_true", help="skip the C5 (sharded bootstrap batch) leg at N > 1")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 (sharded bootstrap batch) leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -274,8 +276,8 @@ def main():
                                                       [elapsed, fwd_ms, fwd_ms_isolated], "cuda")
 
     c5 = None
-    if world > 1 and not args.no_c5:
-        c5 = c5_leg(dist, torch, world, rank, local_rank)
+    if not args.no_c5:
+        c5 = c5_leg(dist if world > 1 else None, torch, world, rank, local_rank)
 
     # parity spot-check of the last buffer state is done by tests/; here just sanity
     value = job_throughput(2 * BYTES_PER_TRANSFORM * args.steps, world, elapsed) / 1e9
@@ -320,9 +322,6 @@ def main():
             out["c3"] = c3_leg(PA, lib, torch)
         if not args.no_c4 and world == 1:
             out["c4"] = c4_leg()
-            if "ms_median" in out["c4"]:
-                out["c5"] = {"workload": "C5 at one GPU (from C4)", "ranks": 1,
-                             "bootstraps_per_s": round(1e3 / out["c4"]["ms_median"], 3), "scaling": "weak"}
         if c5 is not None:
             out["c5"] = c5
         if not args.no_cpu_baseline and world == 1:

@@ -345,7 +345,7 @@ static bool& in_parallel_section() {
 template <typename Task>
 static void run_parallel(const PhantomContext& cc, int k, Task&& task) {
   std::vector<hipStream_t> pool;
-  if (!in_parallel_section() && !StreamScope::current()) {
+  if (!in_parallel_section()) {
     for (int i = 0; i < PhantomContext::kAuxStreams; ++i) pool.push_back(cc.aux_stream(i));
   } else if (StreamScope::spare()) {
     pool.push_back(StreamScope::spare());
@@ -369,8 +369,10 @@ static void run_parallel(const PhantomContext& cc, int k, Task&& task) {
   for (int i = 1; i < k; ++i) PHX_CHECK(hipStreamWaitEvent(pool[i - 1], fork, 0));
   std::vector<std::exception_ptr> err(k);
   std::vector<std::thread> workers;
+  const int lane = LaneScope::current();
   for (int i = 1; i < k; ++i)
     workers.emplace_back([&, i] {
+      LaneScope::current() = lane;
       in_parallel_section() = true;
       try {
         StreamScope scope(pool[i - 1]);
@@ -589,6 +591,7 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
         baby[j] = EvalFastRotationExt(cc, ct, galois_keys_, static_cast<int>(r), digits.get(), true);
     }
   });
+  for (auto& b : baby) b.retag(s);  // read and freed on this stream from here on
   digits.release();
   // every giant step's inner sum in one launch
   std::vector<PhantomCiphertext> inner(lv.b);
@@ -626,8 +629,10 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
     }
   });
   PhantomCiphertext acc = std::move(part[0]);
-  for (int t = 1; t < k; ++t)
+  for (int t = 1; t < k; ++t) {
+    part[t].retag(s);
     if (part[t].size()) EvalAddExtInPlace(cc, acc, part[t]);
+  }
   inner.clear();
   acc.set_scale(ct.scale() * sf_.at(lv.chain - 1));
   acc.SetNoiseScaleDeg(2);
@@ -663,6 +668,7 @@ PhantomCiphertext FHECKKSRNS::EvalChebyshevSeries(const PhantomCiphertext& ct, c
     run_parallel(cc, k, [&](int t) {
       for (size_t m = t; m < members.size(); m += k) ev.get(members[m]);
     });
+    for (int i : members) const_cast<PhantomCiphertext&>(ev.get(i)).retag(cc.stream());
   }
   return ev.eval(coeffs);
 }
@@ -710,6 +716,52 @@ static void trace(const PhantomContext& cc, const char* stage, const PhantomCiph
                ct.chain_index(), ct.coeff_modulus_size(), ct.scale(), ct.GetNoiseScaleDeg(), hipGetErrorString(e));
 }
 
+std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<PhantomCiphertext>& in,
+                                                              const PhantomContext& cc, int lanes) const {
+  const int k = std::max(1, std::min({lanes, PhantomContext::kLanes, static_cast<int>(in.size())}));
+  std::vector<PhantomCiphertext> out(in.size());
+  if (k == 1 || in_parallel_section()) {
+    for (size_t i = 0; i < in.size(); ++i) out[i] = EvalBootstrap(in[i], cc);
+    return out;
+  }
+  const hipStream_t s0 = cc.stream();
+  hipEvent_t fork;
+  std::vector<hipEvent_t> join(k);
+  PHX_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+  for (auto& e : join) PHX_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  PHX_CHECK(hipEventRecord(fork, s0));
+  for (int t = 0; t < k; ++t) PHX_CHECK(hipStreamWaitEvent(cc.lane_stream(t == 0 ? 0 : t), fork, 0));
+  // lane t bootstraps ciphertexts t, t + k, ... from its own thread and streams; the inputs
+  // (main-stream buffers) stay alive until the main stream has joined every lane
+  std::vector<std::exception_ptr> err(k);
+  std::vector<std::thread> workers;
+  for (int t = 0; t < k; ++t)
+    workers.emplace_back([&, t] {
+      try {
+        LaneGuard lane(cc, t);
+        for (size_t i = t; i < in.size(); i += k) out[i] = EvalBootstrap(in[i], cc);
+      } catch (...) {
+        err[t] = std::current_exception();
+      }
+    });
+  for (auto& w : workers) w.join();
+  hipError_t e = hipSuccess;
+  for (int t = 0; t < k; ++t) {
+    if (e == hipSuccess) e = hipEventRecord(join[t], cc.lane_stream(t));
+    if (e == hipSuccess) e = hipStreamWaitEvent(s0, join[t], 0);
+  }
+  for (auto& c : out) c.retag(s0);
+  bool failed = e != hipSuccess;
+  for (auto& x : err) failed |= static_cast<bool>(x);
+  if (failed) (void)hipDeviceSynchronize();
+  (void)hipEventDestroy(fork);
+  for (auto& j : join) (void)hipEventDestroy(j);
+  for (auto& x : err)
+    if (x) std::rethrow_exception(x);
+  PHX_CHECK(e);
+  return out;
+}
+
 PhantomCiphertext FHECKKSRNS::EvalBootstrap(const PhantomCiphertext& in, const PhantomContext& cc) const {
   if (enc_.empty()) throw std::invalid_argument("Precomputations were not generated: call EvalBootstrapSetup");
   const uint32_t N = static_cast<uint32_t>(cc.poly_degree()), M = 2 * N;
@@ -738,6 +790,7 @@ PhantomCiphertext FHECKKSRNS::EvalBootstrap(const PhantomCiphertext& in, const P
       MultByMonomialInPlace(cc, im, M / 4);  // times i
     }
   });
+  im.retag(cc.stream());
   trace(cc, "evalmod", enc);
   EvalAddAutoInplace(cc, enc, im, sf_);
   // SlotToCoeff and undo the correction scaling

@@ -69,6 +69,10 @@ class FHECKKSRNS {
   void EvalMultKeyGen(PhantomSecretKey& sk, const PhantomContext& cc);
   // EvalBootstrap (bootstrap.cu:843-1129); the input needs at least two limbs
   PhantomCiphertext EvalBootstrap(const PhantomCiphertext& ct, const PhantomContext& cc) const;
+  // a batch of independent bootstraps, `lanes` at a time side by side (each on its own thread
+  // and stream lane, PhantomContext::kLanes at most); the results are ordered on cc.stream()
+  std::vector<PhantomCiphertext> EvalBootstrapBatch(const std::vector<PhantomCiphertext>& in,
+                                                    const PhantomContext& cc, int lanes) const;
 
   // stages, exposed for tests and the benchmark
   PhantomCiphertext EvalCoeffsToSlots(const PhantomCiphertext& ct, const PhantomContext& cc) const;

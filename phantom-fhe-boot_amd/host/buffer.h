@@ -131,6 +131,9 @@ class DeviceBuffer {
   T* get() const { return ptr_; }
   size_t size() const { return count_; }
   hipStream_t stream() const { return stream_; }
+  // make `s` the stream the buffer is freed on (its event and immediate reuse): for a buffer
+  // made on one stream whose later uses are all ordered on `s`
+  void set_stream(hipStream_t s) { stream_ = s; }
   explicit operator bool() const { return ptr_ != nullptr; }
 
  private:

@@ -69,6 +69,9 @@ class PhantomCiphertext {
   void save(std::ostream& os) const;
   void load(const PhantomContext& ctx, std::istream& is);
   bool is_asymmetric() const { return is_asymmetric_; }
+  // hand the buffer to stream `s` (DeviceBuffer::set_stream): after a concurrent section, for a
+  // result made on a side stream that the joining stream uses from now on
+  void retag(hipStream_t s) { data_.set_stream(s); }
   void set_asymmetric(bool b) { is_asymmetric_ = b; }
 
   // host transfer helpers (the reference's save/load staging, ciphertext.h:184-225)

@@ -14,9 +14,15 @@ PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t s
     PHX_CHECK(hipStreamCreateWithFlags(&stream_.s, hipStreamNonBlocking));
     stream_.owned = true;
   }
-  for (auto& a : aux_) {
-    PHX_CHECK(hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking));
-    a.owned = true;
+  for (int l = 1; l < kLanes; ++l) {
+    PHX_CHECK(hipStreamCreateWithFlags(&lane_main_[l].s, hipStreamNonBlocking));
+    lane_main_[l].owned = true;
+  }
+  for (auto& lane : aux_) {
+    for (auto& a : lane) {
+      PHX_CHECK(hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking));
+      a.owned = true;
+    }
   }
   hipStream_t s = stream_.s;
   if (params.scheme() != scheme_type::ckks) throw std::invalid_argument("only CKKS is supported by this engine");

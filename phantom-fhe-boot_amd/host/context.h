@@ -95,6 +95,15 @@ class StreamScope {
   hipStream_t prev_;
 };
 
+// lane of the calling thread (PhantomContext::lane_stream / aux_stream); see LaneScope below
+class LaneScope {
+ public:
+  static int& current() {
+    static thread_local int lane = 0;
+    return lane;
+  }
+};
+
 class PhantomContext {
  public:
   // stream: where setup work and the façade's operations run; nullptr = a stream owned by the
@@ -124,20 +133,41 @@ class PhantomContext {
     const hipStream_t o = StreamScope::current();
     return o ? o : stream_.s;
   }
-  // further streams owned by the context, for work that runs beside stream()
+  // further streams owned by the context, for work that runs beside stream().  Streams come
+  // in lanes: lane 0 is stream() + its aux streams; a thread inside a LaneScope(k) issues to
+  // lane k's main stream and aux streams, so independent evaluations (a batch of bootstraps)
+  // run side by side without sharing a stream.
   static constexpr int kAuxStreams = 3;
-  hipStream_t aux_stream(int i = 0) const { return aux_[i].s; }
+  static constexpr int kLanes = 4;
+  hipStream_t aux_stream(int i = 0) const { return aux_[LaneScope::current()][i].s; }
+  hipStream_t lane_stream(int lane) const { return lane == 0 ? stream_.s : lane_main_[lane].s; }
   Workspace& workspace() const { return *ws_; }
 
  private:
   OwnedStream stream_;  // first members: destroyed after everything that frees on them
-  OwnedStream aux_[kAuxStreams];
+  OwnedStream aux_[kLanes][kAuxStreams];
+  OwnedStream lane_main_[kLanes];  // [0] unused: lane 0 runs on stream_
   EncryptionParameters params_;
   size_t n_ = 0, size_Q_ = 0, size_P_ = 0;
   std::vector<uint64_t> qp_;
   std::unique_ptr<Workspace> ws_;  // declared before the tools that point into it
   std::unique_ptr<DeviceNttTables> ntt_;
   std::vector<std::unique_ptr<ContextData>> data_;
+};
+
+// runs the calling thread on lane `lane` of `cc`: its main stream (StreamScope) and aux streams
+class LaneGuard {
+ public:
+  LaneGuard(const PhantomContext& cc, int lane) : prev_(LaneScope::current()), scope_(cc.lane_stream(lane)) {
+    LaneScope::current() = lane;
+  }
+  ~LaneGuard() { LaneScope::current() = prev_; }
+  LaneGuard(const LaneGuard&) = delete;
+  LaneGuard& operator=(const LaneGuard&) = delete;
+
+ private:
+  int prev_;
+  StreamScope scope_;
 };
 
 }  // namespace phantom
