@@ -30,7 +30,7 @@ def test_ckks_ops_hoisted_rotation_conjugation_rescale():
     checks = {l["check"]: l for l in lines if "check" in l}
     assert rc == 0, (lines, err)
     for name in ["encrypt_decrypt", "rotate_1", "rotate_-3", "conjugate", "square_rescale", "add_auto_levels",
-                 "monomial_i", "drain_const_mult"]:
+                 "monomial_i", "drain_const_mult", "save_load"]:
         assert checks[name]["ok"], checks[name]
 
 
@@ -41,3 +41,13 @@ def test_full_bootstrap_precision_and_levels():
     # the reference example reaches ~ the same regime: correction factor 7, inputs in [1, 5]
     assert boot["avg_bits"] > 9.0, boot
     assert boot["levels_after"] >= 11, boot
+
+
+def test_bootstrap_batch_on_stream_lanes():
+    """EvalBootstrapBatch: 6 bootstraps, 3 stream lanes side by side (C5's per-GPU path); every
+    output keeps the single-bootstrap precision."""
+    rc, lines, err = _run("batch", "16", "6", "3", timeout=115)
+    assert rc == 0, (lines, err)
+    b = [l for l in lines if l.get("stage") == "batch"][0]
+    assert b["bootstraps"] == 6 and b["lanes"] == 3, b
+    assert b["min_avg_bits"] > 9.0, b
