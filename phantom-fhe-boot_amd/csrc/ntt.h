@@ -76,6 +76,26 @@ struct LimbMap {
 hipError_t ntt_forward(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                        hipStream_t stream);
 
+// Forward NTT with a fused prologue and epilogue (the rescale and moddown tails):
+//  - prologue (bcast != null): buffer limb i of polynomial p is read as bcast[p][k] mod q_row,
+//    one coefficient-form limb broadcast over the limbs (`in` is not read): divide_and_round's
+//    spread of the last limb (src/rns.cu:1128-1139);
+//  - epilogue (epi.out != null): the transform's value y is not stored; instead
+//    epi.out[p][i][k] = (epi.c[p][i][k] - y) * w[i] (+ epi.out[p][i][k] when accumulate), mod q:
+//    the rescale / moddown finish (src/rns.cu:1141-1158, src/ntt/ntt_moddown.cu:199-214).
+// Polynomial p of c / out starts at p * c_stride / p * out_stride (elements).
+struct NttEpilogue {
+  const uint64_t* c = nullptr;
+  size_t c_stride = 0;
+  uint64_t* out = nullptr;
+  size_t out_stride = 0;
+  const uint64_t* w = nullptr;   // per buffer limb
+  const uint64_t* ws = nullptr;  // Shoup quotients
+  bool accumulate = false;
+};
+hipError_t ntt_forward_fused(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
+                             const uint64_t* bcast, size_t bcast_stride, const NttEpilogue& epi, hipStream_t stream);
+
 // Inverse NTT.  When scale/scale_shoup are given (one value per buffer limb, indexed by
 // buffer limb), the output is additionally multiplied by scale[i] (the reference's
 // nwt_2d_radix8_backward_scale used by modup, src/ntt/ntt_modup.cu:356-393).

@@ -295,6 +295,10 @@ struct KArgs {
   int n;
   int limbs;                  // number of processed limbs over all polynomials (excluding skipped)
   int limbs_per_poly;
+  const uint64_t* barrett;    // [row][2] (prologue reduction)
+  const uint64_t* bcast;      // forward prologue (see ntt.h), column pass only
+  size_t bcast_stride;
+  NttEpilogue epi;            // forward epilogue (see ntt.h), row pass only
 };
 
 // y: processed-limb index over the batch -> polynomial, buffer limb within it, table row
@@ -357,10 +361,22 @@ constexpr int kWavesPerEU = PHX_NTT_PERSIST > 0 ? PHX_NTT_PERSIST : PHX_NTT_WAVE
 constexpr bool kPrefetch = PHX_NTT_PERSIST > 0;
 
 struct TileRef {
-  int buf_limb, row;
+  int buf_limb, row, poly;
   size_t off;     // element offset of this lane's first element in the output
   size_t in_off;  // ... and in the input
+  size_t k;       // ... and inside its limb
 };
+
+// forward epilogue: out = (c - y) * w (+ out), for the element `dk` past this lane's first
+__device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr, uint32_t dk, uint64_t y, uint64_t q) {
+  const size_t e = (size_t)tr.buf_limb * a.n + tr.k + dk;
+  const uint64_t c = a.epi.c[tr.poly * a.epi.c_stride + e];
+  uint64_t* o = a.epi.out + tr.poly * a.epi.out_stride + e;
+  uint64_t v = mul_shoup(sub_mod(c, y, q), a.epi.w[tr.buf_limb], a.epi.ws[tr.buf_limb], q);
+  if (a.epi.accumulate) v = add_mod(v, *o, q);
+  store_wt(o, v);
+}
+
 
 // ---------------------------------------------------------------------------------------
 // Column pass: tile = COLS consecutive columns x S1 rows of one limb; 256-thread workgroup.
@@ -377,9 +393,11 @@ __device__ __forceinline__ TileRef col_ref(const KArgs& a, int tile, uint32_t c)
   poly = __builtin_amdgcn_readfirstlane(poly);
   r.buf_limb = __builtin_amdgcn_readfirstlane(r.buf_limb);
   r.row = __builtin_amdgcn_readfirstlane(r.row);
-  const size_t e = (size_t)r.buf_limb * a.n + (tile % CT) * COLS + c;
+  r.poly = poly;
+  r.k = (tile % CT) * COLS + c;
+  const size_t e = (size_t)r.buf_limb * a.n + r.k;
   r.off = poly * a.map.out_stride + e;
-  r.in_off = poly * a.map.in_stride + e;
+  r.in_off = a.bcast ? poly * a.bcast_stride + r.k : poly * a.map.in_stride + e;
   return r;
 }
 
@@ -411,7 +429,8 @@ __global__ __launch_bounds__(CBLOCK, kWavesPerEU) void ntt_col(KArgs a) {
   int tile = blockIdx.x;  // workgroup-uniform
   if (tile >= ntiles) return;
   uint64_t xn[E];
-  col_load<S1_LOG, S2_LOG, RF>(xn, a.in + col_ref<S2_LOG>(a, tile, c).in_off, pf);
+  const uint64_t* src = a.bcast ? a.bcast : a.in;
+  col_load<S1_LOG, S2_LOG, RF>(xn, src + col_ref<S2_LOG>(a, tile, c).in_off, pf);
   for (;;) {
     const TileRef tr = col_ref<S2_LOG>(a, tile, c);
     const int next = tile + gridDim.x;
@@ -421,6 +440,11 @@ __global__ __launch_bounds__(CBLOCK, kWavesPerEU) void ntt_col(KArgs a) {
     for (int j = 0; j < E; ++j) x[j] = xn[j];
     const LimbCtx lc = limb_ctx(a, tr.row);
     uint64_t* dst = a.out + tr.off;
+    if (FWD && a.bcast) {  // prologue: the broadcast limb reduced mod this limb's prime
+      const uint64_t r1 = a.barrett[2 * tr.row + 1];
+#pragma unroll
+      for (int j = 0; j < E; ++j) x[j] = barrett_reduce_64(x[j], lc.q, r1);
+    }
     if (lc.f64) {
       const double* tab = a.col + (size_t)tr.row * SB::S;
       double w[RN][E];
@@ -428,7 +452,7 @@ __global__ __launch_bounds__(CBLOCK, kWavesPerEU) void ntt_col(KArgs a) {
         constexpr int R = decltype(rc)::value;
         load_tw<S1_LOG, R>(w[R], tab, Round<S1_LOG, R>::p_thread(t), 1);
       });
-      if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, a.in + col_ref<S2_LOG>(a, next, c).in_off, pf);
+      if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, src + col_ref<S2_LOG>(a, next, c).in_off, pf);
       double v[E];
 #pragma unroll
       for (int j = 0; j < E; ++j) v[j] = FWD ? u52_to_f64(x[j]) : as_f64(x[j]);
@@ -461,7 +485,7 @@ __global__ __launch_bounds__(CBLOCK, kWavesPerEU) void ntt_col(KArgs a) {
       const uint64_t* tws = a.tws + (size_t)tr.row * a.n;
       // integer path (primes >= 2^50): twiddles and Shoup quotients per round, after the
       // prefetch (fewer registers; such tiles wait for the prefetch)
-      if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, a.in + col_ref<S2_LOG>(a, next, c).in_off, pf);
+      if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, src + col_ref<S2_LOG>(a, next, c).in_off, pf);
       uint64_t(&v)[E] = x;
       static_for<RN>([&](auto rc) {
         constexpr int R = FWD ? decltype(rc)::value : RN - 1 - decltype(rc)::value;
@@ -514,7 +538,9 @@ __device__ __forceinline__ TileRef row_ref(const KArgs& a, int item, uint32_t lr
   tr.buf_limb = __builtin_amdgcn_readfirstlane(tr.buf_limb);
   tr.row = __builtin_amdgcn_readfirstlane(tr.row);
   r = (item % GROUPS) * RW + lr;
-  const size_t e = (size_t)tr.buf_limb * a.n + (size_t)r * S2 + t;
+  tr.poly = poly;
+  tr.k = (size_t)r * S2 + t;
+  const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
   tr.off = poly * a.map.out_stride + e;
   tr.in_off = poly * a.map.in_stride + e;
   return tr;
@@ -628,8 +654,13 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
           ct_round_f64<S2_LOG, R, P::row_fwd.mask>(v, w, lc.qd, lc.qinv);
         });
         if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
+        if (a.epi.out) {
 #pragma unroll
-        for (int j = 0; j < E; ++j) store_wt(dst + j * T, f64_to_canonical(v[j], lc.qd, lc.qinv));
+          for (int j = 0; j < E; ++j) epilogue_store(a, tr, j * T, f64_to_canonical(v[j], lc.qd, lc.qinv), lc.q);
+        } else {
+#pragma unroll
+          for (int j = 0; j < E; ++j) store_wt(dst + j * T, f64_to_canonical(v[j], lc.qd, lc.qinv));
+        }
       } else {
         if constexpr (RN > 1) relayout<S2_LOG, 0, RN - 1>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
         static_for<RN>([&](auto rc) {
@@ -663,8 +694,13 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
         });
         if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, lrow, idx, sync, t);
         const uint64_t q2 = lc.q << 1;
+        if (a.epi.out) {
 #pragma unroll
-        for (int j = 0; j < E; ++j) store_wt(dst + j * T, csub(csub(v[j], q2), lc.q));
+          for (int j = 0; j < E; ++j) epilogue_store(a, tr, j * T, csub(csub(v[j], q2), lc.q), lc.q);
+        } else {
+#pragma unroll
+          for (int j = 0; j < E; ++j) store_wt(dst + j * T, csub(csub(v[j], q2), lc.q));
+        }
       } else {
         if constexpr (RN > 1) relayout<S2_LOG, 0, RN - 1>(v, lrow, idx, sync, t);
         static_for<RN>([&](auto rc) {
@@ -698,7 +734,8 @@ int num_cus() {
 
 template <int S1_LOG, int S2_LOG>
 hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const LimbMap& map, bool inverse,
-                  const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream) {
+                  const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream,
+                  const uint64_t* bcast = nullptr, size_t bcast_stride = 0, const NttEpilogue& epi = NttEpilogue{}) {
   const int per_poly = map.num_limbs - (map.skip_end - map.skip_begin);
   if (per_poly <= 0 || map.polys <= 0) return hipSuccess;
   const int limbs = per_poly * map.polys;
@@ -713,6 +750,9 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   a.n_inv = tb.n_inv; a.n_inv_shoup = tb.n_inv_shoup;
   a.scale = scale; a.scale_shoup = scale_shoup;
   a.map = map; a.n = (int)tb.n; a.limbs = limbs; a.limbs_per_poly = per_poly;
+  a.barrett = tb.barrett;
+  a.bcast = bcast; a.bcast_stride = bcast_stride;
+  a.epi = epi;
   if (a.map.in_stride == 0) a.map.in_stride = (size_t)map.num_limbs * tb.n;
   if (a.map.out_stride == 0) a.map.out_stride = (size_t)map.num_limbs * tb.n;
   constexpr int S1 = 1 << S1_LOG, S2 = 1 << S2_LOG;
@@ -726,9 +766,13 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   // column tiles of small transforms need fewer than BLOCK threads (rounded up to a wavefront)
   const dim3 block_c(std::max(64, COLS * Sub<S1_LOG>::T)), block_r(BLOCK);
   if (!inverse) {
+    NttEpilogue epi_row = a.epi;
+    a.epi = NttEpilogue{};  // the column pass stores its intermediate
     hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true>), grid_c, block_c, 0, stream, a);
     a.in = out;
     a.map.in_stride = a.map.out_stride;
+    a.bcast = nullptr;  // the row pass reads the intermediate
+    a.epi = epi_row;
     hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true>), grid_r, block_r, 0, stream, a);
   } else {
     hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false>), grid_r, block_r, 0, stream, a);
@@ -740,18 +784,16 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
 }
 
 hipError_t dispatch(const NttTables& tb, const uint64_t* in, uint64_t* out, const LimbMap& map, bool inverse,
-                    const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream) {
+                    const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream,
+                    const uint64_t* bcast = nullptr, size_t bcast_stride = 0, const NttEpilogue& epi = NttEpilogue{}) {
+#define PHX_NTT_CASE(LOGN, A, B) \
+  case LOGN: return launch<A, B>(tb, in, out, map, inverse, scale, scale_shoup, stream, bcast, bcast_stride, epi);
   switch (tb.log_n) {
-    case 10: return launch<5, 5>(tb, in, out, map, inverse, scale, scale_shoup, stream);
-    case 11: return launch<5, 6>(tb, in, out, map, inverse, scale, scale_shoup, stream);
-    case 12: return launch<6, 6>(tb, in, out, map, inverse, scale, scale_shoup, stream);
-    case 13: return launch<6, 7>(tb, in, out, map, inverse, scale, scale_shoup, stream);
-    case 14: return launch<7, 7>(tb, in, out, map, inverse, scale, scale_shoup, stream);
-    case 15: return launch<7, 8>(tb, in, out, map, inverse, scale, scale_shoup, stream);
-    case 16: return launch<8, 8>(tb, in, out, map, inverse, scale, scale_shoup, stream);
-    case 17: return launch<8, 9>(tb, in, out, map, inverse, scale, scale_shoup, stream);
+    PHX_NTT_CASE(10, 5, 5) PHX_NTT_CASE(11, 5, 6) PHX_NTT_CASE(12, 6, 6) PHX_NTT_CASE(13, 6, 7)
+    PHX_NTT_CASE(14, 7, 7) PHX_NTT_CASE(15, 7, 8) PHX_NTT_CASE(16, 8, 8) PHX_NTT_CASE(17, 8, 9)
     default: return hipErrorInvalidValue;
   }
+#undef PHX_NTT_CASE
 }
 
 }  // namespace
@@ -759,6 +801,12 @@ hipError_t dispatch(const NttTables& tb, const uint64_t* in, uint64_t* out, cons
 hipError_t ntt_forward(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                        hipStream_t stream) {
   return dispatch(t, in, out, map, false, nullptr, nullptr, stream);
+}
+
+hipError_t ntt_forward_fused(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
+                             const uint64_t* bcast, size_t bcast_stride, const NttEpilogue& epi, hipStream_t stream) {
+  if (epi.out && (!epi.c || !epi.w || !epi.ws)) return hipErrorInvalidValue;
+  return dispatch(t, in, out, map, false, nullptr, nullptr, stream, bcast, bcast_stride, epi);
 }
 
 hipError_t ntt_inverse(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,

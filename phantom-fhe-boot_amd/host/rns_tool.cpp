@@ -197,11 +197,18 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
   ba.in_stride = size_QlP * n_;
   ba.out_stride = size_Ql * n_;
   hip_ok(phx::bconv(ba, n_, s), "moddown bconv");
-  hip_ok(phx::ntt_forward(ntt, delta, delta, phx::LimbMap::contiguous((int)size_Ql, 0).batched(np), s),
-         "moddown NTT");
-  hip_ok(phx::moddown_finish(ct, cx, delta, d_bigPInv_mod_q_.get(), d_bigPInv_mod_q_shoup_.get(), d_Ql_.get(), n_,
-                             size_Ql, accumulate, s, polys, size_QlP * n_),
-         "moddown finish");
+  // NTT(delta) with the finish (cx - delta) P^-1 (+ ct) as its epilogue
+  phx::NttEpilogue epi;
+  epi.c = cx;
+  epi.c_stride = size_QlP * n_;
+  epi.out = ct;
+  epi.out_stride = size_Ql * n_;
+  epi.w = d_bigPInv_mod_q_.get();
+  epi.ws = d_bigPInv_mod_q_shoup_.get();
+  epi.accumulate = accumulate;
+  hip_ok(phx::ntt_forward_fused(ntt, delta, delta, phx::LimbMap::contiguous((int)size_Ql, 0).batched(np), nullptr, 0,
+                                epi, s),
+         "moddown NTT + finish");
 }
 
 void RnsTool::moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTables& ntt, hipStream_t s) const {
@@ -251,11 +258,16 @@ void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables&
   ba.in_stride = size_QlP * n_;
   ba.out_stride = Ln * n_;
   hip_ok(phx::bconv(ba, n_, s), "moddown-rescale bconv");
-  hip_ok(phx::ntt_forward(ntt, delta, delta, phx::LimbMap::contiguous((int)Ln, 0).batched(np), s),
-         "moddown-rescale NTT");
-  hip_ok(phx::moddown_finish(out, cx, delta, d_PQinv_.get(), d_PQinv_shoup_.get(), d_Ql_.get(), n_, Ln, false, s,
-                             polys, size_QlP * n_),
-         "moddown-rescale finish");
+  phx::NttEpilogue epi;
+  epi.c = cx;
+  epi.c_stride = size_QlP * n_;
+  epi.out = out;
+  epi.out_stride = Ln * n_;
+  epi.w = d_PQinv_.get();
+  epi.ws = d_PQinv_shoup_.get();
+  hip_ok(phx::ntt_forward_fused(ntt, delta, delta, phx::LimbMap::contiguous((int)Ln, 0).batched(np), nullptr, 0, epi,
+                                s),
+         "moddown-rescale NTT + finish");
 }
 
 void RnsTool::rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const phx::NttTables& ntt,
@@ -265,16 +277,21 @@ void RnsTool::rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const
   const size_t Ln = L - 1;
   const int np = static_cast<int>(polys);
   uint64_t* last = ws_->get(s, Workspace::kRescaleLast, polys * n_);
-  uint64_t* tmp = ws_->get(s, Workspace::kRescaleTmp, polys * Ln * n_);
   // all polynomials in one launch per stage
   hip_ok(phx::ntt_inverse(ntt, in + Ln * n_, last, phx::LimbMap::contiguous(1, (int)Ln).batched(np, L * n_, n_),
                           nullptr, nullptr, s),
          "rescale INTT(last)");
-  hip_ok(phx::rescale_spread_last(last, tmp, d_Ql_.get(), d_Ql_barrett_.get(), n_, Ln, s, polys), "rescale spread");
-  hip_ok(phx::ntt_forward(ntt, tmp, tmp, phx::LimbMap::contiguous((int)Ln, 0).batched(np), s), "rescale NTT");
-  hip_ok(phx::rescale_finish(in, tmp, out, d_inv_qlast_.get(), d_inv_qlast_shoup_.get(), d_Ql_.get(), n_, Ln, s,
-                             polys, L * n_),
-         "rescale finish");
+  // NTT of the last limb spread over the others (the prologue reduces it per limb), with the
+  // finish (c - NTT) q_last^-1 as the epilogue; `out` holds the intermediate of the two passes
+  phx::NttEpilogue epi;
+  epi.c = in;
+  epi.c_stride = L * n_;
+  epi.out = out;
+  epi.out_stride = Ln * n_;
+  epi.w = d_inv_qlast_.get();
+  epi.ws = d_inv_qlast_shoup_.get();
+  hip_ok(phx::ntt_forward_fused(ntt, nullptr, out, phx::LimbMap::contiguous((int)Ln, 0).batched(np), last, n_, epi, s),
+         "rescale NTT + finish");
 }
 
 }  // namespace phantom
