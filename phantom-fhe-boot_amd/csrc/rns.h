@@ -1,7 +1,8 @@
 // rns.h — RNS polynomial kernels on gfx950: elementwise arithmetic (src/polymath.cu), fast
 // base conversion (src/rns_bconv.cu), hybrid key-switch pieces (src/rns_bconv.cu:530-843,
-// src/eval_key_switch.cu), CKKS rescale (src/rns.cu:1128-1184), NTT-domain automorphism
-// (src/galois.cu:104-119) and the bootstrap helpers (src/evaluate.cu:2414-2554).
+// src/eval_key_switch.cu; the moddown and rescale finishes run as forward-NTT epilogues, ntt.h),
+// NTT-domain automorphism (src/galois.cu:104-119) and the bootstrap helpers
+// (src/evaluate.cu:2414-2554).
 //
 // Every launcher enqueues on `stream` and returns hipGetLastError().  Modulus arrays are
 // device arrays indexed by limb; `barrett` is [limb][2] = floor(2^128/q) {lo, hi}.
@@ -88,14 +89,6 @@ hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const*
                                 const uint64_t* qp_mod, const uint64_t* qp_barrett, size_t n, size_t size_ql,
                                 size_t size_q, size_t size_p, size_t beta, hipStream_t s,
                                 const KsAddend& add = KsAddend{});
-// moddown tail + add_to_ct (src/ntt/ntt_moddown.cu:199-214, src/rns_bconv.cu:763-789):
-//   ct[j] = ct[j] + (cx[j] - delta[j]) * Pinv[j] mod q_j   (accumulate = true)
-//   ct[j] =         (cx[j] - delta[j]) * Pinv[j] mod q_j   (accumulate = false)
-// for `polys` polynomials: ct and delta contiguous [polys][size_ql][n], cx at cx + p * cx_stride
-hipError_t moddown_finish(uint64_t* ct, const uint64_t* cx, const uint64_t* delta, const uint64_t* pinv,
-                          const uint64_t* pinv_shoup, const uint64_t* q, size_t n, size_t size_ql, bool accumulate,
-                          hipStream_t s, size_t polys = 1, size_t cx_stride = 0);
-
 // Coefficient-domain moddown whose result goes straight into a modup (a giant-step rotation of
 // an extended-basis ciphertext): c1 and delta [size_ql][n] coefficient form,
 //   y = (c1 - delta) P^-1 mod q_l -> t_mod_up[l / alpha][l]  (the digit's own limb)
@@ -110,17 +103,6 @@ struct ModdownModupConsts {
 hipError_t moddown_modup_finish(const uint64_t* c1, const uint64_t* delta, const ModdownModupConsts& k,
                                 uint64_t* t_cks, uint64_t* t_mod_up, size_t n, size_t size_ql, size_t size_qlp,
                                 size_t alpha, hipStream_t s);
-
-// ---- rescale --------------------------------------------------------------------------
-// divide_and_round_reduce_q_last_kernel (src/rns.cu:1128-1139): tmp[j] = c_last mod q_j, j < L-1
-// for `polys` polynomials: c_last [polys][n], tmp [polys][L_next][n]
-hipError_t rescale_spread_last(const uint64_t* c_last, uint64_t* tmp, const uint64_t* q, const uint64_t* barrett,
-                               size_t n, size_t L_next, hipStream_t s, size_t polys = 1);
-// divide_and_round_ntt_inv_scalar_kernel (src/rns.cu:1141-1158): out[j] = (c[j] - tmp[j]) * qlast_inv[j]
-// for `polys` polynomials: c at c + p * c_stride (0: (L_next + 1) n), tmp and out contiguous
-hipError_t rescale_finish(const uint64_t* c, const uint64_t* tmp, uint64_t* out, const uint64_t* inv,
-                          const uint64_t* inv_shoup, const uint64_t* q, size_t n, size_t L_next, hipStream_t s,
-                          size_t polys = 1, size_t c_stride = 0);
 
 // ---- automorphism ---------------------------------------------------------------------
 // apply_galois_ntt_permutation_direct (src/galois.cu:104-119): out[l][j] = in[l][perm[j]]

@@ -351,62 +351,6 @@ __global__ __launch_bounds__(kBlock) void moddown_modup_finish_kernel(const uint
   }
 }
 
-template <bool ACC>
-__global__ __launch_bounds__(kBlock) void moddown_finish_kernel(uint64_t* ct, const uint64_t* cx, const uint64_t* delta,
-                                                                const uint64_t* pinv, const uint64_t* pinvs,
-                                                                const uint64_t* q, uint32_t log_n, size_t pairs,
-                                                                size_t cx_stride) {
-  // blockIdx.y: polynomial (ct and delta contiguous [polys][Ql][n], cx strided)
-  ct += blockIdx.y * 2 * pairs;
-  delta += blockIdx.y * 2 * pairs;
-  cx += blockIdx.y * cx_stride;
-  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
-    const size_t e = 2 * i;
-    const uint32_t l = static_cast<uint32_t>(e >> log_n);
-    const uint64_t m = q[l], w = pinv[l], ws = pinvs[l];
-    const u64x2 c = ld2(cx + e), d = ld2(delta + e);
-    uint64_t x = mul_shoup(sub_mod(c.x, d.x, m), w, ws, m);
-    uint64_t y = mul_shoup(sub_mod(c.y, d.y, m), w, ws, m);
-    if constexpr (ACC) {
-      const u64x2 o = ld2(ct + e);
-      x = add_mod(o.x, x, m);
-      y = add_mod(o.y, y, m);
-    }
-    st2(ct + e, x, y);
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void rescale_spread_kernel(const uint64_t* c_last, uint64_t* tmp,
-                                                                const uint64_t* q, const uint64_t* qb, uint32_t log_n,
-                                                                size_t pairs) {
-  c_last += (size_t)blockIdx.y << log_n;  // blockIdx.y: polynomial
-  tmp += blockIdx.y * 2 * pairs;
-  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
-    const size_t e = 2 * i;
-    const uint32_t l = static_cast<uint32_t>(e >> log_n);
-    const size_t k = e & ((size_t(1) << log_n) - 1);
-    const uint64_t m = q[l], r1 = qb[2 * l + 1];
-    const u64x2 c = ld2(c_last + k);
-    st2(tmp + e, barrett_reduce_64(c.x, m, r1), barrett_reduce_64(c.y, m, r1));
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void rescale_finish_kernel(const uint64_t* c, const uint64_t* tmp, uint64_t* out,
-                                                                const uint64_t* inv, const uint64_t* invs,
-                                                                const uint64_t* q, uint32_t log_n, size_t pairs,
-                                                                size_t c_stride) {
-  c += blockIdx.y * c_stride;  // blockIdx.y: polynomial
-  tmp += blockIdx.y * 2 * pairs;
-  out += blockIdx.y * 2 * pairs;
-  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
-    const size_t e = 2 * i;
-    const uint32_t l = static_cast<uint32_t>(e >> log_n);
-    const uint64_t m = q[l], w = inv[l], ws = invs[l];
-    const u64x2 x = ld2(c + e), t = ld2(tmp + e);
-    st2(out + e, mul_shoup(sub_mod(x.x, t.x, m), w, ws, m), mul_shoup(sub_mod(x.y, t.y, m), w, ws, m));
-  }
-}
-
 // hoisted-rotation epilogue: out[t][l][j] (+)= x[t][l][perm j] with x = cx + (t == 0 ? c0 term : 0)
 // (MODE 0: none, 1: P c0 on the Ql limbs, 2: an extended-basis c0 on every limb)
 template <int MODE>
@@ -561,44 +505,12 @@ hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const*
   return hipGetLastError();
 }
 
-hipError_t moddown_finish(uint64_t* ct, const uint64_t* cx, const uint64_t* delta, const uint64_t* pinv,
-                          const uint64_t* pinv_shoup, const uint64_t* q, size_t n, size_t size_ql, bool accumulate,
-                          hipStream_t s, size_t polys, size_t cx_stride) {
-  const size_t pairs = n * size_ql / 2;
-  const dim3 g = poly_grid(pairs, polys);
-  if (accumulate)
-    moddown_finish_kernel<true><<<g, kBlock, 0, s>>>(ct, cx, delta, pinv, pinv_shoup, q, __builtin_ctzll(n), pairs,
-                                                     cx_stride);
-  else
-    moddown_finish_kernel<false><<<g, kBlock, 0, s>>>(ct, cx, delta, pinv, pinv_shoup, q, __builtin_ctzll(n), pairs,
-                                                      cx_stride);
-  return hipGetLastError();
-}
-
 hipError_t moddown_modup_finish(const uint64_t* c1, const uint64_t* delta, const ModdownModupConsts& k,
                                 uint64_t* t_cks, uint64_t* t_mod_up, size_t n, size_t size_ql, size_t size_qlp,
                                 size_t alpha, hipStream_t s) {
   const size_t pairs = n * size_ql / 2;
   moddown_modup_finish_kernel<<<grid_for(pairs), kBlock, 0, s>>>(c1, delta, k, t_cks, t_mod_up, __builtin_ctzll(n),
                                                                  pairs, static_cast<uint32_t>(alpha), size_qlp * n);
-  return hipGetLastError();
-}
-
-hipError_t rescale_spread_last(const uint64_t* c_last, uint64_t* tmp, const uint64_t* q, const uint64_t* barrett,
-                               size_t n, size_t L_next, hipStream_t s, size_t polys) {
-  const size_t pairs = n * L_next / 2;
-  const dim3 g = poly_grid(pairs, polys);
-  rescale_spread_kernel<<<g, kBlock, 0, s>>>(c_last, tmp, q, barrett, __builtin_ctzll(n), pairs);
-  return hipGetLastError();
-}
-
-hipError_t rescale_finish(const uint64_t* c, const uint64_t* tmp, uint64_t* out, const uint64_t* inv,
-                          const uint64_t* inv_shoup, const uint64_t* q, size_t n, size_t L_next, hipStream_t s,
-                          size_t polys, size_t c_stride) {
-  const size_t pairs = n * L_next / 2;
-  const dim3 g = poly_grid(pairs, polys);
-  rescale_finish_kernel<<<g, kBlock, 0, s>>>(c, tmp, out, inv, inv_shoup, q, __builtin_ctzll(n), pairs,
-                                             c_stride ? c_stride : n * (L_next + 1));
   return hipGetLastError();
 }
 

@@ -161,7 +161,7 @@ class Workspace {
     for (auto& kv : bufs_)
       for (auto& b : kv.second) b.release_sync();
   }
-  enum Slot : int { kModupInv = 0, kModdownDelta, kRescaleLast, kRescaleTmp, kKsModup, kKsCx, kSlots };
+  enum Slot : int { kModupInv = 0, kModdownDelta, kRescaleLast, kKsModup, kKsCx, kSlots };
   uint64_t* get(hipStream_t s, Slot slot, size_t count) {
     std::lock_guard<std::mutex> lk(mu_);
     DeviceBuffer<uint64_t>& b = bufs_[s][slot];
