@@ -36,25 +36,39 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 RING_BYTES = 320 << 20  # > 256 MiB Infinity Cache
 
 
-def cpu_baseline(mods, seconds=12.0):
-    """Scalar oracle NTT (forward + inverse of the same [44][65536] batch), 1 thread."""
-    import oracle_lib as O
+def _oracle_ntt_rate(O, mods, threads, seconds):
     plan = O.lib().or_ntt_plan_create(N, L, O.P(O.arr(mods)))
     a = O.random_limbs(np.random.default_rng(0x5EED), N, mods)
     steps = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        O.lib().or_ntt_plan_fwd(plan, O.P(a), L, 1)
-        O.lib().or_ntt_plan_inv(plan, O.P(a), L, 1)
+        O.lib().or_ntt_plan_fwd(plan, O.P(a), L, threads)
+        O.lib().or_ntt_plan_inv(plan, O.P(a), L, threads)
         steps += 1
     dt = time.perf_counter() - t0
     O.lib().or_ntt_plan_destroy(plan)
+    return 2 * BYTES_PER_TRANSFORM * steps / dt / 1e9, steps, dt
+
+
+def cpu_baseline(mods, seconds=8.0):
+    """The oracle's C NTT (the reference has no CPU path), forward + inverse of the
+    same [44][65536] batch on the host, OpenMP over limbs with the host's CPU share (at most 16
+    threads, the GPU box's share per GPU), and the same on 1 thread for reference."""
+    import oracle_lib as O
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    threads = max(1, min(16, share, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    v, steps, dt = _oracle_ntt_rate(O, mods, threads, seconds)
+    v1, steps1, dt1 = _oracle_ntt_rate(O, mods, 1, seconds)
     return {
-        "value": round(2 * BYTES_PER_TRANSFORM * steps / dt / 1e9, 3),
+        "value": round(v, 3),
         "unit": "GB/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"{steps} steps of fwd+inv NTT on one [44][65536] batch, scalar C oracle, {dt:.1f}s",
+        "sample": f"{steps} steps of fwd+inv NTT on one [44][65536] batch, C oracle, {threads} OpenMP threads, {dt:.1f}s",
+        "single_core": {"value": round(v1, 3), "cores": 1, "sample": f"{steps1} steps, {dt1:.1f}s"},
     }
 
 
