@@ -121,6 +121,78 @@ __global__ __launch_bounds__(256) void fused(uint64_t* d, unsigned* counters, un
   }
 }
 
+
+// fusedq: one launch, per-XCD work queues.  A workgroup reads its XCC id, and takes tasks from
+// that XCD's queue only, so every hand-off stays inside one XCD's L2: column tasks store their
+// intermediate with plain stores (the line stays in the L2), row tasks load it with nt loads
+// (L1 bypassed, served by the same L2) after the limb's counter shows all 16 column tiles.
+// Queue of XCD x (limbs x, x+8, ...; m of them): C(0..D-1), then R(s-D), C(s) interleaved.
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 7;
+}
+template <int D, int SL = 1>
+__global__ __launch_bounds__(256) void fusedq(uint64_t* d, unsigned* ctr, unsigned* tmo) {
+  // ctr[0..7] queue heads, ctr[8..8+L) limb counters, ctr[63] finish counter
+  __shared__ int s_task;
+  const unsigned x = xcc_id();
+  if (threadIdx.x == 0) atomicAdd(tmo + 1 + x, 1u);  // workgroups seen per XCC id
+  const int m = (L - (int)x + 7) / 8;
+  const int ntask = 32 * m;
+  for (int iter = 0; iter < 4096; ++iter) {
+    if (threadIdx.x == 0) s_task = (int)__hip_atomic_fetch_add(ctr + 32 * x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int task = __builtin_amdgcn_readfirstlane(s_task);
+    __syncthreads();
+    if (task >= ntask) break;
+    // decode: C(0..D-1); then R(s-D), C(s) for s in [D, m); then R(m-D..m-1)
+    bool col; int li, part;
+    if (task < 16 * D) { col = true; li = task / 16; part = task % 16; }
+    else if (task - 16 * D < 32 * (m - D)) {
+      const int u = task - 16 * D, s = u / 32 + D, r = u % 32;
+      col = r >= 16; li = col ? s : s - D; part = r % 16;
+    } else {
+      const int v = task - 16 * D - 32 * (m - D);
+      col = false; li = m - D + v / 16; part = v % 16;
+    }
+    const int limb = (int)x + 8 * li;
+    if (col) {
+      col_tile<0, false>(d, limb, part);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr + 32 * (8 + limb), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (threadIdx.x < 64) {  // wave 0 polls (wave-uniform loop)
+        for (unsigned spins = 0;; ++spins) {
+          const unsigned v = __builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(ctr + 32 * (8 + limb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          if (v >= 16u) break;
+          if (spins > (1u << 14)) { if (threadIdx.x == 0) atomicAdd(tmo, 1u); break; }
+          __builtin_amdgcn_s_sleep(SL);
+        }
+      }
+      __syncthreads();
+      const int w = threadIdx.x / 64;
+      const int lane = threadIdx.x % 64, lr = lane / 16, t = lane % 16;
+      uint64_t* base = d + (size_t)limb * N + (size_t)((part * 4 + w) * 4 + lr) * S2 + t;
+      uint64_t v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = __builtin_nontemporal_load(base + 16 * j);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) st<2>(base + 16 * j, v[j] + 1);
+    }
+  }
+  // last workgroup out resets the counters for the next launch
+  if (threadIdx.x == 0) {
+    const unsigned f = __hip_atomic_fetch_add(ctr + 32 * 60, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (f == gridDim.x - 1) {
+      for (int i = 0; i < 60; ++i) __hip_atomic_store(ctr + 32 * i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 32 * 60, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 int main() {
   setvbuf(stdout, nullptr, _IONBF, 0);
   hipEvent_t e0, e1;
@@ -129,12 +201,12 @@ int main() {
   std::vector<uint64_t*> buf(ring);
   for (auto& b : buf) { CK(hipMalloc(&b, TOT * 8)); CK(hipMemset(b, 0, TOT * 8)); }
   unsigned *counters, *tmo;
-  CK(hipMalloc(&counters, 64 * sizeof(unsigned))); CK(hipMemset(counters, 0, 64 * sizeof(unsigned)));
+  CK(hipMalloc(&counters, 64 * 32 * sizeof(unsigned))); CK(hipMemset(counters, 0, 64 * 32 * sizeof(unsigned)));
   CK(hipMalloc(&tmo, sizeof(unsigned))); CK(hipMemset(tmo, 0, sizeof(unsigned)));
   unsigned epoch = 0;
   auto time = [&](const char* name, auto launch) {
     CK(hipDeviceSynchronize());
-    CK(hipMemset(counters, 0, 64 * sizeof(unsigned)));
+    CK(hipMemset(counters, 0, 64 * 32 * sizeof(unsigned)));
     CK(hipDeviceSynchronize());
     epoch = 0;
     for (int i = 0; i < 10; ++i) launch(buf[i % ring]);
@@ -156,6 +228,7 @@ int main() {
            TOT * 16.0 / us / 1e3);
     return 0;
   };
+  if (!getenv("FUSEDQ")) {
   time("touch8 plain", [&](uint64_t* b) { touch8<0><<<2048, 256>>>(b, TOT); });
   time("touch8 nt", [&](uint64_t* b) { touch8<1><<<2048, 256>>>(b, TOT); });
   time("touch8 sc1", [&](uint64_t* b) { touch8<2><<<2048, 256>>>(b, TOT); });
@@ -173,6 +246,45 @@ int main() {
   time("xcd two-pass nt/sc1", [&](uint64_t* b) { colpass_x<1><<<GX, 256>>>(b); rowpass_x<2><<<GX, 256>>>(b); });
   time("xcd rowpass sc1 alone", [&](uint64_t* b) { rowpass_x<2><<<GX, 256>>>(b); });
   time("xcd colpass plain alone", [&](uint64_t* b) { colpass_x<0><<<GX, 256>>>(b); });
+  }
+  if (getenv("FUSEDQ")) {
+    CK(hipMalloc(&tmo, 16 * sizeof(unsigned)));
+    auto check = [&](int grid) -> int {
+      CK(hipMemset(counters, 0, 64 * 32 * sizeof(unsigned)));
+      CK(hipMemset(tmo, 0, 16 * sizeof(unsigned)));
+      CK(hipMemset(buf[0], 0, TOT * 8));
+      CK(hipDeviceSynchronize());
+      hipEvent_t a, z; CK(hipEventCreate(&a)); CK(hipEventCreate(&z));
+      CK(hipEventRecord(a));
+      fusedq<1><<<grid, 256>>>(buf[0], counters, tmo);
+      CK(hipEventRecord(z));
+      CK(hipDeviceSynchronize());
+      float ms; CK(hipEventElapsedTime(&ms, a, z));
+      std::vector<uint64_t> h(TOT);
+      CK(hipMemcpy(h.data(), buf[0], TOT * 8, hipMemcpyDeviceToHost));
+      size_t bad = 0;
+      for (size_t i = 0; i < TOT; ++i) bad += h[i] != 2;
+      unsigned t[16], c[64];
+      CK(hipMemcpy(t, tmo, sizeof t, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(c, counters, sizeof c, hipMemcpyDeviceToHost));
+      printf("fusedq grid %d: %.3f ms, %zu bad, timeouts %u, per-xcc", grid, ms, bad, t[0]);
+      for (int i = 0; i < 8; ++i) printf(" %u", t[1 + i]);
+      printf(" | ctr0 %u\n", c[0]);
+      return (bad || t[0]) ? 1 : 0;
+    };
+    if (check(256) || check(512)) return 1;
+    for (int per : {1, 2}) {
+      char nm[64];
+#define FQ(DD, SLP) \
+      snprintf(nm, sizeof nm, "fusedq D=%d sl=%d %d/CU", DD, SLP, per); \
+      time(nm, [&, per](uint64_t* b) { fusedq<DD, SLP><<<256 * per, 256>>>(b, counters, tmo); });
+      FQ(1, 1) FQ(2, 1) FQ(2, 8) FQ(3, 8) FQ(2, 32)
+    }
+    unsigned t;
+    CK(hipMemcpy(&t, tmo, sizeof t, hipMemcpyDeviceToHost));
+    printf("spin timeouts %u\n", t);
+    return 0;
+  }
   if (getenv("FUSED") == nullptr) return 0;
   auto fz = [&](auto kern, int G) {
     return [&, kern, G](uint64_t* b) { kern<<<8 * G * ((L + 7) / 8), 256>>>(b, counters, epoch++, tmo); };
