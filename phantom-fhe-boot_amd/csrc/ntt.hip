@@ -367,13 +367,29 @@ struct TileRef {
   size_t k;       // ... and inside its limb
 };
 
-// forward epilogue: out = (c - y) * w (+ out), for the element `dk` past this lane's first
-__device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr, uint32_t dk, uint64_t y, uint64_t q) {
-  const size_t e = (size_t)tr.buf_limb * a.n + tr.k + dk;
-  const uint64_t c = a.epi.c[tr.poly * a.epi.c_stride + e];
+// Forward epilogue: out = (c - y) * w (+ out).  Its operands c (and out when accumulating) are
+// loaded with the tile, behind the twiddle loads, so their latency hides under the butterflies
+// instead of sitting between the last round and the stores.
+struct EpiOperands {
+  uint64_t c[E], o[E];
+};
+__device__ __forceinline__ void epilogue_load(const KArgs& a, const TileRef& tr, uint32_t T, EpiOperands& eo) {
+  const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
+  const uint64_t* c = a.epi.c + tr.poly * a.epi.c_stride + e;
+  const uint64_t* o = a.epi.out + tr.poly * a.epi.out_stride + e;
+#pragma unroll
+  for (int j = 0; j < E; ++j) eo.c[j] = __builtin_nontemporal_load(c + j * T);
+  if (a.epi.accumulate) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) eo.o[j] = __builtin_nontemporal_load(o + j * T);
+  }
+}
+__device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr, uint32_t j, uint32_t T,
+                                               const EpiOperands& eo, uint64_t y, uint64_t q) {
+  const size_t e = (size_t)tr.buf_limb * a.n + tr.k + j * T;
   uint64_t* o = a.epi.out + tr.poly * a.epi.out_stride + e;
-  uint64_t v = mul_shoup(sub_mod(c, y, q), a.epi.w[tr.buf_limb], a.epi.ws[tr.buf_limb], q);
-  if (a.epi.accumulate) v = add_mod(v, *o, q);
+  uint64_t v = mul_shoup(sub_mod(eo.c[j], y, q), a.epi.w[tr.buf_limb], a.epi.ws[tr.buf_limb], q);
+  if (a.epi.accumulate) v = add_mod(v, eo.o[j], q);
   store_wt(o, v);
 }
 
@@ -552,7 +568,7 @@ __device__ __forceinline__ void row_load(uint64_t (&x)[E], const uint64_t* src) 
   for (int j = 0; j < E; ++j) x[j] = __builtin_nontemporal_load(src + j * Sub<S2_LOG>::T);
 }
 
-template <int S1_LOG, int S2_LOG, bool FWD>
+template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false>
 __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
   using SB = Sub<S2_LOG>;
   using P = Plan<S1_LOG, S2_LOG>;
@@ -589,6 +605,7 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
     const LimbCtx lc = limb_ctx(a, tr.row);
     uint64_t* dst = a.out + tr.off;
     uint32_t rn = 0;
+    EpiOperands eo;
     if (lc.f64) {
       const double* A = a.row_a + ((size_t)tr.row * S1 + r) * 16;
       const double* Bt = a.row_b + (size_t)tr.row * S2;
@@ -620,6 +637,7 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
         }
       });
       if (kPrefetch && more) row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, next, lr, t, rn).in_off);
+      if constexpr (FWD && EPI) epilogue_load(a, tr, T, eo);
 #pragma unroll
       for (int k = 0; k < K0; ++k) {
         const uint32_t e = t + 1 + T * k;
@@ -654,9 +672,9 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
           ct_round_f64<S2_LOG, R, P::row_fwd.mask>(v, w, lc.qd, lc.qinv);
         });
         if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
-        if (a.epi.out) {
+        if constexpr (EPI) {
 #pragma unroll
-          for (int j = 0; j < E; ++j) epilogue_store(a, tr, j * T, f64_to_canonical(v[j], lc.qd, lc.qinv), lc.q);
+          for (int j = 0; j < E; ++j) epilogue_store(a, tr, j, T, eo, f64_to_canonical(v[j], lc.qd, lc.qinv), lc.q);
         } else {
 #pragma unroll
           for (int j = 0; j < E; ++j) store_wt(dst + j * T, f64_to_canonical(v[j], lc.qd, lc.qinv));
@@ -690,13 +708,14 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
           if constexpr (R > 0) relayout<S2_LOG, R - 1, R>(v, lrow, idx, sync, t);
           uint64_t w[E], ws[E];
           get_tw(rc, w, ws);
+          if constexpr (EPI && R == RN - 1) epilogue_load(a, tr, T, eo);  // behind the last twiddles
           ct_round_int<S2_LOG, R>(v, w, ws, lc.q);
         });
         if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, lrow, idx, sync, t);
         const uint64_t q2 = lc.q << 1;
-        if (a.epi.out) {
+        if constexpr (EPI) {
 #pragma unroll
-          for (int j = 0; j < E; ++j) epilogue_store(a, tr, j * T, csub(csub(v[j], q2), lc.q), lc.q);
+          for (int j = 0; j < E; ++j) epilogue_store(a, tr, j, T, eo, csub(csub(v[j], q2), lc.q), lc.q);
         } else {
 #pragma unroll
           for (int j = 0; j < E; ++j) store_wt(dst + j * T, csub(csub(v[j], q2), lc.q));
@@ -773,7 +792,10 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
     a.map.in_stride = a.map.out_stride;
     a.bcast = nullptr;  // the row pass reads the intermediate
     a.epi = epi_row;
-    hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true>), grid_r, block_r, 0, stream, a);
+    if (a.epi.out)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true>), grid_r, block_r, 0, stream, a);
+    else
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, false>), grid_r, block_r, 0, stream, a);
   } else {
     hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false>), grid_r, block_r, 0, stream, a);
     a.in = out;

@@ -15,7 +15,11 @@ N, L = 1 << 16, 44
 iters = int(os.environ.get("ITERS", "30"))
 inverse = os.environ.get("INV", "1") == "1"
 lib = PA.load()
-mods = PA.coeff_modulus_create(N, [60] + [50] * 44 + [60] * 15)[:L]
+# BITS=60: 44 60-bit primes (the integer Shoup path every C4 bootstrap limb takes)
+if os.environ.get("BITS", "50") == "60":
+    mods = PA.coeff_modulus_create(N, [60] * L)
+else:
+    mods = PA.coeff_modulus_create(N, [60] + [50] * 44 + [60] * 15)[:L]
 t = PA.NttTables(N, mods)
 rng = np.random.default_rng(1)
 base = np.concatenate([rng.integers(0, q, size=N, dtype=np.uint64) for q in mods])

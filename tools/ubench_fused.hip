@@ -193,6 +193,59 @@ __global__ __launch_bounds__(256) void fusedq(uint64_t* d, unsigned* ctr, unsign
   }
 }
 
+// fusedx: one launch, every workgroup co-resident (grid = 8 * 16 * ceil(L / 8)), per-XCD ticket
+// queues ordered column tasks first, then row tasks (a row task waits only on column tasks with
+// smaller tickets, so any residency makes progress).  Column tasks store plain (the line stays
+// dirty in this XCD's L2), row tasks poll the limb counter, then load the intermediate with sc1
+// loads (L1 bypassed, same L2) and store the result with store flavour RS (0 plain, 2 sc1).
+template <int RS>
+__global__ __launch_bounds__(256) void fusedx(uint64_t* d, unsigned* ctr, unsigned* tmo) {
+  __shared__ int s_task;
+  const unsigned x = xcc_id();
+  const int m = (L - (int)x + 7) / 8;
+  const int ncol = 16 * m, ntask = 32 * m;
+  for (int iter = 0; iter < 64; ++iter) {
+    if (threadIdx.x == 0) s_task = (int)__hip_atomic_fetch_add(ctr + 32 * x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int task = __builtin_amdgcn_readfirstlane(s_task);
+    __syncthreads();
+    if (task >= ntask) break;
+    if (task < ncol) {
+      const int limb = (int)x + 8 * (task / 16);
+      col_tile<0, false>(d, limb, task % 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr + 32 * (8 + limb), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const int u = task - ncol, limb = (int)x + 8 * (u / 16), part = u % 16;
+      if (threadIdx.x < 64) {
+        for (unsigned spins = 0;; ++spins) {
+          const unsigned v = __builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(ctr + 32 * (8 + limb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          if (v >= 16u) break;
+          if (spins > (1u << 14)) { if (threadIdx.x == 0) atomicAdd(tmo, 1u); break; }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      __syncthreads();
+      const int w = threadIdx.x / 64, lane = threadIdx.x % 64, lr = lane / 16, t = lane % 16;
+      uint64_t* base = d + (size_t)limb * N + (size_t)((part * 4 + w) * 4 + lr) * S2 + t;
+      uint64_t v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = ld_sc1(base + 16 * j);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) st<RS>(base + 16 * j, v[j] + 1);
+    }
+  }
+  if (threadIdx.x == 0) {
+    const unsigned f = __hip_atomic_fetch_add(ctr + 32 * 60, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (f == gridDim.x - 1) {
+      for (int i = 0; i < 60; ++i) __hip_atomic_store(ctr + 32 * i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 32 * 60, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 int main() {
   setvbuf(stdout, nullptr, _IONBF, 0);
   hipEvent_t e0, e1;
@@ -228,6 +281,36 @@ int main() {
            TOT * 16.0 / us / 1e3);
     return 0;
   };
+  if (getenv("FUSEDX")) {
+    CK(hipMalloc(&tmo, 16 * sizeof(unsigned)));
+    const int GX = 8 * 16 * ((L + 7) / 8);
+    // correctness: one launch on zeros -> every element 2, no timeouts
+    CK(hipMemset(counters, 0, 64 * 32 * sizeof(unsigned)));
+    CK(hipMemset(tmo, 0, 16 * sizeof(unsigned)));
+    for (int rs = 0; rs < 2; ++rs) {
+      printf("fusedx check RS=%d launching\n", rs);
+      CK(hipMemset(buf[0], 0, TOT * 8));
+      CK(hipDeviceSynchronize());
+      if (rs == 0) fusedx<0><<<GX, 256>>>(buf[0], counters, tmo);
+      else fusedx<2><<<GX, 256>>>(buf[0], counters, tmo);
+      CK(hipDeviceSynchronize());
+      std::vector<uint64_t> h(TOT);
+      CK(hipMemcpy(h.data(), buf[0], TOT * 8, hipMemcpyDeviceToHost));
+      size_t bad = 0;
+      for (size_t i = 0; i < TOT; ++i) bad += h[i] != 2;
+      unsigned t;
+      CK(hipMemcpy(&t, tmo, sizeof t, hipMemcpyDeviceToHost));
+      printf("fusedx RS=%d check: %zu bad, timeouts %u\n", rs ? 2 : 0, bad, t);
+      if (bad || t) return 1;
+    }
+    time("two-pass both sc1", [&](uint64_t* b) { colpass<2><<<L * 16, 256>>>(b); rowpass<2><<<L * 16, 256>>>(b); });
+    time("fusedx plain/sc1ld/plain", [&](uint64_t* b) { fusedx<0><<<GX, 256>>>(b, counters, tmo); });
+    time("fusedx plain/sc1ld/sc1", [&](uint64_t* b) { fusedx<2><<<GX, 256>>>(b, counters, tmo); });
+    unsigned t;
+    CK(hipMemcpy(&t, tmo, sizeof t, hipMemcpyDeviceToHost));
+    printf("spin timeouts %u\n", t);
+    return 0;
+  }
   if (!getenv("FUSEDQ")) {
   time("touch8 plain", [&](uint64_t* b) { touch8<0><<<2048, 256>>>(b, TOT); });
   time("touch8 nt", [&](uint64_t* b) { touch8<1><<<2048, 256>>>(b, TOT); });
