@@ -4,22 +4,12 @@
 #include <algorithm>
 
 #include "arith.h"
+#include "prng.h"
 
 namespace phx {
 namespace {
 
 constexpr int kBlock = 256;
-
-__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-// counter-based generator: word w of element i of stream (seed, sid)
-__device__ __forceinline__ uint64_t rand_word(uint64_t seed, uint64_t sid, uint64_t i, uint32_t w) {
-  return mix64(mix64(seed ^ (sid * 0x9E3779B97F4A7C15ull)) + (i * 4 + w) * 0xD1B54A32D192ED03ull);
-}
 
 __global__ __launch_bounds__(kBlock) void uniform_kernel(uint64_t* out, const uint64_t* q, const uint64_t* barrett,
                                                          uint32_t log_n, size_t total, uint64_t seed, uint64_t sid) {

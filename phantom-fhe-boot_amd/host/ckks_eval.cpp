@@ -281,7 +281,7 @@ PhantomCiphertext RelinearizeRescale(const PhantomContext& ctx, const PhantomCip
   add.pmod = rt.bigP_mod_q();
   add.pmod_shoup = rt.bigP_mod_q_shoup();
   hip_ok(phx::keyswitch_inner_prod(t_mod_up, rlk.public_keys_ptr(), cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, Ql,
-                                   ctx.size_Q(), ctx.size_P(), beta, s, add),
+                                   ctx.size_Q(), ctx.size_P(), beta, s, add, rlk.seeds()),
          "relinearize inner product");
   PhantomCiphertext out;
   out.resize(ctx, d.chain_index() + 1, 2, s, false);
@@ -438,7 +438,8 @@ PhantomCiphertext EvalFastAutomorphismExt(const PhantomContext& ctx, const Phant
   hipStream_t s = ctx.stream();
   uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * QlP * n);
   hip_ok(phx::keyswitch_inner_prod(digits, keys.get(elt).public_keys_ptr(), cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n,
-                                   Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s),
+                                   Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s, phx::KsAddend{},
+                                   keys.get(elt).seeds()),
          "fast rotation inner product");
   PhantomCiphertext out;
   out.resize(2, QlP, n, s, false);
@@ -473,7 +474,8 @@ void EvalRotateExtAccumulate(const PhantomContext& ctx, PhantomCiphertext& ext, 
   rt.moddown_modup(digits.get(), ext.data() + QlP * n, ctx.gpu_rns_tables(), s);
   uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * QlP * n);
   hip_ok(phx::keyswitch_inner_prod(digits.get(), keys.get(elt).public_keys_ptr(), cx, ctx.mod_QP().q,
-                                   ctx.mod_QP().barrett, n, Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s),
+                                   ctx.mod_QP().barrett, n, Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s,
+                                   phx::KsAddend{}, keys.get(elt).seeds()),
          "giant step inner product");
   if (!accumulate) {
     acc.resize(2, QlP, n, s, false);

@@ -15,7 +15,7 @@ static void hip_ok(hipError_t e, const char* what) {
 }
 
 void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, const uint64_t* c2,
-                   const uint64_t* const* evk, hipStream_t s) {
+                   const uint64_t* const* evk, hipStream_t s, const phx::KsSeeds* seeds) {
   if (ctx.size_P() == 0) throw std::invalid_argument("key switching requires special primes");
   if (chain_index < 1 || chain_index >= ctx.total_parm_size()) throw std::invalid_argument("invalid chain index");
   const size_t n = ctx.poly_degree();
@@ -26,14 +26,14 @@ void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, 
   rt.modup(t_mod_up, c2, ctx.gpu_rns_tables(), s);
   uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * size_QlP * n);
   hip_ok(phx::keyswitch_inner_prod(t_mod_up, evk, cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, size_Ql,
-                                   ctx.size_Q(), ctx.size_P(), beta, s),
+                                   ctx.size_Q(), ctx.size_P(), beta, s, phx::KsAddend{}, seeds),
          "keyswitch inner product");
   rt.moddown_add(ct, cx, true, ctx.gpu_rns_tables(), s, 2);
 }
 
 void keyswitch_inplace(const PhantomContext& ctx, PhantomCiphertext& ct, const uint64_t* c2,
-                       const uint64_t* const* evk) {
-  keyswitch_raw(ctx, ct.chain_index(), ct.data(), c2, evk, ctx.stream());
+                       const uint64_t* const* evk, const phx::KsSeeds* seeds) {
+  keyswitch_raw(ctx, ct.chain_index(), ct.data(), c2, evk, ctx.stream(), seeds);
 }
 
 static void check_same(const PhantomCiphertext& a, const PhantomCiphertext& b) {
@@ -103,7 +103,7 @@ void relinearize_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const 
   if (a.size() != 3) throw std::invalid_argument("destination_size must be 3");
   if (!a.is_ntt_form()) throw std::invalid_argument("CKKS encrypted must be in NTT form");
   const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
-  keyswitch_inplace(ctx, a, a.data() + 2 * L * n, rlk.public_keys_ptr());
+  keyswitch_inplace(ctx, a, a.data() + 2 * L * n, rlk.public_keys_ptr(), rlk.seeds());
   a.resize(2, L, n, ctx.stream());
 }
 
@@ -180,7 +180,7 @@ void apply_galois_inplace(const PhantomContext& ctx, PhantomCiphertext& a, uint3
   PHX_CHECK(hipMemcpyAsync(c0, temp.get(), L * n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
   hip_ok(phx::galois_ntt(c1, temp.get(), perm, n, L, s), "galois c1");
   PHX_CHECK(hipMemsetAsync(c1, 0, L * n * sizeof(uint64_t), s));
-  keyswitch_inplace(ctx, a, temp.get(), keys.get(elt).public_keys_ptr());
+  keyswitch_inplace(ctx, a, temp.get(), keys.get(elt).public_keys_ptr(), keys.get(elt).seeds());
 }
 
 void rotate_inplace(const PhantomContext& ctx, PhantomCiphertext& a, int step, const PhantomGaloisKey& keys) {

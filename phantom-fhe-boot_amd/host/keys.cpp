@@ -1,5 +1,7 @@
 #include "keys.h"
 
+#include <cstdlib>
+
 #include <cmath>
 #include <random>
 #include <stdexcept>
@@ -16,7 +18,16 @@ static void hip_ok(hipError_t e, const char* what) {
   if (e != hipSuccess) throw hip_error(e, what);
 }
 
+const phx::KsSeeds* PhantomKSwitchKey::seeds() const {
+  static const bool regen = [] {
+    const char* e = std::getenv("PHX_KS_REGEN");
+    return !(e && e[0] == '0');
+  }();
+  return (has_seeds_ && regen) ? &seeds_ : nullptr;
+}
+
 void PhantomKSwitchKey::adopt(std::vector<DeviceBuffer<uint64_t>>&& digits, hipStream_t s) {
+  has_seeds_ = false;
   digits_ = std::move(digits);
   std::vector<uint64_t*> p;
   for (auto& d : digits_) p.push_back(d.get());
@@ -191,6 +202,7 @@ PhantomKSwitchKey PhantomSecretKey::make_kswitch_key(const PhantomContext& ctx, 
   hipStream_t s = ctx.stream();
   const size_t dnum = (Q + alpha - 1) / alpha;
   const RnsTool& rt = ctx.get_context_data(1).gpu_rns_tool();
+  phx::KsSeeds seeds;
   std::vector<DeviceBuffer<uint64_t>> digits;
   DeviceBuffer<uint64_t> e(QP * n, s), tmp(QP * n, s);
   const phx::ModView mqp = ctx.mod_QP();
@@ -198,6 +210,10 @@ PhantomKSwitchKey PhantomSecretKey::make_kswitch_key(const PhantomContext& ctx, 
     DeviceBuffer<uint64_t> key(2 * QP * n, s);
     uint64_t* b = key.get();
     uint64_t* a = key.get() + QP * n;
+    if (d < static_cast<size_t>(phx::kMaxKsDigits)) {
+      seeds.seed[d] = seed_state_;  // the stream sample_uniform draws from next
+      seeds.sid[d] = draws_;
+    }
     sample_uniform(ctx, a, QP);   // uniform in NTT form is uniform
     sample_error(ctx, e.get(), QP);
     hip_ok(phx::poly_mul_add(a, enc_key, e.get(), tmp.get(), mqp, n, QP, s), "a*s+e");
@@ -213,6 +229,7 @@ PhantomKSwitchKey PhantomSecretKey::make_kswitch_key(const PhantomContext& ctx, 
   }
   PhantomKSwitchKey k;
   k.adopt(std::move(digits), s);
+  if (dnum <= static_cast<size_t>(phx::kMaxKsDigits)) k.set_seeds(seeds);
   PHX_CHECK(hipStreamSynchronize(s));
   return k;
 }

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "buffer.h"
+#include "../csrc/rns.h"
 #include "ciphertext.h"
 #include "context.h"
 
@@ -35,10 +36,17 @@ class PhantomKSwitchKey {
   // 2-polynomial key-level ciphertext (chain index 0, size_QP limbs, NTT form)
   void save(const PhantomContext& ctx, std::ostream& os) const;
   void load(const PhantomContext& ctx, std::istream& is);
+  // Per-digit (seed, stream) of the uniform half when this library sampled it: the inner
+  // product then regenerates that half instead of reading it (phx::KsSeeds).  Null for loaded
+  // or adopted keys, and when PHX_KS_REGEN=0.
+  const phx::KsSeeds* seeds() const;
+  void set_seeds(const phx::KsSeeds& s) { seeds_ = s; has_seeds_ = true; }
 
  private:
   std::vector<DeviceBuffer<uint64_t>> digits_;
   DeviceBuffer<uint64_t*> ptrs_;
+  phx::KsSeeds seeds_;
+  bool has_seeds_ = false;
 };
 
 class PhantomRelinKey : public PhantomKSwitchKey {};
