@@ -478,18 +478,38 @@ void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const s
     lv.chain = first_chain + gi;
     const double scale = sf_.at(lv.chain - 1);
     lv.pts.resize(lv.D);
+    // the level's diagonals: their host encodings (FFT + exact RNS rounding) run on host threads,
+    // a chunk at a time, each chunk's uploads + NTTs queued behind it on the stream
+    std::vector<std::pair<int, const boot::cvec*>> jobs;
     for (int u = 0; u < lv.D; ++u) {
       const long off = static_cast<long>(u - lv.center) * lv.stride;
       const int key = static_cast<int>(((off % static_cast<long>(n)) + static_cast<long>(n)) % static_cast<long>(n));
       auto it = T.find(key);
-      if (it == T.end()) continue;
-      // pre-rotate by -(g i stride) so the giant rotation can follow the inner sum
-      const size_t sh = static_cast<size_t>((u / lv.g) * lv.g) * lv.stride % n;
-      boot::cvec rot(n);
-      for (size_t p = 0; p < n; ++p) rot[p] = it->second[(p + n - sh) % n];
-      auto pt = std::make_unique<PhantomPlaintext>();
-      encoder_.encode_ext(cc, rot, scale, *pt, lv.chain);
-      lv.pts[u] = std::move(pt);
+      if (it != T.end()) jobs.emplace_back(u, &it->second);
+    }
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::vector<uint64_t>> host(nt);
+    for (size_t c0 = 0; c0 < jobs.size(); c0 += nt) {
+      const size_t cnt = std::min<size_t>(nt, jobs.size() - c0);
+      auto work = [&](size_t w) {
+        const int u = jobs[c0 + w].first;
+        const boot::cvec& diag = *jobs[c0 + w].second;
+        // pre-rotate by -(g i stride) so the giant rotation can follow the inner sum
+        const size_t sh = static_cast<size_t>((u / lv.g) * lv.g) * lv.stride % n;
+        boot::cvec rot(n);
+        for (size_t p = 0; p < n; ++p) rot[p] = diag[(p + n - sh) % n];
+        encoder_.encode_ext_host(cc, rot, scale, lv.chain, host[w], 1);
+      };
+      std::vector<std::thread> th;
+      for (size_t w = 1; w < cnt; ++w) th.emplace_back(work, w);
+      work(0);
+      for (auto& t : th) t.join();
+      for (size_t w = 0; w < cnt; ++w) {
+        auto pt = std::make_unique<PhantomPlaintext>();
+        encoder_.upload_ext_async(cc, host[w], scale, *pt, lv.chain);
+        lv.pts[jobs[c0 + w].first] = std::move(pt);
+      }
+      PHX_CHECK(hipStreamSynchronize(cc.stream()));  // host[] is rewritten by the next chunk
     }
     // pointer table [b][g] for the kernel; absent diagonals read a zero plaintext
     std::vector<const uint64_t*> ptrs(static_cast<size_t>(lv.b) * lv.g, nullptr);

@@ -93,7 +93,7 @@ static inline uint64_t double_to_residue(double x, uint64_t q) {
 }
 
 void PhantomCKKSEncoder::to_rns(const std::vector<double>& coeffs, double scale, const std::vector<uint64_t>& moduli,
-                                std::vector<uint64_t>& out) {
+                                std::vector<uint64_t>& out, unsigned threads) {
   const size_t n = coeffs.size(), L = moduli.size();
   out.resize(L * n);
   std::vector<double> x(n);
@@ -101,7 +101,9 @@ void PhantomCKKSEncoder::to_rns(const std::vector<double>& coeffs, double scale,
   for (size_t k = 0; k < n; ++k)
     if (!std::isfinite(x[k]) || std::fabs(x[k]) >= std::ldexp(1.0, 1000)) throw std::invalid_argument("encoded values are too large");
   // exact residues; limbs spread over host threads (bootstrap setup encodes ~1,000 plaintexts)
-  const unsigned nt = static_cast<unsigned>(std::min<size_t>(L, std::max(1u, std::min(16u, std::thread::hardware_concurrency()))));
+  const unsigned nt = threads ? threads
+                              : static_cast<unsigned>(std::min<size_t>(
+                                    L, std::max(1u, std::min(16u, std::thread::hardware_concurrency()))));
   auto work = [&](unsigned w) {
     for (size_t l = w; l < L; l += nt)
       for (size_t k = 0; k < n; ++k) out[l * n + k] = double_to_residue(x[k], moduli[l]);
@@ -142,22 +144,43 @@ void PhantomCKKSEncoder::encode(const PhantomContext& ctx, const std::vector<dou
   encode(ctx, v, scale, out, chain_index);
 }
 
-void PhantomCKKSEncoder::encode_ext(const PhantomContext& ctx, const std::vector<std::complex<double>>& values,
-                                    double scale, PhantomPlaintext& out, size_t chain_index) const {
+static std::vector<uint64_t> ext_moduli(const PhantomContext& ctx, size_t chain_index) {
   std::vector<uint64_t> mods = ctx.get_context_data(chain_index).moduli();
-  const size_t size_Ql = mods.size();
   const auto& qp = ctx.key_moduli();
   mods.insert(mods.end(), qp.begin() + ctx.size_Q(), qp.end());
-  std::vector<uint64_t> host;
-  to_rns(slots_to_coeffs(values), scale, mods, host);
-  out.resize_ext(ctx, chain_index, mods.size(), ctx.stream());
+  return mods;
+}
+
+void PhantomCKKSEncoder::encode_ext_host(const PhantomContext& ctx, const std::vector<std::complex<double>>& values,
+                                         double scale, size_t chain_index, std::vector<uint64_t>& host,
+                                         unsigned rns_threads) const {
+  to_rns(slots_to_coeffs(values), scale, ext_moduli(ctx, chain_index), host, rns_threads);
+}
+
+void PhantomCKKSEncoder::upload_ext_async(const PhantomContext& ctx, const std::vector<uint64_t>& host, double scale,
+                                          PhantomPlaintext& out, size_t chain_index) const {
+  const size_t size_Ql = ctx.get_context_data(chain_index).coeff_modulus_size();
+  const size_t limbs = size_Ql + ctx.size_P();
+  if (host.size() != limbs * n_) throw std::invalid_argument("host residues do not match the extended basis");
+  hipStream_t s = ctx.stream();
+  out.resize_ext(ctx, chain_index, limbs, s);
   out.set_scale(scale);
   phx::LimbMap m;
-  m.num_limbs = static_cast<int>(mods.size());
+  m.num_limbs = static_cast<int>(limbs);
   m.split = static_cast<int>(size_Ql);
   m.first_a = 0;
   m.first_b = static_cast<int>(ctx.size_Q());
-  upload_ntt(ctx, host, out, m);
+  PHX_CHECK(hipMemcpyAsync(out.data(), host.data(), host.size() * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  const hipError_t e = phx::ntt_forward(ctx.gpu_rns_tables(), out.data(), out.data(), m, s);
+  if (e != hipSuccess) throw hip_error(e, "encode NTT");
+}
+
+void PhantomCKKSEncoder::encode_ext(const PhantomContext& ctx, const std::vector<std::complex<double>>& values,
+                                    double scale, PhantomPlaintext& out, size_t chain_index) const {
+  std::vector<uint64_t> host;
+  encode_ext_host(ctx, values, scale, chain_index, host);
+  upload_ext_async(ctx, host, scale, out, chain_index);
+  PHX_CHECK(hipStreamSynchronize(ctx.stream()));  // `host` is freed on return
 }
 
 void PhantomCKKSEncoder::decode(const PhantomContext& ctx, const PhantomPlaintext& plain,

@@ -34,6 +34,14 @@ class PhantomCKKSEncoder {
   // followed by the special primes P, NTT form ([size_Ql + size_P][n]).
   void encode_ext(const PhantomContext& ctx, const std::vector<std::complex<double>>& values, double scale,
                   PhantomPlaintext& out, size_t chain_index) const;
+  // encode_ext in two halves, so many plaintexts can be prepared on host threads at once: the
+  // host residues (coefficient form, limb-major; `rns_threads` 0 = spread limbs over threads)
+  // and their upload + NTT on the context's stream.  `host` must stay alive until the stream
+  // has run the upload (synchronise it before reusing or freeing `host`).
+  void encode_ext_host(const PhantomContext& ctx, const std::vector<std::complex<double>>& values, double scale,
+                       size_t chain_index, std::vector<uint64_t>& host, unsigned rns_threads = 0) const;
+  void upload_ext_async(const PhantomContext& ctx, const std::vector<uint64_t>& host, double scale,
+                        PhantomPlaintext& out, size_t chain_index) const;
 
   // decode(context, plain, values) (src/ckks.cu): exact CRT composition of each coefficient,
   // centered, divided by the plaintext's scale, then the canonical embedding.
@@ -49,7 +57,7 @@ class PhantomCKKSEncoder {
  private:
   // rounds coeffs * scale and writes residues for `moduli` (limb-major) to `out` (host)
   static void to_rns(const std::vector<double>& coeffs, double scale, const std::vector<uint64_t>& moduli,
-                     std::vector<uint64_t>& out);
+                     std::vector<uint64_t>& out, unsigned threads = 0);
   void fft(std::vector<std::complex<double>>& a, bool inverse) const;
 
   size_t n_ = 0;
