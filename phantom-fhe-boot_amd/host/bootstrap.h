@@ -114,7 +114,7 @@ class FHECKKSRNS {
   uint32_t correction_ = 0;
   std::vector<LTLevel> enc_, dec_;
   std::vector<double> cheb_;
-  int giant_streams_ = 2;  // PHX_BOOT_GIANT_STREAMS: concurrent giant-step chains per level
+  int giant_streams_ = 3;  // PHX_BOOT_GIANT_STREAMS: concurrent giant-step chains per level (profiles/r01/giant_streams_sweep.txt)
   mutable LeafTableCache leaf_tables_;
   PhantomRelinKey mul_key_;
   PhantomGaloisKey galois_keys_;  // fused keys
