@@ -162,6 +162,23 @@ int phantom_poly_op(const phantom_context *ctx, int op, const uint64_t *a, const
 int phantom_switch_modulus_raise(const phantom_context *ctx, const uint64_t *in_q0, uint64_t *out,
                                  size_t coeff_modulus_size, hipStream_t stream);
 
+/* ---- random sampling (src/prng.cu; seeds: include/prng.cuh:13-24) ---------------------
+ * Every draw of key generation and encryption is ChaCha20 keystream (RFC 8439 block function,
+ * 64-bit block counter in state words 12-13, 64-bit nonce in words 14-15): draw `nonce` of the
+ * stream keyed by key[8].  The reference samples from Salsa20 seeded by std::random_device. */
+/* out[16] = ChaCha20 block (host only, no GPU) */
+int phantom_chacha20_block(const uint32_t *key, uint64_t counter, uint64_t nonce, uint32_t *out);
+/* device polynomial [coeff_modulus_size][n] over the first limbs of the key-level chain:
+ *   PHANTOM_SAMPLE_UNIFORM: element e = 128-bit keystream word pair e mod q (sample_uniform_poly)
+ *   PHANTOM_SAMPLE_CBD:     centered binomial 21+21 bits of 64-bit word k (sample_error_poly)
+ *   PHANTOM_SAMPLE_TERNARY: 64-bit word k mod 3 minus 1 (sample_ternary_poly)
+ * the last two write the same signed value to every limb (coefficient form). */
+#define PHANTOM_SAMPLE_UNIFORM 0
+#define PHANTOM_SAMPLE_CBD 1
+#define PHANTOM_SAMPLE_TERNARY 2
+int phantom_sample_poly(const phantom_context *ctx, int kind, const uint32_t *key, uint64_t nonce, uint64_t *out,
+                        size_t coeff_modulus_size, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,8 +20,8 @@
 struct phantom_context {
   std::unique_ptr<phantom::PhantomContext> ctx;
   std::mutex mu;
+  static constexpr size_t kMaxKeyArrays = 256;
   std::map<std::vector<const uint64_t*>, phantom::DeviceBuffer<const uint64_t*>> key_ptrs;  // cached device arrays
-  std::map<uint32_t, phantom::DeviceBuffer<uint32_t>> perms;                               // galois tables
 
   const uint64_t* const* device_key_array(const uint64_t* const* host, size_t dnum, size_t need) {
     if (!host || dnum < need) throw std::invalid_argument("not enough key-switching key digits");
@@ -29,6 +29,12 @@ struct phantom_context {
     std::lock_guard<std::mutex> lk(mu);
     auto it = key_ptrs.find(v);
     if (it == key_ptrs.end()) {
+      // bounded: callers that reallocate their keys would otherwise grow the cache forever.
+      // Enqueued inner products may still read the arrays, so drain the device first.
+      if (key_ptrs.size() >= kMaxKeyArrays) {
+        (void)hipDeviceSynchronize();
+        key_ptrs.clear();
+      }
       phantom::DeviceBuffer<const uint64_t*> d;
       d.upload(v, nullptr);
       it = key_ptrs.emplace(v, std::move(d)).first;
@@ -39,6 +45,11 @@ struct phantom_context {
 
 using phantom::capi::fail;
 using phantom::capi::from_hip;
+
+const phantom::PhantomContext& phantom_capi_context(const phantom_context* c) {
+  if (!c || !c->ctx) throw std::invalid_argument("null context");
+  return *c->ctx;
+}
 
 namespace {
 const phantom::RnsTool& tool(const phantom_context* c, size_t chain_index) {
@@ -182,10 +193,16 @@ int phantom_ciphertext_deserialize(const uint8_t* in, size_t len, phantom_ct_hea
                                    size_t capacity_words, size_t* words) {
   PHX_CAPI_GUARD({
     if (!in || !h || !words) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
-    std::istringstream is(std::string(reinterpret_cast<const char*>(in), len));
+    if (len < phantom::ser::kCiphertextHeaderBytes) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "serialized object truncated");
     phantom::ser::CiphertextHeader c;
     std::vector<uint64_t> v;
     try {
+      // the payload must be in the buffer: check the header's word count against len first
+      std::istringstream hs(std::string(reinterpret_cast<const char*>(in), phantom::ser::kCiphertextHeaderBytes));
+      phantom::ser::read_ciphertext_header(hs, c);
+      if (c.words() > (len - phantom::ser::kCiphertextHeaderBytes) / sizeof(uint64_t))
+        return fail(PHANTOM_ERR_INVALID_ARGUMENT, "serialized object truncated");
+      std::istringstream is(std::string(reinterpret_cast<const char*>(in), len));
       phantom::ser::read_ciphertext(is, c, v);
     } catch (const std::runtime_error& e) {
       return fail(PHANTOM_ERR_INVALID_ARGUMENT, e.what());
@@ -224,24 +241,7 @@ int phantom_apply_galois_ntt(const phantom_context* ctx, uint32_t galois_elt, co
     if (!ctx) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null context");
     const size_t n = ctx->ctx->poly_degree();
     if (!(galois_elt & 1) || galois_elt >= 2 * n) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "invalid Galois element");
-    auto* c = const_cast<phantom_context*>(ctx);
-    const uint32_t* perm;
-    {
-      std::lock_guard<std::mutex> lk(c->mu);
-      auto it = c->perms.find(galois_elt);
-      if (it == c->perms.end()) {
-        const int logn = phantom::arith::log2_exact(n);
-        std::vector<uint32_t> p(n);
-        for (uint32_t j = 0; j < n; ++j) {
-          const uint64_t idx = ((2ull * j + 1) * galois_elt) % (2ull * n);
-          p[phantom::arith::reverse_bits(j, logn)] = phantom::arith::reverse_bits(static_cast<uint32_t>(idx >> 1), logn);
-        }
-        phantom::DeviceBuffer<uint32_t> d;
-        d.upload(p, nullptr);
-        it = c->perms.emplace(galois_elt, std::move(d)).first;
-      }
-      perm = it->second.get();
-    }
+    const uint32_t* perm = ctx->ctx->galois_perm(galois_elt);
     return from_hip(phx::galois_ntt(in, out, perm, n, L, stream));
   });
 }

@@ -4,32 +4,56 @@
 #include <algorithm>
 
 #include "arith.h"
-#include "prng.h"
+#include "chacha.h"
 
 namespace phx {
 namespace {
 
 constexpr int kBlock = 256;
 
+// Draw `nonce` of a ChaCha20 stream: block b holds 8 64-bit words.
+// uniform: element e of [L][n] takes words 2(e mod 4), 2(e mod 4) + 1 of block e / 4, a 128-bit
+// value reduced mod q (statistical distance from uniform < q / 2^128).
 __global__ __launch_bounds__(kBlock) void uniform_kernel(uint64_t* out, const uint64_t* q, const uint64_t* barrett,
-                                                         uint32_t log_n, size_t total, uint64_t seed, uint64_t sid) {
-  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
-    const uint32_t l = static_cast<uint32_t>(e >> log_n);
-    const u128 x{rand_word(seed, sid, e, 0), rand_word(seed, sid, e, 1)};
-    out[e] = barrett_reduce_128(x, q[l], barrett[2 * l], barrett[2 * l + 1]);
+                                                         uint32_t log_n, size_t blocks, ChaChaKey key, uint64_t nonce) {
+  for (size_t b = blockIdx.x * (size_t)kBlock + threadIdx.x; b < blocks; b += (size_t)gridDim.x * kBlock) {
+    uint32_t w[16];
+    chacha20_block(key, b, nonce, w);
+    const uint32_t l = static_cast<uint32_t>((4 * b) >> log_n);  // n >= 4: the 4 elements share a limb
+    const uint64_t ql = q[l], r0 = barrett[2 * l], r1 = barrett[2 * l + 1];
+    uint64_t v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = barrett_reduce_128(u128{chacha_word64(w, 2 * i), chacha_word64(w, 2 * i + 1)}, ql, r0, r1);
+    *reinterpret_cast<ulonglong2*>(out + 4 * b) = make_ulonglong2(v[0], v[1]);
+    *reinterpret_cast<ulonglong2*>(out + 4 * b + 2) = make_ulonglong2(v[2], v[3]);
   }
 }
 
-__global__ __launch_bounds__(kBlock) void cbd_kernel(uint64_t* out, const uint64_t* q, uint32_t log_n, size_t total,
-                                                     uint64_t seed, uint64_t sid) {
+// small signed samples, one 64-bit word per coefficient k (block k / 8), the same value written
+// to every limb: MODE 0 centered binomial (21 + 21 bits, sigma = sqrt(10.5) ~ 3.24, as the
+// reference's sample_error_poly draws a CBD), MODE 1 ternary {-1, 0, 1} uniform (word mod 3,
+// bias < 2^-62; sample_ternary_poly)
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void small_kernel(uint64_t* out, const uint64_t* q, uint32_t log_n, uint32_t L,
+                                                       size_t blocks, ChaChaKey key, uint64_t nonce) {
   const size_t n = size_t(1) << log_n;
-  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
-    const uint32_t l = static_cast<uint32_t>(e >> log_n);
-    const size_t k = e & (n - 1);
-    const uint64_t r = rand_word(seed, sid, k, 0);  // same sample for every limb
-    const int v = __popcll(r & 0x1FFFFFull) - __popcll((r >> 21) & 0x1FFFFFull);
-    const uint64_t ql = q[l];
-    out[e] = v >= 0 ? static_cast<uint64_t>(v) : ql - static_cast<uint64_t>(-v);
+  for (size_t b = blockIdx.x * (size_t)kBlock + threadIdx.x; b < blocks; b += (size_t)gridDim.x * kBlock) {
+    uint32_t w[16];
+    chacha20_block(key, b, nonce, w);
+    int v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint64_t r = chacha_word64(w, i);
+      if constexpr (MODE == 0) v[i] = __popcll(r & 0x1FFFFFull) - __popcll((r >> 21) & 0x1FFFFFull);
+      else v[i] = static_cast<int>(r % 3) - 1;
+    }
+    const size_t k0 = 8 * b;
+    if (k0 >= n) continue;
+    const int cnt = n - k0 < 8 ? static_cast<int>(n - k0) : 8;
+    for (uint32_t l = 0; l < L; ++l) {
+      const uint64_t ql = q[l];
+      for (int i = 0; i < cnt; ++i) out[(size_t)l * n + k0 + i] = v[i] >= 0 ? static_cast<uint64_t>(v[i]) : ql - static_cast<uint64_t>(-v[i]);
+    }
   }
 }
 
@@ -233,17 +257,29 @@ int grid_for(size_t items) {
 
 }  // namespace
 
-hipError_t sample_uniform(uint64_t* out, const uint64_t* q, const uint64_t* barrett, size_t n, size_t L, uint64_t seed,
-                          uint64_t stream_id, hipStream_t s) {
-  const size_t total = n * L;
-  uniform_kernel<<<grid_for(total), kBlock, 0, s>>>(out, q, barrett, __builtin_ctzll(n), total, seed, stream_id);
+hipError_t sample_uniform(uint64_t* out, const uint64_t* q, const uint64_t* barrett, size_t n, size_t L,
+                          const ChaChaKey& key, uint64_t nonce, hipStream_t s) {
+  if (n < 8 || (n & (n - 1))) return hipErrorInvalidValue;
+  const size_t blocks = n * L / 4;
+  uniform_kernel<<<grid_for(blocks), kBlock, 0, s>>>(out, q, barrett, __builtin_ctzll(n), blocks, key, nonce);
   return hipGetLastError();
 }
 
-hipError_t sample_cbd(uint64_t* out, const uint64_t* q, size_t n, size_t L, uint64_t seed, uint64_t stream_id,
+hipError_t sample_cbd(uint64_t* out, const uint64_t* q, size_t n, size_t L, const ChaChaKey& key, uint64_t nonce,
                       hipStream_t s) {
-  const size_t total = n * L;
-  cbd_kernel<<<grid_for(total), kBlock, 0, s>>>(out, q, __builtin_ctzll(n), total, seed, stream_id);
+  if (n < 8 || (n & (n - 1))) return hipErrorInvalidValue;
+  const size_t blocks = n / 8;
+  small_kernel<0><<<grid_for(blocks), kBlock, 0, s>>>(out, q, __builtin_ctzll(n), static_cast<uint32_t>(L), blocks, key,
+                                                     nonce);
+  return hipGetLastError();
+}
+
+hipError_t sample_ternary(uint64_t* out, const uint64_t* q, size_t n, size_t L, const ChaChaKey& key, uint64_t nonce,
+                          hipStream_t s) {
+  if (n < 8 || (n & (n - 1))) return hipErrorInvalidValue;
+  const size_t blocks = n / 8;
+  small_kernel<1><<<grid_for(blocks), kBlock, 0, s>>>(out, q, __builtin_ctzll(n), static_cast<uint32_t>(L), blocks, key,
+                                                     nonce);
   return hipGetLastError();
 }
 

@@ -85,18 +85,10 @@ struct KsAddend {
   const uint64_t* pmod = nullptr;
   const uint64_t* pmod_shoup = nullptr;
 };
-// A key made by this library's sampler holds, per digit, the (seed, stream) its uniform half
-// a = uniform(seed, sid) was drawn from (ckks.hip sample_uniform, a counter-based generator).
-// Given them, the inner product regenerates a[e] instead of reading it: half the key traffic.
-constexpr int kMaxKsDigits = 16;
-struct KsSeeds {
-  uint64_t seed[kMaxKsDigits] = {};
-  uint64_t sid[kMaxKsDigits] = {};
-};
 hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const* evk, uint64_t* cx,
                                 const uint64_t* qp_mod, const uint64_t* qp_barrett, size_t n, size_t size_ql,
                                 size_t size_q, size_t size_p, size_t beta, hipStream_t s,
-                                const KsAddend& add = KsAddend{}, const KsSeeds* seeds = nullptr);
+                                const KsAddend& add = KsAddend{});
 // Coefficient-domain moddown whose result goes straight into a modup (a giant-step rotation of
 // an extended-basis ciphertext): c1 and delta [size_ql][n] coefficient form,
 //   y = (c1 - delta) P^-1 mod q_l -> t_mod_up[l / alpha][l]  (the digit's own limb)

@@ -6,7 +6,6 @@
 #include <algorithm>
 
 #include "arith.h"
-#include "prng.h"
 
 namespace phx {
 namespace {
@@ -295,16 +294,12 @@ __global__ __launch_bounds__(kBlock) void modup_copy_kernel(const uint64_t* c2, 
   }
 }
 
-// REGEN: the key's uniform half (its second polynomial) is regenerated from the digit's
-// (seed, stream) exactly as sample_uniform drew it (ckks.hip uniform_kernel: element index over
-// [size_QP][n], two generator words Barrett-reduced mod q) instead of being read.
-template <bool REGEN>
 __global__ __launch_bounds__(kBlock) void ks_inner_kernel(const uint64_t* __restrict__ tmu,
                                                           const uint64_t* const* __restrict__ evk, uint64_t* cx,
                                                           const uint64_t* qp, const uint64_t* qpb, uint32_t log_n,
                                                           size_t pairs, uint32_t size_ql, uint32_t size_q,
                                                           size_t size_qlp_n, size_t size_qp_n, uint32_t beta,
-                                                          KsAddend add, KsSeeds seeds) {
+                                                          KsAddend add) {
   for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
     const size_t e = 2 * i;
     const uint32_t nid = static_cast<uint32_t>(e >> log_n);
@@ -317,14 +312,7 @@ __global__ __launch_bounds__(kBlock) void ks_inner_kernel(const uint64_t* __rest
       const u64x2 c = ld2(tmu + b * size_qlp_n + e);
       const uint64_t* key = evk[b];
       const u64x2 k0 = ld2(key + eidx);
-      u64x2 k1;
-      if constexpr (REGEN) {
-        const uint64_t sk = rand_stream(seeds.seed[b], seeds.sid[b]);
-        k1.x = barrett_reduce_128(u128{rand_word_k(sk, eidx, 0), rand_word_k(sk, eidx, 1)}, q, r0, r1);
-        k1.y = barrett_reduce_128(u128{rand_word_k(sk, eidx + 1, 0), rand_word_k(sk, eidx + 1, 1)}, q, r0, r1);
-      } else {
-        k1 = ld2(key + size_qp_n + eidx);
-      }
+      const u64x2 k1 = ld2(key + size_qp_n + eidx);
       add128(a0x, mul_wide(c.x, k0.x));
       add128(a0y, mul_wide(c.y, k0.y));
       add128(a1x, mul_wide(c.x, k1.x));
@@ -509,21 +497,12 @@ hipError_t modup_copy_digits(const uint64_t* c2, uint64_t* t_mod_up, size_t n, s
 
 hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const* evk, uint64_t* cx,
                                 const uint64_t* qp_mod, const uint64_t* qp_barrett, size_t n, size_t size_ql,
-                                size_t size_q, size_t size_p, size_t beta, hipStream_t s, const KsAddend& add,
-                                const KsSeeds* seeds) {
+                                size_t size_q, size_t size_p, size_t beta, hipStream_t s, const KsAddend& add) {
   const size_t size_qlp = size_ql + size_p;
   const size_t pairs = n * size_qlp / 2;
-  if (seeds && beta > static_cast<size_t>(kMaxKsDigits)) return hipErrorInvalidValue;
-  const KsSeeds sd = seeds ? *seeds : KsSeeds{};
-  if (seeds)
-    ks_inner_kernel<true><<<grid_for(pairs), kBlock, 0, s>>>(t_mod_up, evk, cx, qp_mod, qp_barrett, __builtin_ctzll(n),
-                                                             pairs, (uint32_t)size_ql, (uint32_t)size_q, size_qlp * n,
-                                                             (size_q + size_p) * n, (uint32_t)beta, add, sd);
-  else
-    ks_inner_kernel<false><<<grid_for(pairs), kBlock, 0, s>>>(t_mod_up, evk, cx, qp_mod, qp_barrett,
-                                                              __builtin_ctzll(n), pairs, (uint32_t)size_ql,
-                                                              (uint32_t)size_q, size_qlp * n, (size_q + size_p) * n,
-                                                              (uint32_t)beta, add, sd);
+  ks_inner_kernel<<<grid_for(pairs), kBlock, 0, s>>>(t_mod_up, evk, cx, qp_mod, qp_barrett, __builtin_ctzll(n), pairs,
+                                                    (uint32_t)size_ql, (uint32_t)size_q, size_qlp * n,
+                                                    (size_q + size_p) * n, (uint32_t)beta, add);
   return hipGetLastError();
 }
 

@@ -1,0 +1,335 @@
+// ckks_example — the reference's examples/3_ckks.cu on this engine: the same calls in the same
+// order (encode/decode, symmetric and asymmetric encryption, add/sub, multiply_plain, the
+// x*y*x HomMul with relinearize / rescale_to_next / mod_switch_to_next, fused rotation and
+// conjugation, the small-parameter apply_galois), with the reference's correctness rule: every
+// slot within |real difference| < 1e-3 (3_ckks.cu:19,33-41), a std::logic_error otherwise.
+//
+// Documented substitutions (no CUDA names in this engine): std::complex<double> for
+// cuDoubleComplex, std::mt19937_64 for rand() so a failing run can be replayed (--seed).
+//
+// usage: ckks_example [alpha ...] [--seed S]
+//   alpha selects the reference's parameter sets (3_ckks.cu:761-818): 1, 2, 3, 4 at N = 2^15 with
+//   40-bit primes, 15 = the C3 chain at N = 2^16 (Q = {60, 44 x 50}, P = 15 x 60).
+//   Default: 15.  Prints one JSON line per example; exit status 0 iff all pass.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../host/ckks_eval.h"
+#include "../host/encoder.h"
+#include "../host/evaluate.h"
+#include "../host/keys.h"
+#include "../host/modulus.h"
+
+using namespace phantom;
+using namespace phantom::arith;
+using cplx = std::complex<double>;
+
+static constexpr double EPSINON = 0.001;  // 3_ckks.cu:19
+static std::mt19937_64 g_rng;
+
+static double rnd() { return std::uniform_real_distribution<double>(0.0, 1.0)(g_rng); }
+// operator== of 3_ckks.cu:33-36 compares the real parts only
+static bool eq(const cplx& a, const cplx& b) { return std::fabs(a.real() - b.real()) < EPSINON; }
+static bool eq(double a, double b) { return std::fabs(a - b) < EPSINON; }  // compare_double
+
+static std::vector<cplx> random_msg(size_t n) {
+  std::vector<cplx> v(n);
+  for (auto& x : v) {
+    const double re = rnd();
+    x = cplx(re, rnd());
+  }
+  return v;
+}
+
+static void require(bool ok, const char* what) {
+  if (!ok) throw std::logic_error(what);
+}
+
+static void example_ckks_enc(PhantomContext& context, double scale) {
+  PhantomSecretKey secret_key(context);
+  PhantomPublicKey public_key = secret_key.gen_publickey(context);
+  PhantomCKKSEncoder encoder(context);
+  const size_t slot_count = encoder.slot_count();
+  std::vector<cplx> input = random_msg(slot_count);
+  PhantomPlaintext x_plain;
+  encoder.encode(context, input, scale, x_plain, 1);
+  std::vector<cplx> result;
+  encoder.decode(context, x_plain, result);
+  bool correctness = true;
+  for (size_t i = 0; i < slot_count; i++) correctness &= eq(result[i], input[i]);
+  require(correctness, "encode/decode complex vector error");
+
+  std::vector<double> input_double(slot_count);
+  for (auto& v : input_double) v = rnd();
+  PhantomPlaintext pt;
+  encoder.encode(context, input_double, scale, pt, 1);
+  std::vector<double> result_double;
+  encoder.decode(context, pt, result_double);
+  correctness = true;
+  for (size_t i = 0; i < slot_count; i++) correctness &= eq(result_double[i], input_double[i]);
+  require(correctness, "encode/decode double vector error");
+
+  PhantomCiphertext x_symmetric_cipher;
+  secret_key.encrypt_symmetric(context, x_plain, x_symmetric_cipher);
+  PhantomPlaintext x_symmetric_plain;
+  secret_key.decrypt(context, x_symmetric_cipher, x_symmetric_plain);
+  encoder.decode(context, x_symmetric_plain, result);
+  correctness = true;
+  for (size_t i = 0; i < slot_count; i++) correctness &= eq(result[i], input[i]);
+  require(correctness, "Symmetric encryption error");
+
+  PhantomCiphertext x_asymmetric_cipher;
+  public_key.encrypt_asymmetric(context, x_plain, x_asymmetric_cipher);
+  PhantomPlaintext x_asymmetric_plain;
+  secret_key.decrypt(context, x_asymmetric_cipher, x_asymmetric_plain);
+  encoder.decode(context, x_asymmetric_plain, result);
+  correctness = true;
+  for (size_t i = 0; i < slot_count; i++) correctness &= eq(result[i], input[i]);
+  require(correctness, "Asymmetric encryption error");
+}
+
+static void example_ckks_add(PhantomContext& context, double scale) {
+  PhantomSecretKey secret_key(context);
+  PhantomPublicKey public_key = secret_key.gen_publickey(context);
+  PhantomCKKSEncoder encoder(context);
+  const size_t slot_count = encoder.slot_count();
+  std::vector<cplx> input1 = random_msg(slot_count), input2 = random_msg(slot_count), result;
+  PhantomPlaintext x_plain, y_plain;
+  encoder.encode(context, input1, scale, x_plain);
+  encoder.encode(context, input2, scale, y_plain);
+
+  PhantomCiphertext x_sym_cipher, y_sym_cipher;
+  secret_key.encrypt_symmetric(context, x_plain, x_sym_cipher);
+  secret_key.encrypt_symmetric(context, y_plain, y_sym_cipher);
+  add_inplace(context, x_sym_cipher, y_sym_cipher);
+  PhantomPlaintext p;
+  secret_key.decrypt(context, x_sym_cipher, p);
+  encoder.decode(context, p, result);
+  bool correctness = true;
+  for (size_t i = 0; i < slot_count; i++) correctness &= eq(result[i], input1[i] + input2[i]);
+  require(correctness, "Symmetric HomAdd error");
+  sub_inplace(context, x_sym_cipher, y_sym_cipher);
+  secret_key.decrypt(context, x_sym_cipher, p);
+  encoder.decode(context, p, result);
+  correctness = true;
+  for (size_t i = 0; i < slot_count; i++) correctness &= eq(result[i], input1[i]);
+  require(correctness, "Symmetric HomSub error");
+
+  PhantomCiphertext x_asym_cipher, y_asym_cipher;
+  public_key.encrypt_asymmetric(context, x_plain, x_asym_cipher);
+  public_key.encrypt_asymmetric(context, y_plain, y_asym_cipher);
+  add_inplace(context, y_asym_cipher, x_asym_cipher);
+  secret_key.decrypt(context, y_asym_cipher, p);
+  encoder.decode(context, p, result);
+  correctness = true;
+  for (size_t i = 0; i < slot_count; i++) correctness &= eq(result[i], input1[i] + input2[i]);
+  require(correctness, "Asymmetric HomAdd error");
+  sub_inplace(context, x_asym_cipher, y_asym_cipher, true);  // x <- y - x
+  secret_key.decrypt(context, x_asym_cipher, p);
+  encoder.decode(context, p, result);
+  correctness = true;
+  for (size_t i = 0; i < slot_count; i++) correctness &= eq(result[i], input2[i]);
+  require(correctness, "Asymmetric HomSub error");
+}
+
+static void example_ckks_mul_plain(PhantomContext& context, double scale) {
+  PhantomSecretKey secret_key(context);
+  PhantomPublicKey public_key = secret_key.gen_publickey(context);
+  PhantomCKKSEncoder encoder(context);
+  const size_t slot_count = encoder.slot_count();
+  size_t msg_size = slot_count;
+  std::vector<cplx> msg_vec = random_msg(msg_size), const_vec = random_msg(slot_count), result;
+  PhantomPlaintext plain, const_plain;
+  encoder.encode(context, msg_vec, scale, plain);
+  encoder.encode(context, const_vec, scale, const_plain);
+  PhantomCiphertext sym_cipher;
+  secret_key.encrypt_symmetric(context, plain, sym_cipher);
+  multiply_plain_inplace(context, sym_cipher, const_plain);
+  secret_key.decrypt(context, sym_cipher, plain);
+  encoder.decode(context, plain, result);
+  bool correctness = true;
+  for (size_t i = 0; i < msg_size; i++) correctness &= eq(result[i], msg_vec[i] * const_vec[i]);
+  require(correctness, "Symmetric cipher multiply plain vector error");
+
+  msg_size >>= 2;
+  msg_vec = random_msg(msg_size);
+  const_vec.assign(128, cplx(0.0, 0.0));
+  {
+    const double re = rnd();
+    const_vec[2] = cplx(re, rnd());
+  }
+  encoder.encode(context, msg_vec, scale, plain);
+  encoder.encode(context, const_vec, scale, const_plain);
+  PhantomCiphertext asym_cipher;
+  public_key.encrypt_asymmetric(context, plain, asym_cipher);
+  multiply_plain_inplace(context, asym_cipher, const_plain);
+  secret_key.decrypt(context, asym_cipher, plain);
+  encoder.decode(context, plain, result);
+  correctness = true;
+  for (size_t i = 0; i < msg_size; i++)
+    correctness &= i == 2 ? eq(result[i], msg_vec[i] * const_vec[i]) : eq(result[i], cplx(0.0, 0.0));
+  require(correctness, "Asymmetric cipher multiply plain vector error");
+}
+
+static void example_ckks_mul(PhantomContext& context, double scale) {
+  PhantomSecretKey secret_key(context);
+  PhantomPublicKey public_key = secret_key.gen_publickey(context);
+  PhantomRelinKey relin_keys = secret_key.gen_relinkey(context);
+  PhantomCKKSEncoder encoder(context);
+  const size_t slot_count = encoder.slot_count();
+  std::vector<cplx> x_msg = random_msg(slot_count), y_msg = random_msg(slot_count);
+  PhantomPlaintext x_plain, y_plain;
+  encoder.encode(context, x_msg, scale, x_plain);
+  encoder.encode(context, y_msg, scale, y_plain);
+  PhantomCiphertext x_cipher, y_cipher;
+  public_key.encrypt_asymmetric(context, x_plain, x_cipher);
+  public_key.encrypt_asymmetric(context, y_plain, y_cipher);
+  // Compute x*y*x (3_ckks.cu:538-549)
+  PhantomCiphertext xy_cipher = multiply(context, x_cipher, y_cipher);
+  relinearize_inplace(context, xy_cipher, relin_keys);
+  rescale_to_next_inplace(context, xy_cipher);
+  xy_cipher.set_scale(scale);
+  mod_switch_to_next_inplace(context, x_cipher);
+  PhantomCiphertext x2y_cipher = multiply(context, xy_cipher, x_cipher);
+  relinearize_inplace(context, x2y_cipher, relin_keys);
+  rescale_to_next_inplace(context, x2y_cipher);
+  PhantomPlaintext x2y_plain = secret_key.decrypt(context, x2y_cipher);
+  auto result = encoder.decode<cplx>(context, x2y_plain);
+  bool correctness = true;
+  for (size_t i = 0; i < slot_count; i++) correctness &= eq(result[i], x_msg[i] * (x_msg[i] * y_msg[i]));
+  require(correctness, "Homomorphic multiplication error");
+}
+
+static void example_ckks_rotation(PhantomContext& context, double scale) {
+  PhantomSecretKey secret_key(context);
+  PhantomPublicKey public_key = secret_key.gen_publickey(context);
+  PhantomGaloisKeyFused fused_keys = secret_key.EvalRotateKeyGen(context, {1, 11, 15, 35});
+  const int step = 35;
+  PhantomCKKSEncoder encoder(context);
+  const size_t slot_count = encoder.slot_count();
+  std::vector<cplx> x_msg = random_msg(slot_count), result;
+  PhantomPlaintext x_plain, x_rot_plain;
+  encoder.encode(context, x_msg, scale, x_plain);
+  PhantomCiphertext x_cipher;
+  public_key.encrypt_asymmetric(context, x_plain, x_cipher);
+  PhantomCiphertext x_cipher_rot;
+  EvalRotateFused(context, fused_keys, x_cipher, x_cipher_rot, step);
+  secret_key.decrypt(context, x_cipher_rot, x_rot_plain);
+  encoder.decode(context, x_rot_plain, result);
+  bool correctness = true;
+  for (size_t i = 0; i < slot_count; i++) correctness &= eq(result[i], x_msg[(i + step) % slot_count]);
+  require(correctness, "Homomorphic rotation error");
+
+  x_msg = random_msg(slot_count);
+  PhantomPlaintext x_conj_plain;
+  encoder.encode(context, x_msg, scale, x_plain);
+  public_key.encrypt_asymmetric(context, x_plain, x_cipher);
+  PhantomCiphertext x_cipher_conj;
+  EvalConjFused(context, fused_keys, x_cipher, x_cipher_conj);
+  secret_key.decrypt(context, x_cipher_conj, x_conj_plain);
+  encoder.decode(context, x_conj_plain, result);
+  correctness = true;
+  // the reference compares real parts only; the imaginary parts are checked here as well
+  for (size_t i = 0; i < slot_count; i++)
+    correctness &= eq(result[i], std::conj(x_msg[i])) && std::fabs(result[i].imag() + x_msg[i].imag()) < EPSINON;
+  require(correctness, "Homomorphic conjugate error");
+}
+
+static void example_ckks_small_param() {
+  EncryptionParameters parms(scheme_type::ckks);
+  const size_t N = 1 << 13;
+  parms.set_poly_modulus_degree(N);
+  parms.set_special_modulus_size(1);
+  parms.set_coeff_modulus(CoeffModulus::Create(N, {60, 40, 60}));
+  parms.set_galois_elts({1});
+  PhantomContext context(parms);
+  PhantomCKKSEncoder encoder(context);
+  PhantomSecretKey secret_key(context);
+  PhantomPublicKey public_key = secret_key.gen_publickey(context);
+  PhantomRelinKey relin_key = secret_key.gen_relinkey(context);
+  PhantomGaloisKey galois_keys = secret_key.create_galois_keys(context);
+  std::vector<double> output, input(encoder.slot_count(), 1.0);
+  PhantomPlaintext plain;
+  PhantomCiphertext cipher;
+  encoder.encode(context, input, std::pow(2.0, 40), plain);
+  public_key.encrypt_asymmetric(context, plain, cipher);
+  apply_galois_inplace(context, cipher, 1, galois_keys);
+  secret_key.decrypt(context, cipher, plain);
+  encoder.decode(context, plain, output);
+  for (int i = 0; i < 10; i++)
+    if (!eq(input[i], output[i])) throw std::logic_error("error in example_ckks_small_param");
+}
+
+// 3_ckks.cu:761-818
+static EncryptionParameters params_for(int alpha, double& scale) {
+  EncryptionParameters parms(scheme_type::ckks);
+  size_t poly_modulus_degree = size_t(1) << 15;
+  scale = std::pow(2.0, 40);
+  std::vector<int> bits;
+  switch (alpha) {
+    case 1: bits = {60}; bits.insert(bits.end(), 18, 40); bits.push_back(60); break;
+    case 2: bits = {60}; bits.insert(bits.end(), 15, 40); bits.insert(bits.end(), 2, 60); break;
+    case 3: bits = {60}; bits.insert(bits.end(), 14, 40); bits.insert(bits.end(), 3, 60); break;
+    case 4: bits = {60}; bits.insert(bits.end(), 11, 40); bits.insert(bits.end(), 4, 60); break;
+    case 15:
+      poly_modulus_degree = size_t(1) << 16;
+      bits = {60};
+      bits.insert(bits.end(), 44, 50);
+      bits.insert(bits.end(), 15, 60);
+      scale = std::pow(2.0, 50);
+      break;
+    default: throw std::invalid_argument("unsupported alpha params");
+  }
+  parms.set_poly_modulus_degree(poly_modulus_degree);
+  parms.set_coeff_modulus(CoeffModulus::Create(poly_modulus_degree, bits));
+  parms.set_special_modulus_size(static_cast<size_t>(alpha));
+  return parms;
+}
+
+int main(int argc, char** argv) {
+  std::vector<int> alphas;
+  uint64_t seed = 1;
+  for (int i = 1; i < argc; ++i) {
+    if (!std::strcmp(argv[i], "--seed") && i + 1 < argc) seed = std::strtoull(argv[++i], nullptr, 0);
+    else alphas.push_back(std::atoi(argv[i]));
+  }
+  if (alphas.empty()) alphas = {15};
+  g_rng.seed(seed);
+  bool all = true;
+  auto run = [&](const char* name, int alpha, auto&& fn) {
+    bool ok = true;
+    std::string err;
+    try {
+      fn();
+    } catch (const std::exception& e) {
+      ok = false;
+      err = e.what();
+    }
+    all &= ok;
+    std::printf("{\"example\": \"%s\", \"alpha\": %d, \"ok\": %s, \"error\": \"%s\"}\n", name, alpha,
+                ok ? "true" : "false", err.c_str());
+    std::fflush(stdout);
+  };
+  for (int alpha : alphas) {
+    double scale = 0;
+    EncryptionParameters parms = params_for(alpha, scale);
+    PhantomContext context(parms);
+    run("ckks_enc", alpha, [&] { example_ckks_enc(context, scale); });
+    run("ckks_add", alpha, [&] { example_ckks_add(context, scale); });
+    run("ckks_mul_plain", alpha, [&] { example_ckks_mul_plain(context, scale); });
+    run("ckks_mul", alpha, [&] { example_ckks_mul(context, scale); });
+    run("ckks_rotation", alpha, [&] { example_ckks_rotation(context, scale); });
+  }
+  run("ckks_small_param", 1, [&] { example_ckks_small_param(); });
+  std::printf("{\"done\": \"ckks_example\", \"ok\": %s}\n", all ? "true" : "false");
+  return all ? 0 : 1;
+}

@@ -53,7 +53,12 @@ void PhantomCiphertext::load(const PhantomContext& ctx, std::istream& is) {
   ser::CiphertextHeader h;
   std::vector<uint64_t> v;
   ser::read_ciphertext(is, h, v);
+  // everything a kernel will index by must match the context before anything is allocated
   if (h.poly_modulus_degree != ctx.poly_degree()) throw std::invalid_argument("ciphertext degree mismatch");
+  if (h.chain_index >= ctx.total_parm_size()) throw std::invalid_argument("ciphertext chain index out of range");
+  if (h.size < 2 || h.size > 3) throw std::invalid_argument("ciphertext size must be 2 or 3");
+  if (h.coeff_modulus_size != ctx.get_context_data(h.chain_index).coeff_modulus_size())
+    throw std::invalid_argument("ciphertext limb count does not match its chain index");
   resize(h.size, h.coeff_modulus_size, h.poly_modulus_degree, ctx.stream(), false);
   if (!v.empty()) {
     PHX_CHECK(hipMemcpyAsync(data_.get(), v.data(), v.size() * sizeof(uint64_t), hipMemcpyHostToDevice, ctx.stream()));
@@ -86,6 +91,11 @@ void PhantomPlaintext::load(const PhantomContext& ctx, std::istream& is) {
   std::vector<uint64_t> v;
   ser::read_plaintext(is, h, v);
   if (h.poly_modulus_degree != ctx.poly_degree()) throw std::invalid_argument("plaintext degree mismatch");
+  if (h.chain_index >= ctx.total_parm_size()) throw std::invalid_argument("plaintext chain index out of range");
+  // a chain's Ql limbs, or Ql u P for an extended-basis plaintext
+  const size_t ql = ctx.get_context_data(h.chain_index).coeff_modulus_size();
+  if (h.coeff_modulus_size != ql && h.coeff_modulus_size != ql + ctx.size_P())
+    throw std::invalid_argument("plaintext limb count does not match its chain index");
   chain_index_ = h.chain_index;
   n_ = h.poly_modulus_degree;
   L_ = h.coeff_modulus_size;
@@ -95,6 +105,25 @@ void PhantomPlaintext::load(const PhantomContext& ctx, std::istream& is) {
     PHX_CHECK(hipMemcpyAsync(data_.get(), v.data(), v.size() * sizeof(uint64_t), hipMemcpyHostToDevice, ctx.stream()));
     PHX_CHECK(hipStreamSynchronize(ctx.stream()));
   }
+}
+
+void PhantomCiphertext::PreComputeScale(const PhantomContext& ctx, double scale) {
+  const size_t sizeQ = ctx.size_Q();
+  const auto& m = ctx.key_moduli();
+  sf_.assign(sizeQ, 0.0);
+  if (sizeQ == 1) {
+    sf_[0] = scale;
+  } else {
+    sf_[0] = static_cast<double>(m[sizeQ - 1]);
+    for (size_t k = 1; k < sizeQ; ++k) {
+      sf_[k] = sf_[k - 1] * sf_[k - 1] / static_cast<double>(m[sizeQ - k]);
+      const double ratio = sf_[k] / sf_[0];
+      if (ratio <= 0.5 || ratio >= 2.0)
+        throw std::invalid_argument("FLEXIBLEAUTO cannot support this number of levels in this parameter setting");
+    }
+  }
+  sf_big_.assign(sizeQ > 0 ? sizeQ - 1 : 0, 0.0);
+  for (size_t k = 0; k < sf_big_.size(); ++k) sf_big_[k] = sf_[k] * sf_[k];
 }
 
 void PhantomCiphertext::copy_from(const PhantomCiphertext& o) {
@@ -107,6 +136,8 @@ void PhantomCiphertext::copy_from(const PhantomCiphertext& o) {
   noise_scale_deg_ = o.noise_scale_deg_;
   is_ntt_form_ = o.is_ntt_form_;
   is_asymmetric_ = o.is_asymmetric_;
+  sf_ = o.sf_;
+  sf_big_ = o.sf_big_;
   const size_t count = size_ * L_ * n_;
   // the copy runs on this thread's stream (a StreamScope's), else on the source's stream
   hipStream_t s = StreamScope::current() ? StreamScope::current() : o.data_.stream();

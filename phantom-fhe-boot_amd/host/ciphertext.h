@@ -31,6 +31,8 @@ class PhantomCiphertext {
       is_ntt_form_ = o.is_ntt_form_;
       is_asymmetric_ = o.is_asymmetric_;
       data_ = std::move(o.data_);
+      sf_ = std::move(o.sf_);
+      sf_big_ = std::move(o.sf_big_);
       o.size_ = o.L_ = o.n_ = 0;
     }
     return *this;
@@ -74,6 +76,12 @@ class PhantomCiphertext {
   void retag(hipStream_t s) { data_.set_stream(s); }
   void set_asymmetric(bool b) { is_asymmetric_ = b; }
 
+  // PreComputeScale (include/ciphertext.h:320-367): the FLEXIBLEAUTO scaling factor of every level,
+  // sf[0] = q_last, sf[k] = sf[k-1]^2 / q_(size_Q - k), and their squares ("big" factors)
+  void PreComputeScale(const PhantomContext& ctx, double scale);
+  std::vector<double>& getScalingFactorsReal() { return sf_; }
+  std::vector<double>& getScalingFactorsRealBig() { return sf_big_; }
+
   // host transfer helpers (the reference's save/load staging, ciphertext.h:184-225)
   std::vector<uint64_t> to_host(hipStream_t s) const;
   void from_host(const PhantomContext& ctx, size_t chain_index, size_t size, const std::vector<uint64_t>& v,
@@ -88,6 +96,7 @@ class PhantomCiphertext {
   bool is_ntt_form_ = true;
   bool is_asymmetric_ = false;
   DeviceBuffer<uint64_t> data_;
+  std::vector<double> sf_, sf_big_;
 };
 
 class PhantomPlaintext {

@@ -119,27 +119,7 @@ void EvalAddConstInplace(const PhantomContext& ctx, PhantomCiphertext& ct, doubl
 void MultByMonomialInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, uint32_t power) {
   const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size();
   hipStream_t s = ctx.stream();
-  // NTT(X^power) over the first L limbs, cached per (power mod 2n, L)
-  static std::mutex mu;
-  static auto& cache = *new std::map<std::pair<uint32_t, std::vector<uint64_t>>, DeviceBuffer<uint64_t>>();
-  const uint32_t pr = power % (2 * n);
-  const uint64_t* mono;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    auto key = std::make_pair(pr, std::vector<uint64_t>(ctx.key_moduli().begin(), ctx.key_moduli().begin() + L));
-    auto it = cache.find(key);
-    if (it == cache.end()) {
-      const auto& mods = ctx.key_moduli();
-      std::vector<uint64_t> h(L * n, 0);
-      for (size_t l = 0; l < L; ++l) h[l * n + pr % n] = pr < n ? 1 : mods[l] - 1;
-      DeviceBuffer<uint64_t> d;
-      d.upload(h, s);
-      hip_ok(phx::ntt_forward(ctx.gpu_rns_tables(), d.get(), d.get(), phx::LimbMap::contiguous((int)L, 0), s),
-             "monomial NTT");
-      it = cache.emplace(key, std::move(d)).first;
-    }
-    mono = it->second.get();
-  }
+  const uint64_t* mono = ctx.monomial_ntt(power, L);
   hip_ok(phx::poly_mul(ct.data(), mono, ct.data(), ctx.mod_QP(), n, L, s, ct.size(), 0), "monomial");
 }
 
@@ -281,7 +261,7 @@ PhantomCiphertext RelinearizeRescale(const PhantomContext& ctx, const PhantomCip
   add.pmod = rt.bigP_mod_q();
   add.pmod_shoup = rt.bigP_mod_q_shoup();
   hip_ok(phx::keyswitch_inner_prod(t_mod_up, rlk.public_keys_ptr(), cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, Ql,
-                                   ctx.size_Q(), ctx.size_P(), beta, s, add, rlk.seeds()),
+                                   ctx.size_Q(), ctx.size_P(), beta, s, add),
          "relinearize inner product");
   PhantomCiphertext out;
   out.resize(ctx, d.chain_index() + 1, 2, s, false);
@@ -400,27 +380,6 @@ uint32_t FindAutomorphismIndex2nComplex(int index, size_t n) {
   return static_cast<uint32_t>(g);
 }
 
-static const uint32_t* perm_table(const PhantomContext& ctx, uint32_t elt) {
-  static std::mutex mu;
-  static auto& cache = *new std::map<std::pair<size_t, uint32_t>, DeviceBuffer<uint32_t>>();
-  const size_t n = ctx.poly_degree();
-  std::lock_guard<std::mutex> lk(mu);
-  auto key = std::make_pair(n, elt);
-  auto it = cache.find(key);
-  if (it == cache.end()) {
-    const int logn = log2_exact(n);
-    std::vector<uint32_t> perm(n);
-    for (uint32_t j = 0; j < n; ++j) {
-      const uint64_t idx = ((2ull * j + 1) * elt) % (2ull * n);
-      perm[reverse_bits(j, logn)] = reverse_bits(static_cast<uint32_t>(idx >> 1), logn);
-    }
-    DeviceBuffer<uint32_t> d;
-    d.upload(perm, ctx.stream());
-    it = cache.emplace(key, std::move(d)).first;
-  }
-  return it->second.get();
-}
-
 DeviceBuffer<uint64_t> EvalFastRotationPrecompute(const PhantomContext& ctx, const PhantomCiphertext& ct) {
   const RnsTool& rt = ctx.get_context_data(ct.chain_index()).gpu_rns_tool();
   const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P();
@@ -438,8 +397,7 @@ PhantomCiphertext EvalFastAutomorphismExt(const PhantomContext& ctx, const Phant
   hipStream_t s = ctx.stream();
   uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * QlP * n);
   hip_ok(phx::keyswitch_inner_prod(digits, keys.get(elt).public_keys_ptr(), cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n,
-                                   Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s, phx::KsAddend{},
-                                   keys.get(elt).seeds()),
+                                   Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s, phx::KsAddend{}),
          "fast rotation inner product");
   PhantomCiphertext out;
   out.resize(2, QlP, n, s, false);
@@ -453,7 +411,7 @@ PhantomCiphertext EvalFastAutomorphismExt(const PhantomContext& ctx, const Phant
   g.pmod = rt.bigP_mod_q();
   g.pmod_shoup = rt.bigP_mod_q_shoup();
   g.out = out.data();
-  g.perm = perm_table(ctx, elt);
+  g.perm = ctx.galois_perm(elt);
   g.q = rt.mod_QlP().q;
   g.ql = static_cast<uint32_t>(Ql);
   g.qlp = static_cast<uint32_t>(QlP);
@@ -475,7 +433,7 @@ void EvalRotateExtAccumulate(const PhantomContext& ctx, PhantomCiphertext& ext, 
   uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * QlP * n);
   hip_ok(phx::keyswitch_inner_prod(digits.get(), keys.get(elt).public_keys_ptr(), cx, ctx.mod_QP().q,
                                    ctx.mod_QP().barrett, n, Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s,
-                                   phx::KsAddend{}, keys.get(elt).seeds()),
+                                   phx::KsAddend{}),
          "giant step inner product");
   if (!accumulate) {
     acc.resize(2, QlP, n, s, false);
@@ -488,7 +446,7 @@ void EvalRotateExtAccumulate(const PhantomContext& ctx, PhantomCiphertext& ext, 
   g.cx = cx;
   g.c0 = ext.data();
   g.out = acc.data();
-  g.perm = perm_table(ctx, elt);
+  g.perm = ctx.galois_perm(elt);
   g.q = rt.mod_QlP().q;
   g.ql = static_cast<uint32_t>(Ql);
   g.qlp = static_cast<uint32_t>(QlP);

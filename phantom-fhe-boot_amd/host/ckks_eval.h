@@ -113,6 +113,16 @@ PhantomCiphertext EvalRotateFused(const PhantomContext& ctx, const PhantomCipher
                                   const PhantomGaloisKey& fused_keys, int index);
 PhantomCiphertext EvalConjFused(const PhantomContext& ctx, const PhantomCiphertext& ct,
                                 const PhantomGaloisKey& fused_keys);
+// the reference's argument order (include/evaluate.cuh: EvalRotateFused(context, keys, in, out, index),
+// EvalConjFused(context, keys, in, out))
+inline void EvalRotateFused(const PhantomContext& ctx, const PhantomGaloisKey& fused_keys, const PhantomCiphertext& in,
+                            PhantomCiphertext& out, int index) {
+  out = EvalRotateFused(ctx, in, fused_keys, index);
+}
+inline void EvalConjFused(const PhantomContext& ctx, const PhantomGaloisKey& fused_keys, const PhantomCiphertext& in,
+                          PhantomCiphertext& out) {
+  out = EvalConjFused(ctx, in, fused_keys);
+}
 
 // Galois element of a slot rotation (FindAutomorphismIndex2nComplex, src/util.cu:908-935)
 uint32_t FindAutomorphismIndex2nComplex(int index, size_t n);

@@ -4,6 +4,8 @@
 #include <thread>
 
 #include "hip_check.h"
+#include "numth.h"
+#include "../csrc/ntt.h"
 
 namespace phantom {
 
@@ -74,6 +76,38 @@ PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t s
     data_[c]->set_rns_tool(std::move(tools[c]));
   }
   PHX_CHECK(hipStreamSynchronize(s));
+}
+
+const uint32_t* PhantomContext::galois_perm(uint32_t elt) const {
+  std::lock_guard<std::mutex> lk(cache_mu_);
+  auto it = perms_.find(elt);
+  if (it != perms_.end()) return it->second.get();
+  if (!(elt & 1) || elt >= 2 * n_) throw std::invalid_argument("invalid Galois element");
+  const int logn = arith::log2_exact(n_);
+  std::vector<uint32_t> perm(n_);
+  for (uint32_t j = 0; j < n_; ++j) {
+    const uint64_t idx = ((2ull * j + 1) * elt) % (2ull * n_);
+    perm[arith::reverse_bits(j, logn)] = arith::reverse_bits(static_cast<uint32_t>(idx >> 1), logn);
+  }
+  DeviceBuffer<uint32_t> d;
+  d.upload(perm, stream_.s);
+  return perms_.emplace(elt, std::move(d)).first->second.get();
+}
+
+const uint64_t* PhantomContext::monomial_ntt(uint32_t power, size_t L) const {
+  const uint32_t pr = power % static_cast<uint32_t>(2 * n_);
+  std::lock_guard<std::mutex> lk(cache_mu_);
+  auto key = std::make_pair(pr, L);
+  auto it = monomials_.find(key);
+  if (it != monomials_.end()) return it->second.get();
+  if (L > qp_.size()) throw std::invalid_argument("too many limbs");
+  std::vector<uint64_t> h(L * n_, 0);
+  for (size_t l = 0; l < L; ++l) h[l * n_ + pr % n_] = pr < n_ ? 1 : qp_[l] - 1;
+  DeviceBuffer<uint64_t> d;
+  d.upload(h, stream_.s);
+  PHX_CHECK(phx::ntt_forward(ntt_->get(), d.get(), d.get(), phx::LimbMap::contiguous(static_cast<int>(L), 0), stream_.s));
+  PHX_CHECK(hipStreamSynchronize(stream_.s));
+  return monomials_.emplace(key, std::move(d)).first->second.get();
 }
 
 }  // namespace phantom

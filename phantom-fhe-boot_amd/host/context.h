@@ -4,7 +4,10 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <map>
 #include <memory>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "modulus.h"
@@ -143,6 +146,13 @@ class PhantomContext {
   hipStream_t lane_stream(int lane) const { return lane == 0 ? stream_.s : lane_main_[lane].s; }
   Workspace& workspace() const { return *ws_; }
 
+  // NTT-domain permutation of Galois element `elt`: out[j] = in[perm[j]] applies X -> X^elt to an
+  // NTT-form polynomial (PrecomputeAutoMapKernel, src/util.cu:941-958; the reference rebuilds it
+  // on every call).  Built once per context, so every table lives on the context's device.
+  const uint32_t* galois_perm(uint32_t elt) const;
+  // NTT(X^power) over the first L key moduli ([L][n]), cached per context
+  const uint64_t* monomial_ntt(uint32_t power, size_t L) const;
+
  private:
   OwnedStream stream_;  // first members: destroyed after everything that frees on them
   OwnedStream aux_[kLanes][kAuxStreams];
@@ -153,6 +163,9 @@ class PhantomContext {
   std::unique_ptr<Workspace> ws_;  // declared before the tools that point into it
   std::unique_ptr<DeviceNttTables> ntt_;
   std::vector<std::unique_ptr<ContextData>> data_;
+  mutable std::mutex cache_mu_;
+  mutable std::map<uint32_t, DeviceBuffer<uint32_t>> perms_;
+  mutable std::map<std::pair<uint32_t, size_t>, DeviceBuffer<uint64_t>> monomials_;
 };
 
 // runs the calling thread on lane `lane` of `cc`: its main stream (StreamScope) and aux streams

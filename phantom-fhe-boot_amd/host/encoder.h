@@ -47,6 +47,14 @@ class PhantomCKKSEncoder {
   // centered, divided by the plaintext's scale, then the canonical embedding.
   void decode(const PhantomContext& ctx, const PhantomPlaintext& plain, std::vector<std::complex<double>>& out) const;
   void decode(const PhantomContext& ctx, const PhantomPlaintext& plain, std::vector<double>& out) const;
+  // decode<T>(context, plain) (include/ckks.h:174-206): T = std::complex<double> (the reference's
+  // cuDoubleComplex) or double
+  template <class T>
+  std::vector<T> decode(const PhantomContext& ctx, const PhantomPlaintext& plain) const {
+    std::vector<T> v;
+    decode(ctx, plain, v);
+    return v;
+  }
 
   // host-side maps, exposed for the bootstrap precomputation and tests
   // slots -> real coefficients (inverse canonical embedding, coefficients not scaled)

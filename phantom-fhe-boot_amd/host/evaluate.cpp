@@ -15,7 +15,7 @@ static void hip_ok(hipError_t e, const char* what) {
 }
 
 void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, const uint64_t* c2,
-                   const uint64_t* const* evk, hipStream_t s, const phx::KsSeeds* seeds) {
+                   const uint64_t* const* evk, hipStream_t s) {
   if (ctx.size_P() == 0) throw std::invalid_argument("key switching requires special primes");
   if (chain_index < 1 || chain_index >= ctx.total_parm_size()) throw std::invalid_argument("invalid chain index");
   const size_t n = ctx.poly_degree();
@@ -26,14 +26,14 @@ void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, 
   rt.modup(t_mod_up, c2, ctx.gpu_rns_tables(), s);
   uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * size_QlP * n);
   hip_ok(phx::keyswitch_inner_prod(t_mod_up, evk, cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, size_Ql,
-                                   ctx.size_Q(), ctx.size_P(), beta, s, phx::KsAddend{}, seeds),
+                                   ctx.size_Q(), ctx.size_P(), beta, s),
          "keyswitch inner product");
   rt.moddown_add(ct, cx, true, ctx.gpu_rns_tables(), s, 2);
 }
 
 void keyswitch_inplace(const PhantomContext& ctx, PhantomCiphertext& ct, const uint64_t* c2,
-                       const uint64_t* const* evk, const phx::KsSeeds* seeds) {
-  keyswitch_raw(ctx, ct.chain_index(), ct.data(), c2, evk, ctx.stream(), seeds);
+                       const uint64_t* const* evk) {
+  keyswitch_raw(ctx, ct.chain_index(), ct.data(), c2, evk, ctx.stream());
 }
 
 static void check_same(const PhantomCiphertext& a, const PhantomCiphertext& b) {
@@ -103,7 +103,7 @@ void relinearize_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const 
   if (a.size() != 3) throw std::invalid_argument("destination_size must be 3");
   if (!a.is_ntt_form()) throw std::invalid_argument("CKKS encrypted must be in NTT form");
   const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
-  keyswitch_inplace(ctx, a, a.data() + 2 * L * n, rlk.public_keys_ptr(), rlk.seeds());
+  keyswitch_inplace(ctx, a, a.data() + 2 * L * n, rlk.public_keys_ptr());
   a.resize(2, L, n, ctx.stream());
 }
 
@@ -145,34 +145,11 @@ void mod_switch_to_inplace(const PhantomContext& ctx, PhantomCiphertext& a, size
   if (chain_index > a.chain_index()) a = mod_switch_to(ctx, a, chain_index);
 }
 
-// NTT-domain permutation tables per Galois element (PrecomputeAutoMapKernel, src/util.cu:941-958),
-// built once per (degree, element) and cached.
-static const uint32_t* galois_perm(size_t n, uint32_t elt, hipStream_t s) {
-  static std::mutex mu;
-  // intentionally never destroyed: device memory must not be freed after HIP teardown
-  static auto& cache = *new std::map<std::pair<size_t, uint32_t>, DeviceBuffer<uint32_t>>();
-  std::lock_guard<std::mutex> lk(mu);
-  auto key = std::make_pair(n, elt);
-  auto it = cache.find(key);
-  if (it != cache.end()) return it->second.get();
-  const int logn = arith::log2_exact(n);
-  std::vector<uint32_t> perm(n);
-  for (uint32_t j = 0; j < n; ++j) {
-    const uint64_t idx = ((2ull * j + 1) * elt) % (2ull * n);
-    perm[arith::reverse_bits(j, logn)] = arith::reverse_bits(static_cast<uint32_t>(idx >> 1), logn);
-  }
-  DeviceBuffer<uint32_t> d;
-  d.upload(perm, s);
-  const uint32_t* p = d.get();
-  cache.emplace(key, std::move(d));
-  return p;
-}
-
 void apply_galois_inplace(const PhantomContext& ctx, PhantomCiphertext& a, uint32_t elt, const PhantomGaloisKey& keys) {
   if (a.size() != 2) throw std::invalid_argument("encrypted size must be 2");
   const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
   hipStream_t s = ctx.stream();
-  const uint32_t* perm = galois_perm(n, elt, s);
+  const uint32_t* perm = ctx.galois_perm(elt);
   DeviceBuffer<uint64_t> temp(L * n, s);
   uint64_t* c0 = a.data();
   uint64_t* c1 = a.data() + L * n;
@@ -180,7 +157,7 @@ void apply_galois_inplace(const PhantomContext& ctx, PhantomCiphertext& a, uint3
   PHX_CHECK(hipMemcpyAsync(c0, temp.get(), L * n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
   hip_ok(phx::galois_ntt(c1, temp.get(), perm, n, L, s), "galois c1");
   PHX_CHECK(hipMemsetAsync(c1, 0, L * n * sizeof(uint64_t), s));
-  keyswitch_inplace(ctx, a, temp.get(), keys.get(elt).public_keys_ptr(), keys.get(elt).seeds());
+  keyswitch_inplace(ctx, a, temp.get(), keys.get(elt).public_keys_ptr());
 }
 
 void rotate_inplace(const PhantomContext& ctx, PhantomCiphertext& a, int step, const PhantomGaloisKey& keys) {

@@ -10,13 +10,12 @@
 namespace phantom {
 
 // keyswitch_inplace (src/eval_key_switch.cu:112-212): (c0, c1) += KeySwitch(c2) under `evk`
-// (device array of dnum digit pointers).  `seeds` (PhantomKSwitchKey::seeds()): regenerate the
-// key's uniform half instead of reading it; null reads the whole key.
+// (device array of dnum digit pointers).
 void keyswitch_inplace(const PhantomContext& ctx, PhantomCiphertext& encrypted, const uint64_t* c2,
-                       const uint64_t* const* evk, const phx::KsSeeds* seeds = nullptr);
+                       const uint64_t* const* evk);
 // the same on raw device buffers: ct is [2][size_Ql][n] at `chain_index`, c2 [size_Ql][n]
 void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, const uint64_t* c2,
-                   const uint64_t* const* evk, hipStream_t s, const phx::KsSeeds* seeds = nullptr);
+                   const uint64_t* const* evk, hipStream_t s);
 
 void add_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b);
 void sub_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b, bool negate = false);

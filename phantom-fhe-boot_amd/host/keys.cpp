@@ -1,14 +1,13 @@
 #include "keys.h"
 
-#include <cstdlib>
-
+#include <algorithm>
 #include <cmath>
-#include <random>
 #include <stdexcept>
 
 #include "../csrc/ckks.h"
 #include "../csrc/ntt.h"
 #include "../csrc/rns.h"
+#include "evaluate.h"
 #include "numth.h"
 #include "serialize.h"
 
@@ -18,16 +17,7 @@ static void hip_ok(hipError_t e, const char* what) {
   if (e != hipSuccess) throw hip_error(e, what);
 }
 
-const phx::KsSeeds* PhantomKSwitchKey::seeds() const {
-  static const bool regen = [] {
-    const char* e = std::getenv("PHX_KS_REGEN");
-    return !(e && e[0] == '0');
-  }();
-  return (has_seeds_ && regen) ? &seeds_ : nullptr;
-}
-
 void PhantomKSwitchKey::adopt(std::vector<DeviceBuffer<uint64_t>>&& digits, hipStream_t s) {
-  has_seeds_ = false;
   digits_ = std::move(digits);
   std::vector<uint64_t*> p;
   for (auto& d : digits_) p.push_back(d.get());
@@ -99,19 +89,17 @@ void PhantomSecretKey::save(const PhantomContext& ctx, std::ostream& os) const {
   ser::write_secret_key(os, 1, n, QP, h.data());
 }
 
-PhantomSecretKey PhantomSecretKey::load(const PhantomContext& ctx, std::istream& is, uint64_t seed) {
+PhantomSecretKey PhantomSecretKey::load(const PhantomContext& ctx, std::istream& is) {
   uint64_t power = 0, n = 0, limbs = 0;
   std::vector<uint64_t> v;
   ser::read_secret_key(is, power, n, limbs, v);
   if (power < 1 || n != ctx.poly_degree() || limbs != ctx.size_QP())
     throw std::invalid_argument("secret key does not match the context");
   v.resize(n * limbs);  // s itself; higher powers are recomputed
-  PhantomSecretKey k;
-  k.seed_state_ = seed;
+  PhantomSecretKey k;  // fresh entropy-seeded stream
   hipStream_t s = ctx.stream();
   k.s_.upload(v, s);
-  k.s2_.allocate(limbs * n, s);
-  hip_ok(phx::poly_mul(k.s_.get(), k.s_.get(), k.s2_.get(), ctx.mod_QP(), n, limbs, s), "sk^2");
+  k.init_powers(ctx);
   // ternary coefficients from limb 0 in coefficient form
   DeviceBuffer<uint64_t> c(n, s);
   hip_ok(phx::ntt_inverse(ctx.gpu_rns_tables(), k.s_.get(), c.get(), phx::LimbMap::contiguous(1, 0), nullptr, nullptr, s),
@@ -144,14 +132,6 @@ uint32_t galois_elt_from_step(int step, size_t n) {
   return static_cast<uint32_t>(g);
 }
 
-uint64_t PhantomSecretKey::next() {
-  // splitmix64 stream over the seed
-  uint64_t z = (seed_state_ += 0x9E3779B97F4A7C15ull);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
 static std::vector<uint64_t> signed_to_rns(const std::vector<int64_t>& c, const std::vector<uint64_t>& mods) {
   const size_t n = c.size();
   std::vector<uint64_t> out(mods.size() * n);
@@ -164,35 +144,67 @@ static std::vector<uint64_t> signed_to_rns(const std::vector<int64_t>& c, const 
   return out;
 }
 
-PhantomSecretKey::PhantomSecretKey(const PhantomContext& ctx, uint64_t seed) : seed_state_(seed) {
-  const size_t n = ctx.poly_degree(), L = ctx.size_QP();
-  hipStream_t s = ctx.stream();
+void sample_uniform_poly(const PhantomContext& ctx, RandomStream& rng, uint64_t* dst, size_t L) {
+  hip_ok(phx::sample_uniform(dst, ctx.mod_QP().q, ctx.mod_QP().barrett, ctx.poly_degree(), L, rng.key(),
+                             rng.next_draw(), ctx.stream()),
+         "sample uniform");
+}
+
+void sample_error_poly_ntt(const PhantomContext& ctx, RandomStream& rng, uint64_t* dst, size_t L) {
+  hip_ok(phx::sample_cbd(dst, ctx.mod_QP().q, ctx.poly_degree(), L, rng.key(), rng.next_draw(), ctx.stream()),
+         "sample e");
+  hip_ok(phx::ntt_forward(ctx.gpu_rns_tables(), dst, dst, phx::LimbMap::contiguous((int)L, 0), ctx.stream()), "e NTT");
+}
+
+void sample_ternary_poly_ntt(const PhantomContext& ctx, RandomStream& rng, uint64_t* dst, size_t L) {
+  hip_ok(phx::sample_ternary(dst, ctx.mod_QP().q, ctx.poly_degree(), L, rng.key(), rng.next_draw(), ctx.stream()),
+         "sample u");
+  hip_ok(phx::ntt_forward(ctx.gpu_rns_tables(), dst, dst, phx::LimbMap::contiguous((int)L, 0), ctx.stream()), "u NTT");
+}
+
+PhantomSecretKey::PhantomSecretKey(const PhantomContext& ctx) : PhantomSecretKey(ctx, RandomStream(), false) {}
+
+PhantomSecretKey PhantomSecretKey::for_testing(const PhantomContext& ctx, uint64_t seed) {
+  return PhantomSecretKey(ctx, RandomStream::for_testing(seed), true);
+}
+
+PhantomSecretKey::PhantomSecretKey(const PhantomContext& ctx, RandomStream rng, bool deterministic)
+    : rng_(rng), deterministic_(deterministic) {
+  const size_t n = ctx.poly_degree();
+  // ternary s (sample_ternary_poly): one 64-bit keystream word per coefficient, mod 3
+  std::vector<uint64_t> w(n);
+  rng_.host_words(w.data(), n);
   coeffs_.resize(n);
   std::vector<int64_t> c(n);
   for (size_t k = 0; k < n; ++k) {
-    coeffs_[k] = static_cast<int8_t>(static_cast<int>(next() % 3) - 1);  // ternary (sample_ternary_poly)
+    coeffs_[k] = static_cast<int8_t>(static_cast<int>(w[k] % 3) - 1);
     c[k] = coeffs_[k];
   }
-  s_.upload(signed_to_rns(c, ctx.key_moduli()), s);
-  hip_ok(phx::ntt_forward(ctx.gpu_rns_tables(), s_.get(), s_.get(), phx::LimbMap::contiguous((int)L, 0), s), "sk NTT");
+  s_.upload(signed_to_rns(c, ctx.key_moduli()), ctx.stream());
+  hip_ok(phx::ntt_forward(ctx.gpu_rns_tables(), s_.get(), s_.get(), phx::LimbMap::contiguous((int)ctx.size_QP(), 0),
+                          ctx.stream()),
+         "sk NTT");
+  init_powers(ctx);
+}
+
+void PhantomSecretKey::init_powers(const PhantomContext& ctx) {
+  const size_t n = ctx.poly_degree(), L = ctx.size_QP();
+  hipStream_t s = ctx.stream();
   s2_.allocate(L * n, s);
   hip_ok(phx::poly_mul(s_.get(), s_.get(), s2_.get(), ctx.mod_QP(), n, L, s), "sk^2");
   PHX_CHECK(hipStreamSynchronize(s));
 }
 
-// Randomness comes from device-side counter-based generators keyed by (seed, draw counter), so
-// key generation for hundreds of rotation keys stays on the GPU (the reference samples on the
-// GPU as well: src/prng.cu, sample_uniform_poly / sample_error_poly in src/secretkey.cu).
-void PhantomSecretKey::sample_uniform(const PhantomContext& ctx, uint64_t* dst, size_t L) {
-  hip_ok(phx::sample_uniform(dst, ctx.mod_QP().q, ctx.mod_QP().barrett, ctx.poly_degree(), L, seed_state_, draws_++,
-                             ctx.stream()),
-         "sample uniform");
-}
-
-void PhantomSecretKey::sample_error(const PhantomContext& ctx, uint64_t* dst, size_t L) {
-  // centered binomial, sigma ~ 3.2 (sample_error_poly uses a CBD as well), then NTT
-  hip_ok(phx::sample_cbd(dst, ctx.mod_QP().q, ctx.poly_degree(), L, seed_state_, draws_++, ctx.stream()), "sample e");
-  hip_ok(phx::ntt_forward(ctx.gpu_rns_tables(), dst, dst, phx::LimbMap::contiguous((int)L, 0), ctx.stream()), "e NTT");
+void PhantomSecretKey::encrypt_zero_raw(const PhantomContext& ctx, uint64_t* c0, uint64_t* c1, size_t L,
+                                        const uint64_t* enc_key) const {
+  const size_t n = ctx.poly_degree();
+  hipStream_t s = ctx.stream();
+  DeviceBuffer<uint64_t> e(L * n, s);
+  sample_uniform_poly(ctx, rng_, c1, L);  // uniform in NTT form is uniform
+  sample_error_poly_ntt(ctx, rng_, e.get(), L);
+  const phx::ModView m = ctx.mod_QP();
+  hip_ok(phx::poly_mul_add(c1, enc_key ? enc_key : s_.get(), e.get(), c0, m, n, L, s), "a*s+e");
+  hip_ok(phx::poly_negate(c0, c0, m, n, L, s), "-(a*s+e)");
 }
 
 PhantomKSwitchKey PhantomSecretKey::make_kswitch_key(const PhantomContext& ctx, const uint64_t* new_key,
@@ -202,22 +214,14 @@ PhantomKSwitchKey PhantomSecretKey::make_kswitch_key(const PhantomContext& ctx, 
   hipStream_t s = ctx.stream();
   const size_t dnum = (Q + alpha - 1) / alpha;
   const RnsTool& rt = ctx.get_context_data(1).gpu_rns_tool();
-  phx::KsSeeds seeds;
   std::vector<DeviceBuffer<uint64_t>> digits;
-  DeviceBuffer<uint64_t> e(QP * n, s), tmp(QP * n, s);
+  DeviceBuffer<uint64_t> tmp(QP * n, s);
   const phx::ModView mqp = ctx.mod_QP();
   for (size_t d = 0; d < dnum; ++d) {
     DeviceBuffer<uint64_t> key(2 * QP * n, s);
     uint64_t* b = key.get();
     uint64_t* a = key.get() + QP * n;
-    if (d < static_cast<size_t>(phx::kMaxKsDigits)) {
-      seeds.seed[d] = seed_state_;  // the stream sample_uniform draws from next
-      seeds.sid[d] = draws_;
-    }
-    sample_uniform(ctx, a, QP);   // uniform in NTT form is uniform
-    sample_error(ctx, e.get(), QP);
-    hip_ok(phx::poly_mul_add(a, enc_key, e.get(), tmp.get(), mqp, n, QP, s), "a*s+e");
-    hip_ok(phx::poly_negate(tmp.get(), b, mqp, n, QP, s), "-(a*s+e)");
+    encrypt_zero_raw(ctx, b, a, QP, enc_key);
     // + P * new_key on this digit's primes (multiply_temp_mod_and_add_rns_poly)
     const size_t l0 = d * alpha, l1 = std::min(Q, l0 + alpha);
     phx::ModView sub{mqp.q + l0, mqp.barrett + 2 * l0};
@@ -229,7 +233,6 @@ PhantomKSwitchKey PhantomSecretKey::make_kswitch_key(const PhantomContext& ctx, 
   }
   PhantomKSwitchKey k;
   k.adopt(std::move(digits), s);
-  if (dnum <= static_cast<size_t>(phx::kMaxKsDigits)) k.set_seeds(seeds);
   PHX_CHECK(hipStreamSynchronize(s));
   return k;
 }
@@ -262,6 +265,37 @@ PhantomGaloisKey PhantomSecretKey::create_galois_keys(const PhantomContext& ctx,
   return gk;
 }
 
+PhantomGaloisKey PhantomSecretKey::create_galois_keys(const PhantomContext& ctx) {
+  std::vector<uint32_t> elts = ctx.params().galois_elts();
+  if (elts.empty()) {
+    const size_t n = ctx.poly_degree();
+    for (size_t step = 1; step < n / 2; step <<= 1) {
+      elts.push_back(galois_elt_from_step(static_cast<int>(step), n));
+      elts.push_back(galois_elt_from_step(-static_cast<int>(step), n));
+    }
+    elts.push_back(static_cast<uint32_t>(2 * n - 1));
+  }
+  return create_galois_keys(ctx, elts);
+}
+
+PhantomGaloisKey PhantomSecretKey::EvalRotateKeyGen(const PhantomContext& ctx, const std::vector<int32_t>& index_list) {
+  const size_t n = ctx.poly_degree();
+  std::vector<uint32_t> elts;
+  for (int32_t i : index_list) {
+    // FindAutomorphismIndex2nComplex (src/util.cu:908-935)
+    const int64_t slots = static_cast<int64_t>(n / 2);
+    int64_t r = i % slots;
+    if (r < 0) r += slots;
+    uint64_t g = 1;
+    for (int64_t e = 0; e < r; ++e) g = g * 5 % (2 * n);
+    elts.push_back(static_cast<uint32_t>(g));
+  }
+  elts.push_back(static_cast<uint32_t>(2 * n - 1));
+  std::sort(elts.begin(), elts.end());
+  elts.erase(std::unique(elts.begin(), elts.end()), elts.end());
+  return create_galois_keys_fused(ctx, elts);
+}
+
 PhantomGaloisKey PhantomSecretKey::create_galois_keys_fused(const PhantomContext& ctx,
                                                            const std::vector<uint32_t>& elts) {
   const size_t n = ctx.poly_degree(), QP = ctx.size_QP();
@@ -287,26 +321,25 @@ PhantomGaloisKey PhantomSecretKey::create_galois_keys_fused(const PhantomContext
 }
 
 void PhantomSecretKey::encrypt_symmetric(const PhantomContext& ctx, const PhantomPlaintext& plain,
-                                         PhantomCiphertext& out) {
+                                         PhantomCiphertext& out) const {
   const size_t n = ctx.poly_degree(), ci = plain.chain_index();
+  if (ci < 1 || ci >= ctx.total_parm_size()) throw std::invalid_argument("invalid plaintext chain index");
   const size_t L = ctx.get_context_data(ci).coeff_modulus_size();
   hipStream_t s = ctx.stream();
   out.resize(ctx, ci, 2, s, false);
   out.set_ntt_form(true);
   out.set_scale(plain.scale());
-  uint64_t* c0 = out.data();
-  uint64_t* c1 = out.data() + L * n;
-  DeviceBuffer<uint64_t> e(L * n, s), t(L * n, s);
-  sample_uniform(ctx, c1, L);
-  sample_error(ctx, e.get(), L);
-  const phx::ModView m = ctx.mod_QP();
-  hip_ok(phx::poly_mul_add(c1, s_.get(), e.get(), t.get(), m, n, L, s), "a*s+e");
-  hip_ok(phx::poly_sub(plain.data(), t.get(), c0, m, n, L, s), "m-(a*s+e)");
+  out.set_correction_factor(1);
+  out.SetNoiseScaleDeg(1);
+  out.set_asymmetric(false);
+  encrypt_zero_raw(ctx, out.data(), out.data() + L * n, L);
+  hip_ok(phx::poly_add(out.data(), plain.data(), out.data(), ctx.mod_QP(), n, L, s), "m - (a s + e)");
   PHX_CHECK(hipStreamSynchronize(s));
 }
 
-void PhantomSecretKey::decrypt(const PhantomContext& ctx, const PhantomCiphertext& ct, PhantomPlaintext& out) {
+void PhantomSecretKey::decrypt(const PhantomContext& ctx, const PhantomCiphertext& ct, PhantomPlaintext& out) const {
   const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size();
+  if (ct.size() < 2 || ct.size() > 3) throw std::invalid_argument("unsupported ciphertext size");
   hipStream_t s = ctx.stream();
   out.resize(ctx, ct.chain_index(), s);
   out.set_scale(ct.scale());
@@ -316,6 +349,81 @@ void PhantomSecretKey::decrypt(const PhantomContext& ctx, const PhantomCiphertex
   if (ct.size() == 3)
     hip_ok(phx::poly_mul_add(ct.data() + 2 * L * n, s2_.get(), out.data(), out.data(), m, n, L, s), "+ c2 s^2");
   PHX_CHECK(hipStreamSynchronize(s));
+}
+
+PhantomPublicKey PhantomSecretKey::gen_publickey(const PhantomContext& ctx) const {
+  PhantomPublicKey pk;
+  const size_t n = ctx.poly_degree(), QP = ctx.size_QP();
+  pk.pk_.resize(ctx, 0, 2, ctx.stream(), false);
+  pk.pk_.set_ntt_form(true);
+  encrypt_zero_raw(ctx, pk.pk_.data(), pk.pk_.data() + QP * n, QP);
+  // the encryptor's own stream: fresh entropy, or derived for reproducible tests
+  pk.rng_ = deterministic_ ? rng_.derive() : RandomStream();
+  PHX_CHECK(hipStreamSynchronize(ctx.stream()));
+  return pk;
+}
+
+void PhantomPublicKey::encrypt_zero_raw(const PhantomContext& ctx, PhantomCiphertext& out, size_t ci) {
+  if (pk_.size() != 2 || pk_.coeff_modulus_size() != ctx.size_QP())
+    throw std::invalid_argument("PhantomPublicKey has not been generated");
+  if (ci < 1 || ci >= ctx.total_parm_size()) throw std::invalid_argument("invalid chain index");
+  const size_t n = ctx.poly_degree(), QP = ctx.size_QP();
+  hipStream_t s = ctx.stream();
+  const phx::ModView m = ctx.mod_QP();
+  // (c0, c1) = (pk0 u + e0, pk1 u + e1) over Q u P (encrypt_zero_asymmetric_internal_internal,
+  // src/secretkey.cu:12-86)
+  DeviceBuffer<uint64_t> u(QP * n, s), e(QP * n, s), cx(2 * QP * n, s);
+  sample_ternary_poly_ntt(ctx, rng_, u.get(), QP);
+  for (size_t i = 0; i < 2; ++i) {
+    sample_error_poly_ntt(ctx, rng_, e.get(), QP);
+    hip_ok(phx::poly_mul_add(u.get(), pk_.data() + i * QP * n, e.get(), cx.get() + i * QP * n, m, n, QP, s), "pk u + e");
+  }
+  // divide by P: the moddown of encrypt_zero_asymmetric_internal (src/secretkey.cu:113-121)
+  PhantomCiphertext z;
+  z.resize(ctx, 1, 2, s, false);
+  ctx.get_context_data(1).gpu_rns_tool().moddown_add(z.data(), cx.get(), false, ctx.gpu_rns_tables(), s, 2);
+  z.set_ntt_form(true);
+  // the reference moves between levels by modulus switching; dropping the leading limbs keeps an
+  // encryption of zero (its noise is far below the dropped primes)
+  out = ci > 1 ? mod_switch_to(ctx, z, ci) : std::move(z);
+  out.set_scale(1.0);
+  out.set_correction_factor(1);
+  out.SetNoiseScaleDeg(1);
+  out.set_asymmetric(true);
+}
+
+PhantomCiphertext PhantomPublicKey::encrypt_zero_asymmetric(const PhantomContext& ctx) {
+  PhantomCiphertext c;
+  encrypt_zero_raw(ctx, c, 1);
+  PHX_CHECK(hipStreamSynchronize(ctx.stream()));
+  return c;
+}
+
+void PhantomPublicKey::encrypt_asymmetric(const PhantomContext& ctx, const PhantomPlaintext& plain,
+                                          PhantomCiphertext& out) {
+  encrypt_zero_raw(ctx, out, plain.chain_index());
+  if (out.coeff_modulus_size() != plain.coeff_modulus_size())
+    throw std::invalid_argument("plaintext does not match its chain index");
+  // c0 = c0 + plaintext
+  hip_ok(phx::poly_add(out.data(), plain.data(), out.data(), ctx.mod_QP(), ctx.poly_degree(), out.coeff_modulus_size(),
+                       ctx.stream()),
+         "c0 + m");
+  out.set_scale(plain.scale());
+  PHX_CHECK(hipStreamSynchronize(ctx.stream()));
+}
+
+void PhantomPublicKey::save(std::ostream& os) const {
+  if (pk_.size() != 2) throw std::invalid_argument("PhantomPublicKey has not been generated");
+  pk_.save(os);
+}
+
+void PhantomPublicKey::load(const PhantomContext& ctx, std::istream& is) {
+  PhantomCiphertext k;
+  k.load(ctx, is);
+  if (k.size() != 2 || k.chain_index() != 0 || k.coeff_modulus_size() != ctx.size_QP())
+    throw std::invalid_argument("public key does not match the context");
+  pk_ = std::move(k);
+  rng_ = RandomStream();
 }
 
 }  // namespace phantom

@@ -1,11 +1,15 @@
-// keys.h — PhantomSecretKey / PhantomRelinKey / PhantomGaloisKey (include/secretkey.h).
+// keys.h — PhantomSecretKey / PhantomPublicKey / PhantomRelinKey / PhantomGaloisKey
+// (include/secretkey.h).
 //
-// Key generation and encryption are the test harness, not the accelerated path:
-// randomness comes from a caller-supplied seed (std::mt19937_64) instead of the reference's
-// std::random_device-seeded Salsa20, so keys and ciphertexts are reproducible.  Key formats
-// match the reference: a key-switching key is dnum digits of [2][size_QP][n] NTT-form
-// polynomials (b_i, a_i) with b_i = -(a_i s + e_i) + P * s' on digit i's primes
-// (src/secretkey.cu:362-406, multiply_temp_mod_and_add_rns_poly).
+// Key generation and encryption are the harness around the accelerated path, but
+// they are real cryptography: every draw comes from a ChaCha20 stream (host/random.h) keyed from
+// the operating system's CSPRNG, as the reference seeds Salsa20 from std::random_device
+// (include/prng.cuh:13-24).  Reproducible keys exist only through the explicitly named
+// PhantomSecretKey::for_testing.  Key formats match the reference:
+//   * public key: (-(a s + e), a) at the key level Q u P, NTT form (gen_publickey,
+//     src/secretkey.cu:493-504);
+//   * key-switching key: dnum digits of [2][size_QP][n] NTT-form polynomials (b_i, a_i) with
+//     b_i = -(a_i s + e_i) + P * s' on digit i's primes (src/secretkey.cu:362-406).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -17,9 +21,9 @@
 #include <vector>
 
 #include "buffer.h"
-#include "../csrc/rns.h"
 #include "ciphertext.h"
 #include "context.h"
+#include "random.h"
 
 namespace phantom {
 
@@ -36,17 +40,10 @@ class PhantomKSwitchKey {
   // 2-polynomial key-level ciphertext (chain index 0, size_QP limbs, NTT form)
   void save(const PhantomContext& ctx, std::ostream& os) const;
   void load(const PhantomContext& ctx, std::istream& is);
-  // Per-digit (seed, stream) of the uniform half when this library sampled it: the inner
-  // product then regenerates that half instead of reading it (phx::KsSeeds).  Null for loaded
-  // or adopted keys, and when PHX_KS_REGEN=0.
-  const phx::KsSeeds* seeds() const;
-  void set_seeds(const phx::KsSeeds& s) { seeds_ = s; has_seeds_ = true; }
 
  private:
   std::vector<DeviceBuffer<uint64_t>> digits_;
   DeviceBuffer<uint64_t*> ptrs_;
-  phx::KsSeeds seeds_;
-  bool has_seeds_ = false;
 };
 
 class PhantomRelinKey : public PhantomKSwitchKey {};
@@ -67,45 +64,122 @@ class PhantomGaloisKey {
   std::map<uint32_t, PhantomKSwitchKey> keys_;
 };
 
+// PhantomPublicKey (include/secretkey.h:17-101)
+class PhantomPublicKey {
+ public:
+  PhantomPublicKey() = default;
+  PhantomPublicKey(const PhantomPublicKey&) = delete;
+  PhantomPublicKey& operator=(const PhantomPublicKey&) = delete;
+  PhantomPublicKey(PhantomPublicKey&&) = default;
+  PhantomPublicKey& operator=(PhantomPublicKey&&) = default;
+
+  // encrypt_asymmetric (src/secretkey.cu:130-185): (pk0 u + e0, pk1 u + e1) over Q u P with u
+  // ternary and e0, e1 centered binomial, divided by P (moddown) to Q, dropped to the
+  // plaintext's level, then m added to c0.  The ciphertext takes the plaintext's scale.
+  void encrypt_asymmetric(const PhantomContext& ctx, const PhantomPlaintext& plain, PhantomCiphertext& out);
+  PhantomCiphertext encrypt_asymmetric(const PhantomContext& ctx, const PhantomPlaintext& plain) {
+    PhantomCiphertext c;
+    encrypt_asymmetric(ctx, plain, c);
+    return c;
+  }
+  // encrypt_zero_asymmetric (include/secretkey.h:78-84): an encryption of 0 at chain index 1
+  PhantomCiphertext encrypt_zero_asymmetric(const PhantomContext& ctx);
+
+  // save / load (include/secretkey.h:86-101): the key-level ciphertext pk_.  A loaded key
+  // encrypts with a fresh entropy-seeded stream.
+  void save(std::ostream& os) const;
+  void load(const PhantomContext& ctx, std::istream& is);
+  const PhantomCiphertext& key() const { return pk_; }
+
+ private:
+  friend class PhantomSecretKey;
+  void encrypt_zero_raw(const PhantomContext& ctx, PhantomCiphertext& out, size_t chain_index);
+  PhantomCiphertext pk_;
+  RandomStream rng_;
+};
+
 class PhantomSecretKey {
  public:
-  PhantomSecretKey(const PhantomContext& ctx, uint64_t seed);
+  // PhantomSecretKey(context) (src/secretkey.cu:470-491): ternary s from a fresh entropy-seeded
+  // ChaCha20 stream
+  explicit PhantomSecretKey(const PhantomContext& ctx);
+  // reproducible key for tests only: every draw (s, errors, uniform halves) follows from `seed`
+  static PhantomSecretKey for_testing(const PhantomContext& ctx, uint64_t seed);
+  PhantomSecretKey(PhantomSecretKey&&) = default;
+  PhantomSecretKey& operator=(PhantomSecretKey&&) = default;
+
   // save / load (include/secretkey.h:405-440): sk_max_power (1), n, size_QP, then s in NTT
-  // form.  A loaded key samples its later randomness from `seed`.
+  // form.  A loaded key draws its later randomness from a fresh entropy-seeded stream.
   void save(const PhantomContext& ctx, std::ostream& os) const;
-  static PhantomSecretKey load(const PhantomContext& ctx, std::istream& is, uint64_t seed);
+  static PhantomSecretKey load(const PhantomContext& ctx, std::istream& is);
   // s in NTT form over the full Q u P chain, [size_QP][n]
   const uint64_t* secret_key_array() const { return s_.get(); }
   const std::vector<int8_t>& coefficients() const { return coeffs_; }
 
+  // gen_publickey (src/secretkey.cu:493-504): a symmetric encryption of zero at the key level
+  PhantomPublicKey gen_publickey(const PhantomContext& ctx) const;
   PhantomRelinKey gen_relinkey(const PhantomContext& ctx);
   PhantomGaloisKey create_galois_keys(const PhantomContext& ctx, const std::vector<uint32_t>& galois_elts);
+  // create_galois_keys(context) (src/secretkey.cu:534-570): the context's galois_elts, or when none
+  // were set, every rotation by +-2^i and the conjugation (PhantomGaloisTool::get_elts_all,
+  // include/galois.cuh:84-92)
+  PhantomGaloisKey create_galois_keys(const PhantomContext& ctx);
   // keys for hoisted rotations (the reference's PhantomGaloisKeyFused): the key for element k
   // switches from s to s(X^(k^-1)), so the automorphism can be applied after the inner product
   // of the shared modup digits (EvalFastRotationExt, src/evaluate.cu:3656-3748)
   PhantomGaloisKey create_galois_keys_fused(const PhantomContext& ctx, const std::vector<uint32_t>& galois_elts);
+  // EvalRotateKeyGen / EvalAtIndexKeyGen (include/secretkey.h:453-457, src/secretkey.cu:956-1022):
+  // fused keys for the slot rotations in `index_list` plus the conjugation key
+  PhantomGaloisKey EvalRotateKeyGen(const PhantomContext& ctx, const std::vector<int32_t>& index_list);
+  PhantomGaloisKey EvalAtIndexKeyGen(const PhantomContext& ctx, const std::vector<int32_t>& index_list) {
+    return EvalRotateKeyGen(ctx, index_list);
+  }
 
-  // symmetric encryption of an NTT-form plaintext at `chain_index` (src/secretkey.cu:576-644)
-  void encrypt_symmetric(const PhantomContext& ctx, const PhantomPlaintext& plain, PhantomCiphertext& out);
-  // decryption c0 + c1 s (+ c2 s^2) in NTT form (ckks_decrypt, src/secretkey.cu:646-682)
-  void decrypt(const PhantomContext& ctx, const PhantomCiphertext& ct, PhantomPlaintext& out);
+  // symmetric encryption of an NTT-form plaintext at its chain index (src/secretkey.cu:576-644)
+  void encrypt_symmetric(const PhantomContext& ctx, const PhantomPlaintext& plain, PhantomCiphertext& out) const;
+  PhantomCiphertext encrypt_symmetric(const PhantomContext& ctx, const PhantomPlaintext& plain) const {
+    PhantomCiphertext c;
+    encrypt_symmetric(ctx, plain, c);
+    return c;
+  }
+  // decryption c0 + c1 s (+ c2 s^2) in NTT form (ckks_decrypt, src/secretkey.cu:646-682, 806-830)
+  void decrypt(const PhantomContext& ctx, const PhantomCiphertext& ct, PhantomPlaintext& out) const;
+  PhantomPlaintext decrypt(const PhantomContext& ctx, const PhantomCiphertext& ct) const {
+    PhantomPlaintext p;
+    decrypt(ctx, ct, p);
+    return p;
+  }
 
   // kswitch key for new_key (NTT form over QP) -> enc_key (default s) (generate_one_kswitch_key)
   PhantomKSwitchKey make_kswitch_key(const PhantomContext& ctx, const uint64_t* new_key,
                                      const uint64_t* enc_key = nullptr);
 
  private:
+  PhantomSecretKey(const PhantomContext& ctx, RandomStream rng, bool deterministic);
   PhantomSecretKey() = default;
-  void sample_uniform(const PhantomContext& ctx, uint64_t* dst, size_t L);
-  void sample_error(const PhantomContext& ctx, uint64_t* dst, size_t L);  // NTT form
-  uint64_t next();
-  uint64_t seed_state_ = 0;
-  uint64_t draws_ = 0;  // counter of device sampling draws
+  void init_powers(const PhantomContext& ctx);
+  // symmetric encryption of zero over the first L limbs of Q u P under enc_key (default s):
+  // (-(a s + e), a), NTT form
+  void encrypt_zero_raw(const PhantomContext& ctx, uint64_t* c0, uint64_t* c1, size_t L,
+                        const uint64_t* enc_key = nullptr) const;
+  mutable RandomStream rng_;
+  bool deterministic_ = false;
   std::vector<int8_t> coeffs_;
   DeviceBuffer<uint64_t> s_, s2_;
 };
 
+// the reference's name for the fused (hoisted-rotation) key set (include/secretkey.h:226-262)
+using PhantomGaloisKeyFused = PhantomGaloisKey;
+
 // galois element for a slot rotation by `step` (FindAutomorphismIndex2nComplex, src/util.cu:908-935)
 uint32_t galois_elt_from_step(int step, size_t n);
+
+// draws of a ChaCha20 stream into device polynomials over the first L limbs of Q u P
+// (the reference's sample_uniform_poly / sample_error_poly / sample_ternary_poly, src/prng.cu)
+void sample_uniform_poly(const PhantomContext& ctx, RandomStream& rng, uint64_t* dst, size_t L);
+// centered-binomial error, returned in NTT form
+void sample_error_poly_ntt(const PhantomContext& ctx, RandomStream& rng, uint64_t* dst, size_t L);
+// ternary polynomial, returned in NTT form
+void sample_ternary_poly_ntt(const PhantomContext& ctx, RandomStream& rng, uint64_t* dst, size_t L);
 
 }  // namespace phantom

@@ -27,20 +27,27 @@ struct CiphertextHeader {
   double scale = 1.0;
   uint64_t correction_factor = 1, noise_scale_deg = 1;
   bool is_ntt_form = true, is_asymmetric = false;
-  uint64_t words() const { return size * coeff_modulus_size * poly_modulus_degree; }
+  // size * coeff_modulus_size * poly_modulus_degree; throws std::runtime_error on overflow
+  uint64_t words() const;
 };
 constexpr size_t kCiphertextHeaderBytes = 4 * 8 + 8 + 8 + 8 + 1 + 1;  // 58
 
 struct PlaintextHeader {
   uint64_t chain_index = 0, poly_modulus_degree = 0, coeff_modulus_size = 0;
   double scale = 1.0;
-  uint64_t words() const { return coeff_modulus_size * poly_modulus_degree; }
+  uint64_t words() const;
 };
 constexpr size_t kPlaintextHeaderBytes = 3 * 8 + 8;  // 32
 
+// a * b * c, std::runtime_error if the product does not fit 64 bits
+uint64_t checked_words(uint64_t a, uint64_t b, uint64_t c);
+
 void write_ciphertext(std::ostream& os, const CiphertextHeader& h, const uint64_t* data);
-// throws std::runtime_error on a short or inconsistent stream
+// throws std::runtime_error on a short or inconsistent stream.  The payload is read in bounded
+// chunks, so a header that claims more words than the stream holds fails after reading what is
+// there instead of allocating what it claims.
 void read_ciphertext(std::istream& is, CiphertextHeader& h, std::vector<uint64_t>& data);
+void read_ciphertext_header(std::istream& is, CiphertextHeader& h);
 void write_plaintext(std::ostream& os, const PlaintextHeader& h, const uint64_t* data);
 void read_plaintext(std::istream& is, PlaintextHeader& h, std::vector<uint64_t>& data);
 void write_secret_key(std::ostream& os, uint64_t max_power, uint64_t n, uint64_t limbs, const uint64_t* data);

@@ -46,6 +46,8 @@ _SIGS = {
     "phantom_apply_galois_ntt": (ctypes.c_int, [vp, ctypes.c_uint32, vp, vp, sz, vp]),
     "phantom_poly_op": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, sz, sz, vp]),
     "phantom_switch_modulus_raise": (ctypes.c_int, [vp, vp, vp, sz, vp]),
+    "phantom_chacha20_block": (ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
+    "phantom_sample_poly": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_uint64, vp, sz, vp]),
 }
 
 _lib = None

@@ -226,3 +226,29 @@ def test_poly_ops(small, rng, op):
     else:
         O.lib().or_poly_negate(O.P(a), O.P(want), small.n, L, O.P(m))
     assert np.array_equal(to_host(do), want)
+
+
+# ---- samplers (src/prng.cu sample_*_poly) against the numpy ChaCha20 restatement -----------
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_device_samplers_match_chacha20(kind):
+    import chacha_np as C
+    n = 4096
+    mods = PA.coeff_modulus_create(n, [60, 50, 40, 60])
+    ctx = PA.Context(n, mods, 1)
+    key = [0x01234567, 0x89ABCDEF, 7, 11, 13, 17, 19, 0xFFFFFFF1]
+    nonce = (5 << 40) | 3
+    L = 3
+    out = to_dev(np.zeros(L * n, dtype=np.uint64))
+    k = (ctypes.c_uint32 * 8)(*key)
+    PA.check(PA.load().phantom_sample_poly(ctx.handle, kind, k, nonce, ptr(out), L, stream()))
+    got = to_host(out)
+    want = [C.sample_uniform, C.sample_cbd, C.sample_ternary][kind](key, nonce, mods[:L], n)
+    assert np.array_equal(got, want)
+    if kind == 0:  # residues, and not a constant: every limb covers most of its range
+        for l, q in enumerate(mods[:L]):
+            assert got[l * n:(l + 1) * n].max() < q and got[l * n:(l + 1) * n].max() > q // 2
+    else:
+        small = np.where(got[:n] > mods[0] // 2, got[:n].astype(np.float64) - mods[0], got[:n].astype(np.float64))
+        assert np.abs(small).max() <= (21 if kind == 1 else 1)
+    ctx.close()
