@@ -8,8 +8,10 @@ already resident in HBM.  Each step uses the next buffer of a ring whose total s
 value = algorithmic bytes (16 B per coefficient per transform, the convention of the
 reference's benchmark/ntt_bench.cu:96-97) of all steps on all ranks / max-over-ranks time.
 
-Multi-GPU: one process per GPU; each rank transforms its own independent batches (weak
-scaling, no data-path collective: ciphertext limbs are independent).
+Multi-GPU: one process per GPU (`--gpus N` without a launcher spawns the N ranks itself); each
+rank transforms its own independent batches (weak scaling, no data-path collective: ciphertext
+limbs are independent).  The C5 leg scatters one fixed batch of bootstraps over the
+ranks and gathers the results (strong scaling of that batch, RCCL over xGMI).
 
 roofline: the forward transform (column pass + row pass kernels) timed with HIP events on
 the stream the kernels run on; achieved = 46,137,344 B / average forward duration.
@@ -172,31 +174,81 @@ def job_throughput(units_per_rank, world, max_seconds):
     return units_per_rank * world / max_seconds
 
 
-def c5_leg(dist, torch, world, rank, local_rank, batch=16, lanes=4, timeout=600):
-    """Config C5: a batch of independent bootstraps sharded over the ranks, one
-    process per GPU, replicas only (no collective on the data path: every rank holds its own
-    context and keys and bootstraps its own ciphertexts).  Each rank runs `batch` bootstraps in
-    the example binary on its GPU, `lanes` side by side (FHECKKSRNS::EvalBootstrapBatch);
-    throughput = all bootstraps / max-over-ranks wall time of the timed batches."""
-    import subprocess
-    exe = os.path.join(ROOT, "phantom-fhe-boot_amd", "bin", "bootstrapping_example")
-    env = dict(os.environ, HIP_VISIBLE_DEVICES=str(local_rank))
-    out = subprocess.run([exe, "batch", "16", str(batch), str(lanes)], capture_output=True, text=True,
-                         timeout=timeout, env=env)
-    rows = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{") and '"sample"' not in l]
-    boot = [r for r in rows if r.get("stage") == "batch"]
-    ok = out.returncode == 0 and bool(boot)
-    total_ms = boot[0]["ms_total"] if ok else float("inf")
-    max_ms = max_over_ranks(dist, [total_ms], "cuda")[0]
-    if not all_ranks_ok(dist, ok, "cuda"):
-        return {"error": (out.stderr or out.stdout)[-300:]}
-    return {
-        "workload": "C5: independent bootstraps (C4 parameters) sharded over ranks, replicas only",
-        "bootstraps_per_rank": batch, "lanes_per_rank": lanes, "ranks": world,
-        "min_avg_bits": boot[0]["min_avg_bits"],
-        "bootstraps_per_s": round(job_throughput(batch, world, max_ms / 1e3), 3),
-        "max_rank_ms": round(max_ms, 2), "scaling": "weak",
-    }
+def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, verify=None):
+    """Config C5: `total` independent C4 bootstraps sharded over the ranks, one
+    process per GPU.  Every rank regenerates the same keys from a 32-byte seed rank 0 broadcasts
+    (no key traffic).  Rank 0 encrypts the batch — 2^15 reals in [1, 5] per ciphertext at chain
+    index `chain` (the level the example's 25 EvalMultConst drains leave, bootstrapping_example.cu:
+    150-153) — and the timed region is first scatter -> bootstraps (EvalBootstrapBatch, `lanes`
+    side by side per GPU) -> last gather of the serialized results (RCCL over xGMI for N > 1).
+    Afterwards rank 0 decrypts every gathered result (or the first `verify`) and reports the worst
+    average bit precision (compute_bit_precision, bootstrapping_example.cu:17-41).
+    Throughput = total / max-over-ranks time."""
+    import phantom_amd as PA
+    import shard
+    if total % world:
+        raise ValueError(f"C5 batch {total} does not divide over {world} ranks")
+    per = total // world
+    dev = torch.device("cuda", local_rank)
+    seed = shard.broadcast_seed(dist, dev)
+    t_setup = time.perf_counter()
+    sess = PA.BootSession(seed)
+    setup_s = time.perf_counter() - t_setup
+    align = 256
+    in_bytes = sess.input_bytes(chain)
+    out_bytes = sess.output_bytes()
+    sin = (in_bytes + align - 1) // align * align
+    sout = (out_bytes + align - 1) // align * align
+    rng = np.random.default_rng(0xC5)
+    values = rng.uniform(1.0, 5.0, size=(total if rank == 0 else 0, sess.slots))
+    full = None
+    if rank == 0:
+        full = torch.empty((total, sin), dtype=torch.uint8, device=dev)
+        sess.encrypt(values, chain, full.data_ptr(), sin)
+    # warm-up on every rank (first-use allocations and code loading), untimed
+    warm_n = min(lanes, per)
+    warm_in = torch.empty((warm_n, sin), dtype=torch.uint8, device=dev)
+    sess.encrypt(rng.uniform(1.0, 5.0, size=(warm_n, sess.slots)), chain, warm_in.data_ptr(), sin)
+    warm_out = torch.empty((warm_n, sout), dtype=torch.uint8, device=dev)
+    sess.run(warm_in.data_ptr(), sin, warm_n, warm_out.data_ptr(), sout, lanes)
+    del warm_in, warm_out
+    local_out = torch.empty((per, sout), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    local_in = shard.scatter_rows(dist, full, per, sin, dev)
+    torch.cuda.synchronize()
+    sess.run(local_in.data_ptr(), sin, per, local_out.data_ptr(), sout, lanes)
+    torch.cuda.synchronize()
+    gathered = shard.gather_rows(dist, local_out, dev)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    max_s = max_over_ranks(dist, [elapsed], "cuda")[0]
+    res = None
+    if rank == 0:
+        nver = total if verify is None else min(verify, total)
+        bits = []
+        for i in range(nver):
+            got = sess.decrypt(gathered[i].data_ptr(), sout)
+            bits.append(PA.bit_precision(values[i], got))
+        res = {
+            "workload": f"C5: {total} independent C4 bootstraps (input chain index {chain}) sharded over {world} rank(s), "
+                        "scatter -> EvalBootstrapBatch -> gather of serialized ciphertexts",
+            "bootstraps": total, "bootstraps_per_rank": per, "lanes_per_rank": lanes, "ranks": world,
+            "bootstraps_per_s": round(total / max_s, 3), "max_rank_s": round(max_s, 3),
+            "scatter_gather_bytes": total * (sin + sout),
+            "verified": nver, "min_avg_bits": round(min(bits), 2), "mean_avg_bits": round(float(np.mean(bits)), 2),
+            "setup_s": round(setup_s, 2), "scaling": "strong",
+            "keys": "regenerated on every rank from a broadcast 32-byte seed",
+        }
+    del full, gathered, local_out
+    sess.close()
+    return res
 
 
 # HBM bytes per forward-NTT launch (column + row pass) from PMC counters: FETCH_SIZE and
@@ -223,7 +275,15 @@ def main():
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 (mult+relin+rescale) leg")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (bootstrap latency) leg")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (sharded bootstrap batch) leg")
+    ap.add_argument("--c5-batch", type=int, default=1024, help="C5: bootstraps in the whole batch")
+    ap.add_argument("--c5-lanes", type=int, default=4, help="C5: concurrent bootstraps per GPU")
+    ap.add_argument("--c5-verify", type=int, default=None, help="C5: decrypt-check only the first K results")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: become the launcher (one process per GPU), before anything touches a GPU
+        import shard
+        sys.exit(shard.spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -291,7 +351,8 @@ def main():
 
     c5 = None
     if not args.no_c5:
-        c5 = c5_leg(dist if world > 1 else None, torch, world, rank, local_rank)
+        c5 = c5_leg(dist if world > 1 else None, torch, world, rank, local_rank, total=args.c5_batch,
+                    lanes=args.c5_lanes, verify=args.c5_verify)
 
     # parity spot-check of the last buffer state is done by tests/; here just sanity
     value = job_throughput(2 * BYTES_PER_TRANSFORM * args.steps, world, elapsed) / 1e9

@@ -162,6 +162,38 @@ int phantom_poly_op(const phantom_context *ctx, int op, const uint64_t *a, const
 int phantom_switch_modulus_raise(const phantom_context *ctx, const uint64_t *in_q0, uint64_t *out,
                                  size_t coeff_modulus_size, hipStream_t stream);
 
+/* ---- bootstrapping sessions (bootstrapping/bootstrapping_example.cu:69-160; src/bootstrap.cu) ----
+ * A session is the SimpleBootstrapExample set-up as one object: N = 2^log_n, Q = {60, depth x 59},
+ * P = special x 60 (CoeffModulus::Create), scale 2^59, levelBudget {enc, dec}, num_slots slots
+ * (0 = N/2; a smaller power of two = sparse packing, SparseBootStrapping :200-309), numIterations
+ * and precision of EvalBootstrap (src/bootstrap.cu:843-900).  Keys are derived from the 32-byte
+ * secret `seed`: every rank of a multi-GPU job that passes the same seed regenerates the same keys,
+ * so no key crosses the interconnect.
+ * Ciphertexts cross this boundary serialized in PhantomCiphertext::save's byte format
+ * (include/ciphertext.h:184-225) and held in DEVICE memory, `stride` bytes apart: the form in which
+ * a batch is scattered to ranks and gathered back. */
+/* EvalMod's Chebyshev interpolant (host only): out[degree + 1] = coefficients c of
+ * (2 pi)^(-2^-r) cos(2 pi (K y - 1/4) / 2^r) on [-1, 1], r = double_angle_iterations, with
+ * p(y) = sum_k c_k T_k(y) (c_0 NOT halved; the reference's tables g_coefficientsUniform/Sparse,
+ * include/bootstrap.cuh:217-255, hold 2 c_0 first) */
+int phantom_eval_mod_coefficients(uint32_t K, uint32_t double_angle_iterations, int degree, double *out);
+typedef struct phantom_boot_session phantom_boot_session;
+int phantom_boot_session_create(int log_n, int depth, int special, const uint32_t *level_budget, uint32_t num_slots,
+                                uint32_t num_iterations, uint32_t precision, const uint8_t *seed,
+                                phantom_boot_session **out);
+int phantom_boot_session_destroy(phantom_boot_session *s);
+/* encrypt `count` vectors of num_slots reals (values[count][num_slots]) at chain_index with that
+ * level's FLEXIBLEAUTO scale; *ct_bytes = the size of one serialized ciphertext */
+int phantom_boot_encrypt(phantom_boot_session *s, const double *values, size_t count, size_t chain_index,
+                         uint8_t *dev_out, size_t stride, size_t *ct_bytes);
+/* size of one serialized bootstrap output */
+int phantom_boot_output_bytes(phantom_boot_session *s, size_t *bytes);
+/* EvalBootstrap of `count` serialized ciphertexts, `lanes` side by side (EvalBootstrapBatch) */
+int phantom_boot_run(phantom_boot_session *s, const uint8_t *dev_in, size_t in_stride, size_t count, uint8_t *dev_out,
+                     size_t out_stride, int lanes);
+/* decrypt + decode one serialized ciphertext: the real parts of its num_slots slots */
+int phantom_boot_decrypt(phantom_boot_session *s, const uint8_t *dev_in, size_t capacity, double *values_out);
+
 /* ---- random sampling (src/prng.cu; seeds: include/prng.cuh:13-24) ---------------------
  * Every draw of key generation and encryption is ChaCha20 keystream (RFC 8439 block function,
  * 64-bit block counter in state words 12-13, 64-bit nonce in words 14-15): draw `nonce` of the

@@ -1,0 +1,223 @@
+// capi_boot.cpp — C-ABI of the bootstrapping harness (declared in include/phantom_amd.h): the
+// SimpleBootstrapExample set-up of bootstrapping/bootstrapping_example.cu:69-160 as one session
+// object, and batches of bootstraps over serialized ciphertexts held in device memory — the form
+// in which a multi-GPU job scatters its inputs and gathers its results (bench.py, config C5).
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../host/bootstrap.h"
+#include "../host/capi_internal.h"
+#include "../host/ckks_eval.h"
+#include "../host/encoder.h"
+#include "../host/evaluate.h"
+#include "../host/keys.h"
+#include "../host/modulus.h"
+#include "../host/serialize.h"
+#include "phantom_amd.h"
+
+using phantom::capi::fail;
+using phantom::capi::from_hip;
+using namespace phantom;
+using phantom::arith::CoeffModulus;
+
+struct phantom_boot_session {
+  std::unique_ptr<PhantomContext> ctx;
+  std::unique_ptr<PhantomCKKSEncoder> enc;
+  std::unique_ptr<PhantomSecretKey> sk;
+  std::unique_ptr<FHECKKSRNS> boot;
+  std::vector<double> sf;
+  uint32_t slots = 0, iterations = 1, precision = 0;
+};
+
+namespace {
+
+// a ciphertext from its serialized bytes in device memory (the format of PhantomCiphertext::save,
+// include/ciphertext.h:184-225): the 58-byte header comes to the host, the words are copied device
+// to device (they start at byte 58, so the copy also aligns them)
+PhantomCiphertext load_device(const PhantomContext& ctx, const uint8_t* dev, size_t capacity) {
+  if (capacity < ser::kCiphertextHeaderBytes) throw std::invalid_argument("serialized ciphertext truncated");
+  hipStream_t s = ctx.stream();
+  char hb[ser::kCiphertextHeaderBytes];
+  PHX_CHECK(hipMemcpyAsync(hb, dev, sizeof(hb), hipMemcpyDeviceToHost, s));
+  PHX_CHECK(hipStreamSynchronize(s));
+  std::istringstream is(std::string(hb, sizeof(hb)));
+  ser::CiphertextHeader h;
+  ser::read_ciphertext_header(is, h);
+  check_ciphertext_header(ctx, h);
+  if (h.words() > (capacity - ser::kCiphertextHeaderBytes) / sizeof(uint64_t))
+    throw std::invalid_argument("serialized ciphertext truncated");
+  PhantomCiphertext ct;
+  ct.resize(ctx, h.chain_index, h.size, s, false);
+  PHX_CHECK(hipMemcpyAsync(ct.data(), dev + ser::kCiphertextHeaderBytes, h.words() * sizeof(uint64_t),
+                           hipMemcpyDeviceToDevice, s));
+  ct.set_scale(h.scale);
+  ct.set_correction_factor(h.correction_factor);
+  ct.SetNoiseScaleDeg(h.noise_scale_deg);
+  ct.set_ntt_form(h.is_ntt_form);
+  ct.set_asymmetric(h.is_asymmetric);
+  return ct;
+}
+
+size_t serialized_bytes(const PhantomCiphertext& ct) {
+  return ser::kCiphertextHeaderBytes + ct.size() * ct.coeff_modulus_size() * ct.poly_modulus_degree() * sizeof(uint64_t);
+}
+
+void save_device(const PhantomContext& ctx, const PhantomCiphertext& ct, uint8_t* dev, size_t capacity) {
+  const size_t need = serialized_bytes(ct);
+  if (capacity < need) throw std::invalid_argument("output slot too small for the serialized ciphertext");
+  ser::CiphertextHeader h;
+  h.chain_index = ct.chain_index();
+  h.size = ct.size();
+  h.poly_modulus_degree = ct.poly_modulus_degree();
+  h.coeff_modulus_size = ct.coeff_modulus_size();
+  h.scale = ct.scale();
+  h.correction_factor = ct.correction_factor();
+  h.noise_scale_deg = ct.GetNoiseScaleDeg();
+  h.is_ntt_form = ct.is_ntt_form();
+  h.is_asymmetric = ct.is_asymmetric();
+  std::ostringstream os;
+  ser::write_ciphertext_header(os, h);  // the words follow device to device
+  const std::string hb = os.str();
+  hipStream_t s = ctx.stream();
+  PHX_CHECK(hipMemcpyAsync(dev, hb.data(), hb.size(), hipMemcpyHostToDevice, s));
+  PHX_CHECK(hipMemcpyAsync(dev + ser::kCiphertextHeaderBytes, ct.data(), need - ser::kCiphertextHeaderBytes,
+                           hipMemcpyDeviceToDevice, s));
+  PHX_CHECK(hipStreamSynchronize(s));  // the header's host source is a temporary
+}
+
+phantom_boot_session& session(phantom_boot_session* s) {
+  if (!s || !s->ctx) throw std::invalid_argument("null bootstrap session");
+  return *s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int phantom_eval_mod_coefficients(uint32_t K, uint32_t double_angle_iterations, int degree, double* out) {
+  PHX_CAPI_GUARD({
+    if (!out || degree < 1 || degree > 1024 || K < 1) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "bad arguments");
+    const double args[2] = {static_cast<double>(K), static_cast<double>(double_angle_iterations)};
+    const std::vector<double> c = boot::chebyshev_coefficients(boot::scaled_cosine, args, degree);
+    std::memcpy(out, c.data(), c.size() * sizeof(double));
+    return PHANTOM_OK;
+  });
+}
+
+int phantom_boot_session_create(int log_n, int depth, int special, const uint32_t* level_budget, uint32_t num_slots,
+                                uint32_t num_iterations, uint32_t precision, const uint8_t* seed,
+                                phantom_boot_session** out) {
+  PHX_CAPI_GUARD({
+    if (!level_budget || !seed || !out) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (log_n < 10 || log_n > 17 || depth < 1 || special < 1) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "bad parameters");
+    auto b = std::make_unique<phantom_boot_session>();
+    const size_t N = size_t(1) << log_n;
+    // bootstrapping_example.cu:76-116: {60, depth x 59, special x 60}, scale 2^59
+    std::vector<int> bits(1, 60);
+    bits.insert(bits.end(), static_cast<size_t>(depth), 59);
+    bits.insert(bits.end(), static_cast<size_t>(special), 60);
+    EncryptionParameters parms(scheme_type::ckks);
+    parms.set_poly_modulus_degree(N);
+    parms.set_special_modulus_size(static_cast<size_t>(special));
+    parms.set_coeff_modulus(CoeffModulus::Create(N, bits));
+    const double scale = std::pow(2.0, 59);
+    b->ctx = std::make_unique<PhantomContext>(parms);
+    b->enc = std::make_unique<PhantomCKKSEncoder>(*b->ctx);
+    if (num_slots) b->enc->set_sparse_encode(2 * size_t(num_slots));
+    b->sk = std::make_unique<PhantomSecretKey>(PhantomSecretKey::from_seed(*b->ctx, seed));
+    PhantomCiphertext tmp;
+    tmp.PreComputeScale(*b->ctx, scale);
+    b->sf = tmp.getScalingFactorsReal();
+    b->slots = num_slots ? num_slots : static_cast<uint32_t>(N / 2);
+    b->iterations = num_iterations ? num_iterations : 1;
+    b->precision = precision;
+    b->boot = std::make_unique<FHECKKSRNS>(*b->enc);
+    b->boot->EvalBootstrapSetup(*b->ctx, {level_budget[0], level_budget[1]}, scale, b->sf, 0, b->slots);
+    b->boot->EvalMultKeyGen(*b->sk, *b->ctx);
+    b->boot->EvalBootstrapKeyGen(*b->sk, *b->ctx, b->slots);
+    PHX_CHECK(hipDeviceSynchronize());
+    *out = b.release();
+    return PHANTOM_OK;
+  });
+}
+
+int phantom_boot_session_destroy(phantom_boot_session* s) {
+  if (s) (void)hipDeviceSynchronize();
+  delete s;
+  return PHANTOM_OK;
+}
+
+int phantom_boot_encrypt(phantom_boot_session* s, const double* values, size_t count, size_t chain_index,
+                         uint8_t* dev_out, size_t stride, size_t* ct_bytes) {
+  PHX_CAPI_GUARD({
+    auto& b = session(s);
+    if (!values || !dev_out || !ct_bytes) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (chain_index < 1 || chain_index > b.ctx->size_Q() - 1)
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "a bootstrap input needs at least two limbs");
+    const size_t need = ser::kCiphertextHeaderBytes +
+                        2 * b.ctx->get_context_data(chain_index).coeff_modulus_size() * b.ctx->poly_degree() * 8;
+    *ct_bytes = need;
+    if (stride < need) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "stride smaller than one serialized ciphertext");
+    for (size_t i = 0; i < count; ++i) {
+      std::vector<double> v(values + i * b.slots, values + (i + 1) * b.slots);
+      PhantomPlaintext pt;
+      // FLEXIBLEAUTO: a ciphertext at level l carries scale sf[l] (chain index = l + 1)
+      if (b.slots < b.ctx->poly_degree() / 2) b.enc->encode_sparse(*b.ctx, v, b.sf.at(chain_index - 1), pt, chain_index);
+      else b.enc->encode(*b.ctx, v, b.sf.at(chain_index - 1), pt, chain_index);
+      PhantomCiphertext ct = b.sk->encrypt_symmetric(*b.ctx, pt);
+      save_device(*b.ctx, ct, dev_out + i * stride, stride);
+    }
+    return PHANTOM_OK;
+  });
+}
+
+int phantom_boot_output_bytes(phantom_boot_session* s, size_t* bytes) {
+  PHX_CAPI_GUARD({
+    auto& b = session(s);
+    if (!bytes) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    *bytes = ser::kCiphertextHeaderBytes +
+             2 * b.ctx->get_context_data(b.boot->output_chain_index(b.slots, b.iterations)).coeff_modulus_size() * b.ctx->poly_degree() * 8;
+    return PHANTOM_OK;
+  });
+}
+
+int phantom_boot_run(phantom_boot_session* s, const uint8_t* dev_in, size_t in_stride, size_t count, uint8_t* dev_out,
+                     size_t out_stride, int lanes) {
+  PHX_CAPI_GUARD({
+    auto& b = session(s);
+    if ((!dev_in || !dev_out) && count) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    std::vector<PhantomCiphertext> in;
+    in.reserve(count);
+    for (size_t i = 0; i < count; ++i) in.push_back(load_device(*b.ctx, dev_in + i * in_stride, in_stride));
+    std::vector<PhantomCiphertext> out;
+    if (b.iterations > 1) {
+      for (auto& c : in) out.push_back(b.boot->EvalBootstrap(c, *b.ctx, b.slots, b.iterations, b.precision));
+    } else {
+      out = b.boot->EvalBootstrapBatch(in, *b.ctx, lanes, b.slots);
+    }
+    for (size_t i = 0; i < count; ++i) save_device(*b.ctx, out[i], dev_out + i * out_stride, out_stride);
+    return PHANTOM_OK;
+  });
+}
+
+int phantom_boot_decrypt(phantom_boot_session* s, const uint8_t* dev_in, size_t capacity, double* values_out) {
+  PHX_CAPI_GUARD({
+    auto& b = session(s);
+    if (!dev_in || !values_out) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    PhantomCiphertext ct = load_device(*b.ctx, dev_in, capacity);
+    // dropping limbs is exact (the plaintext is unchanged); decoding two limbs is cheaper
+    const size_t two = b.ctx->size_Q() - 1;
+    if (ct.chain_index() < two) mod_switch_to_inplace(*b.ctx, ct, two);
+    PhantomPlaintext pt = b.sk->decrypt(*b.ctx, ct);
+    std::vector<double> v;
+    b.enc->decode(*b.ctx, pt, v);
+    std::memcpy(values_out, v.data(), b.slots * sizeof(double));
+    return PHANTOM_OK;
+  });
+}
+
+}  // extern "C"

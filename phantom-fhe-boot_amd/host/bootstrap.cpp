@@ -16,10 +16,6 @@
 
 namespace phantom {
 
-static void hip_ok(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw hip_error(e, what);
-}
-
 // ======================================================================================
 // host-side math
 // ======================================================================================
@@ -81,6 +77,28 @@ DiagMap compose(const DiagMap& A, const DiagMap& B, size_t n) {
       if (dst.empty()) dst.assign(n, {0.0, 0.0});
       for (size_t p = 0; p < n; ++p) dst[p] += alpha[p] * beta[(p + a) % n];
     }
+  return out;
+}
+
+DiagMap lift_blocks(const DiagMap& T, size_t n, size_t S, const cvec* out_mask, const cvec* in_mask) {
+  if (S % n) throw std::invalid_argument("slot count not a multiple of the block size");
+  DiagMap out;
+  for (const auto& [a, d] : T) {
+    for (size_t p = 0; p < S; ++p) {
+      const size_t r = p % n;
+      std::complex<double> v = d[r];
+      if (v == std::complex<double>(0.0, 0.0)) continue;
+      // the pair (p, p + a) of the n-dim map stays inside p's block: offset a or a - n
+      const long off = r + static_cast<size_t>(a) < n ? static_cast<long>(a) : static_cast<long>(a) - static_cast<long>(n);
+      const size_t key = static_cast<size_t>(((off % static_cast<long>(S)) + static_cast<long>(S)) % static_cast<long>(S));
+      const size_t q = (p + key) % S;
+      if (out_mask) v *= (*out_mask)[p % out_mask->size()];
+      if (in_mask) v *= (*in_mask)[q % in_mask->size()];
+      cvec& dst = out[static_cast<int>(key)];
+      if (dst.empty()) dst.assign(S, {0.0, 0.0});
+      dst[p] += v;
+    }
+  }
   return out;
 }
 
@@ -439,27 +457,47 @@ uint32_t FHECKKSRNS::GetBootstrapDepth(const std::vector<uint32_t>& levelBudget)
 }
 
 void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const std::vector<int>& sizes,
-                              double constant, size_t first_chain, std::vector<LTLevel>& out) const {
-  const size_t n = cc.poly_degree() / 2;
-  const int logslots = arith::log2_exact(n);
+                              double constant, size_t first_chain, uint32_t slots, uint32_t dim1,
+                              std::vector<LTLevel>& out) const {
+  const size_t n = cc.poly_degree() / 2;  // slots of the ring
+  const size_t ns = slots;                // slots of the (sub)problem: n = full packing
+  const int logslots = arith::log2_exact(ns);
   std::vector<int> order;
   for (int s = 1; s <= logslots; ++s) order.push_back(s);
   if (encode_dir) std::reverse(order.begin(), order.end());
+  // sparse packing (ns < n): the ns-slot maps act on every ns-block of the ring's slots.  The
+  // CoeffToSlot output w = c_lo + i c_hi (ns-periodic) is multiplied by 1 on even blocks and -i on
+  // odd ones, so w + conj(w) holds [c_lo | c_hi] in 2 ns-periodic real slots; SlotToCoeff reads
+  // them as [c_lo | i c_hi], and a final rotation by ns adds the two halves (EvalBootstrap).
+  boot::cvec out_mask, in_mask;
+  if (ns < n) {
+    out_mask.assign(2 * ns, {1.0, 0.0});
+    in_mask.assign(2 * ns, {1.0, 0.0});
+    for (size_t p = ns; p < 2 * ns; ++p) {
+      out_mask[p] = {0.0, -1.0};
+      in_mask[p] = {0.0, 1.0};
+    }
+  }
   out.clear();
   size_t idx = 0;
   for (size_t gi = 0; gi < sizes.size(); ++gi) {
     boot::DiagMap T;
-    T.emplace(0, boot::cvec(n, {1.0, 0.0}));
+    T.emplace(0, boot::cvec(ns, {1.0, 0.0}));
     int s_min = logslots;
     for (int t = 0; t < sizes[gi]; ++t) {
       const int s = order[idx++];
       s_min = std::min(s_min, s);
-      T = boot::compose(boot::stage(n, s, encode_dir), T, n);
+      T = boot::compose(boot::stage(ns, s, encode_dir), T, ns);
     }
     const bool scale_here = encode_dir ? gi == 0 : gi + 1 == sizes.size();
     if (scale_here)
       for (auto& kv : T)
         for (auto& x : kv.second) x *= constant;
+    if (ns < n) {
+      const bool last_enc = encode_dir && gi + 1 == sizes.size();
+      const bool first_dec = !encode_dir && gi == 0;
+      T = boot::lift_blocks(T, ns, n, last_enc ? &out_mask : nullptr, first_dec ? &in_mask : nullptr);
+    }
     LTLevel lv;
     lv.stride = 1 << (s_min - 1);
     int kmin = 0, kmax = 0;
@@ -473,7 +511,12 @@ void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const s
     lv.center = -kmin;
     lv.D = kmax - kmin + 1;
     lv.g = 1;
-    while (lv.g * lv.g < lv.D) lv.g *= 2;
+    if (dim1) {
+      if (dim1 & (dim1 - 1)) throw std::invalid_argument("dim1 must be a power of two");
+      lv.g = static_cast<int>(std::min<uint32_t>(dim1, static_cast<uint32_t>(phx::kLtMaxG)));
+    } else {
+      while (lv.g * lv.g < lv.D) lv.g *= 2;
+    }
     lv.b = (lv.D + lv.g - 1) / lv.g;
     lv.chain = first_chain + gi;
     const double scale = sf_.at(lv.chain - 1);
@@ -532,11 +575,15 @@ void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const s
 }
 
 void FHECKKSRNS::EvalBootstrapSetup(const PhantomContext& cc, const std::vector<uint32_t>& levelBudget, double scale,
-                                    const std::vector<double>& sf, uint32_t correctionFactor) {
+                                    const std::vector<double>& sf, uint32_t correctionFactor, uint32_t slots_in,
+                                    const std::vector<uint32_t>& dim1) {
   (void)scale;
   sf_ = sf;
   budget_ = levelBudget;
-  const size_t N = cc.poly_degree(), slots = N / 2;
+  const size_t N = cc.poly_degree();
+  const uint32_t slots = slots_in ? slots_in : static_cast<uint32_t>(N / 2);
+  if (slots > N / 2 || (slots & (slots - 1)) || slots < 2)
+    throw std::invalid_argument("the number of slots must be a power of two between 2 and N/2");
   const int logslots = arith::log2_exact(slots);
   if (correctionFactor == 0) {
     const double tmp = std::round(-0.265 * (2 * std::log2(static_cast<double>(N)) + std::log2(static_cast<double>(slots))) + 19.1);
@@ -558,34 +605,66 @@ void FHECKKSRNS::EvalBootstrapSetup(const PhantomContext& cc, const std::vector<
   const size_t depth_mod = static_cast<size_t>(cheb_depth(kChebDegree)) + R_UNIFORM;
   if (1 + depth_enc + depth_mod + depth_dec > cc.size_Q())
     throw std::invalid_argument("not enough levels in the modulus chain for bootstrapping");
+  // the sparse partial sum multiplies the coefficients it keeps by N / (2 slots)
+  const double gap = static_cast<double>(N / 2) / slots;
+  Precom pc;
+  pc.slots = slots;
   // CoeffToSlot: slots become (t_lo + i t_hi) / (2 q0 K) (the conjugate split doubles them)
-  build_levels(cc, true, enc_sizes, sf_.at(0) / (2.0 * q0 * K_UNIFORM), 1, enc_);
+  build_levels(cc, true, enc_sizes, sf_.at(0) / (2.0 * gap * q0 * K_UNIFORM), 1, slots, dim1.size() > 0 ? dim1[0] : 0,
+               pc.enc);
   // SlotToCoeff: from (t0_lo + i t0_hi) / q0 back to the message at the raise scale sf[0]
-  build_levels(cc, false, dec_sizes, q0 / sf_.at(0), 1 + depth_enc + depth_mod, dec_);
+  build_levels(cc, false, dec_sizes, q0 / sf_.at(0), 1 + depth_enc + depth_mod, slots, dim1.size() > 1 ? dim1[1] : 0,
+               pc.dec);
+  precom_[slots] = std::move(pc);
   const double args[2] = {static_cast<double>(K_UNIFORM), static_cast<double>(R_UNIFORM)};
   cheb_ = boot::chebyshev_coefficients(boot::scaled_cosine, args, kChebDegree);
 }
 
-std::vector<int> FHECKKSRNS::rotation_indices() const {
+const FHECKKSRNS::Precom& FHECKKSRNS::precom(uint32_t numSlots, const PhantomContext& cc) const {
+  const uint32_t slots = numSlots ? numSlots : static_cast<uint32_t>(cc.poly_degree() / 2);
+  auto it = precom_.find(slots);
+  if (it == precom_.end())
+    throw std::invalid_argument("Precomputations for " + std::to_string(slots) +
+                                " slots were not generated: call EvalBootstrapSetup and then EvalBootstrapKeyGen");
+  return it->second;
+}
+
+size_t FHECKKSRNS::output_chain_index(uint32_t numSlots, uint32_t numIterations) const {
+  const uint32_t slots = numSlots ? numSlots : static_cast<uint32_t>(encoder_.slot_count());
+  auto it = precom_.find(slots);
+  if (it == precom_.end() || it->second.dec.empty()) throw std::invalid_argument("bootstrap setup missing");
+  return it->second.dec.back().chain + 1 + (numIterations > 1 ? 1 : 0);
+}
+
+std::vector<int> FHECKKSRNS::rotation_indices(uint32_t numSlots) const {
   std::vector<int> r;
   const int n = static_cast<int>(encoder_.slot_count());
   auto add = [&](long x) {
     const int v = static_cast<int>(((x % n) + n) % n);
     if (v != 0 && std::find(r.begin(), r.end(), v) == r.end()) r.push_back(v);
   };
-  for (const auto* lvs : {&enc_, &dec_})
+  const uint32_t slots = numSlots ? numSlots : static_cast<uint32_t>(n);
+  auto it = precom_.find(slots);
+  if (it == precom_.end()) throw std::invalid_argument("bootstrap setup missing for this slot count");
+  for (const auto* lvs : {&it->second.enc, &it->second.dec})
     for (const LTLevel& lv : *lvs) {
       for (int j = 0; j < lv.g; ++j) add(static_cast<long>(j - lv.center) * lv.stride);
       for (int i = 1; i < lv.b; ++i) add(static_cast<long>(lv.g) * i * lv.stride);
     }
+  // sparse packing: the partial sums before CoeffToSlot and the block fold after SlotToCoeff
+  for (long j = 1; j * static_cast<long>(slots) < n; j <<= 1) add(j * static_cast<long>(slots));
   return r;
 }
 
-void FHECKKSRNS::EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext& cc) {
+void FHECKKSRNS::EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext& cc, uint32_t numSlots) {
   std::vector<uint32_t> elts;
-  for (int r : rotation_indices()) elts.push_back(FindAutomorphismIndex2nComplex(r, cc.poly_degree()));
+  for (int r : rotation_indices(numSlots)) elts.push_back(FindAutomorphismIndex2nComplex(r, cc.poly_degree()));
   elts.push_back(static_cast<uint32_t>(2 * cc.poly_degree() - 1));  // conjugation
-  galois_keys_ = sk.create_galois_keys_fused(cc, elts);
+  // keys of earlier setups (other slot counts) stay; only the missing elements are generated
+  std::vector<uint32_t> need;
+  for (uint32_t e : elts)
+    if (!galois_keys_.has(e)) need.push_back(e);
+  galois_keys_.merge(sk.create_galois_keys_fused(cc, need));
 }
 
 void FHECKKSRNS::EvalMultKeyGen(PhantomSecretKey& sk, const PhantomContext& cc) { mul_key_ = sk.gen_relinkey(cc); }
@@ -659,15 +738,19 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
   return KeySwitchDownRescale(cc, acc);
 }
 
-PhantomCiphertext FHECKKSRNS::EvalCoeffsToSlots(const PhantomCiphertext& ct, const PhantomContext& cc) const {
-  PhantomCiphertext r = apply_level(cc, ct, enc_.at(0));
-  for (size_t i = 1; i < enc_.size(); ++i) r = apply_level(cc, r, enc_[i]);
+PhantomCiphertext FHECKKSRNS::EvalCoeffsToSlots(const PhantomCiphertext& ct, const PhantomContext& cc,
+                                                uint32_t numSlots) const {
+  const Precom& pc = precom(numSlots, cc);
+  PhantomCiphertext r = apply_level(cc, ct, pc.enc.at(0));
+  for (size_t i = 1; i < pc.enc.size(); ++i) r = apply_level(cc, r, pc.enc[i]);
   return r;
 }
 
-PhantomCiphertext FHECKKSRNS::EvalSlotsToCoeffs(const PhantomCiphertext& ct, const PhantomContext& cc) const {
-  PhantomCiphertext r = apply_level(cc, ct, dec_.at(0));
-  for (size_t i = 1; i < dec_.size(); ++i) r = apply_level(cc, r, dec_[i]);
+PhantomCiphertext FHECKKSRNS::EvalSlotsToCoeffs(const PhantomCiphertext& ct, const PhantomContext& cc,
+                                                uint32_t numSlots) const {
+  const Precom& pc = precom(numSlots, cc);
+  PhantomCiphertext r = apply_level(cc, ct, pc.dec.at(0));
+  for (size_t i = 1; i < pc.dec.size(); ++i) r = apply_level(cc, r, pc.dec[i]);
   return r;
 }
 
@@ -737,11 +820,12 @@ static void trace(const PhantomContext& cc, const char* stage, const PhantomCiph
 }
 
 std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<PhantomCiphertext>& in,
-                                                              const PhantomContext& cc, int lanes) const {
+                                                              const PhantomContext& cc, int lanes,
+                                                              uint32_t numSlots) const {
   const int k = std::max(1, std::min({lanes, PhantomContext::kLanes, static_cast<int>(in.size())}));
   std::vector<PhantomCiphertext> out(in.size());
   if (k == 1 || in_parallel_section()) {
-    for (size_t i = 0; i < in.size(); ++i) out[i] = EvalBootstrap(in[i], cc);
+    for (size_t i = 0; i < in.size(); ++i) out[i] = EvalBootstrap(in[i], cc, numSlots);
     return out;
   }
   const hipStream_t s0 = cc.stream();
@@ -759,7 +843,7 @@ std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<
     workers.emplace_back([&, t] {
       try {
         LaneGuard lane(cc, t);
-        for (size_t i = t; i < in.size(); i += k) out[i] = EvalBootstrap(in[i], cc);
+        for (size_t i = t; i < in.size(); i += k) out[i] = EvalBootstrap(in[i], cc, numSlots);
       } catch (...) {
         err[t] = std::current_exception();
       }
@@ -782,40 +866,101 @@ std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<
   return out;
 }
 
-PhantomCiphertext FHECKKSRNS::EvalBootstrap(const PhantomCiphertext& in, const PhantomContext& cc) const {
-  if (enc_.empty()) throw std::invalid_argument("Precomputations were not generated: call EvalBootstrapSetup");
+PhantomCiphertext FHECKKSRNS::EvalBootstrap(const PhantomCiphertext& in, const PhantomContext& cc, uint32_t numSlots,
+                                            uint32_t numIterations, uint32_t precision) const {
+  const Precom& pc = precom(numSlots, cc);
+  if (numIterations <= 1) return bootstrap_once(in, cc, pc);
+  // iterative bootstrapping (bootstrap.cu:856-900): the first bootstrap's error, scaled up by
+  // 2^precision, is bootstrapped again and subtracted
+  if (precision < 1 || precision > 30) throw std::invalid_argument("iterative bootstrapping needs a precision in [1, 30]");
+  const uint64_t pow2 = uint64_t(1) << precision;
+  const size_t initSizeQ = in.coeff_modulus_size();
+  PhantomCiphertext ctScaledUp = in;
+  if (ctScaledUp.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, ctScaledUp, 1);
+  MultByIntegerInPlace(cc, ctScaledUp, pow2);
+  PhantomCiphertext ctInitialBootstrap = EvalBootstrap(in, cc, numSlots, numIterations - 1, precision);
+  // (the reference rescales a pending product here; this engine's bootstraps return degree 1)
+  if (ctInitialBootstrap.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, ctInitialBootstrap, 1);
+  MultByIntegerInPlace(cc, ctInitialBootstrap, pow2);
+  const size_t bootSizeQ = ctInitialBootstrap.coeff_modulus_size();
+  if (bootSizeQ <= initSizeQ) return in;  // nothing gained: return the input, as the reference does
+  // the bootstrapping error 2^p e at the input's level.  The reference drops limbs and subtracts
+  // (ModSwitchLevelInPlace + EvalSubAuto), leaving the two operands at different FLEXIBLEAUTO
+  // scales (sf[out] vs sf[in], 1.1e-4 apart at C4), which leaves 2^p m (sf_out/sf_in - 1) in the
+  // error and caps the result near 13 bits; here EvalSubAuto brings the bootstrapped ciphertext
+  // to the input's level and scale (integer mod-switch multiply + rescale) so 2^p m cancels.
+  PhantomCiphertext ctBootstrappingError = ctInitialBootstrap;
+  EvalSubAutoInplace(cc, ctBootstrappingError, ctScaledUp, sf_);
+  PhantomCiphertext ctBootstrappedError = bootstrap_once(ctBootstrappingError, cc, pc);
+  if (ctBootstrappedError.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, ctBootstrappedError, 1);
+  PhantomCiphertext finalCiphertext = std::move(ctInitialBootstrap);
+  EvalSubAutoInplace(cc, finalCiphertext, ctBootstrappedError, sf_);
+  // scale back down by 2^precision
+  EvalMultConstInplace(cc, finalCiphertext, 1.0 / static_cast<double>(pow2), sf_);
+  EvalModReduceInPlace(cc, finalCiphertext, 1);
+  return finalCiphertext;
+}
+
+PhantomCiphertext FHECKKSRNS::bootstrap_once(const PhantomCiphertext& in, const PhantomContext& cc,
+                                             const Precom& pc) const {
   const uint32_t N = static_cast<uint32_t>(cc.poly_degree()), M = 2 * N;
+  const uint32_t slots = pc.slots;
   trace(cc, "start", in);
   PhantomCiphertext raised = RaiseWithCorrection(in, cc);
   trace(cc, "raise", raised);
-  // CoeffToSlot, then split the real and imaginary parts with one conjugation
-  PhantomCiphertext enc = EvalCoeffsToSlots(raised, cc);
-  trace(cc, "cts", enc);
-  PhantomCiphertext conj = EvalConjFused(cc, enc, galois_keys_);
-  PhantomCiphertext enc_i = enc;
-  sub_inplace(cc, enc_i, conj);
-  add_inplace(cc, enc, conj);
-  MultByMonomialInPlace(cc, enc_i, 3 * M / 4);  // times -i
-  trace(cc, "conj-split", enc_i);
-  // approximate modular reduction of both halves, concurrently: the imaginary half runs on the
-  // context's second stream from a second host thread (both are chains of small, dependent
-  // launches that leave most of the GPU idle on their own)
-  // enc_i (allocated on the main stream) stays alive until the main stream has joined
-  PhantomCiphertext im;
-  run_parallel(cc, 2, [&](int t) {
-    if (t == 0) {
-      enc = eval_mod(enc, cc);
-    } else {
-      im = eval_mod(enc_i, cc);
-      MultByMonomialInPlace(cc, im, M / 4);  // times i
+  PhantomCiphertext dec;
+  if (slots == N / 2) {
+    // CoeffToSlot, then split the real and imaginary parts with one conjugation
+    PhantomCiphertext enc = EvalCoeffsToSlots(raised, cc, slots);
+    trace(cc, "cts", enc);
+    PhantomCiphertext conj = EvalConjFused(cc, enc, galois_keys_);
+    PhantomCiphertext enc_i = enc;
+    sub_inplace(cc, enc_i, conj);
+    add_inplace(cc, enc, conj);
+    MultByMonomialInPlace(cc, enc_i, 3 * M / 4);  // times -i
+    trace(cc, "conj-split", enc_i);
+    // approximate modular reduction of both halves, concurrently: the imaginary half runs on the
+    // context's second stream from a second host thread (both are chains of small, dependent
+    // launches that leave most of the GPU idle on their own)
+    // enc_i (allocated on the main stream) stays alive until the main stream has joined
+    PhantomCiphertext im;
+    run_parallel(cc, 2, [&](int t) {
+      if (t == 0) {
+        enc = eval_mod(enc, cc);
+      } else {
+        im = eval_mod(enc_i, cc);
+        MultByMonomialInPlace(cc, im, M / 4);  // times i
+      }
+    });
+    im.retag(cc.stream());
+    trace(cc, "evalmod", enc);
+    EvalAddAutoInplace(cc, enc, im, sf_);
+    // SlotToCoeff
+    dec = EvalSlotsToCoeffs(enc, cc, slots);
+  } else {
+    // sparse packing (bootstrap.cu:1044-1109).  PartialSum: the trace onto the subring of the
+    // slots keeps the coefficients at multiples of N / (2 slots) (times that factor, which the
+    // CoeffToSlot constants divide out)
+    for (uint32_t j = 1; j * slots < N / 2; j <<= 1) {
+      PhantomCiphertext t = EvalRotateFused(cc, raised, galois_keys_, static_cast<int>(j * slots));
+      add_inplace(cc, raised, t);
     }
-  });
-  im.retag(cc.stream());
-  trace(cc, "evalmod", enc);
-  EvalAddAutoInplace(cc, enc, im, sf_);
-  // SlotToCoeff and undo the correction scaling
-  PhantomCiphertext dec = EvalSlotsToCoeffs(enc, cc);
+    trace(cc, "partial-sum", raised);
+    // CoeffToSlot leaves w' = [c_lo | -i c_hi] (2 slots-periodic); w' + conj(w') = 2 [c_lo | c_hi]
+    PhantomCiphertext enc = EvalCoeffsToSlots(raised, cc, slots);
+    PhantomCiphertext conj = EvalConjFused(cc, enc, galois_keys_);
+    add_inplace(cc, enc, conj);
+    trace(cc, "cts", enc);
+    enc = eval_mod(enc, cc);
+    trace(cc, "evalmod", enc);
+    // SlotToCoeff maps block 0 and block 1 to their halves of the embedding; the rotation by
+    // `slots` adds them
+    dec = EvalSlotsToCoeffs(enc, cc, slots);
+    PhantomCiphertext r = EvalRotateFused(cc, dec, galois_keys_, static_cast<int>(slots));
+    add_inplace(cc, dec, r);
+  }
   trace(cc, "stc", dec);
+  // undo the correction scaling
   MultByIntegerInPlace(cc, dec, uint64_t(1) << correction_);
   return dec;
 }

@@ -36,6 +36,11 @@ using DiagMap = std::map<int, cvec>;
 DiagMap stage(size_t slots, int s, bool inverse);
 // A * B (B applied first)
 DiagMap compose(const DiagMap& A, const DiagMap& B, size_t slots);
+// a map T on n slots applied to every n-block of an S-slot vector independently (S a multiple of
+// n): each diagonal of T becomes the within-block offsets it really is, so the result is correct
+// on inputs that are not n-periodic.  out_mask (period 2n) scales output slot p, in_mask (period
+// 2n) input slot q; null = 1.
+DiagMap lift_blocks(const DiagMap& T, size_t n, size_t S, const cvec* out_mask, const cvec* in_mask);
 // apply a DiagMap to a vector (tests)
 cvec apply(const DiagMap& T, const cvec& v);
 // Chebyshev interpolation coefficients of f on [-1, 1] (p(y) = sum_k c_k T_k(y), c_0 not halved)
@@ -59,24 +64,43 @@ class FHECKKSRNS {
  public:
   explicit FHECKKSRNS(PhantomCKKSEncoder& encoder);
 
-  // EvalBootstrapSetup (bootstrap.cu:15-181): linear-transform plaintexts and EvalMod constants.
-  // `sf` are the FLEXIBLEAUTO scaling factors (precompute_scaling_factors).
+  // EvalBootstrapSetup (bootstrap.cu:15-181, include/bootstrap.cuh:98-101): linear-transform
+  // plaintexts and EvalMod constants for `slots` slots (0: N/2, full packing; a power of two below
+  // N/2: sparse packing).  `sf` are the FLEXIBLEAUTO scaling factors (PreComputeScale).  dim1:
+  // baby-step sizes {CoeffToSlot, SlotToCoeff} of the baby-step giant-step evaluation (0: chosen
+  // per level).  Setups for several slot counts coexist (the reference's m_bootPrecomMap).
   void EvalBootstrapSetup(const PhantomContext& cc, const std::vector<uint32_t>& levelBudget, double scale,
-                          const std::vector<double>& sf, uint32_t correctionFactor = 0);
+                          const std::vector<double>& sf, uint32_t correctionFactor = 0, uint32_t slots = 0,
+                          const std::vector<uint32_t>& dim1 = {0, 0});
+  // the reference's argument list (scalingFactorsRealBig is accepted for drop-in calls; this engine
+  // derives everything it needs from scalingFactorsReal)
+  void EvalBootstrapSetup(const PhantomContext& cc, const std::vector<uint32_t>& levelBudget, double scale,
+                          const std::vector<double>& sf, const std::vector<double>& sf_big,
+                          const std::vector<uint32_t>& dim1 = {0, 0}, uint32_t slots = 0,
+                          uint32_t correctionFactor = 0, bool precompute = true) {
+    (void)sf_big;
+    (void)precompute;
+    EvalBootstrapSetup(cc, levelBudget, scale, sf, correctionFactor, slots, dim1);
+  }
   // EvalBootstrapKeyGen / EvalMultKeyGen (bootstrap.cu:566-841): fused rotation keys for the
-  // baby/giant steps and conjugation, and the relinearization key.
-  void EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext& cc);
+  // baby/giant steps, the sparse partial sums and conjugation, and the relinearization key.
+  void EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext& cc, uint32_t numSlots = 0);
   void EvalMultKeyGen(PhantomSecretKey& sk, const PhantomContext& cc);
-  // EvalBootstrap (bootstrap.cu:843-1129); the input needs at least two limbs
-  PhantomCiphertext EvalBootstrap(const PhantomCiphertext& ct, const PhantomContext& cc) const;
+  // EvalBootstrap (bootstrap.cu:843-1129); the input needs at least two limbs.  numSlots: the
+  // setup to use (0: N/2).  numIterations > 1: iterative bootstrapping (bootstrap.cu:856-900):
+  // bootstrap, scale the residual error up by 2^precision, bootstrap it and subtract.
+  PhantomCiphertext EvalBootstrap(const PhantomCiphertext& ct, const PhantomContext& cc, uint32_t numSlots = 0,
+                                  uint32_t numIterations = 1, uint32_t precision = 0) const;
   // a batch of independent bootstraps, `lanes` at a time side by side (each on its own thread
   // and stream lane, PhantomContext::kLanes at most); the results are ordered on cc.stream()
   std::vector<PhantomCiphertext> EvalBootstrapBatch(const std::vector<PhantomCiphertext>& in,
-                                                    const PhantomContext& cc, int lanes) const;
+                                                    const PhantomContext& cc, int lanes, uint32_t numSlots = 0) const;
 
-  // stages, exposed for tests and the benchmark
-  PhantomCiphertext EvalCoeffsToSlots(const PhantomCiphertext& ct, const PhantomContext& cc) const;
-  PhantomCiphertext EvalSlotsToCoeffs(const PhantomCiphertext& ct, const PhantomContext& cc) const;
+  // stages, exposed for tests and the benchmark (full packing setup unless numSlots is given)
+  PhantomCiphertext EvalCoeffsToSlots(const PhantomCiphertext& ct, const PhantomContext& cc,
+                                      uint32_t numSlots = 0) const;
+  PhantomCiphertext EvalSlotsToCoeffs(const PhantomCiphertext& ct, const PhantomContext& cc,
+                                      uint32_t numSlots = 0) const;
   PhantomCiphertext EvalChebyshevSeries(const PhantomCiphertext& ct, const PhantomContext& cc,
                                         const std::vector<double>& coeffs) const;
   void ApplyDoubleAngleIterations(PhantomCiphertext& ct, const PhantomContext& cc, uint32_t numIter) const;
@@ -84,7 +108,10 @@ class FHECKKSRNS {
   PhantomCiphertext RaiseWithCorrection(const PhantomCiphertext& ct, const PhantomContext& cc) const;
 
   static uint32_t GetBootstrapDepth(const std::vector<uint32_t>& levelBudget);
-  std::vector<int> rotation_indices() const;
+  // rotations (slot offsets) whose keys a bootstrap with `numSlots` slots needs
+  std::vector<int> rotation_indices(uint32_t numSlots = 0) const;
+  // chain index of a bootstrap's output
+  size_t output_chain_index(uint32_t numSlots = 0, uint32_t numIterations = 1) const;
   uint32_t correction_factor() const { return correction_; }
   const std::vector<double>& eval_mod_coefficients() const { return cheb_; }
   const std::vector<double>& scaling_factors() const { return sf_; }
@@ -103,16 +130,23 @@ class FHECKKSRNS {
     DeviceBuffer<const uint64_t*> d_pts;                // [b][g] device pointer table (zero-padded)
     DeviceBuffer<uint64_t> zero;                        // the zero plaintext absent diagonals point at
   };
+  // the precomputation of one slot count (the reference's CKKSBootstrapPrecom)
+  struct Precom {
+    uint32_t slots = 0;
+    std::vector<LTLevel> enc, dec;
+  };
   void build_levels(const PhantomContext& cc, bool encode_dir, const std::vector<int>& group_sizes, double constant,
-                    size_t first_chain, std::vector<LTLevel>& out) const;
+                    size_t first_chain, uint32_t slots, uint32_t dim1, std::vector<LTLevel>& out) const;
+  const Precom& precom(uint32_t numSlots, const PhantomContext& cc) const;
   PhantomCiphertext apply_level(const PhantomContext& cc, const PhantomCiphertext& ct, const LTLevel& lv) const;
   PhantomCiphertext eval_mod(const PhantomCiphertext& ct, const PhantomContext& cc) const;
+  PhantomCiphertext bootstrap_once(const PhantomCiphertext& ct, const PhantomContext& cc, const Precom& pc) const;
 
   PhantomCKKSEncoder& encoder_;
   std::vector<double> sf_;
   std::vector<uint32_t> budget_;
   uint32_t correction_ = 0;
-  std::vector<LTLevel> enc_, dec_;
+  std::map<uint32_t, Precom> precom_;
   std::vector<double> cheb_;
   int giant_streams_ = 3;  // PHX_BOOT_GIANT_STREAMS: concurrent giant-step chains per level (profiles/r01/giant_streams_sweep.txt)
   mutable LeafTableCache leaf_tables_;

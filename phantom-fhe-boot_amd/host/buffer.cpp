@@ -2,6 +2,14 @@
 
 namespace phantom {
 
+bool debug_sync_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PHX_DEBUG_SYNC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 DevicePool& DevicePool::instance() {
   static DevicePool* p = new DevicePool();  // never destroyed: blocks outlive static teardown
   return *p;
@@ -29,11 +37,33 @@ hipEvent_t DevicePool::take_event() {
   return e;
 }
 
+// hipEventQuery of a pending event returns hipErrorNotReady, and HIP keeps every API return value
+// as the thread's last error: left there, it would be reported by the next launch's
+// hipGetLastError() as that launch's failure.  Clear it.
+static bool event_done(hipEvent_t e) {
+  const hipError_t r = hipEventQuery(e);
+  if (r == hipSuccess) return true;
+  if (r == hipErrorNotReady) (void)hipGetLastError();
+  return false;
+}
+
+void DevicePool::forget_stream(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto& kv : free_)
+    for (Block& b : kv.second)
+      if (b.stream == s) {
+        // the caller has synchronised s: its blocks are free for any stream from now on
+        if (b.ev) spare_.push_back(b.ev);
+        b.ev = nullptr;
+        b.stream = nullptr;
+      }
+}
+
 void DevicePool::release_cached_locked() {
   for (auto& kv : free_) {
     std::vector<Block> keep;
     for (Block& b : kv.second) {
-      if (b.ev && hipEventQuery(b.ev) != hipSuccess) {
+      if (b.ev && !event_done(b.ev)) {
         keep.push_back(b);
         continue;
       }
@@ -55,7 +85,7 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
       auto& v = it->second;
       for (size_t i = v.size(); i-- > 0;) {
         Block& b = v[i];
-        const bool ready = !b.ev || b.stream == s || hipEventQuery(b.ev) == hipSuccess;
+        const bool ready = !b.ev || b.stream == s || event_done(b.ev);
         if (!ready) continue;
         void* p = b.p;
         if (b.ev) spare_.push_back(b.ev);
@@ -91,6 +121,12 @@ void DevicePool::free(void* p, size_t bytes, hipStream_t s, bool completed) {
   }
   live_.erase(it);
   Block b{p, s, nullptr};
+#ifdef PHX_GUARD
+  // debug builds: poison the block in the freeing stream's order, so a stream that still reads it
+  // after this free (a buffer freed on a stream other than its last user's) reads garbage and the
+  // results show it
+  if (!completed) PHX_CHECK(hipMemsetAsync(p, 0xFF, size_class(bytes), s));
+#endif
   if (!completed) {
     b.ev = take_event();
     PHX_CHECK(hipEventRecord(b.ev, s));

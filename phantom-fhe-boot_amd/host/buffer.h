@@ -31,6 +31,10 @@ class DevicePool {
   void free(void* p, size_t bytes, hipStream_t s, bool completed = false);
   // size class of a request (blocks are reused only within a class)
   static size_t size_class(size_t bytes);
+  // stream `s` is about to be destroyed and has been synchronised: its cached blocks become
+  // plain free blocks (a later stream may reuse the handle value; an event recorded on a
+  // destroyed stream must not be queried)
+  void forget_stream(hipStream_t s);
 
  private:
   struct Block {

@@ -49,16 +49,19 @@ void PhantomCiphertext::save(std::ostream& os) const {
   ser::write_ciphertext(os, h, v.data());
 }
 
-void PhantomCiphertext::load(const PhantomContext& ctx, std::istream& is) {
-  ser::CiphertextHeader h;
-  std::vector<uint64_t> v;
-  ser::read_ciphertext(is, h, v);
-  // everything a kernel will index by must match the context before anything is allocated
+void check_ciphertext_header(const PhantomContext& ctx, const ser::CiphertextHeader& h) {
   if (h.poly_modulus_degree != ctx.poly_degree()) throw std::invalid_argument("ciphertext degree mismatch");
   if (h.chain_index >= ctx.total_parm_size()) throw std::invalid_argument("ciphertext chain index out of range");
   if (h.size < 2 || h.size > 3) throw std::invalid_argument("ciphertext size must be 2 or 3");
   if (h.coeff_modulus_size != ctx.get_context_data(h.chain_index).coeff_modulus_size())
     throw std::invalid_argument("ciphertext limb count does not match its chain index");
+}
+
+void PhantomCiphertext::load(const PhantomContext& ctx, std::istream& is) {
+  ser::CiphertextHeader h;
+  std::vector<uint64_t> v;
+  ser::read_ciphertext(is, h, v);
+  check_ciphertext_header(ctx, h);
   resize(h.size, h.coeff_modulus_size, h.poly_modulus_degree, ctx.stream(), false);
   if (!v.empty()) {
     PHX_CHECK(hipMemcpyAsync(data_.get(), v.data(), v.size() * sizeof(uint64_t), hipMemcpyHostToDevice, ctx.stream()));

@@ -99,6 +99,13 @@ class PhantomCiphertext {
   std::vector<double> sf_, sf_big_;
 };
 
+namespace ser {
+struct CiphertextHeader;
+}
+// throws std::invalid_argument unless a serialized header fits the context: degree, chain index,
+// size 2 or 3 and the chain's limb count (everything a kernel will index by)
+void check_ciphertext_header(const PhantomContext& ctx, const ser::CiphertextHeader& h);
+
 class PhantomPlaintext {
  public:
   uint64_t* data() const { return data_.get(); }

@@ -15,10 +15,6 @@ namespace phantom {
 
 using namespace arith;
 
-static void hip_ok(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw hip_error(e, what);
-}
-
 // exact residue of round(x) mod q for any finite double
 static uint64_t residue_of_double(double x, uint64_t q) {
   const double r = std::nearbyint(x);

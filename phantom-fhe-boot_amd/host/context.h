@@ -70,6 +70,7 @@ struct OwnedStream {
   ~OwnedStream() {
     if (owned && s) {
       (void)hipStreamSynchronize(s);
+      DevicePool::instance().forget_stream(s);
       (void)hipStreamDestroy(s);
     }
   }

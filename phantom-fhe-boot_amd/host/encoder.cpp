@@ -271,4 +271,19 @@ void PhantomCKKSEncoder::decode(const PhantomContext& ctx, const PhantomPlaintex
   for (size_t i = 0; i < z.size(); ++i) out[i] = z[i].real();
 }
 
+void PhantomCKKSEncoder::encode_sparse(const PhantomContext& ctx, const std::vector<std::complex<double>>& values,
+                                       double scale, PhantomPlaintext& out, size_t chain_index) const {
+  const size_t slots = n_ / 2, ns = sparse_slots_ ? sparse_slots_ : slots;
+  if (ns > slots || (ns & (ns - 1)) || values.size() > ns)
+    throw std::invalid_argument("sparse slot count must be a power of two <= N/2 holding every value");
+  std::vector<std::complex<double>> v(slots, {0.0, 0.0});
+  for (size_t j = 0; j < slots; ++j) v[j] = (j % ns) < values.size() ? values[j % ns] : std::complex<double>(0.0, 0.0);
+  encode(ctx, v, scale, out, chain_index);
+}
+
+void PhantomCKKSEncoder::encode_sparse(const PhantomContext& ctx, const std::vector<double>& values, double scale,
+                                       PhantomPlaintext& out, size_t chain_index) const {
+  encode_sparse(ctx, std::vector<std::complex<double>>(values.begin(), values.end()), scale, out, chain_index);
+}
+
 }  // namespace phantom

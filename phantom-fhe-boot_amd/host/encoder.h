@@ -30,6 +30,17 @@ class PhantomCKKSEncoder {
               PhantomPlaintext& out, size_t chain_index = 1) const;
   void encode(const PhantomContext& ctx, const std::vector<double>& values, double scale, PhantomPlaintext& out,
               size_t chain_index = 1) const;
+  // sparse packing (the reference's set_sparse_encode / encode_sparse, include/ckks.h:82-117,
+  // bootstrapping_example.cu:262-263): `values` (at most sparse_slots of them, zero-padded) fill
+  // every block of sparse_slots slots, i.e. the plaintext is m'(X^(N / (2 sparse_slots))), the form
+  // a sparse bootstrap expects.  set_sparse_encode takes the subring dimension 2 * sparse_slots.
+  void set_sparse_encode(size_t subring_degree) { sparse_slots_ = subring_degree / 2; }
+  void encode_sparse(const PhantomContext& ctx, const std::vector<double>& values, double scale, PhantomPlaintext& out,
+                     size_t chain_index = 1) const;
+  void encode_sparse(const PhantomContext& ctx, const std::vector<std::complex<double>>& values, double scale,
+                     PhantomPlaintext& out, size_t chain_index = 1) const;
+  size_t sparse_slots() const { return sparse_slots_; }
+
   // encode_ext (the hoisted linear transforms' plaintexts): the Ql basis of `chain_index`
   // followed by the special primes P, NTT form ([size_Ql + size_P][n]).
   void encode_ext(const PhantomContext& ctx, const std::vector<std::complex<double>>& values, double scale,
@@ -70,6 +81,7 @@ class PhantomCKKSEncoder {
 
   size_t n_ = 0;
   int logn_ = 0;
+  size_t sparse_slots_ = 0;
   std::vector<std::complex<double>> zeta_pows_;  // zeta^j, j < 2n
   std::vector<uint32_t> slot_index_;             // (5^j mod 2n - 1) / 2 for j < n/2
   std::vector<uint32_t> brev_;

@@ -10,10 +10,6 @@
 
 namespace phantom {
 
-static void hip_ok(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw hip_error(e, what);
-}
-
 void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, const uint64_t* c2,
                    const uint64_t* const* evk, hipStream_t s) {
   if (ctx.size_P() == 0) throw std::invalid_argument("key switching requires special primes");

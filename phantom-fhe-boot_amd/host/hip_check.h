@@ -16,6 +16,18 @@ class hip_error : public std::runtime_error {
   hipError_t code;
 };
 
+// Status of a kernel launch (or any HIP call) -> exception.  PHX_DEBUG_SYNC=1 also synchronises
+// the device after every checked call, so an asynchronous failure is reported by the launch that
+// caused it (debugging aid; off by default).
+bool debug_sync_enabled();
+inline void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw hip_error(e, what);
+  if (debug_sync_enabled()) {
+    const hipError_t s = hipDeviceSynchronize();
+    if (s != hipSuccess) throw hip_error(s, what);
+  }
+}
+
 }  // namespace phantom
 
 #define PHX_CHECK(call)                                         \

@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <stdexcept>
 
 #include "../csrc/ckks.h"
@@ -12,10 +13,6 @@
 #include "serialize.h"
 
 namespace phantom {
-
-static void hip_ok(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw hip_error(e, what);
-}
 
 void PhantomKSwitchKey::adopt(std::vector<DeviceBuffer<uint64_t>>&& digits, hipStream_t s) {
   digits_ = std::move(digits);
@@ -166,6 +163,12 @@ PhantomSecretKey::PhantomSecretKey(const PhantomContext& ctx) : PhantomSecretKey
 
 PhantomSecretKey PhantomSecretKey::for_testing(const PhantomContext& ctx, uint64_t seed) {
   return PhantomSecretKey(ctx, RandomStream::for_testing(seed), true);
+}
+
+PhantomSecretKey PhantomSecretKey::from_seed(const PhantomContext& ctx, const uint8_t seed[32]) {
+  phx::ChaChaKey k;
+  std::memcpy(k.k, seed, sizeof(k.k));
+  return PhantomSecretKey(ctx, RandomStream::from_key(k), true);
 }
 
 PhantomSecretKey::PhantomSecretKey(const PhantomContext& ctx, RandomStream rng, bool deterministic)

@@ -53,6 +53,11 @@ class PhantomGaloisKey {
   const PhantomKSwitchKey& get(uint32_t galois_elt) const;
   bool has(uint32_t galois_elt) const { return keys_.count(galois_elt) != 0; }
   void set(uint32_t galois_elt, PhantomKSwitchKey&& k) { keys_[galois_elt] = std::move(k); }
+  // move every key of `other` in (replacing keys of the same element)
+  void merge(PhantomGaloisKey&& other) {
+    for (auto& kv : other.keys_) keys_[kv.first] = std::move(kv.second);
+    other.keys_.clear();
+  }
   // PhantomGaloisKey::save / load (include/secretkey.h:195-220): the number of keys, then each
   // as a relin key.  The reference indexes keys by position in its galois_elts list; here the
   // element itself is the key, so the count is followed by the elements (uint32_t each, in
@@ -105,6 +110,9 @@ class PhantomSecretKey {
   explicit PhantomSecretKey(const PhantomContext& ctx);
   // reproducible key for tests only: every draw (s, errors, uniform halves) follows from `seed`
   static PhantomSecretKey for_testing(const PhantomContext& ctx, uint64_t seed);
+  // key and every later draw derived from a 256-bit secret seed: replicas of one key owner (the
+  // ranks of a multi-GPU job) regenerate identical keys from a shared seed instead of moving them
+  static PhantomSecretKey from_seed(const PhantomContext& ctx, const uint8_t seed[32]);
   PhantomSecretKey(PhantomSecretKey&&) = default;
   PhantomSecretKey& operator=(PhantomSecretKey&&) = default;
 

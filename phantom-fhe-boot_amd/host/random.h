@@ -27,6 +27,9 @@ class RandomStream {
   // a reproducible stream for tests: the key is derived from `seed` through ChaCha20 under a
   // fixed label, so it is not the seed itself but anyone who knows the seed knows the stream
   static RandomStream for_testing(uint64_t seed);
+  // a stream keyed by a caller-held 256-bit secret (e.g. one the key owner drew from the OS and
+  // shares with the replicas that must regenerate identical keys)
+  static RandomStream from_key(const phx::ChaChaKey& k) { return RandomStream(k); }
   // a child stream keyed by 32 bytes of this stream's output (itself one draw)
   RandomStream derive();
 

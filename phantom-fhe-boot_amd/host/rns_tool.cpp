@@ -137,10 +137,6 @@ RnsTool::RnsTool(size_t n, const std::vector<uint64_t>& qp, size_t size_P, size_
   }
 }
 
-static void hip_ok(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw hip_error(e, what);
-}
-
 void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables& ntt, hipStream_t s) const {
   const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_, alpha = size_P_;
   uint64_t* t_cks = ws_->get(s, Workspace::kModupInv, size_Ql * n_);

@@ -57,6 +57,11 @@ uint64_t CiphertextHeader::words() const { return checked_words(size, coeff_modu
 uint64_t PlaintextHeader::words() const { return checked_words(1, coeff_modulus_size, poly_modulus_degree); }
 
 void write_ciphertext(std::ostream& os, const CiphertextHeader& h, const uint64_t* data) {
+  write_ciphertext_header(os, h);
+  put_words(os, data, h.words());
+}
+
+void write_ciphertext_header(std::ostream& os, const CiphertextHeader& h) {
   put(os, h.chain_index);
   put(os, h.size);
   put(os, h.poly_modulus_degree);
@@ -66,7 +71,6 @@ void write_ciphertext(std::ostream& os, const CiphertextHeader& h, const uint64_
   put(os, h.noise_scale_deg);
   put(os, h.is_ntt_form);
   put(os, h.is_asymmetric);
-  put_words(os, data, h.words());
 }
 
 void read_ciphertext(std::istream& is, CiphertextHeader& h, std::vector<uint64_t>& data) {

@@ -43,6 +43,7 @@ constexpr size_t kPlaintextHeaderBytes = 3 * 8 + 8;  // 32
 uint64_t checked_words(uint64_t a, uint64_t b, uint64_t c);
 
 void write_ciphertext(std::ostream& os, const CiphertextHeader& h, const uint64_t* data);
+void write_ciphertext_header(std::ostream& os, const CiphertextHeader& h);
 // throws std::runtime_error on a short or inconsistent stream.  The payload is read in bounded
 // chunks, so a header that claims more words than the stream holds fails after reading what is
 // there instead of allocating what it claims.

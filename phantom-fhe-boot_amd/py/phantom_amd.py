@@ -48,6 +48,14 @@ _SIGS = {
     "phantom_switch_modulus_raise": (ctypes.c_int, [vp, vp, vp, sz, vp]),
     "phantom_chacha20_block": (ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
     "phantom_sample_poly": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_uint64, vp, sz, vp]),
+    "phantom_boot_session_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_uint32,
+                                                   ctypes.c_uint32, ctypes.c_uint32, vp, ctypes.POINTER(vp)]),
+    "phantom_boot_session_destroy": (ctypes.c_int, [vp]),
+    "phantom_eval_mod_coefficients": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp]),
+    "phantom_boot_encrypt": (ctypes.c_int, [vp, vp, sz, sz, vp, sz, ctypes.POINTER(sz)]),
+    "phantom_boot_output_bytes": (ctypes.c_int, [vp, ctypes.POINTER(sz)]),
+    "phantom_boot_run": (ctypes.c_int, [vp, vp, sz, sz, vp, sz, ctypes.c_int]),
+    "phantom_boot_decrypt": (ctypes.c_int, [vp, vp, sz, vp]),
 }
 
 _lib = None
@@ -161,3 +169,69 @@ class NttTables:
             self.close()
         except Exception:
             pass
+
+
+class BootSession:
+    """Owning handle of a phantom_boot_session (the SimpleBootstrapExample set-up; C4/C5)."""
+
+    def __init__(self, seed, log_n=16, depth=29, special=10, level_budget=(2, 2), num_slots=0, iterations=1,
+                 precision=0):
+        lib = load()
+        assert len(seed) == 32
+        self.seed = bytes(seed)
+        lb = (ctypes.c_uint32 * 2)(*level_budget)
+        h = vp()
+        check(lib.phantom_boot_session_create(log_n, depth, special, lb, num_slots, iterations, precision,
+                                              self.seed, ctypes.byref(h)))
+        self.handle = h
+        self.n = 1 << log_n
+        self.slots = num_slots or self.n // 2
+        self.depth = depth
+
+    def output_bytes(self):
+        b = sz(0)
+        check(load().phantom_boot_output_bytes(self.handle, ctypes.byref(b)))
+        return b.value
+
+    def input_bytes(self, chain_index):
+        return 58 + 2 * (self.depth + 1 - (chain_index - 1)) * self.n * 8
+
+    def encrypt(self, values, chain_index, dev_ptr, stride):
+        """values: float64 [count, slots]; writes serialized ciphertexts at dev_ptr + i * stride."""
+        import numpy as np
+        v = np.ascontiguousarray(values, dtype=np.float64)
+        b = sz(0)
+        check(load().phantom_boot_encrypt(self.handle, v.ctypes.data, v.shape[0], chain_index, dev_ptr, stride,
+                                          ctypes.byref(b)))
+        return b.value
+
+    def run(self, dev_in, in_stride, count, dev_out, out_stride, lanes=4):
+        check(load().phantom_boot_run(self.handle, dev_in, in_stride, count, dev_out, out_stride, lanes))
+
+    def decrypt(self, dev_ptr, capacity):
+        import numpy as np
+        out = np.zeros(self.slots, dtype=np.float64)
+        check(load().phantom_boot_decrypt(self.handle, dev_ptr, capacity, out.ctypes.data))
+        return out
+
+    def close(self):
+        if self.handle:
+            load().phantom_boot_session_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def bit_precision(ref, actual):
+    """compute_bit_precision of bootstrapping_example.cu:17-41: mean of -log2 relative error."""
+    import numpy as np
+    ref = np.asarray(ref, dtype=np.float64)
+    actual = np.asarray(actual, dtype=np.float64)
+    keep = np.abs(ref) >= 1e-20
+    rel = np.abs(ref[keep] - actual[keep]) / np.abs(ref[keep])
+    rel = np.maximum(rel, 1e-40)
+    return float(np.mean(-np.log2(rel))) if rel.size else 0.0

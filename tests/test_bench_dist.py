@@ -59,3 +59,19 @@ def test_single_process_helpers_without_a_group():
     assert bench.max_over_ranks(None, [3.0, 4.0], "cpu") == [3.0, 4.0]
     assert bench.all_ranks_ok(None, False, "cpu") is False
     assert bench.job_throughput(10, 1, 2.0) == 5.0
+
+
+def test_c5_spawn_scatter_gather_two_ranks_gloo():
+    """bench.py's C5 data path end to end on host buffers: shard.spawn_ranks starts 2 ranks with the
+    rendezvous environment (what `bench.py --gpus 2` does without a launcher), rank 0 scatters
+    serialized ciphertexts, each rank transforms its slice, rank 0 gathers and verifies order and
+    contents (tests/c5_gloo_worker.py)."""
+    import json
+    import subprocess
+    code = ("import sys; sys.path.insert(0, %r); import shard; "
+            "sys.exit(shard.spawn_ranks(2, [sys.executable, %r], timeout=240))"
+            % (os.path.join(ROOT, "phantom-fhe-boot_amd", "py"), os.path.join(ROOT, "tests", "c5_gloo_worker.py")))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rows = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert rows == [{"ok": True, "world": 2, "total": 12, "seed_bytes": 32}], (rows, out.stderr[-2000:])

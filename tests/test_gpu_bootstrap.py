@@ -38,8 +38,8 @@ def test_full_bootstrap_precision_and_levels():
     rc, lines, err = _run("boot", "16", "1", timeout=115)
     assert rc == 0, (lines, err)
     boot = [l for l in lines if l.get("stage") == "bootstrap"][0]
-    # the reference example reaches ~ the same regime: correction factor 7, inputs in [1, 5]
-    assert boot["avg_bits"] > 9.0, boot
+    # correction factor 7, inputs in [1, 5]: 10.0-10.08 measured on MI355X (profiles/r01/, r02/)
+    assert boot["avg_bits"] > 9.85, boot
     assert boot["levels_after"] >= 11, boot
 
 
@@ -50,4 +50,65 @@ def test_bootstrap_batch_on_stream_lanes():
     assert rc == 0, (lines, err)
     b = [l for l in lines if l.get("stage") == "batch"][0]
     assert b["bootstraps"] == 6 and b["lanes"] == 3, b
-    assert b["min_avg_bits"] > 9.0, b
+    assert b["min_avg_bits"] > 9.85, b
+
+
+# ---- bootstrapping sessions through the C-ABI (include/phantom_amd.h phantom_boot_*) ------------
+
+def _session_run(num_slots=0, iterations=1, precision=0, count=2, chain=26, lanes=2):
+    import numpy as np
+    import torch
+    import phantom_amd as PA
+    sess = PA.BootSession(bytes(range(32)), num_slots=num_slots, iterations=iterations, precision=precision)
+    rng = np.random.default_rng(0xB0 + num_slots + iterations)
+    vals = rng.uniform(1.0, 5.0, size=(count, sess.slots))
+    sin = sess.input_bytes(chain)
+    sout = sess.output_bytes()
+    dev_in = torch.empty((count, sin), dtype=torch.uint8, device="cuda")
+    dev_out = torch.empty((count, sout), dtype=torch.uint8, device="cuda")
+    assert sess.encrypt(vals, chain, dev_in.data_ptr(), sin) == sin
+    sess.run(dev_in.data_ptr(), sin, count, dev_out.data_ptr(), sout, lanes)
+    torch.cuda.synchronize()
+    bits = [PA.bit_precision(vals[i], sess.decrypt(dev_out[i].data_ptr(), sout)) for i in range(count)]
+    # the input itself decrypts to the message (encrypt / serialize path)
+    in_bits = PA.bit_precision(vals[0], sess.decrypt(dev_in[0].data_ptr(), sin))
+    sess.close()
+    return bits, in_bits
+
+
+def test_session_full_packing_bootstrap():
+    bits, in_bits = _session_run()
+    assert in_bits > 30, in_bits
+    assert min(bits) > 9.85, bits
+
+
+def test_sparse_bootstrap_n_over_8_slots():
+    """SparseBootStrapping (bootstrapping_example.cu:200-309): numSlots = N/8, the message in every
+    block of N/8 slots; partial sums, one EvalMod, SlotToCoeff + the fold rotation."""
+    bits, in_bits = _session_run(num_slots=(1 << 16) // 8)
+    assert in_bits > 30, in_bits
+    assert min(bits) > 9.85, bits
+
+
+def test_two_iteration_bootstrap_gains_precision():
+    """EvalBootstrap(ct, cc, 0, numIterations = 2, precision) (bootstrap.cu:856-900): the second
+    bootstrap removes most of the first one's error."""
+    one, _ = _session_run(count=1)
+    two, _ = _session_run(iterations=2, precision=8, count=1)
+    # measured on MI355X: 10.0 -> 22.5 bits (precision 6 / 8 / 10: 20.5 / 22.5 / 20.5)
+    assert two[0] > 21.0 and two[0] > one[0] + 10.0, (one, two)
+
+
+def test_bench_c5_leg_single_gpu():
+    """bench.py's C5 leg at world size 1 with a small batch: encrypt on rank 0, scatter, batch
+    bootstrap on lanes, gather, decrypt-check every result."""
+    import json
+    import sys
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--no-c3",
+                          "--no-c4", "--no-cpu-baseline", "--c5-batch", "8", "--c5-lanes", "4"],
+                         capture_output=True, text=True, timeout=115)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    c5 = line["c5"]
+    assert c5["bootstraps"] == 8 and c5["verified"] == 8 and c5["ranks"] == 1, c5
+    assert c5["min_avg_bits"] > 9.85, c5

@@ -325,3 +325,26 @@ def test_relinearize_decrypts_to_tensor(rng):
             x -= Q
         # key-switch noise ~ sum over digits of |c2 digit| * |e| / P + rounding: tiny vs Q
         assert abs(x) < 2 ** 40, x
+
+
+# ---- EvalMod coefficients pinned to the reference's own tables ------------------------------
+
+@pytest.mark.parametrize("which", ["uniform", "sparse"])
+def test_eval_mod_coefficients_match_reference_tables(which):
+    """The engine interpolates EvalMod's scaled cosine itself (host/bootstrap.cpp
+    chebyshev_coefficients); the reference ships the same series as fixed tables
+    (include/bootstrap.cuh:217-255, tests/golden/eval_mod_coefficients.json).  Same function, same
+    degree: the coefficients agree to 1e-13 (the tables' printed precision), with the reference's
+    c[0]/2 free-term convention (src/evaluate.cu:3259)."""
+    import ctypes
+    import json
+    import os
+    import phantom_amd as PA
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "eval_mod_coefficients.json")))[which]
+    ref = np.array(g["coefficients"])
+    out = (ctypes.c_double * ref.size)()
+    PA.check(PA.load().phantom_eval_mod_coefficients(g["K"], g["double_angle_iterations"], ref.size - 1, out))
+    ours = np.array(out[:])
+    want = ref.copy()
+    want[0] /= 2
+    assert np.max(np.abs(ours - want)) < 1e-13, np.max(np.abs(ours - want))
