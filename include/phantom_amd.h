@@ -124,6 +124,51 @@ int phantom_moddown_modup(const phantom_context *ctx, size_t chain_index, uint64
                           hipStream_t stream);
 int phantom_moddown_rescale(const phantom_context *ctx, size_t chain_index, uint64_t *cx, uint64_t *out,
                             size_t polys, hipStream_t stream);
+/* ---- the bootstrap's own kernels (src/bootstrap.cu:1157-1405, src/evaluate.cu:2299-3940) ------
+ * Extended-basis ("Ext") polynomials are [Ql + P][n] at chain_index: the chain's data limbs, then
+ * the special primes; Ext ciphertexts are [2][Ql + P][n].  Host arrays carry device pointers or
+ * per-limb residues (copied into the launch here). */
+/* EvalLinearTransform's hoisted inner sums (src/bootstrap.cu:1322-1332: EvalMultExt +
+ * EvalAddExtInPlace, src/evaluate.cu:3786-3874), all giant steps in one launch:
+ * outs[i] = sum_{j<g} babies[j] * pts[i g + j] for i < b (babies / outs Ext ciphertexts, pts Ext
+ * plaintexts, host arrays of device pointers; g a power of two <= 32, b <= 64) */
+int phantom_lt_bsgs(const phantom_context *ctx, size_t chain_index, const uint64_t *const *babies, size_t g,
+                    const uint64_t *const *pts, size_t b, uint64_t *const *outs, hipStream_t stream);
+/* KeySwitchExt (src/evaluate.cu:3876-3940): ct [2][Ql][n] -> out = P ct in the Ext basis */
+int phantom_keyswitch_ext(const phantom_context *ctx, size_t chain_index, const uint64_t *ct, uint64_t *out,
+                          hipStream_t stream);
+/* EvalFastRotationExt (src/evaluate.cu:3660-3755) with a fused key: inner product of the shared
+ * modup digits [beta][Ql+P][n] with the key, + P c0 when add_first (ct's c0 [Ql][n]), then the
+ * NTT-domain automorphism of both polynomials: out [2][Ql+P][n] */
+int phantom_fast_rotation_ext(const phantom_context *ctx, size_t chain_index, const uint64_t *ct,
+                              const uint64_t *digits, const uint64_t *const *key_digits, size_t dnum,
+                              uint32_t galois_elt, int add_first, uint64_t *out, hipStream_t stream);
+/* a giant step of the linear transforms (src/bootstrap.cu:1335-1348: KeySwitchDown + Precompute +
+ * EvalFastRotationExt + EvalAddExtInPlace) with c0 kept in the Ext basis:
+ * acc (+)= automorphism(KS(modup(moddown(ext c1))) + (ext c0, 0)); ext's c1 P limbs are clobbered */
+int phantom_rotate_ext_accumulate(const phantom_context *ctx, size_t chain_index, uint64_t *ext,
+                                  const uint64_t *const *key_digits, size_t dnum, uint32_t galois_elt, uint64_t *acc,
+                                  int accumulate, hipStream_t stream);
+/* tensor_prod_2x2 with MulAddRescale's linear epilogue: out [3][Ql][n] = f (ct1 x ct2), then
+ * out[p] += c t[p] for p < 2 (t[p] at t + p t_stride; f, c: host residues per limb or NULL) */
+int phantom_tensor_lin(const phantom_context *ctx, size_t chain_index, const uint64_t *ct1, const uint64_t *ct2,
+                       uint64_t *out, const uint64_t *f, const uint64_t *t, size_t t_stride, const uint64_t *c,
+                       hipStream_t stream);
+/* d[p] = d[p] ca (ca NULL: unscaled) + (p < t_polys ? t[p] cb : 0), d [d_polys][Ql][n] */
+int phantom_lin_comb(const phantom_context *ctx, size_t chain_index, uint64_t *d, size_t d_polys, const uint64_t *ca,
+                     const uint64_t *t, size_t t_polys, size_t t_stride, const uint64_t *cb, hipStream_t stream);
+/* EvalMultConstInplaceCore / MultByIntegerInPlace in residue form (src/evaluate.cu:2299-2412,
+ * :3942-3970): out[p] = in[p] c (+ acc[p]) for `polys` polynomials, in[p] at in + p in_stride
+ * (0: contiguous) — a larger stride reads the leading Ql limbs of longer polynomials */
+int phantom_mul_scalar(const phantom_context *ctx, size_t chain_index, const uint64_t *in, size_t in_stride,
+                       const uint64_t *c, const uint64_t *acc, uint64_t *out, size_t polys, hipStream_t stream);
+/* Chebyshev leaves of EvalChebyshevSeriesPS (src/evaluate.cu:3264-3535; EvalLinearWSumMutable
+ * :3537-3600 + the free term): out[m] = sum_k in[k] coef[m][k] + (cadd[m], 0) for m < M, k < K
+ * (in[k] [2][>= Ql][n] with polynomial stride in_stride[k]; coef host [M][K][Ql], cadd [M][Ql]) */
+int phantom_leaf_combine(const phantom_context *ctx, size_t chain_index, const uint64_t *const *in,
+                         const size_t *in_stride, size_t K, const uint64_t *coef, const uint64_t *cadd,
+                         uint64_t *const *out, size_t M, hipStream_t stream);
+
 /* ---- serialization (host memory; no GPU involved) ------------------------------------
  * The byte format of PhantomCiphertext::save / load (include/ciphertext.h:184-225): the header
  * fields one by one (4 x size_t, double, uint64_t, size_t, bool, bool = 58 bytes) followed by

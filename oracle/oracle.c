@@ -639,3 +639,178 @@ void or_monomial_ntt(uint64_t *out, size_t n, size_t L, const uint64_t *moduli, 
         or_ntt_fwd(o, n, 1, &moduli[l]);
     }
 }
+
+/* ------------------------------------------------------------------ */
+/* bootstrap kernels (hoisted linear transforms, EvalMod)              */
+/* ------------------------------------------------------------------ */
+
+/* modulus of buffer limb l of an extended-basis (Ql u P) polynomial */
+static uint64_t ext_mod(size_t l, size_t size_ql, size_t size_q, const uint64_t *qp_full) {
+    return l < size_ql ? qp_full[l] : qp_full[size_q + (l - size_ql)];
+}
+
+/* The hoisted baby-step / giant-step inner sums of EvalLinearTransform (src/bootstrap.cu:1322-1332):
+ * for every giant step i < b, out[i] = sum_{j<g} EvalMultExt(baby[j], pt[i g + j]) accumulated with
+ * EvalAddExtInPlace (src/evaluate.cu:3786-3874): both polynomials of a [2][Ql+P][n] extended-basis
+ * ciphertext times a [Ql+P][n] plaintext, limb by limb, mod the limb's prime. */
+void or_lt_bsgs(const uint64_t *const *baby, size_t g, const uint64_t *const *pts, size_t b, uint64_t *const *out,
+                size_t n, size_t size_ql, size_t size_q, size_t size_p, const uint64_t *qp_full) {
+    const size_t qlp = size_ql + size_p;
+#pragma omp parallel for schedule(static)
+    for (size_t l = 0; l < qlp; l++) {
+        const uint64_t q = ext_mod(l, size_ql, size_q, qp_full);
+        for (size_t i = 0; i < b; i++)
+            for (size_t t = 0; t < 2; t++)
+                for (size_t k = 0; k < n; k++) {
+                    uint64_t acc = 0;
+                    for (size_t j = 0; j < g; j++) {
+                        const uint64_t x = baby[j][(t * qlp + l) * n + k];
+                        const uint64_t w = pts[i * g + j][l * n + k];
+                        acc = csub(acc + or_mulmod(x, w, q), q);
+                    }
+                    out[i][(t * qlp + l) * n + k] = acc;
+                }
+    }
+}
+
+/* KeySwitchExt (src/evaluate.cu:3876-3940): (c0, c1) at Ql -> P (c0, c1) in the extended basis,
+ * the P limbs zero.  ct [2][Ql][n] -> out [2][Ql+P][n]. */
+void or_keyswitch_ext(const uint64_t *ct, uint64_t *out, size_t n, size_t size_ql, size_t size_q, size_t size_p,
+                      const uint64_t *qp_full) {
+    const size_t qlp = size_ql + size_p;
+    memset(out, 0, 2 * qlp * n * 8);
+    for (size_t t = 0; t < 2; t++)
+        for (size_t l = 0; l < size_ql; l++) {
+            const uint64_t q = qp_full[l];
+            uint64_t pm = 1;
+            for (size_t i = 0; i < size_p; i++) pm = or_mulmod(pm, qp_full[size_q + i] % q, q);
+            for (size_t k = 0; k < n; k++) out[(t * qlp + l) * n + k] = or_mulmod(ct[(t * size_ql + l) * n + k], pm, q);
+        }
+}
+
+/* EvalFastRotationExt (src/evaluate.cu:3660-3755) with a fused key: cx = the key-switch inner
+ * product of the shared modup digits (or_keyswitch_inner_prod), then, if add_first, cx[0] += P c0
+ * on the Ql limbs, then the NTT-domain automorphism of both polynomials
+ * (apply_galois_ntt_permutation_direct, src/galois.cu:104-119).  c0: [Ql][n]; out [2][Ql+P][n]. */
+void or_fast_rotation_ext(const uint64_t *c0, const uint64_t *digits, const uint64_t *const *evk, uint32_t galois_elt,
+                          int add_first, uint64_t *out, size_t n, size_t size_ql, size_t size_q, size_t size_p,
+                          const uint64_t *qp_full) {
+    const size_t qlp = size_ql + size_p, beta = (size_ql + size_p - 1) / size_p;
+    uint64_t *cx = malloc(2 * qlp * n * 8);
+    or_keyswitch_inner_prod(digits, evk, cx, n, size_ql, size_q, size_p, beta, qp_full);
+    if (add_first)
+        for (size_t l = 0; l < size_ql; l++) {
+            const uint64_t q = qp_full[l];
+            uint64_t pm = 1;
+            for (size_t i = 0; i < size_p; i++) pm = or_mulmod(pm, qp_full[size_q + i] % q, q);
+            for (size_t k = 0; k < n; k++)
+                cx[l * n + k] = csub(cx[l * n + k] + or_mulmod(c0[l * n + k], pm, q), q);
+        }
+    or_apply_galois_ntt(cx, out, n, 2 * qlp, galois_elt);
+    free(cx);
+}
+
+/* A giant step of EvalLinearTransform in the extended basis (src/bootstrap.cu:1335-1348:
+ * KeySwitchDown of the inner sum's c1, EvalFastRotationPrecompute of it, EvalFastRotationExt,
+ * EvalAddExtInPlace into the accumulator), with c0 kept P-scaled in Ql u P:
+ *   digits = modup(moddown(ext c1));  cx = inner product;  x = (cx0 + ext c0, cx1);
+ *   acc (+)= automorphism(x).  ext [2][Ql+P][n] (c1's P limbs clobbered), acc [2][Ql+P][n]. */
+void or_rotate_ext_accumulate(uint64_t *ext, const uint64_t *const *evk, uint32_t galois_elt, uint64_t *acc,
+                              int accumulate, size_t n, size_t size_ql, size_t size_q, size_t size_p,
+                              const uint64_t *qp_full) {
+    const size_t qlp = size_ql + size_p, beta = (size_ql + size_p - 1) / size_p;
+    const uint64_t *p = qp_full + size_q;
+    uint64_t *c1 = malloc(size_ql * n * 8);
+    or_moddown_from_ntt(ext + qlp * n, c1, n, qp_full, size_ql, p, size_p);
+    uint64_t *digits = malloc(beta * qlp * n * 8);
+    or_modup(c1, digits, n, qp_full, size_ql, p, size_p);
+    uint64_t *cx = malloc(2 * qlp * n * 8);
+    or_keyswitch_inner_prod(digits, evk, cx, n, size_ql, size_q, size_p, beta, qp_full);
+    for (size_t l = 0; l < qlp; l++) {
+        const uint64_t q = ext_mod(l, size_ql, size_q, qp_full);
+        for (size_t k = 0; k < n; k++) cx[l * n + k] = csub(cx[l * n + k] + ext[l * n + k], q);
+    }
+    uint64_t *rot = malloc(2 * qlp * n * 8);
+    or_apply_galois_ntt(cx, rot, n, 2 * qlp, galois_elt);
+    for (size_t t = 0; t < 2; t++)
+        for (size_t l = 0; l < qlp; l++) {
+            const uint64_t q = ext_mod(l, size_ql, size_q, qp_full);
+            for (size_t k = 0; k < n; k++) {
+                const size_t e = (t * qlp + l) * n + k;
+                acc[e] = accumulate ? csub(acc[e] + rot[e], q) : rot[e];
+            }
+        }
+    free(rot);
+    free(cx);
+    free(digits);
+    free(c1);
+}
+
+/* multiply every polynomial by per-limb integer constants, optionally accumulating:
+ * out[p][l] = in[p][l] * c[l] (+ acc[p][l]) mod q_l — the residue form of EvalMultConstInplaceCore
+ * / MultByIntegerInPlace (src/evaluate.cu:2299-2412, :3942-3970).  in[p] at in + p * in_stride. */
+void or_mul_scalar_acc(const uint64_t *in, size_t in_stride, const uint64_t *c, const uint64_t *acc, uint64_t *out,
+                       size_t polys, size_t n, size_t L, const uint64_t *moduli) {
+    for (size_t p = 0; p < polys; p++)
+        for (size_t l = 0; l < L; l++)
+            for (size_t k = 0; k < n; k++) {
+                const size_t e = l * n + k;
+                uint64_t v = or_mulmod(in[p * in_stride + e], c[l], moduli[l]);
+                if (acc) v = csub(v + acc[p * L * n + e], moduli[l]);
+                out[p * L * n + e] = v;
+            }
+}
+
+/* tensor product with a linear epilogue — EvalMult (tensor_prod_2x2_rns_poly, src/polymath.cu:501-536)
+ * times the integer f (EvalMultConst), plus c * t added to the first two polynomials (EvalAdd of a
+ * constant multiple): d = f (ct1 x ct2); d[p] += c t[p] for p < 2.  f / c: per-limb residues or NULL. */
+void or_tensor_lin(const uint64_t *ct1, const uint64_t *ct2, uint64_t *out, size_t n, size_t L,
+                   const uint64_t *moduli, const uint64_t *f, const uint64_t *t, size_t t_stride, const uint64_t *c) {
+    or_tensor_prod_2x2(ct1, ct2, out, n, L, moduli);
+    for (size_t p = 0; p < 3; p++)
+        for (size_t l = 0; l < L; l++) {
+            const uint64_t q = moduli[l];
+            for (size_t k = 0; k < n; k++) {
+                uint64_t *d = &out[(p * L + l) * n + k];
+                if (f) *d = or_mulmod(*d, f[l], q);
+                if (t && c && p < 2) *d = csub(*d + or_mulmod(t[p * t_stride + l * n + k], c[l], q), q);
+            }
+        }
+}
+
+/* d[p] = d[p] * ca (if ca) + (p < t_polys ? t[p] * cb : 0), t[p] at t + p * t_stride */
+void or_lin_comb(uint64_t *d, size_t d_polys, const uint64_t *ca, const uint64_t *t, size_t t_polys,
+                 size_t t_stride, const uint64_t *cb, size_t n, size_t L, const uint64_t *moduli) {
+    for (size_t p = 0; p < d_polys; p++)
+        for (size_t l = 0; l < L; l++) {
+            const uint64_t q = moduli[l];
+            for (size_t k = 0; k < n; k++) {
+                uint64_t *x = &d[(p * L + l) * n + k];
+                if (ca) *x = or_mulmod(*x, ca[l], q);
+                if (t && p < t_polys) *x = csub(*x + or_mulmod(t[p * t_stride + l * n + k], cb[l], q), q);
+            }
+        }
+}
+
+/* The Chebyshev leaves of EvalChebyshevSeriesPS (src/evaluate.cu:3264-3535): each leaf is a
+ * weighted sum of the power ciphertexts T_1..T_K plus a constant, EvalLinearWSumMutable
+ * (:3537-3600) + EvalAddConst: out[m][t][l] = sum_k in[k][t][l] coef[m][k][l] + (t == 0 ? cadd[m][l] : 0).
+ * in[k] is [2][>= L][n] with polynomial stride in_stride[k]; out[m] is [2][L][n];
+ * coef [M][K][L], cadd [M][L] are residues. */
+void or_leaf_combine(const uint64_t *const *in, const size_t *in_stride, size_t K, const uint64_t *coef,
+                     const uint64_t *cadd, uint64_t *const *out, size_t M, size_t n, size_t L, const uint64_t *moduli) {
+    for (size_t m = 0; m < M; m++)
+        for (size_t t = 0; t < 2; t++)
+            for (size_t l = 0; l < L; l++) {
+                const uint64_t q = moduli[l];
+                for (size_t k = 0; k < n; k++) {
+                    u128 acc = 0;
+                    for (size_t i = 0; i < K; i++)
+                        acc += (u128)in[i][t * in_stride[i] + l * n + k] * coef[(m * K + i) * L + l];
+                    uint64_t v = (uint64_t)(acc % q);
+                    if (t == 0) v = csub(v + cadd[m * L + l], q);
+                    out[m][(t * L + l) * n + k] = v;
+                }
+            }
+}
+

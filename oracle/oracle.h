@@ -98,6 +98,26 @@ void or_switch_modulus_raise(const uint64_t *in_q0, uint64_t *out, size_t n, uin
                              size_t size_ql);
 void or_monomial_ntt(uint64_t *out, size_t n, size_t L, const uint64_t *moduli, uint32_t power);
 
+/* ---- bootstrap kernels (src/bootstrap.cu:1157-1405 linear transforms, src/evaluate.cu:2299-3940) ---- */
+void or_lt_bsgs(const uint64_t *const *baby, size_t g, const uint64_t *const *pts, size_t b, uint64_t *const *out,
+                size_t n, size_t size_ql, size_t size_q, size_t size_p, const uint64_t *qp_full);
+void or_keyswitch_ext(const uint64_t *ct, uint64_t *out, size_t n, size_t size_ql, size_t size_q, size_t size_p,
+                      const uint64_t *qp_full);
+void or_fast_rotation_ext(const uint64_t *c0, const uint64_t *digits, const uint64_t *const *evk, uint32_t galois_elt,
+                          int add_first, uint64_t *out, size_t n, size_t size_ql, size_t size_q, size_t size_p,
+                          const uint64_t *qp_full);
+void or_rotate_ext_accumulate(uint64_t *ext, const uint64_t *const *evk, uint32_t galois_elt, uint64_t *acc,
+                              int accumulate, size_t n, size_t size_ql, size_t size_q, size_t size_p,
+                              const uint64_t *qp_full);
+void or_mul_scalar_acc(const uint64_t *in, size_t in_stride, const uint64_t *c, const uint64_t *acc, uint64_t *out,
+                       size_t polys, size_t n, size_t L, const uint64_t *moduli);
+void or_tensor_lin(const uint64_t *ct1, const uint64_t *ct2, uint64_t *out, size_t n, size_t L,
+                   const uint64_t *moduli, const uint64_t *f, const uint64_t *t, size_t t_stride, const uint64_t *c);
+void or_lin_comb(uint64_t *d, size_t d_polys, const uint64_t *ca, const uint64_t *t, size_t t_polys,
+                 size_t t_stride, const uint64_t *cb, size_t n, size_t L, const uint64_t *moduli);
+void or_leaf_combine(const uint64_t *const *in, const size_t *in_stride, size_t K, const uint64_t *coef,
+                     const uint64_t *cadd, uint64_t *const *out, size_t M, size_t n, size_t L, const uint64_t *moduli);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,237 @@
+// capi_bootk.cpp — C-ABI of the bootstrap's own kernels (declared in include/phantom_amd.h), on
+// raw device buffers, so each can be checked bit for bit against the CPU oracle: the hoisted
+// linear transforms' inner sums (lt_bsgs), EvalFastRotationExt with its fused epilogue
+// (galois_finish), the giant-step rotate-and-accumulate, KeySwitchExt, the tensor product with
+// MulAddRescale's linear epilogue (tensor_lin), the Chebyshev leaves (leaf_combine) and the
+// per-limb scalar kernels.  Host arrays of device pointers and of per-limb residues are copied into
+// the kernels' argument blocks or small device tables here (set-up cost, not on the hot path).
+#include <cstring>
+#include <vector>
+
+#include "../host/buffer.h"
+#include "../host/capi_internal.h"
+#include "../host/ckks_eval.h"
+#include "../host/context.h"
+#include "../host/numth.h"
+#include "ckks.h"
+#include "phantom_amd.h"
+#include "rns.h"
+
+using phantom::capi::fail;
+using phantom::capi::from_hip;
+
+const phantom::PhantomContext& phantom_capi_context(const phantom_context* c);
+const uint64_t* const* phantom_capi_key_array(const phantom_context* c, const uint64_t* const* host, size_t dnum,
+                                              size_t need);
+
+namespace {
+
+const phantom::RnsTool& tool_at(const phantom::PhantomContext& pc, size_t chain) {
+  if (chain < 1 || chain >= pc.total_parm_size()) throw std::invalid_argument("invalid chain index");
+  return pc.get_context_data(chain).gpu_rns_tool();
+}
+
+// per-limb residues (reduced mod the chain's primes) + Shoup quotients as kernel arguments
+phx::LimbScalars scalars(const phantom::PhantomContext& pc, size_t chain, const uint64_t* v) {
+  const auto& mods = pc.get_context_data(chain).moduli();
+  if (mods.size() > static_cast<size_t>(phx::kMaxScalarLimbs)) throw std::invalid_argument("too many limbs");
+  phx::LimbScalars c;
+  for (size_t l = 0; l < mods.size(); ++l) {
+    c.v[l] = v[l] % mods[l];
+    c.vs[l] = phantom::arith::shoup(c.v[l], mods[l]);
+  }
+  return c;
+}
+
+}  // namespace
+
+extern "C" {
+
+int phantom_lt_bsgs(const phantom_context* ctx, size_t chain_index, const uint64_t* const* babies, size_t g,
+                    const uint64_t* const* pts, size_t b, uint64_t* const* outs, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    if (!babies || !pts || !outs) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (g < 1 || g > static_cast<size_t>(phx::kLtMaxG) || (g & (g - 1)) || b < 1 || b > static_cast<size_t>(phx::kLtMaxB))
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "baby steps must be a power of two <= 32, giant steps <= 64");
+    phx::LtArgs a;
+    a.g = static_cast<int>(g);
+    a.b = static_cast<int>(b);
+    a.Ql = static_cast<int>(rt.size_Ql());
+    a.P = static_cast<int>(pc.size_P());
+    a.size_Q = static_cast<int>(pc.size_Q());
+    a.q = pc.mod_QP().q;
+    a.barrett = pc.mod_QP().barrett;
+    for (size_t j = 0; j < g; ++j) a.baby[j] = babies[j];
+    for (size_t i = 0; i < b; ++i) a.out[i] = outs[i];
+    phantom::DeviceBuffer<const uint64_t*> table;
+    table.upload(std::vector<const uint64_t*>(pts, pts + g * b), stream);
+    a.pts = table.get();
+    const hipError_t e = phx::lt_bsgs(a, pc.poly_degree(), stream);
+    PHX_CHECK(hipStreamSynchronize(stream));  // the pointer table is freed on return
+    return from_hip(e);
+  });
+}
+
+int phantom_keyswitch_ext(const phantom_context* ctx, size_t chain_index, const uint64_t* ct, uint64_t* out,
+                          hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    const size_t n = pc.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + pc.size_P();
+    PHX_CHECK(hipMemsetAsync(out, 0, 2 * QlP * n * sizeof(uint64_t), stream));
+    for (size_t i = 0; i < 2; ++i) {
+      const hipError_t e = phx::mul_scalar_add(ct + i * Ql * n, rt.bigP_mod_q(), rt.bigP_mod_q_shoup(), nullptr,
+                                               out + i * QlP * n, pc.mod_QP().q, n, Ql, stream);
+      if (e != hipSuccess) return from_hip(e);
+    }
+    return PHANTOM_OK;
+  });
+}
+
+int phantom_fast_rotation_ext(const phantom_context* ctx, size_t chain_index, const uint64_t* ct,
+                              const uint64_t* digits, const uint64_t* const* key_digits, size_t dnum,
+                              uint32_t galois_elt, int add_first, uint64_t* out, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    const size_t n = pc.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + pc.size_P();
+    const uint64_t* const* evk = phantom_capi_key_array(ctx, key_digits, dnum, rt.beta());
+    phantom::DeviceBuffer<uint64_t> cx(2 * QlP * n, stream);
+    hipError_t e = phx::keyswitch_inner_prod(digits, evk, cx.get(), pc.mod_QP().q, pc.mod_QP().barrett, n, Ql,
+                                             pc.size_Q(), pc.size_P(), rt.beta(), stream);
+    if (e != hipSuccess) return from_hip(e);
+    phx::GaloisFinishArgs g;
+    g.cx = cx.get();
+    g.c0 = ct;
+    g.pmod = rt.bigP_mod_q();
+    g.pmod_shoup = rt.bigP_mod_q_shoup();
+    g.out = out;
+    g.perm = pc.galois_perm(galois_elt);
+    g.q = rt.mod_QlP().q;
+    g.ql = static_cast<uint32_t>(Ql);
+    g.qlp = static_cast<uint32_t>(QlP);
+    return from_hip(phx::galois_finish(g, add_first ? 1 : 0, n, stream));
+  });
+}
+
+int phantom_rotate_ext_accumulate(const phantom_context* ctx, size_t chain_index, uint64_t* ext,
+                                  const uint64_t* const* key_digits, size_t dnum, uint32_t galois_elt, uint64_t* acc,
+                                  int accumulate, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    const size_t n = pc.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + pc.size_P();
+    const uint64_t* const* evk = phantom_capi_key_array(ctx, key_digits, dnum, rt.beta());
+    phantom::DeviceBuffer<uint64_t> digits(rt.beta() * QlP * n, stream), cx(2 * QlP * n, stream);
+    rt.moddown_modup(digits.get(), ext + QlP * n, pc.gpu_rns_tables(), stream);
+    hipError_t e = phx::keyswitch_inner_prod(digits.get(), evk, cx.get(), pc.mod_QP().q, pc.mod_QP().barrett, n, Ql,
+                                             pc.size_Q(), pc.size_P(), rt.beta(), stream);
+    if (e != hipSuccess) return from_hip(e);
+    phx::GaloisFinishArgs g;
+    g.cx = cx.get();
+    g.c0 = ext;
+    g.out = acc;
+    g.perm = pc.galois_perm(galois_elt);
+    g.q = rt.mod_QlP().q;
+    g.ql = static_cast<uint32_t>(Ql);
+    g.qlp = static_cast<uint32_t>(QlP);
+    g.accumulate = accumulate != 0;
+    return from_hip(phx::galois_finish(g, 2, n, stream));
+  });
+}
+
+int phantom_tensor_lin(const phantom_context* ctx, size_t chain_index, const uint64_t* ct1, const uint64_t* ct2,
+                       uint64_t* out, const uint64_t* f, const uint64_t* t, size_t t_stride, const uint64_t* c,
+                       hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    phx::TensorLinArgs a;
+    a.ct1 = ct1;
+    a.ct2 = ct2;
+    a.out = out;
+    a.q = pc.mod_QP().q;
+    a.barrett = pc.mod_QP().barrett;
+    if (f) {
+      a.scale = true;
+      a.f = scalars(pc, chain_index, f);
+    }
+    if (t && c) {
+      a.t = t;
+      a.t_stride = t_stride;
+      a.c = scalars(pc, chain_index, c);
+    }
+    return from_hip(phx::tensor_lin(a, pc.poly_degree(), rt.size_Ql(), stream));
+  });
+}
+
+int phantom_lin_comb(const phantom_context* ctx, size_t chain_index, uint64_t* d, size_t d_polys, const uint64_t* ca,
+                     const uint64_t* t, size_t t_polys, size_t t_stride, const uint64_t* cb, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    if (!cb) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null term constants");
+    const phx::LimbScalars b = scalars(pc, chain_index, cb);
+    phx::LimbScalars a;
+    if (ca) a = scalars(pc, chain_index, ca);
+    return from_hip(phx::lin_comb_v(d, d_polys, ca ? &a : nullptr, t, t_polys, t_stride, b, pc.mod_QP().q,
+                                    pc.poly_degree(), rt.size_Ql(), stream));
+  });
+}
+
+int phantom_mul_scalar(const phantom_context* ctx, size_t chain_index, const uint64_t* in, size_t in_stride,
+                       const uint64_t* c, const uint64_t* acc, uint64_t* out, size_t polys, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    if (!c) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null constants");
+    return from_hip(phx::mul_scalar_v(in, scalars(pc, chain_index, c), out, pc.mod_QP().q, pc.poly_degree(),
+                                      rt.size_Ql(), stream, polys, in_stride, acc));
+  });
+}
+
+int phantom_leaf_combine(const phantom_context* ctx, size_t chain_index, const uint64_t* const* in,
+                         const size_t* in_stride, size_t K, const uint64_t* coef, const uint64_t* cadd,
+                         uint64_t* const* out, size_t M, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    if (!in || !in_stride || !coef || !cadd || !out) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (K < 1 || K > static_cast<size_t>(phx::kLeafMaxK) || M < 1 || M > static_cast<size_t>(phx::kLeafMaxM))
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "leaf count out of range");
+    const size_t L = rt.size_Ql();
+    const auto& mods = pc.get_context_data(chain_index).moduli();
+    // device table [values][shoup][cadd] as the kernel reads it (FHECKKSRNS::eval_leaves layout)
+    std::vector<uint64_t> tab(2 * M * K * L + M * L);
+    for (size_t m = 0; m < M; ++m)
+      for (size_t k = 0; k < K; ++k)
+        for (size_t l = 0; l < L; ++l) {
+          const uint64_t v = coef[(m * K + k) * L + l] % mods[l];
+          tab[(m * K + k) * L + l] = v;
+          tab[M * K * L + (m * K + k) * L + l] = phantom::arith::shoup(v, mods[l]);
+        }
+    for (size_t i = 0; i < M * L; ++i) tab[2 * M * K * L + i] = cadd[i] % mods[i % L];
+    phantom::DeviceBuffer<uint64_t> d;
+    d.upload(tab, stream);
+    phx::LeafArgs a;
+    a.K = static_cast<int>(K);
+    a.M = static_cast<int>(M);
+    a.L = static_cast<int>(L);
+    a.q = pc.mod_QP().q;
+    a.barrett = pc.mod_QP().barrett;
+    a.coef = d.get();
+    a.cadd = d.get() + 2 * M * K * L;
+    for (size_t k = 0; k < K; ++k) {
+      a.in[k] = in[k];
+      a.in_stride[k] = in_stride[k];
+    }
+    for (size_t m = 0; m < M; ++m) a.out[m] = out[m];
+    const hipError_t e = phx::leaf_combine(a, pc.poly_degree(), stream);
+    PHX_CHECK(hipStreamSynchronize(stream));  // the table is freed on return
+    return from_hip(e);
+  });
+}
+
+}  // extern "C"

@@ -51,6 +51,12 @@ const phantom::PhantomContext& phantom_capi_context(const phantom_context* c) {
   return *c->ctx;
 }
 
+const uint64_t* const* phantom_capi_key_array(const phantom_context* c, const uint64_t* const* host, size_t dnum,
+                                              size_t need) {
+  if (!c) throw std::invalid_argument("null context");
+  return const_cast<phantom_context*>(c)->device_key_array(host, dnum, need);
+}
+
 namespace {
 const phantom::RnsTool& tool(const phantom_context* c, size_t chain_index) {
   if (!c) throw std::invalid_argument("null context");

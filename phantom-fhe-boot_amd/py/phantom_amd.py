@@ -51,6 +51,16 @@ _SIGS = {
     "phantom_boot_session_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_uint32,
                                                    ctypes.c_uint32, ctypes.c_uint32, vp, ctypes.POINTER(vp)]),
     "phantom_boot_session_destroy": (ctypes.c_int, [vp]),
+    "phantom_lt_bsgs": (ctypes.c_int, [vp, sz, ctypes.POINTER(vp), sz, ctypes.POINTER(vp), sz, ctypes.POINTER(vp), vp]),
+    "phantom_keyswitch_ext": (ctypes.c_int, [vp, sz, vp, vp, vp]),
+    "phantom_fast_rotation_ext": (ctypes.c_int, [vp, sz, vp, vp, ctypes.POINTER(vp), sz, ctypes.c_uint32, ctypes.c_int,
+                                                 vp, vp]),
+    "phantom_rotate_ext_accumulate": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, ctypes.c_uint32, vp,
+                                                     ctypes.c_int, vp]),
+    "phantom_tensor_lin": (ctypes.c_int, [vp, sz, vp, vp, vp, vp, vp, sz, vp, vp]),
+    "phantom_lin_comb": (ctypes.c_int, [vp, sz, vp, sz, vp, vp, sz, sz, vp, vp]),
+    "phantom_mul_scalar": (ctypes.c_int, [vp, sz, vp, sz, vp, vp, vp, sz, vp]),
+    "phantom_leaf_combine": (ctypes.c_int, [vp, sz, ctypes.POINTER(vp), vp, sz, vp, vp, ctypes.POINTER(vp), sz, vp]),
     "phantom_eval_mod_coefficients": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp]),
     "phantom_boot_encrypt": (ctypes.c_int, [vp, vp, sz, sz, vp, sz, ctypes.POINTER(sz)]),
     "phantom_boot_output_bytes": (ctypes.c_int, [vp, ctypes.POINTER(sz)]),

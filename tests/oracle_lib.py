@@ -60,6 +60,18 @@ def lib():
             "or_apply_galois_ntt": (None, [u64p, u64p, sz, sz, ctypes.c_uint32]),
             "or_switch_modulus_raise": (None, [u64p, u64p, sz, u64, u64p, sz]),
             "or_monomial_ntt": (None, [u64p, sz, sz, u64p, ctypes.c_uint32]),
+            "or_lt_bsgs": (None, [ctypes.POINTER(u64p), sz, ctypes.POINTER(u64p), sz, ctypes.POINTER(u64p), sz, sz, sz,
+                                  sz, u64p]),
+            "or_keyswitch_ext": (None, [u64p, u64p, sz, sz, sz, sz, u64p]),
+            "or_fast_rotation_ext": (None, [u64p, u64p, ctypes.POINTER(u64p), ctypes.c_uint32, ctypes.c_int, u64p, sz,
+                                            sz, sz, sz, u64p]),
+            "or_rotate_ext_accumulate": (None, [u64p, ctypes.POINTER(u64p), ctypes.c_uint32, u64p, ctypes.c_int, sz,
+                                                sz, sz, sz, u64p]),
+            "or_mul_scalar_acc": (None, [u64p, sz, u64p, u64p, u64p, sz, sz, sz, u64p]),
+            "or_tensor_lin": (None, [u64p, u64p, u64p, sz, sz, u64p, u64p, u64p, sz, u64p]),
+            "or_lin_comb": (None, [u64p, sz, u64p, u64p, sz, sz, u64p, sz, sz, u64p]),
+            "or_leaf_combine": (None, [ctypes.POINTER(u64p), ctypes.POINTER(sz), sz, u64p, u64p, ctypes.POINTER(u64p),
+                                       sz, sz, sz, u64p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -114,3 +126,8 @@ def random_limbs(rng, n, moduli):
     for i, q in enumerate(moduli):
         out[i * n:(i + 1) * n] = rng.integers(0, q, size=n, dtype=np.uint64)
     return out
+
+
+def ptrs(arrays):
+    """host array of u64 pointers to numpy arrays (the arrays must stay alive)"""
+    return (u64p * len(arrays))(*[P(a) for a in arrays])
