@@ -142,13 +142,23 @@ def c4_leg(iters=3, timeout=240):
     if out.returncode != 0 or not boot:
         return {"error": (out.stderr or out.stdout)[-300:]}
     b = boot[0]
-    return {
+    res = {
         "workload": "C4: EvalBootstrap, N=65536, Q={60,29x59}, P=10x60, levelBudget {2,2}, full packing",
         "ms_median": b["ms_median"], "ms_min": b["ms_min"], "runs": b["runs"],
         "avg_bits": b["avg_bits"], "levels_after": b["levels_after"],
         "setup_ms": setup[0]["setup_ms"] if setup else None,
         "keygen_ms": setup[0]["keygen_ms"] if setup else None,
     }
+    ab = b.get("alg_bytes")
+    if ab:
+        # algorithmic bytes of one bootstrap (host/traffic.h: key digits, linear-transform
+        # diagonals, ciphertext operands / results) over its latency
+        total = ab["keys"] + ab["plaintexts"] + ab["ciphertexts"]
+        achieved = total / (b["ms_median"] * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes": total,
+                           "bytes": ab, "source": "host/traffic.h counters of one bootstrap"}
+    return res
 
 
 def max_over_ranks(dist, values, device):

@@ -217,6 +217,11 @@ int phantom_switch_modulus_raise(const phantom_context *ctx, const uint64_t *in_
  * Ciphertexts cross this boundary serialized in PhantomCiphertext::save's byte format
  * (include/ciphertext.h:184-225) and held in DEVICE memory, `stride` bytes apart: the form in which
  * a batch is scattered to ranks and gathered back. */
+/* algorithmic HBM bytes of the homomorphic operations issued since the last reset (process-wide,
+ * host/traffic.h): out[0] key-switching key bytes, out[1] linear-transform plaintext bytes,
+ * out[2] ciphertext operand / result bytes — the numerator of the bootstrap's roofline */
+int phantom_traffic_read(uint64_t *out);
+int phantom_traffic_reset(void);
 /* EvalMod's Chebyshev interpolant (host only): out[degree + 1] = coefficients c of
  * (2 pi)^(-2^-r) cos(2 pi (K y - 1/4) / 2^r) on [-1, 1], r = double_angle_iterations, with
  * p(y) = sum_k c_k T_k(y) (c_0 NOT halved; the reference's tables g_coefficientsUniform/Sparse,

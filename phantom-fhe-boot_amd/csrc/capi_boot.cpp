@@ -17,6 +17,7 @@
 #include "../host/keys.h"
 #include "../host/modulus.h"
 #include "../host/serialize.h"
+#include "../host/traffic.h"
 #include "phantom_amd.h"
 
 using phantom::capi::fail;
@@ -97,6 +98,23 @@ phantom_boot_session& session(phantom_boot_session* s) {
 }  // namespace
 
 extern "C" {
+
+int phantom_traffic_read(uint64_t* out) {
+  if (!out) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+  auto& c = traffic::counters();
+  out[0] = c.keys.load();
+  out[1] = c.plaintexts.load();
+  out[2] = c.ciphertexts.load();
+  return PHANTOM_OK;
+}
+
+int phantom_traffic_reset(void) {
+  auto& c = traffic::counters();
+  c.keys = 0;
+  c.plaintexts = 0;
+  c.ciphertexts = 0;
+  return PHANTOM_OK;
+}
 
 int phantom_eval_mod_coefficients(uint32_t K, uint32_t double_angle_iterations, int degree, double* out) {
   PHX_CAPI_GUARD({

@@ -27,6 +27,7 @@
 #include "../host/evaluate.h"
 #include "../host/keys.h"
 #include "../host/modulus.h"
+#include "../host/traffic.h"
 #include "../csrc/rns.h"
 #include "../csrc/ntt.h"
 
@@ -358,10 +359,16 @@ int main(int argc, char** argv) {
 
   PhantomCiphertext out;
   std::vector<double> times;
+  uint64_t tk = 0, tp = 0, tc = 0;
   for (int it = 0; it < std::max(1, iters); ++it) {
     PHX_CHECK(hipDeviceSynchronize());
+    auto& tr = traffic::counters();
+    const uint64_t k0 = tr.keys, p0 = tr.plaintexts, c0 = tr.ciphertexts;
     const double a = now_ms();
     out = boot.EvalBootstrap(ct, ctx);
+    tk = tr.keys - k0;
+    tp = tr.plaintexts - p0;
+    tc = tr.ciphertexts - c0;
     PHX_CHECK(hipDeviceSynchronize());
     times.push_back(now_ms() - a);
   }
@@ -375,9 +382,10 @@ int main(int argc, char** argv) {
   double total = 0;
   for (double t : times) total += t;
   std::printf("{\"stage\": \"bootstrap\", \"ms_total\": %.2f, \"ms_median\": %.2f, \"ms_min\": %.2f, \"runs\": %zu, \"avg_bits\": %.2f, "
-              "\"max_abs_err\": %.3e, \"chain_in\": %zu, \"chain_out\": %zu, \"levels_after\": %zu}\n",
+              "\"max_abs_err\": %.3e, \"chain_in\": %zu, \"chain_out\": %zu, \"levels_after\": %zu, "
+              "\"alg_bytes\": {\"keys\": %llu, \"plaintexts\": %llu, \"ciphertexts\": %llu}}\n",
               total, times[times.size() / 2], times[0], times.size(), bits_avg, err, ct.chain_index(), out.chain_index(),
-              levels_after);
+              levels_after, (unsigned long long)tk, (unsigned long long)tp, (unsigned long long)tc);
   g_ok &= bits_avg > 9.85;
   std::printf("{\"done\": \"boot\", \"ok\": %s}\n", g_ok ? "true" : "false");
   return g_ok ? 0 : 1;

@@ -13,6 +13,7 @@
 #include "../csrc/rns.h"
 #include "evaluate.h"
 #include "numth.h"
+#include "traffic.h"
 
 namespace phantom {
 
@@ -712,6 +713,14 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
     la.out[i] = inner[i].data();
   }
   hip_ok(phx::lt_bsgs(la, n, s), "linear transform inner products");
+  {
+    // the level's non-zero diagonals read once; the baby steps read and the inner sums written
+    // once; the input read once (by the modup) and the output written once (after the giant steps)
+    size_t nz = 0;
+    for (const auto& p : lv.pts) nz += p ? 1 : 0;
+    traffic::plaintexts(traffic::limb_bytes(nz * QlP, n));
+    traffic::ciphertexts(traffic::limb_bytes(2 * QlP * static_cast<size_t>(lv.g + lv.b), n));
+  }
   baby.clear();
   // giant steps accumulate in the extended basis (one moddown at the end), spread over the
   // context's streams (giant i on chain i mod k); inner[] (main-stream buffers) lives until all
@@ -735,6 +744,8 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
   inner.clear();
   acc.set_scale(ct.scale() * sf_.at(lv.chain - 1));
   acc.SetNoiseScaleDeg(2);
+  // giant steps: each inner sum read once, the level's result written once
+  traffic::ciphertexts(traffic::limb_bytes(2 * QlP * static_cast<size_t>(lv.b) + 2 * (Ql - 1), n));
   return KeySwitchDownRescale(cc, acc);
 }
 

@@ -1,6 +1,12 @@
 #include "buffer.h"
+#include "traffic.h"
 
 namespace phantom {
+
+traffic::Counters& traffic::counters() {
+  static Counters c;
+  return c;
+}
 
 bool debug_sync_enabled() {
   static const bool on = [] {

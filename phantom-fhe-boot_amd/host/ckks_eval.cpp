@@ -10,6 +10,7 @@
 #include "../csrc/rns.h"
 #include "evaluate.h"
 #include "numth.h"
+#include "traffic.h"
 
 namespace phantom {
 
@@ -65,6 +66,7 @@ std::vector<double> precompute_scaling_factors(const PhantomContext& ctx, double
 void mult_by_real_integer_inplace(const PhantomContext& ctx, PhantomCiphertext& ct, double k) {
   const auto& mods = ctx.get_context_data(ct.chain_index()).moduli();
   const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size();
+  traffic::ciphertexts(traffic::limb_bytes(2 * ct.size() * L, n));
   std::vector<uint64_t> r(L);
   for (size_t l = 0; l < L; ++l) r[l] = residue_of_double(k, mods[l]);
   if (L <= static_cast<size_t>(phx::kMaxScalarLimbs)) {
@@ -116,6 +118,7 @@ void MultByMonomialInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, uin
   const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size();
   hipStream_t s = ctx.stream();
   const uint64_t* mono = ctx.monomial_ntt(power, L);
+  traffic::ciphertexts(traffic::limb_bytes(2 * ct.size() * L, n));
   hip_ok(phx::poly_mul(ct.data(), mono, ct.data(), ctx.mod_QP(), n, L, s, ct.size(), 0), "monomial");
 }
 
@@ -259,6 +262,8 @@ PhantomCiphertext RelinearizeRescale(const PhantomContext& ctx, const PhantomCip
   hip_ok(phx::keyswitch_inner_prod(t_mod_up, rlk.public_keys_ptr(), cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, Ql,
                                    ctx.size_Q(), ctx.size_P(), beta, s, add),
          "relinearize inner product");
+  traffic::keys(traffic::limb_bytes(beta * 2 * QlP, n));
+  traffic::ciphertexts(traffic::limb_bytes(3 * Ql + 2 * (Ql - 1), n));  // d read, the rescaled result written
   PhantomCiphertext out;
   out.resize(ctx, d.chain_index() + 1, 2, s, false);
   rt.moddown_rescale(out.data(), cx, ctx.gpu_rns_tables(), s, 2);
@@ -318,6 +323,7 @@ PhantomCiphertext MulAddRescale(const PhantomContext& ctx, const PhantomCipherte
     ta.c = limb_scalars(ctx, chain, terms[0].coeff * S / terms[0].ct->scale());
   }
   hip_ok(phx::tensor_lin(ta, n, L, s), "tensor + linear epilogue");
+  traffic::ciphertexts(traffic::limb_bytes(4 * L + 2 * L * terms.size(), n));  // a, b and the terms read
   for (size_t i = 1; i < terms.size(); ++i) {
     const ScaledTerm& t = terms[i];
     const phx::LimbScalars cb = limb_scalars(ctx, chain, t.coeff * S / t.ct->scale());
@@ -358,6 +364,7 @@ PhantomCiphertext RaiseMod(const PhantomContext& ctx, const PhantomCiphertext& c
   out.set_scale(ct.scale());
   out.set_ntt_form(true);
   out.SetNoiseScaleDeg(ct.GetNoiseScaleDeg());
+  traffic::ciphertexts(traffic::limb_bytes(2 + 2 * Q, n));
   return out;
 }
 
@@ -381,6 +388,7 @@ DeviceBuffer<uint64_t> EvalFastRotationPrecompute(const PhantomContext& ctx, con
   const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P();
   DeviceBuffer<uint64_t> digits(rt.beta() * QlP * n, ctx.stream());
   rt.modup(digits.get(), ct.data() + Ql * n, ctx.gpu_rns_tables(), ctx.stream());
+  traffic::ciphertexts(traffic::limb_bytes(2 * Ql, n));  // (c0, c1) of the rotated ciphertext read
   return digits;
 }
 
@@ -395,6 +403,8 @@ PhantomCiphertext EvalFastAutomorphismExt(const PhantomContext& ctx, const Phant
   hip_ok(phx::keyswitch_inner_prod(digits, keys.get(elt).public_keys_ptr(), cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n,
                                    Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s, phx::KsAddend{}),
          "fast rotation inner product");
+  traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP, n));
+  traffic::ciphertexts(traffic::limb_bytes(2 * QlP, n));  // the rotated extended ciphertext written
   PhantomCiphertext out;
   out.resize(2, QlP, n, s, false);
   out.set_chain_index(ct.chain_index());
@@ -431,6 +441,7 @@ void EvalRotateExtAccumulate(const PhantomContext& ctx, PhantomCiphertext& ext, 
                                    ctx.mod_QP().barrett, n, Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s,
                                    phx::KsAddend{}),
          "giant step inner product");
+  traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP, n));
   if (!accumulate) {
     acc.resize(2, QlP, n, s, false);
     acc.set_chain_index(ext.chain_index());
@@ -482,6 +493,7 @@ PhantomCiphertext KeySwitchDown(const PhantomContext& ctx, PhantomCiphertext& ex
   PhantomCiphertext out;
   out.resize(ctx, ext.chain_index(), 2, s, false);
   rt.moddown_add(out.data(), ext.data(), false, ctx.gpu_rns_tables(), s, 2);
+  traffic::ciphertexts(traffic::limb_bytes(2 * QlP + 2 * Ql, ctx.poly_degree()));
   out.set_scale(ext.scale());
   out.SetNoiseScaleDeg(ext.GetNoiseScaleDeg());
   out.set_ntt_form(true);

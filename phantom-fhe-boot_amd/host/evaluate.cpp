@@ -7,6 +7,7 @@
 
 #include "../csrc/rns.h"
 #include "numth.h"
+#include "traffic.h"
 
 namespace phantom {
 
@@ -24,6 +25,8 @@ void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, 
   hip_ok(phx::keyswitch_inner_prod(t_mod_up, evk, cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, size_Ql,
                                    ctx.size_Q(), ctx.size_P(), beta, s),
          "keyswitch inner product");
+  traffic::keys(traffic::limb_bytes(beta * 2 * size_QlP, n));
+  traffic::ciphertexts(traffic::limb_bytes(5 * size_Ql, n));  // c2 + (c0, c1) read, (c0, c1) written
   rt.moddown_add(ct, cx, true, ctx.gpu_rns_tables(), s, 2);
 }
 
@@ -42,6 +45,7 @@ void add_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomC
   if (a.size() != b.size()) throw std::invalid_argument("poly number mismatch");
   const size_t n = ctx.poly_degree(), L = a.coeff_modulus_size();
   hip_ok(phx::poly_add(a.data(), b.data(), a.data(), ctx.mod_QP(), n, L, ctx.stream(), a.size()), "add");
+  traffic::ciphertexts(traffic::limb_bytes(3 * a.size() * L, n));
 }
 
 void sub_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b, bool negate) {
@@ -52,6 +56,7 @@ void sub_inplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomC
   const uint64_t* y = b.data();
   if (negate) hip_ok(phx::poly_sub(y, x, x, ctx.mod_QP(), n, L, ctx.stream(), a.size()), "sub");
   else hip_ok(phx::poly_sub(x, y, x, ctx.mod_QP(), n, L, ctx.stream(), a.size()), "sub");
+  traffic::ciphertexts(traffic::limb_bytes(3 * a.size() * L, n));
 }
 
 void negate_inplace(const PhantomContext& ctx, PhantomCiphertext& a) {

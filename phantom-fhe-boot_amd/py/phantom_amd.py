@@ -51,6 +51,8 @@ _SIGS = {
     "phantom_boot_session_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_uint32,
                                                    ctypes.c_uint32, ctypes.c_uint32, vp, ctypes.POINTER(vp)]),
     "phantom_boot_session_destroy": (ctypes.c_int, [vp]),
+    "phantom_traffic_read": (ctypes.c_int, [vp]),
+    "phantom_traffic_reset": (ctypes.c_int, []),
     "phantom_lt_bsgs": (ctypes.c_int, [vp, sz, ctypes.POINTER(vp), sz, ctypes.POINTER(vp), sz, ctypes.POINTER(vp), vp]),
     "phantom_keyswitch_ext": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_fast_rotation_ext": (ctypes.c_int, [vp, sz, vp, vp, ctypes.POINTER(vp), sz, ctypes.c_uint32, ctypes.c_int,
@@ -234,6 +236,19 @@ class BootSession:
             self.close()
         except Exception:
             pass
+
+
+def traffic():
+    """algorithmic bytes counted since the last reset: {"keys", "plaintexts", "ciphertexts", "total"}"""
+    out = (ctypes.c_uint64 * 3)()
+    check(load().phantom_traffic_read(out))
+    d = {"keys": out[0], "plaintexts": out[1], "ciphertexts": out[2]}
+    d["total"] = sum(d.values())
+    return d
+
+
+def traffic_reset():
+    check(load().phantom_traffic_reset())
 
 
 def bit_precision(ref, actual):
