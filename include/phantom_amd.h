@@ -79,6 +79,30 @@ int phantom_nwt_backward_inplace_include_special_mod(uint64_t *inout, const phan
                                                      size_t coeff_modulus_size, size_t start_modulus_idx,
                                                      size_t size_QP, size_t size_P, hipStream_t stream);
 
+/* nwt_2d_radix8_backward_inplace_scale (include/ntt.cuh:213-215): in place, output times scale[limb] */
+int phantom_nwt_backward_inplace_scale(uint64_t *inout, const phantom_ntt_tables *tables, size_t coeff_modulus_size,
+                                       size_t start_modulus_idx, const uint64_t *scale, const uint64_t *scale_shoup,
+                                       hipStream_t stream);
+/* nwt_2d_radix8_forward_inplace_include_special_mod (include/ntt.cuh:187-190) */
+int phantom_nwt_forward_include_special_mod(uint64_t *inout, const phantom_ntt_tables *tables,
+                                            size_t coeff_modulus_size, size_t start_modulus_idx, size_t size_QP,
+                                            size_t size_P, hipStream_t stream);
+/* nwt_2d_radix8_forward_inplace_fuse_moddown (include/ntt.cuh:176-180, src/ntt/ntt_moddown.cu:106-261):
+ * ct = (cx - NTT(delta)) * bigPInv_mod_q per limb; delta (coefficient form) is the NTT input and
+ * is not written back (this engine's epilogue form) */
+int phantom_nwt_forward_fuse_moddown(uint64_t *ct, const uint64_t *cx, const uint64_t *bigPInv_mod_q,
+                                     const uint64_t *bigPInv_mod_q_shoup, uint64_t *delta,
+                                     const phantom_ntt_tables *tables, size_t coeff_modulus_size,
+                                     size_t start_modulus_idx, hipStream_t stream);
+/* fnwt_1d / inwt_1d (include/ntt.cuh:157-169, src/ntt/ntt_1d.cu): the radix-2 single-workgroup path,
+ * n = 2^3 .. 2^11 (the 2-D launchers above use it for n < 2^10).  inwt_1d multiplies by
+ * scalar[limb] when scalar / scalar_shoup are given (device arrays, may be NULL). */
+int phantom_fnwt_1d(uint64_t *inout, const phantom_ntt_tables *tables, size_t coeff_modulus_size,
+                    size_t start_modulus_idx, hipStream_t stream);
+int phantom_inwt_1d(uint64_t *inout, const phantom_ntt_tables *tables, size_t coeff_modulus_size,
+                    size_t start_modulus_idx, const uint64_t *scalar, const uint64_t *scalar_shoup,
+                    hipStream_t stream);
+
 /* ---- context (PhantomContext, include/context.cuh:133-272; src/context.cu:121-232) ------ */
 typedef struct phantom_context phantom_context;
 /* moduli: the full key-level chain (data primes then special_modulus_size special primes),

@@ -180,4 +180,55 @@ int phantom_nwt_backward_inplace_include_special_mod(uint64_t* inout, const phan
   });
 }
 
+int phantom_nwt_backward_inplace_scale(uint64_t* inout, const phantom_ntt_tables* tables, size_t L, size_t start,
+                                       const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream) {
+  return phantom_nwt_backward_scale(inout, inout, tables, L, start, scale, scale_shoup, stream);
+}
+
+int phantom_nwt_forward_include_special_mod(uint64_t* inout, const phantom_ntt_tables* tables, size_t L, size_t start,
+                                            size_t size_QP, size_t size_P, hipStream_t stream) {
+  return phantom_nwt_forward_include_special_mod_exclude_range(inout, tables, L, start, size_QP, size_P, start, start,
+                                                               stream);
+}
+
+int phantom_nwt_forward_fuse_moddown(uint64_t* ct, const uint64_t* cx, const uint64_t* bigPInv_mod_q,
+                                     const uint64_t* bigPInv_mod_q_shoup, uint64_t* delta,
+                                     const phantom_ntt_tables* tables, size_t L, size_t start, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (int s = check_range(tables, L, start)) return s;
+    if (!ct || !cx || !bigPInv_mod_q || !bigPInv_mod_q_shoup || !delta)
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    const size_t n = tables->dev->n();
+    // NTT(delta) is not stored: the epilogue writes ct = (cx - NTT(delta)) P^-1 directly
+    phx::NttEpilogue epi;
+    epi.c = cx + start * n;
+    epi.out = ct + start * n;
+    epi.w = bigPInv_mod_q + start;
+    epi.ws = bigPInv_mod_q_shoup + start;
+    uint64_t* d = delta + start * n;
+    return from_hip(phx::ntt_forward_fused(tables->dev->get(), d, d, phx::LimbMap::contiguous((int)L, (int)start),
+                                           nullptr, 0, epi, stream));
+  });
+}
+
+int phantom_fnwt_1d(uint64_t* inout, const phantom_ntt_tables* tables, size_t L, size_t start, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (int s = check_range(tables, L, start)) return s;
+    const size_t n = tables->dev->n();
+    return from_hip(phx::ntt_1d_forward(tables->dev->get(), inout + start * n,
+                                        phx::LimbMap::contiguous((int)L, (int)start), stream));
+  });
+}
+
+int phantom_inwt_1d(uint64_t* inout, const phantom_ntt_tables* tables, size_t L, size_t start, const uint64_t* scalar,
+                    const uint64_t* scalar_shoup, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (int s = check_range(tables, L, start)) return s;
+    if ((scalar == nullptr) != (scalar_shoup == nullptr)) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "scalar pair");
+    const size_t n = tables->dev->n();
+    return from_hip(phx::ntt_1d_inverse(tables->dev->get(), inout + start * n,
+                                        phx::LimbMap::contiguous((int)L, (int)start), scalar, scalar_shoup, stream));
+  });
+}
+
 }  // extern "C"

@@ -102,4 +102,11 @@ hipError_t ntt_forward_fused(const NttTables& t, const uint64_t* in, uint64_t* o
 hipError_t ntt_inverse(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                        const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream);
 
+// The 1-D radix-2 path (fnwt_1d / inwt_1d, include/ntt.cuh:157-169, src/ntt/ntt_1d.cu): one
+// workgroup per limb, the limb in LDS; n = 2^3 .. 2^11.  ntt_forward / ntt_inverse use it for
+// n < 2^10; these entry points force it (the reference's test_nwt_1d covers n = 2^8 .. 2^11).
+hipError_t ntt_1d_forward(const NttTables& t, uint64_t* inout, const LimbMap& map, hipStream_t stream);
+hipError_t ntt_1d_inverse(const NttTables& t, uint64_t* inout, const LimbMap& map, const uint64_t* scale,
+                          const uint64_t* scale_shoup, hipStream_t stream);
+
 }  // namespace phx

@@ -738,6 +738,101 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
     sync();  // trow / lrow of the next item are rewritten
   }
 }
+// ---------------------------------------------------------------------------------------
+// 1-D path for small transforms, n = 2^8 .. 2^11 (the reference's radix-2 fnwt_1d / inwt_1d,
+// src/ntt/ntt_1d.cu): one workgroup of n/2 threads per limb, the limb in LDS, one butterfly per
+// thread and stage, the reference's in-place loop order and twiddle indices (tw[m + j]).  Integer
+// Shoup butterflies for every prime; the prologue / epilogue / scale of the 2-D path are honoured
+// so every launcher works at these degrees.
+// ---------------------------------------------------------------------------------------
+constexpr int kMaxLog1D = 11;
+
+template <bool FWD>
+__global__ __launch_bounds__(1024) void ntt_1d(KArgs a) {
+  __shared__ uint64_t v[1 << kMaxLog1D];
+  const int n = a.n, half = n >> 1;
+  int poly, buf_limb, row;
+  resolve_limb(a, blockIdx.x, poly, buf_limb, row);
+  poly = __builtin_amdgcn_readfirstlane(poly);
+  buf_limb = __builtin_amdgcn_readfirstlane(buf_limb);
+  row = __builtin_amdgcn_readfirstlane(row);
+  const uint64_t q = a.modulus[row], q2 = q << 1;
+  const uint64_t* tw = a.tw + (size_t)row * n;
+  const uint64_t* tws = a.tws + (size_t)row * n;
+  const size_t e0 = (size_t)buf_limb * n;
+  const uint32_t i = threadIdx.x;
+  for (int k = i; k < n; k += half) {
+    uint64_t x;
+    if (FWD && a.bcast) x = barrett_reduce_64(a.bcast[poly * a.bcast_stride + k], q, a.barrett[2 * row + 1]);
+    else x = a.in[poly * a.map.in_stride + e0 + k];
+    v[k] = x;
+  }
+  __syncthreads();
+  if constexpr (FWD) {
+    for (int m = 1, t = half; m < n; m <<= 1, t >>= 1) {
+      const int j = i / t, k = i % t, i1 = 2 * j * t + k;
+      uint64_t x = v[i1], y = v[i1 + t];
+      ct_bfly(x, y, tw[m + j], tws[m + j], q);
+      v[i1] = x;
+      v[i1 + t] = y;
+      __syncthreads();
+    }
+  } else {
+    for (int m = half, t = 1; m >= 1; m >>= 1, t <<= 1) {
+      const int j = i / t, k = i % t, i1 = 2 * j * t + k;
+      uint64_t x = v[i1], y = v[i1 + t];
+      gs_bfly(x, y, tw[m + j], tws[m + j], q);
+      v[i1] = x;
+      v[i1 + t] = y;
+      __syncthreads();
+    }
+  }
+  uint64_t* out = a.out + poly * a.map.out_stride + e0;
+  for (int k = i; k < n; k += half) {
+    uint64_t y = v[k];
+    if constexpr (FWD) {
+      y = csub(csub(y, q2), q);
+      if (a.epi.out) {
+        uint64_t* o = a.epi.out + poly * a.epi.out_stride + e0 + k;
+        uint64_t r = mul_shoup(sub_mod(a.epi.c[poly * a.epi.c_stride + e0 + k], y, q), a.epi.w[buf_limb],
+                               a.epi.ws[buf_limb], q);
+        if (a.epi.accumulate) r = add_mod(r, *o, q);
+        *o = r;
+        continue;
+      }
+    } else {
+      y = mul_shoup(y, a.n_inv[row], a.n_inv_shoup[row], q);
+      if (a.scale) y = mul_shoup(y, a.scale[buf_limb], a.scale_shoup[buf_limb], q);
+    }
+    out[k] = y;
+  }
+}
+
+hipError_t launch_1d(const NttTables& tb, const uint64_t* in, uint64_t* out, const LimbMap& map, bool inverse,
+                     const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream, const uint64_t* bcast,
+                     size_t bcast_stride, const NttEpilogue& epi) {
+  if (tb.log_n < 3 || tb.log_n > kMaxLog1D) return hipErrorInvalidValue;
+  const int per_poly = map.num_limbs - (map.skip_end - map.skip_begin);
+  if (per_poly <= 0 || map.polys <= 0) return hipSuccess;
+  KArgs a{};
+  a.in = in; a.out = out; a.modulus = tb.modulus;
+  a.tw = inverse ? tb.itw : tb.tw;
+  a.tws = inverse ? tb.itw_shoup : tb.tw_shoup;
+  a.n_inv = tb.n_inv; a.n_inv_shoup = tb.n_inv_shoup;
+  a.scale = scale; a.scale_shoup = scale_shoup;
+  a.map = map; a.n = (int)tb.n; a.limbs = per_poly * map.polys; a.limbs_per_poly = per_poly;
+  a.barrett = tb.barrett;
+  a.bcast = inverse ? nullptr : bcast;
+  a.bcast_stride = bcast_stride;
+  a.epi = inverse ? NttEpilogue{} : epi;
+  if (a.map.in_stride == 0) a.map.in_stride = (size_t)map.num_limbs * tb.n;
+  if (a.map.out_stride == 0) a.map.out_stride = (size_t)map.num_limbs * tb.n;
+  const dim3 grid(a.limbs), block(std::max<unsigned>(64, (unsigned)tb.n / 2));
+  if (inverse) hipLaunchKernelGGL(ntt_1d<false>, grid, block, 0, stream, a);
+  else hipLaunchKernelGGL(ntt_1d<true>, grid, block, 0, stream, a);
+  return hipGetLastError();
+}
+
 // compute units of the current device (cached per device id)
 int num_cus() {
   static int cache[64] = {0};
@@ -810,6 +905,8 @@ hipError_t dispatch(const NttTables& tb, const uint64_t* in, uint64_t* out, cons
                     const uint64_t* bcast = nullptr, size_t bcast_stride = 0, const NttEpilogue& epi = NttEpilogue{}) {
 #define PHX_NTT_CASE(LOGN, A, B) \
   case LOGN: return launch<A, B>(tb, in, out, map, inverse, scale, scale_shoup, stream, bcast, bcast_stride, epi);
+  if (tb.log_n < 10)
+    return launch_1d(tb, in, out, map, inverse, scale, scale_shoup, stream, bcast, bcast_stride, epi);
   switch (tb.log_n) {
     PHX_NTT_CASE(10, 5, 5) PHX_NTT_CASE(11, 5, 6) PHX_NTT_CASE(12, 6, 6) PHX_NTT_CASE(13, 6, 7)
     PHX_NTT_CASE(14, 7, 7) PHX_NTT_CASE(15, 7, 8) PHX_NTT_CASE(16, 8, 8) PHX_NTT_CASE(17, 8, 9)
@@ -834,6 +931,15 @@ hipError_t ntt_forward_fused(const NttTables& t, const uint64_t* in, uint64_t* o
 hipError_t ntt_inverse(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                        const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream) {
   return dispatch(t, in, out, map, true, scale, scale_shoup, stream);
+}
+
+hipError_t ntt_1d_forward(const NttTables& t, uint64_t* inout, const LimbMap& map, hipStream_t stream) {
+  return launch_1d(t, inout, inout, map, false, nullptr, nullptr, stream, nullptr, 0, NttEpilogue{});
+}
+
+hipError_t ntt_1d_inverse(const NttTables& t, uint64_t* inout, const LimbMap& map, const uint64_t* scale,
+                          const uint64_t* scale_shoup, hipStream_t stream) {
+  return launch_1d(t, inout, inout, map, true, scale, scale_shoup, stream, nullptr, 0, NttEpilogue{});
 }
 
 }  // namespace phx

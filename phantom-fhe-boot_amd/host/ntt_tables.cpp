@@ -41,7 +41,7 @@ DeviceNttTables::DeviceNttTables(size_t n, const std::vector<uint64_t>& moduli, 
   t_.n = n;
   t_.log_n = log2_exact(n);
   t_.num_moduli = L;
-  if (t_.log_n < 10 || t_.log_n > 17) throw std::invalid_argument("unsupported polynomial degree");
+  if (t_.log_n < 3 || t_.log_n > 17) throw std::invalid_argument("unsupported polynomial degree");
 
   std::vector<HostNttTable> host(L);
   {

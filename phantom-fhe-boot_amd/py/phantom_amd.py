@@ -29,6 +29,11 @@ _SIGS = {
     "phantom_nwt_backward_scale": (ctypes.c_int, [vp, vp, vp, sz, sz, vp, vp, vp]),
     "phantom_nwt_forward_include_special_mod_exclude_range": (ctypes.c_int, [vp, vp, sz, sz, sz, sz, sz, sz, vp]),
     "phantom_nwt_backward_inplace_include_special_mod": (ctypes.c_int, [vp, vp, sz, sz, sz, sz, vp]),
+    "phantom_nwt_backward_inplace_scale": (ctypes.c_int, [vp, vp, sz, sz, vp, vp, vp]),
+    "phantom_nwt_forward_include_special_mod": (ctypes.c_int, [vp, vp, sz, sz, sz, sz, vp]),
+    "phantom_nwt_forward_fuse_moddown": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, sz, sz, vp]),
+    "phantom_fnwt_1d": (ctypes.c_int, [vp, vp, sz, sz, vp]),
+    "phantom_inwt_1d": (ctypes.c_int, [vp, vp, sz, sz, vp, vp, vp]),
     "phantom_context_create": (ctypes.c_int, [sz, u64p, sz, sz, ctypes.POINTER(vp)]),
     "phantom_context_destroy": (ctypes.c_int, [vp]),
     "phantom_context_coeff_modulus_size": (sz, [vp, sz]),

@@ -40,7 +40,7 @@ def test_c1_ntt_4096_single_prime(rng):
         assert np.array_equal(to_host(d), a)
 
 
-@pytest.mark.parametrize("log_n", list(range(10, 18)))
+@pytest.mark.parametrize("log_n", list(range(8, 18)))
 @pytest.mark.parametrize("batch", [1, 10])
 def test_ntt_all_degrees(rng, log_n, batch):
     n = 1 << log_n
@@ -131,3 +131,72 @@ def test_invalid_exclude_range_is_rejected(c3):
     rc = PA.load().phantom_nwt_forward_include_special_mod_exclude_range(
         ptr(d), t.handle, 4, 2, 60, 1, 0, 3, stream())
     assert rc == 1 and b"Excluded range" in PA.load().phantom_last_error()
+
+
+@pytest.mark.parametrize("log_n", [8, 9, 10, 11])
+@pytest.mark.parametrize("batch", [1, 10])
+def test_nwt_1d(rng, log_n, batch):
+    """test/ntt_test.cu test_nwt_1d (:7-69): fnwt_1d / inwt_1d at n = 2^8 .. 2^11 with 50-bit primes,
+    the reference's constant-1 input and uniform inputs: INTT(NTT(x)) = x, and both directions
+    bit-exact against the oracle."""
+    n = 1 << log_n
+    mods = O.coeff_modulus_create(n, [50] * batch)
+    t = PA.NttTables(n, mods)
+    lib = PA.load()
+    for a in (np.ones(batch * n, dtype=np.uint64), O.random_limbs(rng, n, mods)):
+        d = to_dev(a)
+        PA.check(lib.phantom_fnwt_1d(ptr(d), t.handle, batch, 0, stream()))
+        assert np.array_equal(to_host(d), O.ntt_fwd(a, n, mods))
+        PA.check(lib.phantom_inwt_1d(ptr(d), t.handle, batch, 0, None, None, stream()))
+        assert np.array_equal(to_host(d), a)
+    t.close()
+
+
+def test_backward_inplace_scale(rng, c3):
+    n, mods, t = c3
+    L = 7
+    a = O.random_limbs(rng, n, mods[:L])
+    scale = [int(x) % q for x, q in zip(rng.integers(1, 2 ** 62, L), mods[:L])]
+    shoup = [(s << 64) // q for s, q in zip(scale, mods[:L])]
+    d = to_dev(a)
+    ds, dss = to_dev(O.arr(scale)), to_dev(O.arr(shoup))
+    PA.check(PA.load().phantom_nwt_backward_inplace_scale(ptr(d), t.handle, L, 0, ptr(ds), ptr(dss), stream()))
+    want = O.ntt_inv(a, n, mods[:L])
+    for l in range(L):
+        want[l * n:(l + 1) * n] = (want[l * n:(l + 1) * n].astype(object) * scale[l] % mods[l]).astype(np.uint64)
+    assert np.array_equal(to_host(d), want)
+
+
+def test_forward_include_special_mod(rng, c3):
+    n, mods, t = c3
+    size_QP, size_P, size_Ql = 60, 15, 9
+    qlp = mods[:size_Ql] + mods[size_QP - size_P:]
+    a = O.random_limbs(rng, n, qlp)
+    d = to_dev(a)
+    PA.check(PA.load().phantom_nwt_forward_include_special_mod(ptr(d), t.handle, size_Ql + size_P, 0, size_QP,
+                                                               size_P, stream()))
+    got = to_host(d)
+    for i, q in enumerate(qlp):
+        sl = slice(i * n, (i + 1) * n)
+        assert np.array_equal(got[sl], O.ntt_fwd(a[sl], n, [q])), i
+
+
+def test_forward_fuse_moddown(rng, c3):
+    """nwt_2d_radix8_forward_inplace_fuse_moddown: ct = (cx - NTT(delta)) * P^-1 per limb."""
+    n, mods, t = c3
+    L = 12
+    cx = O.random_limbs(rng, n, mods[:L])
+    delta = O.random_limbs(rng, n, mods[:L])
+    pinv = [int(x) % q for x, q in zip(rng.integers(1, 2 ** 62, L), mods[:L])]
+    pinvs = [(s << 64) // q for s, q in zip(pinv, mods[:L])]
+    dct, dcx, ddl = to_dev(np.zeros_like(cx)), to_dev(cx), to_dev(delta)
+    dp, dps = to_dev(O.arr(pinv)), to_dev(O.arr(pinvs))
+    PA.check(PA.load().phantom_nwt_forward_fuse_moddown(ptr(dct), ptr(dcx), ptr(dp), ptr(dps), ptr(ddl), t.handle, L,
+                                                        0, stream()))
+    nd = O.ntt_fwd(delta, n, mods[:L])
+    want = np.zeros_like(cx)
+    for l, q in enumerate(mods[:L]):
+        sl = slice(l * n, (l + 1) * n)
+        diff = (cx[sl].astype(object) - nd[sl].astype(object)) % q
+        want[sl] = (diff * pinv[l] % q).astype(np.uint64)
+    assert np.array_equal(to_host(dct), want)
