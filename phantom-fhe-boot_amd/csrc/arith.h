@@ -103,4 +103,46 @@ __device__ __forceinline__ void gs_bfly(uint64_t& x, uint64_t& y, uint64_t w, ui
   y = mul_shoup_lazy(d, w, ws, q);
 }
 
+// ---------------------------------------------------------------------------------------
+// NTT butterflies for the 2-D kernels' integer path (primes q < 2^61; MOD_BIT_COUNT_MAX = 61,
+// include/host/defines.h:4), with an approximate Shoup quotient.
+//
+// a ws = a1 s1 2^64 + (a1 s0 + a0 s1) 2^32 + a0 s0 (32-bit halves), so
+//   floor(a ws / 2^64) - [a1 s1 + hi(a1 s0) + hi(a0 s1)]  in {0, 1, 2}:
+// dropping a0 s0 and the low halves of the cross products loses less than 3 * 2^32 below 2^64.
+// Three multiplies instead of four, and the remainder a w - Q' q lies in [0, 4q) instead of
+// [0, 2q).  The butterflies keep the reference's structure (include/butterfly.cuh:10-37) with
+// the lazy ranges doubled: CT values in [0, 8q), GS values in [0, 4q); 8q < 2^64.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mulhi_approx(uint64_t a, uint64_t s) {
+  const uint32_t a0 = lo32(a), a1 = hi32(a), s0 = lo32(s), s1 = hi32(s);
+  const uint64_t h = static_cast<uint64_t>(__umulhi(a1, s0)) + __umulhi(a0, s1);
+  return static_cast<uint64_t>(a1) * s1 + h;
+}
+
+// a w mod q in [0, 4q) for any a < 2^64, w < q, ws = floor(w 2^64 / q)
+__device__ __forceinline__ uint64_t mul_shoup_lazy4(uint64_t a, uint64_t w, uint64_t ws, uint64_t q) {
+  return a * w - mulhi_approx(a, ws) * q;
+}
+
+// forward CT butterfly: x, y in [0, 8q) -> [0, 8q)
+__device__ __forceinline__ void ct_bfly8(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
+  const uint64_t q4 = q << 2;
+  const uint64_t t = mul_shoup_lazy4(y, w, ws, q);
+  const uint64_t u = csub(x, q4);
+  x = u + t;
+  y = u + q4 - t;
+}
+
+// inverse GS butterfly: x, y in [0, 4q) -> [0, 4q)
+__device__ __forceinline__ void gs_bfly4(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
+  const uint64_t q4 = q << 2;
+  const uint64_t d = x + q4 - y;
+  x = csub(x + y, q4);
+  y = mul_shoup_lazy4(d, w, ws, q);
+}
+
+// [0, 8q) -> [0, q)
+__device__ __forceinline__ uint64_t reduce8(uint64_t v, uint64_t q) { return csub(csub(csub(v, q << 2), q << 1), q); }
+
 }  // namespace phx

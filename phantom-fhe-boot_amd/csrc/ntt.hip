@@ -22,8 +22,9 @@
 //  * Column-pass twiddles come from a per-limb S1-entry table (cache resident); row-pass
 //    twiddles are generated: tw = A_g(row) * B_g(iloc) (host/ntt_tables.cpp), the 15 twiddles
 //    of the first radix-16 round (the same for all lanes of a row) cooperatively through LDS.
-//  * Integer path: the reference's lazy ranges ([0, 4q) forward, [0, 2q) inverse), twiddles and
-//    Shoup quotients read from the full tables, n^-1 applied after the last stage.
+//  * Integer path: the reference's butterflies with an approximate Shoup quotient and doubled lazy
+//    ranges ([0, 8q) forward, [0, 4q) inverse; arith.h), twiddles and Shoup quotients read from
+//    the full tables, n^-1 applied after the last stage.
 #include "ntt.h"
 
 #include <algorithm>
@@ -230,7 +231,7 @@ __device__ __forceinline__ void gs_round_f64(double (&v)[E], const double (&w)[E
   });
 }
 
-// forward CT round, integer path: values in [0, 4q)
+// forward CT round, integer path: values in [0, 8q) (ct_bfly8)
 template <int S_LOG, int R>
 __device__ __forceinline__ void ct_round_int(uint64_t (&v)[E], const uint64_t (&w)[E], const uint64_t (&ws)[E],
                                              uint64_t q) {
@@ -242,12 +243,12 @@ __device__ __forceinline__ void ct_round_int(uint64_t (&v)[E], const uint64_t (&
     for (int j = 0; j < E; ++j) {
       if (j & h) continue;
       const int sl = tw_slot<Rd::ex>(gl, tw_key<Rd::ex>(gl, j));
-      ct_bfly(v[j], v[j | h], w[sl], ws[sl], q);
+      ct_bfly8(v[j], v[j | h], w[sl], ws[sl], q);
     }
   }
 }
 
-// inverse GS round, integer path: stages in reverse order, values in [0, 2q)
+// inverse GS round, integer path: stages in reverse order, values in [0, 4q) (gs_bfly4)
 template <int S_LOG, int R>
 __device__ __forceinline__ void gs_round_int(uint64_t (&v)[E], const uint64_t (&w)[E], const uint64_t (&ws)[E],
                                              uint64_t q) {
@@ -259,7 +260,7 @@ __device__ __forceinline__ void gs_round_int(uint64_t (&v)[E], const uint64_t (&
     for (int j = 0; j < E; ++j) {
       if (j & h) continue;
       const int sl = tw_slot<Rd::ex>(gl, tw_key<Rd::ex>(gl, j));
-      gs_bfly(v[j], v[j | h], w[sl], ws[sl], q);
+      gs_bfly4(v[j], v[j | h], w[sl], ws[sl], q);
     }
   }
 }
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(CBLOCK, kWavesPerEU) void ntt_col(KArgs a) {
       });
       if constexpr (FWD) {
 #pragma unroll
-        for (int j = 0; j < E; ++j) store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, v[j]);  // lazy [0, 4q)
+        for (int j = 0; j < E; ++j) store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, v[j]);  // lazy [0, 8q)
       } else {
         const uint64_t ni = a.n_inv[tr.row], nis = a.n_inv_shoup[tr.row];
         const bool scaled = a.scale != nullptr;
@@ -712,13 +713,12 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
           ct_round_int<S2_LOG, R>(v, w, ws, lc.q);
         });
         if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, lrow, idx, sync, t);
-        const uint64_t q2 = lc.q << 1;
         if constexpr (EPI) {
 #pragma unroll
-          for (int j = 0; j < E; ++j) epilogue_store(a, tr, j, T, eo, csub(csub(v[j], q2), lc.q), lc.q);
+          for (int j = 0; j < E; ++j) epilogue_store(a, tr, j, T, eo, reduce8(v[j], lc.q), lc.q);
         } else {
 #pragma unroll
-          for (int j = 0; j < E; ++j) store_wt(dst + j * T, csub(csub(v[j], q2), lc.q));
+          for (int j = 0; j < E; ++j) store_wt(dst + j * T, reduce8(v[j], lc.q));
         }
       } else {
         if constexpr (RN > 1) relayout<S2_LOG, 0, RN - 1>(v, lrow, idx, sync, t);
@@ -730,7 +730,7 @@ __global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
           gs_round_int<S2_LOG, R>(v, w, ws, lc.q);
         });
 #pragma unroll
-        for (int j = 0; j < E; ++j) store_wt(dst + j * T, v[j]);  // [0, 2q), column pass follows
+        for (int j = 0; j < E; ++j) store_wt(dst + j * T, v[j]);  // [0, 4q), column pass follows
       }
     }
     if (!more) break;
@@ -909,7 +909,7 @@ hipError_t dispatch(const NttTables& tb, const uint64_t* in, uint64_t* out, cons
     return launch_1d(tb, in, out, map, inverse, scale, scale_shoup, stream, bcast, bcast_stride, epi);
   switch (tb.log_n) {
     PHX_NTT_CASE(10, 5, 5) PHX_NTT_CASE(11, 5, 6) PHX_NTT_CASE(12, 6, 6) PHX_NTT_CASE(13, 6, 7)
-    PHX_NTT_CASE(14, 7, 7) PHX_NTT_CASE(15, 7, 8) PHX_NTT_CASE(16, 8, 8) PHX_NTT_CASE(17, 8, 9)
+    PHX_NTT_CASE(14, 7, 7) PHX_NTT_CASE(15, 7, 8) PHX_NTT_CASE(16, PHX_NTT16_S1, 16 - PHX_NTT16_S1) PHX_NTT_CASE(17, 8, 9)
     default: return hipErrorInvalidValue;
   }
 #undef PHX_NTT_CASE

@@ -153,14 +153,31 @@ __global__ __launch_bounds__(kBlock) void tensor_kernel(const uint64_t* ct1, con
 // inputs (L2/MALL hits); J = 3..15 measured within 4% of each other (tools/c3_variants.sh).
 // ---------------------------------------------------------------------------------------
 constexpr int kMaxIbase = 64;
+
+// Block -> (coefficient chunk, output group).  The groups of one chunk read the same inputs, so
+// they are dealt to one XCD back to back (blocks b and b + 8 share an XCD under round-robin
+// placement; speed only, any placement is correct): the inputs come from HBM once and the other
+// groups hit that XCD's L2, instead of every group re-reading them from the Infinity Cache.
+struct BconvBlock {
+  uint32_t chunk;
+  int group;
+};
+__device__ __forceinline__ BconvBlock bconv_block(uint32_t chunks, int groups) {
+  const uint32_t b = blockIdx.x;
+  if (chunks % 8 == 0) {
+    const uint32_t x = b % 8, k = b / 8;
+    return {x + 8 * (k / groups), static_cast<int>(k % groups)};
+  }
+  return {b % chunks, static_cast<int>(b / chunks)};
+}
 #ifndef PHX_BCONV_J
 #define PHX_BCONV_J 5
 #endif
 constexpr int kBconvJ = PHX_BCONV_J;
 
 __device__ __forceinline__ void bconv_outputs(const BconvArgs& a, const uint64_t* tx, const uint64_t* ty, int ib,
-                                              uint32_t n, uint32_t k) {
-  const int j0 = blockIdx.y * kBconvJ, j1 = min(j0 + kBconvJ, a.obase_size);
+                                              uint32_t n, uint32_t k, int group) {
+  const int j0 = group * kBconvJ, j1 = min(j0 + kBconvJ, a.obase_size);
   for (int j = j0; j < j1; ++j) {
     u128 accx{0, 0}, accy{0, 0};
     const uint64_t p = a.obase[j], r0 = a.obase_barrett[2 * j], r1 = a.obase_barrett[2 * j + 1];
@@ -196,11 +213,12 @@ __device__ __forceinline__ void bconv_inputs(const BconvArgs& a, uint64_t* tx, u
 __global__ __launch_bounds__(kBlock) void bconv_kernel(BconvArgs a, uint32_t n, uint32_t pairs, bool prescale) {
   a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial
   a.out += blockIdx.z * a.out_stride;
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const BconvBlock bb = bconv_block((pairs + kBlock - 1) / kBlock, (a.obase_size + kBconvJ - 1) / kBconvJ);
+  const uint32_t i = bb.chunk * kBlock + threadIdx.x;
   if (i >= pairs) return;
   uint64_t tx[kMaxIbase], ty[kMaxIbase];
   bconv_inputs(a, tx, ty, a.ibase_size, n, 2 * i, prescale);
-  bconv_outputs(a, tx, ty, a.ibase_size, n, 2 * i);
+  bconv_outputs(a, tx, ty, a.ibase_size, n, 2 * i, bb.group);
 }
 
 // Fixed ibase <= 15: 30-bit limb splitting.  With t = th 2^30 + tl and c = ch 2^30 + cl (t, c <
@@ -216,7 +234,8 @@ __global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32
   // prove it, so direct reads would be vector loads inside the accumulation loop
   __shared__ uint32_t mlo[IB][kBconvJ], mhi[IB][kBconvJ];
   __shared__ uint64_t mp[kBconvJ][3];
-  const int j0 = blockIdx.y * kBconvJ;
+  const BconvBlock bb = bconv_block((pairs + kBlock - 1) / kBlock, (a.obase_size + kBconvJ - 1) / kBconvJ);
+  const int j0 = bb.group * kBconvJ;
   for (int e = threadIdx.x; e < IB * kBconvJ; e += kBlock) {
     const int sidx = e / kBconvJ, jj = e % kBconvJ;
     const uint64_t c = j0 + jj < a.obase_size ? a.qhat_mod_p[(size_t)sidx * a.obase_size + j0 + jj] : 0;
@@ -230,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32
     mp[threadIdx.x][2] = a.obase_barrett[2 * j + 1];
   }
   __syncthreads();
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i = bb.chunk * kBlock + threadIdx.x;
   if (i >= pairs) return;
   a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial
   a.out += blockIdx.z * a.out_stride;
@@ -470,7 +489,7 @@ hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s) {
   if (a.ibase_size <= 0 || a.ibase_size > kMaxIbase || a.obase_size <= 0) return hipErrorInvalidValue;
   const uint32_t pairs = static_cast<uint32_t>(n / 2);
   if (a.polys < 1) return hipErrorInvalidValue;
-  const dim3 g((pairs + kBlock - 1) / kBlock, (a.obase_size + kBconvJ - 1) / kBconvJ, a.polys);
+  const dim3 g(((pairs + kBlock - 1) / kBlock) * ((a.obase_size + kBconvJ - 1) / kBconvJ), 1, a.polys);
   const bool pre = a.qhat_inv != nullptr;
   switch (a.ibase_size) {
 #define PHX_BCONV_CASE(K)                                                                      \

@@ -6,7 +6,7 @@ build() {
   d=$ROOT/tools/variants/$name
   rm -rf $d && mkdir -p $d && cp -r $ROOT/phantom-fhe-boot_amd/csrc $ROOT/phantom-fhe-boot_amd/host $ROOT/phantom-fhe-boot_amd/examples $ROOT/phantom-fhe-boot_amd/Makefile $d/
   mkdir -p $d/py && cp $ROOT/phantom-fhe-boot_amd/py/phantom_amd.py $d/py/
-  make -C $d -j8 INCDIR=$ROOT/include HIPFLAGS="-std=c++20 -O3 -fPIC -Wall -ffp-contract=off -I$ROOT/include --offload-arch=gfx950 $*" > $d/build.log 2>&1
+  make -C $d -j4 INCDIR=$ROOT/include EXTRA="$*" lib/libphantom_amd.so > $d/build.log 2>&1
   echo built $name
 }
 rm -rf $ROOT/tools/variants

@@ -1,0 +1,11 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 400 python -u tools/time_variants.py > gpurun_out/variants_r02h.log 2>&1 || { tail -20 gpurun_out/variants_r02h.log; exit 1; }
+cat gpurun_out/variants_r02h.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_r02h.log 2>&1
+rc=$?
+tail -5 gpurun_out/pytest_gpu_r02h.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py > gpurun_out/bench_r02h.json 2> gpurun_out/bench_r02h.err || { tail -20 gpurun_out/bench_r02h.err; exit 1; }
+cat gpurun_out/bench_r02h.json

@@ -11,7 +11,12 @@ sys.path.insert(0, sys.argv[1])
 import phantom_amd as PA
 N, L = 1 << 16, 44
 lib = PA.load()
-mods = PA.coeff_modulus_create(N, [60] + [50] * 44 + [60] * 15)[:L]
+BITS = os.environ.get("NTT_BITS", "50")
+if BITS == "60":  # the C4 chain: Q = {60, 29 x 59}, P = 10 x 60 (bootstrapping_example.cu:69-116)
+    L = 40
+    mods = PA.coeff_modulus_create(N, [60] + [59] * 29 + [60] * 10)
+else:
+    mods = PA.coeff_modulus_create(N, [60] + [50] * 44 + [60] * 15)[:L]
 t = PA.NttTables(N, mods)
 rng = np.random.default_rng(1)
 base = np.concatenate([rng.integers(0, q, size=N, dtype=np.uint64) for q in mods])
@@ -46,7 +51,7 @@ print("RESULT", fwd, inv, b2b(lib.phantom_nwt_forward_inplace), b2b(lib.phantom_
 res = {}
 for name in sorted(os.listdir(os.path.join(ROOT, "tools", "variants"))):
     py = os.path.join(ROOT, "tools", "variants", name, "py")
-    out = subprocess.run([sys.executable, "-c", CODE, py], capture_output=True, text=True, timeout=300)
+    out = subprocess.run([sys.executable, "-c", CODE, py], capture_output=True, text=True, timeout=300, env=dict(os.environ))
     line = [l for l in out.stdout.splitlines() if l.startswith("RESULT")]
     if line:
         f, i, fb, ib = map(float, line[0].split()[1:])
@@ -56,4 +61,4 @@ for name in sorted(os.listdir(os.path.join(ROOT, "tools", "variants"))):
     else:
         res[name] = {"error": out.stderr[-500:]}
     print(name, res[name], flush=True)
-json.dump(res, open(os.path.join(ROOT, "gpurun_out", "variants.json"), "w"), indent=1)
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", "variants_%s.json" % os.environ.get("NTT_BITS", "50")), "w"), indent=1)
