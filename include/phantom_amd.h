@@ -215,7 +215,8 @@ int phantom_ciphertext_deserialize(const uint8_t *in, size_t len, phantom_ct_hea
  * in [polys][L][n] at chain_index -> out [polys][L-1][n] */
 int phantom_rescale_to_next(const phantom_context *ctx, size_t chain_index, const uint64_t *in, uint64_t *out,
                             size_t polys, hipStream_t stream);
-/* apply_galois_ntt (src/galois.cu:104-119) with the PrecomputeAutoMapKernel table (src/util.cu:941-958) */
+/* apply_galois_ntt (src/galois.cu:104-119) with the PrecomputeAutoMapKernel table (src/util.cu:941-958);
+ * out must not alias in (PHANTOM_ERR_INVALID_ARGUMENT) */
 int phantom_apply_galois_ntt(const phantom_context *ctx, uint32_t galois_elt, const uint64_t *in, uint64_t *out,
                              size_t coeff_modulus_size, hipStream_t stream);
 /* elementwise ops over limbs [limb_offset, limb_offset + L) of the key-level chain

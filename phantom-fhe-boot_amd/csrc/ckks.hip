@@ -99,21 +99,23 @@ __global__ __launch_bounds__(kBlock, 2) void lt_bsgs_kernel(LtArgs a, uint32_t l
     }
     for (int i = 0; i < a.b; ++i) {
       const uint64_t* const* prow = ptab + i * G;
-      uint64_t w[G];
-      // global (not flat) loads: they count in vmcnt only, so the LDS pointer reads between
-      // them do not wait for the plaintext data
-#pragma unroll
-      for (int j = 0; j < G; ++j) w[j] = ((const __attribute__((address_space(1))) uint64_t*)prow[j])[e];
-      // keep the G loads together in flight: the scheduler would otherwise sink each load to
-      // its first use (one memory round trip per term)
-      __builtin_amdgcn_sched_barrier(0);
       u128 acc[2] = {{0, 0}, {0, 0}};
 #pragma unroll
       for (int c0 = 0; c0 < G; c0 += kChunk) {
+        constexpr int C = G < kChunk ? G : kChunk;
+        uint64_t w[C];
+        // global (not flat) loads: they count in vmcnt only, so the LDS pointer reads between
+        // them do not wait for the plaintext data
+#pragma unroll
+        for (int j = 0; j < C; ++j) w[j] = ((const __attribute__((address_space(1))) uint64_t*)prow[c0 + j])[e];
+        // keep the chunk's loads together in flight: the scheduler would otherwise sink each load
+        // to its first use (one memory round trip per term)
+        __builtin_amdgcn_sched_barrier(0);
         uint64_t ll[2] = {0, 0}, m1[2] = {0, 0}, m2[2] = {0, 0}, hh[2] = {0, 0};
 #pragma unroll
-        for (int j = c0; j < c0 + kChunk && j < G; ++j) {
-          const uint32_t wl = static_cast<uint32_t>(w[j] & kM30), wh = static_cast<uint32_t>(w[j] >> 30);
+        for (int jj = 0; jj < C; ++jj) {
+          const int j = c0 + jj;
+          const uint32_t wl = static_cast<uint32_t>(w[jj] & kM30), wh = static_cast<uint32_t>(w[jj] >> 30);
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
             ll[t] += static_cast<uint64_t>(xl[t][j]) * wl;

@@ -569,8 +569,10 @@ __device__ __forceinline__ void row_load(uint64_t (&x)[E], const uint64_t* src) 
   for (int j = 0; j < E; ++j) x[j] = __builtin_nontemporal_load(src + j * Sub<S2_LOG>::T);
 }
 
+// The epilogue form holds its operands (EpiOperands) through the butterflies: two waves per SIMD
+// give it the registers to do so without spilling (168 VGPRs at three waves spilled 47).
 template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false>
-__global__ __launch_bounds__(BLOCK, kWavesPerEU) void ntt_row(KArgs a) {
+__global__ __launch_bounds__(BLOCK, EPI ? 2 : kWavesPerEU) void ntt_row(KArgs a) {
   using SB = Sub<S2_LOG>;
   using P = Plan<S1_LOG, S2_LOG>;
   constexpr int S1 = 1 << S1_LOG, S2 = SB::S, T = SB::T, RW = cmin(64 / T, S1), RSTR = S2 + S2 / 16, RN = SB::ROUNDS;

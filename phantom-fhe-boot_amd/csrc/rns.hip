@@ -373,22 +373,45 @@ __global__ __launch_bounds__(kBlock) void moddown_modup_finish_kernel(const uint
 
 // hoisted-rotation epilogue: out[t][l][j] (+)= x[t][l][perm j] with x = cx + (t == 0 ? c0 term : 0)
 // (MODE 0: none, 1: P c0 on the Ql limbs, 2: an extended-basis c0 on every limb)
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void galois_finish_kernel(GaloisFinishArgs a, uint32_t log_n, size_t total) {
-  const size_t nmask = (size_t(1) << log_n) - 1;
-  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
-    const uint32_t row = static_cast<uint32_t>(e >> log_n);  // t * QlP + l
-    const uint32_t t = row >= a.qlp ? 1 : 0, l = row - t * a.qlp;
-    const size_t src = (e & ~nmask) | a.perm[e & nmask];
-    const uint64_t q = a.q[l];
-    uint64_t v = a.cx[src];
-    if (t == 0) {
-      if constexpr (MODE == 1) {
-        if (l < a.ql) v = add_mod(v, mul_shoup(a.c0[src], a.pmod[l], a.pmod_shoup[l], q), q);
-      } else if constexpr (MODE == 2) {
-        v = add_mod(v, a.c0[src], q);
-      }
+// NTT-domain automorphisms (src/galois.cu:104-119) move whole blocks: output index i = brv(j)
+// reads brv(k) with k = ((2j + 1) g mod 2n) / 2, and the low m bits of k depend only on the low m
+// bits of j, so the top m bits of the source index depend only on the top m bits of i.  Every
+// output block of kGalB consecutive indices therefore reads one source block of kGalB consecutive
+// indices: a workgroup stages that block in LDS with coalesced loads and gathers from LDS, instead
+// of 64 scattered 8-byte reads per wave instruction from HBM.
+constexpr uint32_t kGalB = 1024;
+
+template <int MODE>  // 0: permute; 1: + P c0 on the Ql limbs of polynomial 0, then permute; 2: + c0
+__global__ __launch_bounds__(kBlock) void galois_finish_kernel(GaloisFinishArgs a, uint32_t log_n, uint32_t bsz) {
+  __shared__ uint64_t sx[kGalB], sc[kGalB];
+  const uint32_t nb = (1u << log_n) / bsz;  // blocks per limb
+  const uint32_t row = blockIdx.x / nb, ob = blockIdx.x % nb;  // row = t * QlP + l
+  const uint32_t t = row >= a.qlp ? 1 : 0, l = row - t * a.qlp;
+  const size_t rbase = (size_t)row << log_n;
+  const uint32_t* pm = a.perm + (size_t)ob * bsz;
+  const uint32_t sb = pm[0] & ~(bsz - 1);
+  const bool addc = t == 0 && (MODE == 2 || (MODE == 1 && l < a.ql));
+  for (uint32_t i = threadIdx.x; i < bsz / 2; i += kBlock) {
+    const u64x2 x = ld2(a.cx + rbase + sb + 2 * i);
+    sx[2 * i] = x.x;
+    sx[2 * i + 1] = x.y;
+    if (addc) {
+      const u64x2 c = ld2(a.c0 + rbase + sb + 2 * i);
+      sc[2 * i] = c.x;
+      sc[2 * i + 1] = c.y;
     }
+  }
+  __syncthreads();
+  const uint64_t q = a.q[l];
+  const uint64_t w = MODE == 1 && addc ? a.pmod[l] : 0, ws = MODE == 1 && addc ? a.pmod_shoup[l] : 0;
+  for (uint32_t i = threadIdx.x; i < bsz; i += kBlock) {
+    const uint32_t src = pm[i] & (bsz - 1);
+    uint64_t v = sx[src];
+    if (addc) {
+      if constexpr (MODE == 1) v = add_mod(v, mul_shoup(sc[src], w, ws, q), q);
+      else if constexpr (MODE == 2) v = add_mod(v, sc[src], q);
+    }
+    const size_t e = rbase + (size_t)ob * bsz + i;
     if (a.accumulate) v = add_mod(v, a.out[e], q);
     a.out[e] = v;
   }
@@ -396,12 +419,20 @@ __global__ __launch_bounds__(kBlock) void galois_finish_kernel(GaloisFinishArgs 
 
 __global__ __launch_bounds__(kBlock) void galois_kernel(const uint64_t* __restrict__ in, uint64_t* out,
                                                         const uint32_t* __restrict__ perm, uint32_t log_n,
-                                                        size_t total) {
-  const size_t mask = (size_t(1) << log_n) - 1;
-  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < total; i += (size_t)gridDim.x * kBlock) {
-    const size_t base = i & ~mask;
-    out[i] = in[base + perm[i & mask]];
+                                                        uint32_t bsz) {
+  __shared__ uint64_t sx[kGalB];
+  const uint32_t nb = (1u << log_n) / bsz;
+  const uint32_t row = blockIdx.x / nb, ob = blockIdx.x % nb;
+  const size_t rbase = (size_t)row << log_n;
+  const uint32_t* pm = perm + (size_t)ob * bsz;
+  const uint32_t sb = pm[0] & ~(bsz - 1);
+  for (uint32_t i = threadIdx.x; i < bsz / 2; i += kBlock) {
+    const u64x2 x = ld2(in + rbase + sb + 2 * i);
+    sx[2 * i] = x.x;
+    sx[2 * i + 1] = x.y;
   }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < bsz; i += kBlock) out[rbase + (size_t)ob * bsz + i] = sx[pm[i] & (bsz - 1)];
 }
 
 __global__ __launch_bounds__(kBlock) void raise_kernel(const uint64_t* in_q0, uint64_t* out, const uint64_t* q,
@@ -535,21 +566,23 @@ hipError_t moddown_modup_finish(const uint64_t* c1, const uint64_t* delta, const
 }
 
 hipError_t galois_finish(const GaloisFinishArgs& a, int mode, size_t n, hipStream_t s) {
-  const size_t total = 2 * n * a.qlp;
-  const uint32_t log_n = __builtin_ctzll(n);
+  if (mode < 0 || mode > 2 || a.qlp == 0) return mode < 0 || mode > 2 ? hipErrorInvalidValue : hipSuccess;
+  const uint32_t log_n = __builtin_ctzll(n), bsz = static_cast<uint32_t>(std::min<size_t>(n, kGalB));
+  const dim3 grid(static_cast<uint32_t>(2 * a.qlp * (n / bsz)));
   switch (mode) {
-    case 0: galois_finish_kernel<0><<<grid_for(total), kBlock, 0, s>>>(a, log_n, total); break;
-    case 1: galois_finish_kernel<1><<<grid_for(total), kBlock, 0, s>>>(a, log_n, total); break;
-    case 2: galois_finish_kernel<2><<<grid_for(total), kBlock, 0, s>>>(a, log_n, total); break;
-    default: return hipErrorInvalidValue;
+    case 0: galois_finish_kernel<0><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
+    case 1: galois_finish_kernel<1><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
+    default: galois_finish_kernel<2><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
   }
   return hipGetLastError();
 }
 
 hipError_t galois_ntt(const uint64_t* in, uint64_t* out, const uint32_t* perm, size_t n, size_t L,
                       hipStream_t s) {
-  const size_t total = n * L;
-  galois_kernel<<<grid_for(total), kBlock, 0, s>>>(in, out, perm, __builtin_ctzll(n), total);
+  if (in == out) return hipErrorInvalidValue;  // blocks are read while others are written
+  if (L == 0) return hipSuccess;
+  const uint32_t bsz = static_cast<uint32_t>(std::min<size_t>(n, kGalB));
+  galois_kernel<<<static_cast<uint32_t>(L * (n / bsz)), kBlock, 0, s>>>(in, out, perm, __builtin_ctzll(n), bsz);
   return hipGetLastError();
 }
 
