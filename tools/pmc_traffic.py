@@ -31,10 +31,12 @@ def main():
         rd = 2 * 1024 * sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"]) if d.get("FETCH_SIZE") else None
         wr = 1024 * sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) if d.get("WRITE_SIZE") else None
         out["kernels"][k] = {"read_bytes": rd, "write_bytes": wr, "dispatches": len(d.get("FETCH_SIZE", []))}
-    fwd = [v for k, v in out["kernels"].items() if k.endswith("true>")]
+    def is_fwd(k):  # ntt_col<S1, S2, FWD> / ntt_row<S1, S2, FWD, EPI>
+        return k.split("<")[1].rstrip(">").split(",")[2].strip() == "true"
+    fwd = [v for k, v in out["kernels"].items() if is_fwd(k)]
     if fwd and all(v["read_bytes"] is not None and v["write_bytes"] is not None for v in fwd):
         out["forward_ntt_bytes_per_launch"] = sum(v["read_bytes"] + v["write_bytes"] for v in fwd)
-    inv = [v for k, v in out["kernels"].items() if k.endswith("false>")]
+    inv = [v for k, v in out["kernels"].items() if not is_fwd(k)]
     if inv and all(v["read_bytes"] is not None and v["write_bytes"] is not None for v in inv):
         out["inverse_ntt_bytes_per_launch"] = sum(v["read_bytes"] + v["write_bytes"] for v in inv)
     print(json.dumps(out, indent=1))
