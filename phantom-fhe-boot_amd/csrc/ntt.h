@@ -99,6 +99,25 @@ struct NttEpilogue {
 hipError_t ntt_forward_fused(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                              const uint64_t* bcast, size_t bcast_stride, const NttEpilogue& epi, hipStream_t stream);
 
+// Forward NTT whose input is a fast base conversion (src/rns_bconv.cu:40-69, 143-179): buffer
+// limb i of polynomial p (processed index j = i minus the limbs of p's exclude range below it) is
+//   x[k] = sum_{s < ib[p]} in[p][s][k] * mat[p][s * ob + j]  mod q_row,
+// computed in the column pass's registers from the ib input limbs (coefficient form, already
+// multiplied by qHat_s^-1 — the INTT's scale), so the converted limbs never go to HBM.  It
+// replaces bconv + NTT in modup (per digit: the complement limbs), moddown (P -> Ql) and
+// moddown-rescale; `epi` is the NttEpilogue above.  Inputs and matrix entries < 2^60, ib <= 15
+// (30-bit split sums).  2-D sizes only (n >= 2^10): hipErrorNotSupported below.
+constexpr int kMaxBconvPolys = 8;
+struct BconvPrologue {
+  const uint64_t* in = nullptr;   // polynomial p's input limb s at in + p * in_stride + s * n
+  size_t in_stride = 0;
+  const uint64_t* mat[kMaxBconvPolys] = {};  // [ib][ob] per polynomial
+  int ib[kMaxBconvPolys] = {};
+  int ob = 0;
+};
+hipError_t ntt_forward_bconv(const NttTables& t, uint64_t* out, const LimbMap& map, const BconvPrologue& bcv,
+                             const NttEpilogue& epi, hipStream_t stream);
+
 // Inverse NTT.  When scale/scale_shoup are given (one value per buffer limb, indexed by
 // buffer limb), the output is additionally multiplied by scale[i] (the reference's
 // nwt_2d_radix8_backward_scale used by modup, src/ntt/ntt_modup.cu:356-393).

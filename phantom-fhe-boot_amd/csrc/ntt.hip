@@ -300,6 +300,7 @@ struct KArgs {
   const uint64_t* bcast;      // forward prologue (see ntt.h), column pass only
   size_t bcast_stride;
   NttEpilogue epi;            // forward epilogue (see ntt.h), row pass only
+  BconvPrologue bcv;          // forward base-conversion prologue (see ntt.h), column pass only
 };
 
 // y: processed-limb index over the batch -> polynomial, buffer limb within it, table row
@@ -395,6 +396,71 @@ __device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr
 }
 
 
+// Base-conversion prologue (ntt.h BconvPrologue): the tile's 16 elements of output limb j are
+// sum_s in[s][k] * mat[s][j] mod q, in two halves of 8 elements; per half the input loads of 4
+// limbs are issued together.  30-bit halves: every partial sum of <= 15 products of 30-bit
+// values stays below 2^64 (the split of bconv_fixed_kernel, rns.hip), one Barrett-128 per element.
+template <int S1_LOG, int S2_LOG, int RF>
+__device__ __forceinline__ void bconv_prologue(uint64_t (&x)[E], const KArgs& a, int tile, const TileRef& tr,
+                                               uint32_t pf, uint64_t q, uint64_t r0, uint64_t r1) {
+  constexpr uint64_t kM30 = (1ull << 30) - 1;
+  constexpr int CT = (1 << S2_LOG) / COLS, H = E / 2, SB = 4;
+  const int poly = tr.poly;
+  const int j = tile / CT - poly * a.limbs_per_poly;  // index among the polynomial's converted limbs
+  const int ib = __builtin_amdgcn_readfirstlane(a.bcv.ib[poly]);
+  const uint64_t* mat = a.bcv.mat[poly] + j;
+  const uint64_t* in = a.bcv.in + poly * a.bcv.in_stride + tr.k;
+  const size_t n = static_cast<size_t>(a.n);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint64_t ll[H] = {}, m1[H] = {}, m2[H] = {}, hh[H] = {};
+    for (int s0 = 0; s0 < ib; s0 += SB) {
+      uint64_t v[SB][H];
+#pragma unroll
+      for (int u = 0; u < SB; ++u)
+#pragma unroll
+        for (int e = 0; e < H; ++e)
+          v[u][e] = s0 + u < ib ? __builtin_nontemporal_load(in + (size_t)(s0 + u) * n +
+                                                             (size_t)(pf | Round<S1_LOG, RF>::p_elem(h * H + e)) * (1 << S2_LOG))
+                                : 0;
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const uint64_t c = s0 + u < ib ? mat[(size_t)(s0 + u) * a.bcv.ob] : 0;
+        const uint32_t cl = static_cast<uint32_t>(c & kM30), ch = static_cast<uint32_t>(c >> 30);
+#pragma unroll
+        for (int e = 0; e < H; ++e) {
+          const uint32_t xl = static_cast<uint32_t>(v[u][e] & kM30), xh = static_cast<uint32_t>(v[u][e] >> 30);
+          ll[e] += static_cast<uint64_t>(xl) * cl;
+          m1[e] += static_cast<uint64_t>(xl) * ch;
+          m2[e] += static_cast<uint64_t>(xh) * cl;
+          hh[e] += static_cast<uint64_t>(xh) * ch;
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < H; ++e) {
+      u128 acc{ll[e], 0};
+      add128(acc, u128{m1[e] << 30, m1[e] >> 34});
+      add128(acc, u128{m2[e] << 30, m2[e] >> 34});
+      add128(acc, u128{hh[e] << 60, hh[e] >> 4});
+      x[h * H + e] = barrett_reduce_128(acc, q, r0, r1);
+    }
+  }
+}
+
+// Tile order of the base-conversion column pass: the converted limbs of one (polynomial, column
+// tile) read the same input tiles, so they are dealt to one XCD back to back (blocks b and b + 8
+// share an XCD under round-robin placement; speed only, any placement is correct) and the inputs
+// come from that XCD's L2 after the first read.
+template <int S2_LOG>
+__device__ __forceinline__ int bcv_tile(const KArgs& a, int b) {
+  constexpr int CT = (1 << S2_LOG) / COLS;
+  const int per = a.limbs_per_poly, groups = a.map.polys * CT;
+  if (groups % 8 != 0) return b;
+  const int x = b % 8, k = b / 8, g = x + 8 * (k / per), jj = k % per;
+  return ((g / CT) * per + jj) * CT + g % CT;
+}
+
 // ---------------------------------------------------------------------------------------
 // Column pass: tile = COLS consecutive columns x S1 rows of one limb; 256-thread workgroup.
 // Any round layout is coalesced here (16 lanes cover one 128 B row segment), so the pass loads
@@ -425,8 +491,8 @@ __device__ __forceinline__ void col_load(uint64_t (&x)[E], const uint64_t* src, 
     x[j] = __builtin_nontemporal_load(src + (size_t)(pf | Round<S1_LOG, RF>::p_elem(j)) * (1 << S2_LOG));
 }
 
-template <int S1_LOG, int S2_LOG, bool FWD>
-__global__ __launch_bounds__(CBLOCK, kWavesPerEU) void ntt_col(KArgs a) {
+template <int S1_LOG, int S2_LOG, bool FWD, bool BCV = false>
+__global__ __launch_bounds__(CBLOCK, BCV ? 2 : kWavesPerEU) void ntt_col(KArgs a) {
   using SB = Sub<S1_LOG>;
   using P = Plan<S1_LOG, S2_LOG>;
   constexpr int T = SB::T, S2 = 1 << S2_LOG, NT = COLS * T, CT = S2 / COLS, RN = SB::ROUNDS;
@@ -443,21 +509,25 @@ __global__ __launch_bounds__(CBLOCK, kWavesPerEU) void ntt_col(KArgs a) {
   auto sync = [] { __syncthreads(); };
   const uint32_t pf = Round<S1_LOG, RF>::p_thread(t), pl = Round<S1_LOG, RL>::p_thread(t);
 
-  int tile = blockIdx.x;  // workgroup-uniform
+  int tile = BCV ? bcv_tile<S2_LOG>(a, blockIdx.x) : blockIdx.x;  // workgroup-uniform
   if (tile >= ntiles) return;
   uint64_t xn[E];
   const uint64_t* src = a.bcast ? a.bcast : a.in;
-  col_load<S1_LOG, S2_LOG, RF>(xn, src + col_ref<S2_LOG>(a, tile, c).in_off, pf);
+  if constexpr (!BCV) col_load<S1_LOG, S2_LOG, RF>(xn, src + col_ref<S2_LOG>(a, tile, c).in_off, pf);
   for (;;) {
     const TileRef tr = col_ref<S2_LOG>(a, tile, c);
     const int next = tile + gridDim.x;
     const bool more = kPrefetch && next < ntiles;
     uint64_t x[E];
-#pragma unroll
-    for (int j = 0; j < E; ++j) x[j] = xn[j];
     const LimbCtx lc = limb_ctx(a, tr.row);
+    if constexpr (BCV) {
+      bconv_prologue<S1_LOG, S2_LOG, RF>(x, a, tile, tr, pf, lc.q, a.barrett[2 * tr.row], a.barrett[2 * tr.row + 1]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < E; ++j) x[j] = xn[j];
+    }
     uint64_t* dst = a.out + tr.off;
-    if (FWD && a.bcast) {  // prologue: the broadcast limb reduced mod this limb's prime
+    if (FWD && !BCV && a.bcast) {  // prologue: the broadcast limb reduced mod this limb's prime
       const uint64_t r1 = a.barrett[2 * tr.row + 1];
 #pragma unroll
       for (int j = 0; j < E; ++j) x[j] = barrett_reduce_64(x[j], lc.q, r1);
@@ -851,7 +921,8 @@ int num_cus() {
 template <int S1_LOG, int S2_LOG>
 hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const LimbMap& map, bool inverse,
                   const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream,
-                  const uint64_t* bcast = nullptr, size_t bcast_stride = 0, const NttEpilogue& epi = NttEpilogue{}) {
+                  const uint64_t* bcast = nullptr, size_t bcast_stride = 0, const NttEpilogue& epi = NttEpilogue{},
+                  const BconvPrologue* bcv = nullptr) {
   const int per_poly = map.num_limbs - (map.skip_end - map.skip_begin);
   if (per_poly <= 0 || map.polys <= 0) return hipSuccess;
   const int limbs = per_poly * map.polys;
@@ -869,6 +940,7 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   a.barrett = tb.barrett;
   a.bcast = bcast; a.bcast_stride = bcast_stride;
   a.epi = epi;
+  if (bcv) a.bcv = *bcv;
   if (a.map.in_stride == 0) a.map.in_stride = (size_t)map.num_limbs * tb.n;
   if (a.map.out_stride == 0) a.map.out_stride = (size_t)map.num_limbs * tb.n;
   constexpr int S1 = 1 << S1_LOG, S2 = 1 << S2_LOG;
@@ -884,7 +956,10 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   if (!inverse) {
     NttEpilogue epi_row = a.epi;
     a.epi = NttEpilogue{};  // the column pass stores its intermediate
-    hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true>), grid_c, block_c, 0, stream, a);
+    if (bcv)
+      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true, true>), grid_c, block_c, 0, stream, a);
+    else
+      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true>), grid_c, block_c, 0, stream, a);
     a.in = out;
     a.map.in_stride = a.map.out_stride;
     a.bcast = nullptr;  // the row pass reads the intermediate
@@ -904,11 +979,14 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
 
 hipError_t dispatch(const NttTables& tb, const uint64_t* in, uint64_t* out, const LimbMap& map, bool inverse,
                     const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream,
-                    const uint64_t* bcast = nullptr, size_t bcast_stride = 0, const NttEpilogue& epi = NttEpilogue{}) {
+                    const uint64_t* bcast = nullptr, size_t bcast_stride = 0, const NttEpilogue& epi = NttEpilogue{},
+                    const BconvPrologue* bcv = nullptr) {
 #define PHX_NTT_CASE(LOGN, A, B) \
-  case LOGN: return launch<A, B>(tb, in, out, map, inverse, scale, scale_shoup, stream, bcast, bcast_stride, epi);
-  if (tb.log_n < 10)
+  case LOGN: return launch<A, B>(tb, in, out, map, inverse, scale, scale_shoup, stream, bcast, bcast_stride, epi, bcv);
+  if (tb.log_n < 10) {
+    if (bcv) return hipErrorNotSupported;
     return launch_1d(tb, in, out, map, inverse, scale, scale_shoup, stream, bcast, bcast_stride, epi);
+  }
   switch (tb.log_n) {
     PHX_NTT_CASE(10, 5, 5) PHX_NTT_CASE(11, 5, 6) PHX_NTT_CASE(12, 6, 6) PHX_NTT_CASE(13, 6, 7)
     PHX_NTT_CASE(14, 7, 7) PHX_NTT_CASE(15, 7, 8) PHX_NTT_CASE(16, PHX_NTT16_S1, 16 - PHX_NTT16_S1) PHX_NTT_CASE(17, 8, 9)
@@ -928,6 +1006,18 @@ hipError_t ntt_forward_fused(const NttTables& t, const uint64_t* in, uint64_t* o
                              const uint64_t* bcast, size_t bcast_stride, const NttEpilogue& epi, hipStream_t stream) {
   if (epi.out && (!epi.c || !epi.w || !epi.ws)) return hipErrorInvalidValue;
   return dispatch(t, in, out, map, false, nullptr, nullptr, stream, bcast, bcast_stride, epi);
+}
+
+hipError_t ntt_forward_bconv(const NttTables& t, uint64_t* out, const LimbMap& map, const BconvPrologue& bcv,
+                             const NttEpilogue& epi, hipStream_t stream) {
+  if (epi.out && (!epi.c || !epi.w || !epi.ws)) return hipErrorInvalidValue;
+  if (!bcv.in || bcv.ob <= 0 || map.polys < 1 || map.polys > kMaxBconvPolys) return hipErrorInvalidValue;
+  const int per_poly = map.num_limbs - (map.skip_end - map.skip_begin);
+  for (int p = 0; p < map.polys; ++p) {
+    if (!bcv.mat[p] || bcv.ib[p] < 1 || bcv.ib[p] > 15) return hipErrorInvalidValue;
+    if (per_poly > bcv.ob) return hipErrorInvalidValue;
+  }
+  return dispatch(t, nullptr, out, map, false, nullptr, nullptr, stream, nullptr, 0, epi, &bcv);
 }
 
 hipError_t ntt_inverse(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,

@@ -1,6 +1,8 @@
 #include "rns_tool.h"
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "numth.h"
@@ -137,6 +139,19 @@ RnsTool::RnsTool(size_t n, const std::vector<uint64_t>& qp, size_t size_P, size_
   }
 }
 
+// Off by default: measured slower than the separate conversion + NTT on MI355X (C3 relinearize
+// 0.416 vs 0.377 ms, bootstrap 32.4 vs 31.2 ms; profiles/r02/fused_bconv_ntt.txt): computed per
+// output element, the conversion re-splits and re-reads its 15 inputs for every output limb
+// (the separate kernel shares them across 5), and the column pass at 210 VGPRs runs 2 waves per
+// SIMD.  PHX_FUSED_BCONV=1 selects it (bit-exact either way).
+bool RnsTool::fused_bconv_ok(size_t ibase) const {
+  static const bool on = [] {
+    const char* e = std::getenv("PHX_FUSED_BCONV");
+    return e && e[0] == '1';
+  }();
+  return on && n_ >= 1024 && ibase >= 1 && ibase <= 15;
+}
+
 void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables& ntt, hipStream_t s) const {
   const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_, alpha = size_P_;
   uint64_t* t_cks = ws_->get(s, Workspace::kModupInv, size_Ql * n_);
@@ -145,18 +160,22 @@ void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables
                           d_partQlHatInv_shoup_.get(), s),
          "modup INTT");
   hip_ok(phx::modup_copy_digits(c2, t_mod_up, n_, size_Ql, size_QlP, alpha, s), "modup copy");
-  for (size_t b = 0; b < converters_.size(); ++b) {
-    const size_t start = digit_start_[b], part = digit_size_[b];
-    uint64_t* dst = t_mod_up + b * size_QlP * n_;
-    phx::BconvArgs a = converters_[b].args(t_cks + start * n_, dst, false);
-    a.skip_at = (int)start;
-    a.skip_len = (int)part;
-    hip_ok(phx::bconv(a, n_, s), "modup bconv");
-  }
-  // NTT of every limb but the digit's own (include_special_mod_exclude_range): the full
-  // digits in one launch (digit b skips [b alpha, (b + 1) alpha)), a short last digit apart
+  // per digit: the complement limbs = NTT(bconv(digit)), every limb but the digit's own
+  // (include_special_mod_exclude_range); the full digits in one launch (digit b skips
+  // [b alpha, (b + 1) alpha)), a short last digit apart.  At n >= 2^10 the conversion is the
+  // column pass's prologue (ntt.h BconvPrologue): its output never goes to HBM.
   const size_t beta = converters_.size();
   const size_t full = digit_size_.back() == alpha ? beta : beta - 1;
+  const bool fused = fused_bconv_ok(alpha);
+  if (!fused) {
+    for (size_t b = 0; b < beta; ++b) {
+      const size_t start = digit_start_[b], part = digit_size_[b];
+      phx::BconvArgs a = converters_[b].args(t_cks + start * n_, t_mod_up + b * size_QlP * n_, false);
+      a.skip_at = (int)start;
+      a.skip_len = (int)part;
+      hip_ok(phx::bconv(a, n_, s), "modup bconv");
+    }
+  }
   auto run = [&](size_t b0, size_t cnt) {
     const size_t part = digit_size_[b0];
     phx::LimbMap m;
@@ -168,9 +187,23 @@ void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables
     m.skip_end = (int)(digit_start_[b0] + part);
     m.skip_step = (int)alpha;
     uint64_t* dst = t_mod_up + b0 * size_QlP * n_;
-    hip_ok(phx::ntt_forward(ntt, dst, dst, m.batched((int)cnt), s), "modup NTT");
+    if (fused) {
+      phx::BconvPrologue bcv;
+      bcv.in = t_cks + digit_start_[b0] * n_;
+      bcv.in_stride = alpha * n_;
+      bcv.ob = (int)(size_QlP - part);
+      for (size_t i = 0; i < cnt; ++i) {
+        bcv.mat[i] = converters_[b0 + i].d_qhat_mod_p.get();
+        bcv.ib[i] = (int)digit_size_[b0 + i];
+      }
+      hip_ok(phx::ntt_forward_bconv(ntt, dst, m.batched((int)cnt), bcv, phx::NttEpilogue{}, s), "modup bconv + NTT");
+    } else {
+      hip_ok(phx::ntt_forward(ntt, dst, dst, m.batched((int)cnt), s), "modup NTT");
+    }
   };
-  if (full > 0) run(0, full);
+  // one launch per group of full digits (at most kMaxBconvPolys prologue tables per launch)
+  const size_t group = fused ? (size_t)phx::kMaxBconvPolys : full;
+  for (size_t b0 = 0; b0 < full; b0 += group) run(b0, std::min(group, full - b0));
   if (full < beta) run(full, 1);
 }
 
@@ -185,14 +218,13 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
   pm.split = 0;
   pm.first_a = 0;
   pm.first_b = (int)size_Q_;
-  hip_ok(phx::ntt_inverse(ntt, cp, cp, pm.batched(np, size_QlP * n_, size_QlP * n_), nullptr, nullptr, s),
+  const bool fused = fused_bconv_ok(size_P_) && polys <= (size_t)phx::kMaxBconvPolys;
+  // with the fused conversion the INTT also applies the converter's qHat^-1 (bconv's prescale)
+  hip_ok(phx::ntt_inverse(ntt, cp, cp, pm.batched(np, size_QlP * n_, size_QlP * n_),
+                          fused ? p_to_ql_.d_qhat_inv.get() : nullptr, fused ? p_to_ql_.d_qhat_inv_shoup.get() : nullptr,
+                          s),
          "moddown INTT(P)");
   uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, polys * size_Ql * n_);
-  phx::BconvArgs ba = p_to_ql_.args(cp, delta, true);
-  ba.polys = np;
-  ba.in_stride = size_QlP * n_;
-  ba.out_stride = size_Ql * n_;
-  hip_ok(phx::bconv(ba, n_, s), "moddown bconv");
   // NTT(delta) with the finish (cx - delta) P^-1 (+ ct) as its epilogue
   phx::NttEpilogue epi;
   epi.c = cx;
@@ -202,9 +234,25 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
   epi.w = d_bigPInv_mod_q_.get();
   epi.ws = d_bigPInv_mod_q_shoup_.get();
   epi.accumulate = accumulate;
-  hip_ok(phx::ntt_forward_fused(ntt, delta, delta, phx::LimbMap::contiguous((int)size_Ql, 0).batched(np), nullptr, 0,
-                                epi, s),
-         "moddown NTT + finish");
+  const phx::LimbMap dm = phx::LimbMap::contiguous((int)size_Ql, 0).batched(np);
+  if (fused) {
+    phx::BconvPrologue bcv;
+    bcv.in = cp;
+    bcv.in_stride = size_QlP * n_;
+    bcv.ob = (int)size_Ql;
+    for (int p = 0; p < np; ++p) {
+      bcv.mat[p] = p_to_ql_.d_qhat_mod_p.get();
+      bcv.ib[p] = (int)size_P_;
+    }
+    hip_ok(phx::ntt_forward_bconv(ntt, delta, dm, bcv, epi, s), "moddown bconv + NTT + finish");
+    return;
+  }
+  phx::BconvArgs ba = p_to_ql_.args(cp, delta, true);
+  ba.polys = np;
+  ba.in_stride = size_QlP * n_;
+  ba.out_stride = size_Ql * n_;
+  hip_ok(phx::bconv(ba, n_, s), "moddown bconv");
+  hip_ok(phx::ntt_forward_fused(ntt, delta, delta, dm, nullptr, 0, epi, s), "moddown NTT + finish");
 }
 
 void RnsTool::moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTables& ntt, hipStream_t s) const {
@@ -246,14 +294,12 @@ void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables&
   dm.split = 1;
   dm.first_a = (int)Ln;
   dm.first_b = (int)size_Q_;
-  hip_ok(phx::ntt_inverse(ntt, dropped, dropped, dm.batched(np, size_QlP * n_, size_QlP * n_), nullptr, nullptr, s),
+  const bool fused = fused_bconv_ok(1 + size_P_) && polys <= (size_t)phx::kMaxBconvPolys;
+  hip_ok(phx::ntt_inverse(ntt, dropped, dropped, dm.batched(np, size_QlP * n_, size_QlP * n_),
+                          fused ? pq_to_ql1_.d_qhat_inv.get() : nullptr,
+                          fused ? pq_to_ql1_.d_qhat_inv_shoup.get() : nullptr, s),
          "moddown-rescale INTT");
   uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, polys * Ln * n_);
-  phx::BconvArgs ba = pq_to_ql1_.args(dropped, delta, true);
-  ba.polys = np;
-  ba.in_stride = size_QlP * n_;
-  ba.out_stride = Ln * n_;
-  hip_ok(phx::bconv(ba, n_, s), "moddown-rescale bconv");
   phx::NttEpilogue epi;
   epi.c = cx;
   epi.c_stride = size_QlP * n_;
@@ -261,9 +307,25 @@ void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables&
   epi.out_stride = Ln * n_;
   epi.w = d_PQinv_.get();
   epi.ws = d_PQinv_shoup_.get();
-  hip_ok(phx::ntt_forward_fused(ntt, delta, delta, phx::LimbMap::contiguous((int)Ln, 0).batched(np), nullptr, 0, epi,
-                                s),
-         "moddown-rescale NTT + finish");
+  const phx::LimbMap om = phx::LimbMap::contiguous((int)Ln, 0).batched(np);
+  if (fused) {
+    phx::BconvPrologue bcv;
+    bcv.in = dropped;
+    bcv.in_stride = size_QlP * n_;
+    bcv.ob = (int)Ln;
+    for (int p = 0; p < np; ++p) {
+      bcv.mat[p] = pq_to_ql1_.d_qhat_mod_p.get();
+      bcv.ib[p] = (int)(1 + size_P_);
+    }
+    hip_ok(phx::ntt_forward_bconv(ntt, delta, om, bcv, epi, s), "moddown-rescale bconv + NTT + finish");
+    return;
+  }
+  phx::BconvArgs ba = pq_to_ql1_.args(dropped, delta, true);
+  ba.polys = np;
+  ba.in_stride = size_QlP * n_;
+  ba.out_stride = Ln * n_;
+  hip_ok(phx::bconv(ba, n_, s), "moddown-rescale bconv");
+  hip_ok(phx::ntt_forward_fused(ntt, delta, delta, om, nullptr, 0, epi, s), "moddown-rescale NTT + finish");
 }
 
 void RnsTool::rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const phx::NttTables& ntt,

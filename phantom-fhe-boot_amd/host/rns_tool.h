@@ -81,6 +81,9 @@ class RnsTool {
   DeviceBuffer<uint64_t> d_Ql_, d_Ql_barrett_, d_QlP_, d_QlP_barrett_;
   // key switching
   DeviceBuffer<uint64_t> d_partQlHatInv_, d_partQlHatInv_shoup_;
+  // the base conversion can run as the forward NTT's column-pass prologue (ntt.h BconvPrologue):
+  // 2-D transform sizes and at most 15 input limbs; opt-in (PHX_FUSED_BCONV=1), see rns_tool.cpp
+  bool fused_bconv_ok(size_t ibase) const;
   std::vector<DeviceBaseConverter> converters_;  // digit beta: part -> complement of QlP
   std::vector<size_t> digit_start_, digit_size_;
   DeviceBaseConverter p_to_ql_;
