@@ -184,7 +184,7 @@ def job_throughput(units_per_rank, world, max_seconds):
     return units_per_rank * world / max_seconds
 
 
-def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, verify=None):
+def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, verify=None, key_seed=None):
     """Config C5: `total` independent C4 bootstraps sharded over the ranks, one
     process per GPU.  Every rank regenerates the same keys from a 32-byte seed rank 0 broadcasts
     (no key traffic).  Rank 0 encrypts the batch — 2^15 reals in [1, 5] per ciphertext at chain
@@ -200,7 +200,9 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, 
         raise ValueError(f"C5 batch {total} does not divide over {world} ranks")
     per = total // world
     dev = torch.device("cuda", local_rank)
-    seed = shard.broadcast_seed(dist, dev)
+    # fresh OS entropy by default; a fixed seed (--c5-key-seed) makes the keys, and with them the
+    # per-ciphertext precision, reproducible
+    seed = bytes.fromhex(key_seed) if key_seed else shard.broadcast_seed(dist, dev)
     t_setup = time.perf_counter()
     sess = PA.BootSession(seed)
     setup_s = time.perf_counter() - t_setup
@@ -288,6 +290,7 @@ def main():
     ap.add_argument("--c5-batch", type=int, default=1024, help="C5: bootstraps in the whole batch")
     ap.add_argument("--c5-lanes", type=int, default=4, help="C5: concurrent bootstraps per GPU")
     ap.add_argument("--c5-verify", type=int, default=None, help="C5: decrypt-check only the first K results")
+    ap.add_argument("--c5-key-seed", default=None, help="C5: 64 hex digits of key seed (default: OS entropy)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -362,7 +365,7 @@ def main():
     c5 = None
     if not args.no_c5:
         c5 = c5_leg(dist if world > 1 else None, torch, world, rank, local_rank, total=args.c5_batch,
-                    lanes=args.c5_lanes, verify=args.c5_verify)
+                    lanes=args.c5_lanes, verify=args.c5_verify, key_seed=args.c5_key_seed)
 
     # parity spot-check of the last buffer state is done by tests/; here just sanity
     value = job_throughput(2 * BYTES_PER_TRANSFORM * args.steps, world, elapsed) / 1e9

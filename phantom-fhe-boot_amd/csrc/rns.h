@@ -68,6 +68,15 @@ struct BconvArgs {
   int polys = 1;
   size_t in_stride = 0;
   size_t out_stride = 0;
+  // digits: with jobs > 1 the `polys` conversions are different converters of one shape (the
+  // modup digits): conversion d uses job_qhat_mod_p[d], job_obase[d], job_obase_barrett[d] and
+  // skips at skip_at + d * skip_step
+  static constexpr int kMaxJobs = 8;
+  int jobs = 1;
+  int skip_step = 0;
+  const uint64_t* job_qhat_mod_p[kMaxJobs] = {};
+  const uint64_t* job_obase[kMaxJobs] = {};
+  const uint64_t* job_obase_barrett[kMaxJobs] = {};
 };
 hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s);
 

@@ -175,6 +175,22 @@ __device__ __forceinline__ BconvBlock bconv_block(uint32_t chunks, int groups) {
 #endif
 constexpr int kBconvJ = PHX_BCONV_J;
 
+// the job of a multi-converter launch (BconvArgs::jobs): its matrix, output base and skip
+__device__ __forceinline__ void bconv_select_job(BconvArgs& a) {
+  if (a.jobs > 1) {
+    const int d = blockIdx.z;
+    // constant indices only: a dynamic index would copy the kernel arguments to scratch
+#pragma unroll
+    for (int k = 0; k < BconvArgs::kMaxJobs; ++k)
+      if (k == d) {
+        a.qhat_mod_p = a.job_qhat_mod_p[k];
+        a.obase = a.job_obase[k];
+        a.obase_barrett = a.job_obase_barrett[k];
+      }
+    a.skip_at += d * a.skip_step;
+  }
+}
+
 __device__ __forceinline__ void bconv_outputs(const BconvArgs& a, const uint64_t* tx, const uint64_t* ty, int ib,
                                               uint32_t n, uint32_t k, int group) {
   const int j0 = group * kBconvJ, j1 = min(j0 + kBconvJ, a.obase_size);
@@ -211,7 +227,8 @@ __device__ __forceinline__ void bconv_inputs(const BconvArgs& a, uint64_t* tx, u
 }
 
 __global__ __launch_bounds__(kBlock) void bconv_kernel(BconvArgs a, uint32_t n, uint32_t pairs, bool prescale) {
-  a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial
+  bconv_select_job(a);
+  a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial (or digit)
   a.out += blockIdx.z * a.out_stride;
   const BconvBlock bb = bconv_block((pairs + kBlock - 1) / kBlock, (a.obase_size + kBconvJ - 1) / kBconvJ);
   const uint32_t i = bb.chunk * kBlock + threadIdx.x;
@@ -234,6 +251,7 @@ __global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32
   // prove it, so direct reads would be vector loads inside the accumulation loop
   __shared__ uint32_t mlo[IB][kBconvJ], mhi[IB][kBconvJ];
   __shared__ uint64_t mp[kBconvJ][3];
+  bconv_select_job(a);
   const BconvBlock bb = bconv_block((pairs + kBlock - 1) / kBlock, (a.obase_size + kBconvJ - 1) / kBconvJ);
   const int j0 = bb.group * kBconvJ;
   for (int e = threadIdx.x; e < IB * kBconvJ; e += kBlock) {
@@ -251,7 +269,7 @@ __global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32
   __syncthreads();
   const uint32_t i = bb.chunk * kBlock + threadIdx.x;
   if (i >= pairs) return;
-  a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial
+  a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial (or digit)
   a.out += blockIdx.z * a.out_stride;
   uint32_t lo[2][IB], hi[2][IB];
   // every input load issued before any use (a branch between them would serialise them)
@@ -520,6 +538,7 @@ hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s) {
   if (a.ibase_size <= 0 || a.ibase_size > kMaxIbase || a.obase_size <= 0) return hipErrorInvalidValue;
   const uint32_t pairs = static_cast<uint32_t>(n / 2);
   if (a.polys < 1) return hipErrorInvalidValue;
+  if (a.jobs > 1 && (a.jobs != a.polys || a.jobs > BconvArgs::kMaxJobs)) return hipErrorInvalidValue;
   const dim3 g(((pairs + kBlock - 1) / kBlock) * ((a.obase_size + kBconvJ - 1) / kBconvJ), 1, a.polys);
   const bool pre = a.qhat_inv != nullptr;
   switch (a.ibase_size) {

@@ -152,6 +152,37 @@ bool RnsTool::fused_bconv_ok(size_t ibase) const {
   return on && n_ >= 1024 && ibase >= 1 && ibase <= 15;
 }
 
+// every digit's conversion to its complement of QlP (digit b: t_cks limbs [b alpha, b alpha + part)
+// -> t_mod_up[b], skipping the digit's own limbs); the full digits in one launch (one converter
+// per blockIdx.z), a short last digit apart
+void RnsTool::digit_bconv(const uint64_t* t_cks, uint64_t* t_mod_up, hipStream_t s) const {
+  const size_t size_QlP = base_Ql_.size() + size_P_, alpha = size_P_, beta = converters_.size();
+  const size_t full = digit_size_.back() == alpha ? beta : beta - 1;
+  for (size_t b0 = 0; b0 < full; b0 += phx::BconvArgs::kMaxJobs) {
+    const size_t cnt = std::min<size_t>(phx::BconvArgs::kMaxJobs, full - b0);
+    phx::BconvArgs a = converters_[b0].args(t_cks + digit_start_[b0] * n_, t_mod_up + b0 * size_QlP * n_, false);
+    a.skip_at = (int)digit_start_[b0];
+    a.skip_len = (int)alpha;
+    a.polys = a.jobs = (int)cnt;
+    a.in_stride = alpha * n_;
+    a.out_stride = size_QlP * n_;
+    a.skip_step = (int)alpha;
+    for (size_t d = 0; d < cnt; ++d) {
+      const DeviceBaseConverter& c = converters_[b0 + d];
+      a.job_qhat_mod_p[d] = c.d_qhat_mod_p.get();
+      a.job_obase[d] = c.d_obase.get();
+      a.job_obase_barrett[d] = c.d_obase_barrett.get();
+    }
+    hip_ok(phx::bconv(a, n_, s), "digit bconv");
+  }
+  if (full < beta) {
+    phx::BconvArgs a = converters_[full].args(t_cks + digit_start_[full] * n_, t_mod_up + full * size_QlP * n_, false);
+    a.skip_at = (int)digit_start_[full];
+    a.skip_len = (int)digit_size_[full];
+    hip_ok(phx::bconv(a, n_, s), "digit bconv (short digit)");
+  }
+}
+
 void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables& ntt, hipStream_t s) const {
   const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_, alpha = size_P_;
   uint64_t* t_cks = ws_->get(s, Workspace::kModupInv, size_Ql * n_);
@@ -167,15 +198,7 @@ void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables
   const size_t beta = converters_.size();
   const size_t full = digit_size_.back() == alpha ? beta : beta - 1;
   const bool fused = fused_bconv_ok(alpha);
-  if (!fused) {
-    for (size_t b = 0; b < beta; ++b) {
-      const size_t start = digit_start_[b], part = digit_size_[b];
-      phx::BconvArgs a = converters_[b].args(t_cks + start * n_, t_mod_up + b * size_QlP * n_, false);
-      a.skip_at = (int)start;
-      a.skip_len = (int)part;
-      hip_ok(phx::bconv(a, n_, s), "modup bconv");
-    }
-  }
+  if (!fused) digit_bconv(t_cks, t_mod_up, s);
   auto run = [&](size_t b0, size_t cnt) {
     const size_t part = digit_size_[b0];
     phx::LimbMap m;
@@ -271,13 +294,7 @@ void RnsTool::moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTabl
                             d_partQlHatInv_shoup_.get()};
   hip_ok(phx::moddown_modup_finish(c1, delta, k, t_cks, t_mod_up, n_, size_Ql, size_QlP, alpha, s),
          "moddown-modup finish");
-  for (size_t b = 0; b < converters_.size(); ++b) {
-    const size_t start = digit_start_[b], part = digit_size_[b];
-    phx::BconvArgs a = converters_[b].args(t_cks + start * n_, t_mod_up + b * size_QlP * n_, false);
-    a.skip_at = (int)start;
-    a.skip_len = (int)part;
-    hip_ok(phx::bconv(a, n_, s), "moddown-modup bconv digits");
-  }
+  digit_bconv(t_cks, t_mod_up, s);
   hip_ok(phx::ntt_forward(ntt, t_mod_up, t_mod_up, all.batched((int)converters_.size()), s), "moddown-modup NTT");
 }
 

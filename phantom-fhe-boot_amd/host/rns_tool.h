@@ -84,6 +84,7 @@ class RnsTool {
   // the base conversion can run as the forward NTT's column-pass prologue (ntt.h BconvPrologue):
   // 2-D transform sizes and at most 15 input limbs; opt-in (PHX_FUSED_BCONV=1), see rns_tool.cpp
   bool fused_bconv_ok(size_t ibase) const;
+  void digit_bconv(const uint64_t* t_cks, uint64_t* t_mod_up, hipStream_t s) const;
   std::vector<DeviceBaseConverter> converters_;  // digit beta: part -> complement of QlP
   std::vector<size_t> digit_start_, digit_size_;
   DeviceBaseConverter p_to_ql_;

