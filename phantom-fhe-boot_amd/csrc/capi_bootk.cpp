@@ -1,7 +1,7 @@
 // capi_bootk.cpp — C-ABI of the bootstrap's own kernels (declared in include/phantom_amd.h), on
 // raw device buffers, so each can be checked bit for bit against the CPU oracle: the hoisted
 // linear transforms' inner sums (lt_bsgs), EvalFastRotationExt with its fused epilogue
-// (galois_finish), the giant-step rotate-and-accumulate, KeySwitchExt, the tensor product with
+// (one fused kernel, keyswitch_rotate), the giant-step rotate-and-accumulate, KeySwitchExt, the tensor product with
 // MulAddRescale's linear epilogue (tensor_lin), the Chebyshev leaves (leaf_combine) and the
 // per-limb scalar kernels.  Host arrays of device pointers and of per-limb residues are copied into
 // the kernels' argument blocks or small device tables here (set-up cost, not on the hot path).
@@ -98,21 +98,22 @@ int phantom_fast_rotation_ext(const phantom_context* ctx, size_t chain_index, co
     const auto& rt = tool_at(pc, chain_index);
     const size_t n = pc.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + pc.size_P();
     const uint64_t* const* evk = phantom_capi_key_array(ctx, key_digits, dnum, rt.beta());
-    phantom::DeviceBuffer<uint64_t> cx(2 * QlP * n, stream);
-    hipError_t e = phx::keyswitch_inner_prod(digits, evk, cx.get(), pc.mod_QP().q, pc.mod_QP().barrett, n, Ql,
-                                             pc.size_Q(), pc.size_P(), rt.beta(), stream);
-    if (e != hipSuccess) return from_hip(e);
-    phx::GaloisFinishArgs g;
-    g.cx = cx.get();
+    phx::KsRotateArgs g;
+    g.digits = digits;
+    g.evk = evk;
+    g.qp = pc.mod_QP().q;
+    g.qp_barrett = pc.mod_QP().barrett;
     g.c0 = ct;
     g.pmod = rt.bigP_mod_q();
     g.pmod_shoup = rt.bigP_mod_q_shoup();
     g.out = out;
     g.perm = pc.galois_perm(galois_elt);
-    g.q = rt.mod_QlP().q;
     g.ql = static_cast<uint32_t>(Ql);
     g.qlp = static_cast<uint32_t>(QlP);
-    return from_hip(phx::galois_finish(g, add_first ? 1 : 0, n, stream));
+    g.size_q = static_cast<uint32_t>(pc.size_Q());
+    g.size_p = static_cast<uint32_t>(pc.size_P());
+    g.beta = static_cast<uint32_t>(rt.beta());
+    return from_hip(phx::keyswitch_rotate(g, add_first ? 1 : 0, n, stream));
   });
 }
 
@@ -124,21 +125,23 @@ int phantom_rotate_ext_accumulate(const phantom_context* ctx, size_t chain_index
     const auto& rt = tool_at(pc, chain_index);
     const size_t n = pc.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + pc.size_P();
     const uint64_t* const* evk = phantom_capi_key_array(ctx, key_digits, dnum, rt.beta());
-    phantom::DeviceBuffer<uint64_t> digits(rt.beta() * QlP * n, stream), cx(2 * QlP * n, stream);
+    phantom::DeviceBuffer<uint64_t> digits(rt.beta() * QlP * n, stream);
     rt.moddown_modup(digits.get(), ext + QlP * n, pc.gpu_rns_tables(), stream);
-    hipError_t e = phx::keyswitch_inner_prod(digits.get(), evk, cx.get(), pc.mod_QP().q, pc.mod_QP().barrett, n, Ql,
-                                             pc.size_Q(), pc.size_P(), rt.beta(), stream);
-    if (e != hipSuccess) return from_hip(e);
-    phx::GaloisFinishArgs g;
-    g.cx = cx.get();
+    phx::KsRotateArgs g;
+    g.digits = digits.get();
+    g.evk = evk;
+    g.qp = pc.mod_QP().q;
+    g.qp_barrett = pc.mod_QP().barrett;
     g.c0 = ext;
     g.out = acc;
     g.perm = pc.galois_perm(galois_elt);
-    g.q = rt.mod_QlP().q;
     g.ql = static_cast<uint32_t>(Ql);
     g.qlp = static_cast<uint32_t>(QlP);
+    g.size_q = static_cast<uint32_t>(pc.size_Q());
+    g.size_p = static_cast<uint32_t>(pc.size_P());
+    g.beta = static_cast<uint32_t>(rt.beta());
     g.accumulate = accumulate != 0;
-    return from_hip(phx::galois_finish(g, 2, n, stream));
+    return from_hip(phx::keyswitch_rotate(g, 2, n, stream));
   });
 }
 

@@ -126,6 +126,29 @@ hipError_t galois_ntt(const uint64_t* in, uint64_t* out, const uint32_t* perm, s
 //   mode 2: x = cx + (c0 on every limb of polynomial 0)             c0 [qlp][n]
 //   out[t][l][j] = (accumulate ? out[t][l][j] : 0) + x[t][l][perm[j]]
 // q: the extended-basis moduli in buffer order.  out must not alias cx or c0.
+// Key switch fused with its automorphism epilogue (EvalFastRotationExt / the giant-step
+// rotate-and-accumulate, src/evaluate.cu:3660-3755): for every limb l of Ql u P and output
+// index i with source j = perm[i],
+//   v_t[j] = sum_b digits[b][l][j] * evk[b][t][row(l)][j]  mod q_l      (the inner product)
+//   mode 1: v_0[j] += P * c0[l][j] for l < Ql;  mode 2: v_0[j] += c0[l][j];  mode 0: nothing
+//   out[t][l][i] = v_t[perm[i]] (+ out[t][l][i] when accumulate)
+// The inner product of a source block is computed into LDS and written permuted, so the key
+// switch's output never makes an HBM round trip before the permutation (galois_finish).
+struct KsRotateArgs {
+  const uint64_t* digits = nullptr;      // [beta][QlP][n]
+  const uint64_t* const* evk = nullptr;  // device array of beta pointers to [2][size_QP][n]
+  const uint64_t* qp = nullptr;          // full-chain modulus / Barrett tables (by table row)
+  const uint64_t* qp_barrett = nullptr;
+  const uint64_t* c0 = nullptr;          // mode 1: [Ql][n]; mode 2: [QlP][n]
+  const uint64_t* pmod = nullptr;        // mode 1: P mod q_l, Shoup
+  const uint64_t* pmod_shoup = nullptr;
+  uint64_t* out = nullptr;               // [2][QlP][n]; must not alias digits / c0
+  const uint32_t* perm = nullptr;
+  uint32_t ql = 0, qlp = 0, size_q = 0, size_p = 0, beta = 0;
+  bool accumulate = false;
+};
+hipError_t keyswitch_rotate(const KsRotateArgs& a, int mode, size_t n, hipStream_t s);
+
 struct GaloisFinishArgs {
   const uint64_t* cx;
   const uint64_t* c0;

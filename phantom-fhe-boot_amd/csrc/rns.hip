@@ -435,6 +435,63 @@ __global__ __launch_bounds__(kBlock) void galois_finish_kernel(GaloisFinishArgs 
   }
 }
 
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void ks_rotate_kernel(KsRotateArgs a, uint32_t log_n, uint32_t bsz) {
+  __shared__ uint64_t s0[kGalB], s1[kGalB];
+  const uint32_t nb = (1u << log_n) / bsz;
+  const uint32_t l = blockIdx.x / nb, ob = blockIdx.x % nb;
+  const uint32_t twr = l >= a.ql ? a.size_q + (l - a.ql) : l;
+  const uint64_t q = a.qp[twr], r0 = a.qp_barrett[2 * twr], r1 = a.qp_barrett[2 * twr + 1];
+  const size_t n = size_t(1) << log_n;
+  const size_t lbase = (size_t)l << log_n, kbase = (size_t)twr << log_n;
+  const size_t qlp_n = (size_t)a.qlp << log_n, qp_n = (size_t)(a.size_q + a.size_p) << log_n;
+  const uint32_t* pm = a.perm + (size_t)ob * bsz;
+  const uint32_t sb = pm[0] & ~(bsz - 1);
+  const bool addc = MODE == 2 || (MODE == 1 && l < a.ql);
+  const uint64_t w = MODE == 1 && addc ? a.pmod[l] : 0, ws = MODE == 1 && addc ? a.pmod_shoup[l] : 0;
+  for (uint32_t i = threadIdx.x; i < bsz / 2; i += kBlock) {
+    const size_t j = sb + 2 * i;
+    u128 a0x{0, 0}, a0y{0, 0}, a1x{0, 0}, a1y{0, 0};
+    for (uint32_t b = 0; b < a.beta; ++b) {
+      const u64x2 c = ld2(a.digits + b * qlp_n + lbase + j);
+      const uint64_t* key = a.evk[b];
+      const u64x2 k0 = ld2(key + kbase + j), k1 = ld2(key + qp_n + kbase + j);
+      add128(a0x, mul_wide(c.x, k0.x));
+      add128(a0y, mul_wide(c.y, k0.y));
+      add128(a1x, mul_wide(c.x, k1.x));
+      add128(a1y, mul_wide(c.y, k1.y));
+    }
+    uint64_t v0x = barrett_reduce_128(a0x, q, r0, r1), v0y = barrett_reduce_128(a0y, q, r0, r1);
+    if (addc) {
+      const u64x2 c0 = ld2(a.c0 + lbase + j);
+      if constexpr (MODE == 1) {
+        v0x = add_mod(v0x, mul_shoup(c0.x, w, ws, q), q);
+        v0y = add_mod(v0y, mul_shoup(c0.y, w, ws, q), q);
+      } else {
+        v0x = add_mod(v0x, c0.x, q);
+        v0y = add_mod(v0y, c0.y, q);
+      }
+    }
+    s0[2 * i] = v0x;
+    s0[2 * i + 1] = v0y;
+    s1[2 * i] = barrett_reduce_128(a1x, q, r0, r1);
+    s1[2 * i + 1] = barrett_reduce_128(a1y, q, r0, r1);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < bsz; i += kBlock) {
+    const uint32_t src = pm[i] & (bsz - 1);
+    const size_t e = lbase + (size_t)ob * bsz + i;
+    uint64_t o0 = s0[src], o1 = s1[src];
+    if (a.accumulate) {
+      o0 = add_mod(o0, a.out[e], q);
+      o1 = add_mod(o1, a.out[qlp_n + e], q);
+    }
+    a.out[e] = o0;
+    a.out[qlp_n + e] = o1;
+  }
+  (void)n;
+}
+
 __global__ __launch_bounds__(kBlock) void galois_kernel(const uint64_t* __restrict__ in, uint64_t* out,
                                                         const uint32_t* __restrict__ perm, uint32_t log_n,
                                                         uint32_t bsz) {
@@ -592,6 +649,21 @@ hipError_t galois_finish(const GaloisFinishArgs& a, int mode, size_t n, hipStrea
     case 0: galois_finish_kernel<0><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
     case 1: galois_finish_kernel<1><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
     default: galois_finish_kernel<2><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t keyswitch_rotate(const KsRotateArgs& a, int mode, size_t n, hipStream_t s) {
+  if (mode < 0 || mode > 2 || !a.digits || !a.evk || !a.out || !a.perm || a.beta == 0) return hipErrorInvalidValue;
+  if (mode > 0 && !a.c0) return hipErrorInvalidValue;
+  if (mode == 1 && (!a.pmod || !a.pmod_shoup)) return hipErrorInvalidValue;
+  if (a.qlp == 0) return hipSuccess;
+  const uint32_t log_n = __builtin_ctzll(n), bsz = static_cast<uint32_t>(std::min<size_t>(n, kGalB));
+  const dim3 grid(static_cast<uint32_t>(a.qlp * (n / bsz)));
+  switch (mode) {
+    case 0: ks_rotate_kernel<0><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
+    case 1: ks_rotate_kernel<1><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
+    default: ks_rotate_kernel<2><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
   }
   return hipGetLastError();
 }

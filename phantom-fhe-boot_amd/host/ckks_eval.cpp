@@ -399,29 +399,31 @@ PhantomCiphertext EvalFastAutomorphismExt(const PhantomContext& ctx, const Phant
   const RnsTool& rt = ctx.get_context_data(ct.chain_index()).gpu_rns_tool();
   const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P();
   hipStream_t s = ctx.stream();
-  uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * QlP * n);
-  hip_ok(phx::keyswitch_inner_prod(digits, keys.get(elt).public_keys_ptr(), cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n,
-                                   Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s, phx::KsAddend{}),
-         "fast rotation inner product");
-  traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP, n));
-  traffic::ciphertexts(traffic::limb_bytes(2 * QlP, n));  // the rotated extended ciphertext written
   PhantomCiphertext out;
   out.resize(2, QlP, n, s, false);
   out.set_chain_index(ct.chain_index());
   out.set_scale(ct.scale());
   out.SetNoiseScaleDeg(ct.GetNoiseScaleDeg());
-  // + P c0, then the permutation, in one pass
-  phx::GaloisFinishArgs g;
-  g.cx = cx;
+  // inner product, + P c0 and the permutation in one pass (the key switch's output never goes to
+  // HBM before the permutation)
+  phx::KsRotateArgs g;
+  g.digits = digits;
+  g.evk = keys.get(elt).public_keys_ptr();
+  g.qp = ctx.mod_QP().q;
+  g.qp_barrett = ctx.mod_QP().barrett;
   g.c0 = ct.data();
   g.pmod = rt.bigP_mod_q();
   g.pmod_shoup = rt.bigP_mod_q_shoup();
   g.out = out.data();
   g.perm = ctx.galois_perm(elt);
-  g.q = rt.mod_QlP().q;
   g.ql = static_cast<uint32_t>(Ql);
   g.qlp = static_cast<uint32_t>(QlP);
-  hip_ok(phx::galois_finish(g, add_first ? 1 : 0, n, s), "fast rotation permute");
+  g.size_q = static_cast<uint32_t>(ctx.size_Q());
+  g.size_p = static_cast<uint32_t>(ctx.size_P());
+  g.beta = static_cast<uint32_t>(rt.beta());
+  hip_ok(phx::keyswitch_rotate(g, add_first ? 1 : 0, n, s), "fast rotation key switch + permute");
+  traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP, n));
+  traffic::ciphertexts(traffic::limb_bytes(2 * QlP, n));  // the rotated extended ciphertext written
   return out;
 }
 
@@ -436,12 +438,6 @@ void EvalRotateExtAccumulate(const PhantomContext& ctx, PhantomCiphertext& ext, 
   // c0 stays P-scaled in QlP
   DeviceBuffer<uint64_t> digits(rt.beta() * QlP * n, s);
   rt.moddown_modup(digits.get(), ext.data() + QlP * n, ctx.gpu_rns_tables(), s);
-  uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * QlP * n);
-  hip_ok(phx::keyswitch_inner_prod(digits.get(), keys.get(elt).public_keys_ptr(), cx, ctx.mod_QP().q,
-                                   ctx.mod_QP().barrett, n, Ql, ctx.size_Q(), ctx.size_P(), rt.beta(), s,
-                                   phx::KsAddend{}),
-         "giant step inner product");
-  traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP, n));
   if (!accumulate) {
     acc.resize(2, QlP, n, s, false);
     acc.set_chain_index(ext.chain_index());
@@ -449,16 +445,23 @@ void EvalRotateExtAccumulate(const PhantomContext& ctx, PhantomCiphertext& ext, 
     acc.SetNoiseScaleDeg(ext.GetNoiseScaleDeg());
     acc.set_ntt_form(true);
   }
-  phx::GaloisFinishArgs g;
-  g.cx = cx;
+  // inner product, + c0 (P-scaled, extended basis), permutation and accumulation in one pass
+  phx::KsRotateArgs g;
+  g.digits = digits.get();
+  g.evk = keys.get(elt).public_keys_ptr();
+  g.qp = ctx.mod_QP().q;
+  g.qp_barrett = ctx.mod_QP().barrett;
   g.c0 = ext.data();
   g.out = acc.data();
   g.perm = ctx.galois_perm(elt);
-  g.q = rt.mod_QlP().q;
   g.ql = static_cast<uint32_t>(Ql);
   g.qlp = static_cast<uint32_t>(QlP);
+  g.size_q = static_cast<uint32_t>(ctx.size_Q());
+  g.size_p = static_cast<uint32_t>(ctx.size_P());
+  g.beta = static_cast<uint32_t>(rt.beta());
   g.accumulate = accumulate;
-  hip_ok(phx::galois_finish(g, 2, n, s), "giant step permute + accumulate");
+  hip_ok(phx::keyswitch_rotate(g, 2, n, s), "giant step key switch + permute + accumulate");
+  traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP, n));
 }
 
 PhantomCiphertext EvalFastRotationExt(const PhantomContext& ctx, const PhantomCiphertext& ct,
