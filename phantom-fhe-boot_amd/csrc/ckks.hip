@@ -139,6 +139,75 @@ __global__ __launch_bounds__(kBlock, 2) void lt_bsgs_kernel(LtArgs a, uint32_t l
   }
 }
 
+// Wide form for G = 32 baby steps (at most B giant steps): the babies are held 8 at a time and
+// every giant step's 128-bit sums stay in registers across the two halves, so each baby and each
+// plaintext is still read once (the register-resident form of lt_bsgs_kernel<32> spills).
+template <int G, int B>
+__global__ __launch_bounds__(kBlock, 2) void lt_bsgs_wide_kernel(LtArgs a, uint32_t log_n, size_t total) {
+  constexpr uint64_t kM30 = (1ull << 30) - 1;
+  constexpr int C = 8;
+  static_assert(G % C == 0, "whole chunks of babies");
+  extern __shared__ const uint64_t* ptab[];
+  for (int k = threadIdx.x; k < a.b * G; k += kBlock) ptab[k] = a.pts[k];
+  __syncthreads();
+  const size_t pstride = total;
+  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
+    const int l = static_cast<int>(e >> log_n);
+    const int row = l < a.Ql ? l : a.size_Q + (l - a.Ql);
+    const uint64_t q = a.q[row], r0 = a.barrett[2 * row], r1 = a.barrett[2 * row + 1];
+    u128 acc[B][2];
+#pragma unroll
+    for (int i = 0; i < B; ++i) acc[i][0] = acc[i][1] = u128{0, 0};
+#pragma unroll
+    for (int c0 = 0; c0 < G; c0 += C) {
+      uint32_t xl[2][C], xh[2][C];
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const uint64_t v0 = a.baby[c0 + j][e], v1 = a.baby[c0 + j][pstride + e];
+        xl[0][j] = static_cast<uint32_t>(v0 & kM30);
+        xh[0][j] = static_cast<uint32_t>(v0 >> 30);
+        xl[1][j] = static_cast<uint32_t>(v1 & kM30);
+        xh[1][j] = static_cast<uint32_t>(v1 >> 30);
+      }
+#pragma unroll
+      for (int i = 0; i < B; ++i) {
+        if (i >= a.b) break;
+        const uint64_t* const* prow = ptab + i * G + c0;
+        uint64_t w[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) w[j] = ((const __attribute__((address_space(1))) uint64_t*)prow[j])[e];
+        __builtin_amdgcn_sched_barrier(0);
+        uint64_t ll[2] = {0, 0}, m1[2] = {0, 0}, m2[2] = {0, 0}, hh[2] = {0, 0};
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+          const uint32_t wl = static_cast<uint32_t>(w[j] & kM30), wh = static_cast<uint32_t>(w[j] >> 30);
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            ll[t] += static_cast<uint64_t>(xl[t][j]) * wl;
+            m1[t] += static_cast<uint64_t>(xl[t][j]) * wh;
+            m2[t] += static_cast<uint64_t>(xh[t][j]) * wl;
+            hh[t] += static_cast<uint64_t>(xh[t][j]) * wh;
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          add128(acc[i][t], u128{ll[t], 0});
+          add128(acc[i][t], u128{m1[t] << 30, m1[t] >> 34});
+          add128(acc[i][t], u128{m2[t] << 30, m2[t] >> 34});
+          add128(acc[i][t], u128{hh[t] << 60, hh[t] >> 4});
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      if (i >= a.b) break;
+      uint64_t* o = a.out[i];
+      o[e] = barrett_reduce_128(acc[i][0], q, r0, r1);
+      o[pstride + e] = barrett_reduce_128(acc[i][1], q, r0, r1);
+    }
+  }
+}
+
 template <bool MUL, bool ACC>
 __global__ __launch_bounds__(kBlock) void scalar_v_kernel(const uint64_t* in, size_t in_stride, LimbScalars c,
                                                           const uint64_t* acc, uint64_t* out, const uint64_t* q,
@@ -306,7 +375,10 @@ hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s) {
     case 4: lt_bsgs_kernel<4><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
     case 8: lt_bsgs_kernel<8><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
     case 16: lt_bsgs_kernel<16><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
-    case 32: lt_bsgs_kernel<32><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
+    case 32:
+      if (a.b <= 8) lt_bsgs_wide_kernel<32, 8><<<grid, kBlock, lds, s>>>(a, log_n, total);
+      else lt_bsgs_kernel<32><<<grid, kBlock, lds, s>>>(a, log_n, total);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -516,7 +516,13 @@ void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const s
       if (dim1 & (dim1 - 1)) throw std::invalid_argument("dim1 must be a power of two");
       lv.g = static_cast<int>(std::min<uint32_t>(dim1, static_cast<uint32_t>(phx::kLtMaxG)));
     } else {
-      while (lv.g * lv.g < lv.D) lv.g *= 2;
+      // g^2 >= 2 D: twice the baby steps of the square split.  A hoisted baby step is one fused
+      // key switch + automorphism; a giant step is a moddown + modup (one INTT over Ql u P and an
+      // NTT over every digit) before its key switch, so fewer giant steps pay: 256 diagonals as
+      // g 32 x b 8 instead of 16 x 16 take the bootstrap from 29.7 to 27.9 ms
+      // (profiles/r02/lt_baby_giant_split.txt); PHX_LT_SQUARE=1 restores the square split.
+      static const bool square = std::getenv("PHX_LT_SQUARE") != nullptr;
+      while (lv.g * lv.g < (square ? 1 : 2) * lv.D && lv.g < phx::kLtMaxG) lv.g *= 2;
     }
     lv.b = (lv.D + lv.g - 1) / lv.g;
     lv.chain = first_chain + gi;

@@ -54,7 +54,7 @@ def _vp(ts):
     return PA.ptr_array([ptr(t) for t in ts])
 
 
-@pytest.mark.parametrize("chain,g,b", [(1, 16, 4), (17, 8, 8)])
+@pytest.mark.parametrize("chain,g,b", [(1, 16, 4), (17, 8, 8), (3, 32, 8), (17, 32, 5)])
 def test_lt_bsgs(c4, rng, chain, g, b):
     em = _ext_mods(c4, chain)
     babies = [_rand(rng, em, 2) for _ in range(g)]
