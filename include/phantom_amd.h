@@ -167,6 +167,15 @@ int phantom_keyswitch_ext(const phantom_context *ctx, size_t chain_index, const 
 int phantom_fast_rotation_ext(const phantom_context *ctx, size_t chain_index, const uint64_t *ct,
                               const uint64_t *digits, const uint64_t *const *key_digits, size_t dnum,
                               uint32_t galois_elt, int add_first, uint64_t *out, hipStream_t stream);
+/* the baby steps of a hoisted linear transform in ONE launch (src/bootstrap.cu:1266-1276: the loop
+ * of EvalFastRotationExt(.., digits, true) with KeySwitchExt for rotation 0): for k < count,
+ * outs[k] [2][Ql+P][n] = phantom_fast_rotation_ext(ct's c0, digits, key_digits[k], galois_elts[k],
+ * add_first = 1), or phantom_keyswitch_ext(ct) where key_digits[k] is NULL; ct [2][Ql][n], the
+ * shared digits read once.  key_digits: host array of `count` host arrays of dnum device pointers */
+int phantom_fast_rotation_ext_batch(const phantom_context *ctx, size_t chain_index, const uint64_t *ct,
+                                    const uint64_t *digits, const uint64_t *const *const *key_digits, size_t dnum,
+                                    const uint32_t *galois_elts, size_t count, uint64_t *const *outs,
+                                    hipStream_t stream);
 /* a giant step of the linear transforms (src/bootstrap.cu:1335-1348: KeySwitchDown + Precompute +
  * EvalFastRotationExt + EvalAddExtInPlace) with c0 kept in the Ext basis:
  * acc (+)= automorphism(KS(modup(moddown(ext c1))) + (ext c0, 0)); ext's c1 P limbs are clobbered */

@@ -117,6 +117,47 @@ int phantom_fast_rotation_ext(const phantom_context* ctx, size_t chain_index, co
   });
 }
 
+int phantom_fast_rotation_ext_batch(const phantom_context* ctx, size_t chain_index, const uint64_t* ct,
+                                    const uint64_t* digits, const uint64_t* const* const* key_digits, size_t dnum,
+                                    const uint32_t* galois_elts, size_t count, uint64_t* const* outs,
+                                    hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (count == 0) return PHANTOM_OK;
+    if (!ct || !digits || !key_digits || !galois_elts || !outs) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    const size_t n = pc.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + pc.size_P();
+    std::vector<phx::KsBatchEntry> e(count);
+    for (size_t k = 0; k < count; ++k) {
+      if (!outs[k]) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null output");
+      if (key_digits[k]) {
+        e[k].evk = phantom_capi_key_array(ctx, key_digits[k], dnum, rt.beta());
+        e[k].perm = pc.galois_perm(galois_elts[k]);
+        e[k].binv = pc.galois_block_inv(galois_elts[k]);
+      }
+      e[k].out_off = outs[k] - outs[0];
+    }
+    phantom::DeviceBuffer<phx::KsBatchEntry> table;
+    table.upload(e, stream);
+    phx::KsRotateBatchArgs a;
+    a.digits = digits;
+    a.entries = table.get();
+    a.count = static_cast<uint32_t>(count);
+    a.qp = pc.mod_QP().q;
+    a.qp_barrett = pc.mod_QP().barrett;
+    a.ct = ct;
+    a.pmod = rt.bigP_mod_q();
+    a.pmod_shoup = rt.bigP_mod_q_shoup();
+    a.out = outs[0];
+    a.ql = static_cast<uint32_t>(Ql);
+    a.qlp = static_cast<uint32_t>(QlP);
+    a.size_q = static_cast<uint32_t>(pc.size_Q());
+    a.size_p = static_cast<uint32_t>(pc.size_P());
+    a.beta = static_cast<uint32_t>(rt.beta());
+    return from_hip(phx::keyswitch_rotate_batch(a, n, stream));
+  });
+}
+
 int phantom_rotate_ext_accumulate(const phantom_context* ctx, size_t chain_index, uint64_t* ext,
                                   const uint64_t* const* key_digits, size_t dnum, uint32_t galois_elt, uint64_t* acc,
                                   int accumulate, hipStream_t stream) {

@@ -149,6 +149,31 @@ struct KsRotateArgs {
 };
 hipError_t keyswitch_rotate(const KsRotateArgs& a, int mode, size_t n, hipStream_t s);
 
+// Batched baby steps: keyswitch_rotate (mode 1) for several rotations of one ciphertext in ONE
+// launch.  A workgroup owns a SOURCE block (limb l, kGaloisBlock consecutive indices), reads the
+// shared digits and c0 there once from HBM, and for each entry writes the output block that block
+// maps to (binv) -- the digits are read once per level instead of once per rotation.
+constexpr uint32_t kGaloisBlock = 1024;  // automorphism block (min(n, this) consecutive indices)
+struct KsBatchEntry {
+  const uint64_t* const* evk = nullptr;  // device array of beta key pointers; nullptr: identity, out = P (c0, c1)
+  const uint32_t* perm = nullptr;        // NTT-domain permutation of the rotation
+  const uint32_t* binv = nullptr;        // source block -> output block (n / min(n, kGaloisBlock) entries)
+  int64_t out_off = 0;                   // output [2][QlP][n] at out + out_off (elements)
+};
+struct KsRotateBatchArgs {
+  const uint64_t* digits = nullptr;        // [beta][QlP][n]
+  const KsBatchEntry* entries = nullptr;   // device array of `count` entries
+  uint32_t count = 0;
+  const uint64_t* qp = nullptr;            // full-chain modulus / Barrett tables (by table row)
+  const uint64_t* qp_barrett = nullptr;
+  const uint64_t* ct = nullptr;            // [2][Ql][n]: c0 (every entry), c1 (identity entries)
+  const uint64_t* pmod = nullptr;          // P mod q_l, Shoup
+  const uint64_t* pmod_shoup = nullptr;
+  uint64_t* out = nullptr;                 // base of the outputs; must not alias digits / ct
+  uint32_t ql = 0, qlp = 0, size_q = 0, size_p = 0, beta = 0;
+};
+hipError_t keyswitch_rotate_batch(const KsRotateBatchArgs& a, size_t n, hipStream_t s);
+
 struct GaloisFinishArgs {
   const uint64_t* cx;
   const uint64_t* c0;

@@ -397,7 +397,7 @@ __global__ __launch_bounds__(kBlock) void moddown_modup_finish_kernel(const uint
 // output block of kGalB consecutive indices therefore reads one source block of kGalB consecutive
 // indices: a workgroup stages that block in LDS with coalesced loads and gathers from LDS, instead
 // of 64 scattered 8-byte reads per wave instruction from HBM.
-constexpr uint32_t kGalB = 1024;
+constexpr uint32_t kGalB = kGaloisBlock;
 
 template <int MODE>  // 0: permute; 1: + P c0 on the Ql limbs of polynomial 0, then permute; 2: + c0
 __global__ __launch_bounds__(kBlock) void galois_finish_kernel(GaloisFinishArgs a, uint32_t log_n, uint32_t bsz) {
@@ -490,6 +490,190 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_kernel(KsRotateArgs a, uint3
     a.out[qlp_n + e] = o1;
   }
   (void)n;
+}
+
+// keyswitch_rotate_batch: workgroup = (limb l, source block sblk); entry k's products go to LDS
+// buffer k & 1 (one barrier per entry: an entry's gather from buffer k & 1 finishes before any
+// thread passes entry k + 1's barrier, so entry k + 2 may overwrite it).
+//
+// Full blocks (BETA > 0): the block's digits and P c0 are loaded once into registers and shared by
+// every entry, so an entry reads only its key halves from HBM; those loads are issued for entry
+// k + 1 before entry k's barrier and gather, so they are in flight while the gather runs.
+template <int BETA>
+__global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchArgs a, uint32_t log_n) {
+  constexpr uint32_t bsz = kGalB;
+  constexpr int PP = kGalB / 2 / kBlock;  // pairs per thread
+  __shared__ uint64_t s0[2][kGalB], s1[2][kGalB];
+  const uint32_t nb = (1u << log_n) / bsz;
+  const uint32_t l = blockIdx.x / nb, sblk = blockIdx.x % nb;
+  const uint32_t twr = l >= a.ql ? a.size_q + (l - a.ql) : l;
+  const uint64_t q = a.qp[twr], r0 = a.qp_barrett[2 * twr], r1 = a.qp_barrett[2 * twr + 1];
+  const size_t lbase = (size_t)l << log_n, kbase = (size_t)twr << log_n;
+  const size_t qlp_n = (size_t)a.qlp << log_n, ql_n = (size_t)a.ql << log_n;
+  const size_t qp_n = (size_t)(a.size_q + a.size_p) << log_n;
+  const size_t j0 = (size_t)sblk * bsz;
+  const bool addc = l < a.ql;
+  const uint64_t w = addc ? a.pmod[l] : 0, ws = addc ? a.pmod_shoup[l] : 0;
+  u64x2 dg[PP][BETA], pc0[PP];
+#pragma unroll
+  for (int p = 0; p < PP; ++p) {
+    const size_t j = j0 + 2 * (threadIdx.x + p * kBlock);
+#pragma unroll
+    for (int b = 0; b < BETA; ++b) dg[p][b] = ld2(a.digits + b * qlp_n + lbase + j);
+    pc0[p] = make_ulonglong2(0, 0);
+    if (addc) {
+      const u64x2 c0 = ld2(a.ct + lbase + j);
+      pc0[p] = make_ulonglong2(mul_shoup(c0.x, w, ws, q), mul_shoup(c0.y, w, ws, q));
+    }
+  }
+  u64x2 k0[PP][BETA], k1[PP][BETA];
+  auto load_keys = [&](const KsBatchEntry& e) {
+    if (!e.evk) return;
+#pragma unroll
+    for (int b = 0; b < BETA; ++b) {
+      const uint64_t* key = e.evk[b];
+#pragma unroll
+      for (int p = 0; p < PP; ++p) {
+        const size_t j = j0 + 2 * (threadIdx.x + p * kBlock);
+        k0[p][b] = ld2(key + kbase + j);
+        k1[p][b] = ld2(key + qp_n + kbase + j);
+      }
+    }
+  };
+  KsBatchEntry e = a.entries[0];
+  load_keys(e);
+  for (uint32_t k = 0; k < a.count; ++k) {
+    uint64_t* t0 = s0[k & 1];
+    uint64_t* t1 = s1[k & 1];
+    const bool ks = e.evk != nullptr;
+#pragma unroll
+    for (int p = 0; p < PP; ++p) {
+      const uint32_t i = threadIdx.x + p * kBlock;
+      uint64_t v0x, v0y, v1x, v1y;
+      if (ks) {
+        u128 a0x{0, 0}, a0y{0, 0}, a1x{0, 0}, a1y{0, 0};
+#pragma unroll
+        for (int b = 0; b < BETA; ++b) {
+          add128(a0x, mul_wide(dg[p][b].x, k0[p][b].x));
+          add128(a0y, mul_wide(dg[p][b].y, k0[p][b].y));
+          add128(a1x, mul_wide(dg[p][b].x, k1[p][b].x));
+          add128(a1y, mul_wide(dg[p][b].y, k1[p][b].y));
+        }
+        v0x = add_mod(barrett_reduce_128(a0x, q, r0, r1), pc0[p].x, q);
+        v0y = add_mod(barrett_reduce_128(a0y, q, r0, r1), pc0[p].y, q);
+        v1x = barrett_reduce_128(a1x, q, r0, r1);
+        v1y = barrett_reduce_128(a1y, q, r0, r1);
+      } else {  // identity: P (c0, c1) on the Ql limbs, zero on P's
+        v0x = pc0[p].x;
+        v0y = pc0[p].y;
+        v1x = v1y = 0;
+        if (addc) {
+          const u64x2 c1 = ld2(a.ct + ql_n + lbase + j0 + 2 * i);
+          v1x = mul_shoup(c1.x, w, ws, q);
+          v1y = mul_shoup(c1.y, w, ws, q);
+        }
+      }
+      t0[2 * i] = v0x;
+      t0[2 * i + 1] = v0y;
+      t1[2 * i] = v1x;
+      t1[2 * i + 1] = v1y;
+    }
+    const KsBatchEntry cur = e;
+    if (k + 1 < a.count) {
+      e = a.entries[k + 1];
+      load_keys(e);  // in flight during this entry's barrier and gather
+    }
+    __syncthreads();
+    uint64_t* out = a.out + cur.out_off;
+    if (ks) {
+      const uint32_t ob = cur.binv[sblk];
+      const uint32_t* pm = cur.perm + (size_t)ob * bsz;
+#pragma unroll
+      for (uint32_t i = threadIdx.x; i < bsz; i += kBlock) {
+        const uint32_t src = pm[i] & (bsz - 1);
+        const size_t d = lbase + (size_t)ob * bsz + i;
+        out[d] = t0[src];
+        out[qlp_n + d] = t1[src];
+      }
+    } else {
+#pragma unroll
+      for (uint32_t i = threadIdx.x; i < bsz; i += kBlock) {
+        out[lbase + j0 + i] = t0[i];
+        out[qlp_n + lbase + j0 + i] = t1[i];
+      }
+    }
+  }
+}
+
+// any block size / beta: per entry, the digits and c0 re-read (L1 / L2 hits after the first)
+__global__ __launch_bounds__(kBlock) void ks_rotate_batch_kernel(KsRotateBatchArgs a, uint32_t log_n, uint32_t bsz) {
+  __shared__ uint64_t s0[2][kGalB], s1[2][kGalB];
+  const uint32_t nb = (1u << log_n) / bsz;
+  const uint32_t l = blockIdx.x / nb, sblk = blockIdx.x % nb;
+  const uint32_t twr = l >= a.ql ? a.size_q + (l - a.ql) : l;
+  const uint64_t q = a.qp[twr], r0 = a.qp_barrett[2 * twr], r1 = a.qp_barrett[2 * twr + 1];
+  const size_t lbase = (size_t)l << log_n, kbase = (size_t)twr << log_n;
+  const size_t qlp_n = (size_t)a.qlp << log_n, ql_n = (size_t)a.ql << log_n;
+  const size_t qp_n = (size_t)(a.size_q + a.size_p) << log_n;
+  const size_t j0 = (size_t)sblk * bsz;
+  const bool addc = l < a.ql;
+  const uint64_t w = addc ? a.pmod[l] : 0, ws = addc ? a.pmod_shoup[l] : 0;
+  for (uint32_t k = 0; k < a.count; ++k) {
+    const KsBatchEntry e = a.entries[k];
+    uint64_t* t0 = s0[k & 1];
+    uint64_t* t1 = s1[k & 1];
+    for (uint32_t i = threadIdx.x; i < bsz / 2; i += kBlock) {
+      const size_t j = j0 + 2 * i;
+      uint64_t v0x = 0, v0y = 0, v1x = 0, v1y = 0;
+      if (e.evk) {
+        u128 a0x{0, 0}, a0y{0, 0}, a1x{0, 0}, a1y{0, 0};
+        for (uint32_t b = 0; b < a.beta; ++b) {
+          const u64x2 c = ld2(a.digits + b * qlp_n + lbase + j);
+          const uint64_t* key = e.evk[b];
+          const u64x2 k0 = ld2(key + kbase + j), k1 = ld2(key + qp_n + kbase + j);
+          add128(a0x, mul_wide(c.x, k0.x));
+          add128(a0y, mul_wide(c.y, k0.y));
+          add128(a1x, mul_wide(c.x, k1.x));
+          add128(a1y, mul_wide(c.y, k1.y));
+        }
+        v0x = barrett_reduce_128(a0x, q, r0, r1);
+        v0y = barrett_reduce_128(a0y, q, r0, r1);
+        v1x = barrett_reduce_128(a1x, q, r0, r1);
+        v1y = barrett_reduce_128(a1y, q, r0, r1);
+      }
+      if (addc) {
+        const u64x2 c0 = ld2(a.ct + lbase + j);
+        v0x = add_mod(v0x, mul_shoup(c0.x, w, ws, q), q);
+        v0y = add_mod(v0y, mul_shoup(c0.y, w, ws, q), q);
+        if (!e.evk) {
+          const u64x2 c1 = ld2(a.ct + ql_n + lbase + j);
+          v1x = mul_shoup(c1.x, w, ws, q);
+          v1y = mul_shoup(c1.y, w, ws, q);
+        }
+      }
+      t0[2 * i] = v0x;
+      t0[2 * i + 1] = v0y;
+      t1[2 * i] = v1x;
+      t1[2 * i + 1] = v1y;
+    }
+    __syncthreads();
+    uint64_t* out = a.out + e.out_off;
+    if (e.evk) {
+      const uint32_t ob = e.binv[sblk];
+      const uint32_t* pm = e.perm + (size_t)ob * bsz;
+      for (uint32_t i = threadIdx.x; i < bsz; i += kBlock) {
+        const uint32_t src = pm[i] & (bsz - 1);
+        const size_t d = lbase + (size_t)ob * bsz + i;
+        out[d] = t0[src];
+        out[qlp_n + d] = t1[src];
+      }
+    } else {
+      for (uint32_t i = threadIdx.x; i < bsz; i += kBlock) {
+        out[lbase + j0 + i] = t0[i];
+        out[qlp_n + lbase + j0 + i] = t1[i];
+      }
+    }
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void galois_kernel(const uint64_t* __restrict__ in, uint64_t* out,
@@ -664,6 +848,22 @@ hipError_t keyswitch_rotate(const KsRotateArgs& a, int mode, size_t n, hipStream
     case 0: ks_rotate_kernel<0><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
     case 1: ks_rotate_kernel<1><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
     default: ks_rotate_kernel<2><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t keyswitch_rotate_batch(const KsRotateBatchArgs& a, size_t n, hipStream_t s) {
+  if (!a.digits || !a.entries || !a.ct || !a.out || !a.pmod || !a.pmod_shoup || a.beta == 0 || a.ql > a.qlp)
+    return hipErrorInvalidValue;
+  if (a.qlp == 0 || a.count == 0) return hipSuccess;
+  const uint32_t log_n = __builtin_ctzll(n), bsz = static_cast<uint32_t>(std::min<size_t>(n, kGalB));
+  const dim3 grid(static_cast<uint32_t>(a.qlp * (n / bsz)));
+  switch (bsz == kGalB ? a.beta : 0) {
+    case 1: ks_rotate_batch_full<1><<<grid, kBlock, 0, s>>>(a, log_n); break;
+    case 2: ks_rotate_batch_full<2><<<grid, kBlock, 0, s>>>(a, log_n); break;
+    case 3: ks_rotate_batch_full<3><<<grid, kBlock, 0, s>>>(a, log_n); break;
+    case 4: ks_rotate_batch_full<4><<<grid, kBlock, 0, s>>>(a, log_n); break;
+    default: ks_rotate_batch_kernel<<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
   }
   return hipGetLastError();
 }

@@ -676,6 +676,32 @@ void FHECKKSRNS::EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext&
 
 void FHECKKSRNS::EvalMultKeyGen(PhantomSecretKey& sk, const PhantomContext& cc) { mul_key_ = sk.gen_relinkey(cc); }
 
+const void* FHECKKSRNS::baby_table(const PhantomContext& cc, const LTLevel& lv, size_t QlP) const {
+  static_assert(sizeof(phx::KsBatchEntry) % sizeof(uint64_t) == 0, "entry of whole words");
+  const size_t n = cc.poly_degree();
+  std::vector<phx::KsBatchEntry> e(lv.g);
+  for (int j = 0; j < lv.g; ++j) {
+    const long r = static_cast<long>(j - lv.center) * lv.stride;
+    const long nn = static_cast<long>(n / 2);
+    if (((r % nn) + nn) % nn != 0) {  // else the identity: P (c0, c1) (KeySwitchExt)
+      const uint32_t elt = FindAutomorphismIndex2nComplex(static_cast<int>(r), n);
+      e[j].evk = galois_keys_.get(elt).public_keys_ptr();
+      e[j].perm = cc.galois_perm(elt);
+      e[j].binv = cc.galois_block_inv(elt);
+    }
+    e[j].out_off = static_cast<int64_t>(j * 2 * QlP * n);
+  }
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(e.data());
+  std::vector<uint64_t> words(w, w + e.size() * sizeof(phx::KsBatchEntry) / sizeof(uint64_t));
+  std::lock_guard<std::mutex> lk(baby_mu_);
+  auto& t = baby_tables_[&lv];
+  if (t.first != words) {
+    t.second.upload(words, cc.stream());
+    t.first = std::move(words);
+  }
+  return t.second.get();
+}
+
 PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const PhantomCiphertext& in,
                                           const LTLevel& lv) const {
   PhantomCiphertext tmp;
@@ -684,20 +710,40 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
   const size_t QlP = Ql + cc.size_P();
   hipStream_t s = cc.stream();
   DeviceBuffer<uint64_t> digits = EvalFastRotationPrecompute(cc, ct);
-  // baby steps from the shared digits, alternating between two streams (ct and the digits,
-  // main-stream buffers, live until both have joined)
-  std::vector<PhantomCiphertext> baby(lv.g);
-  run_parallel(cc, std::min(2, lv.g), [&](int t) {
-    for (int j = t; j < lv.g; j += 2) {
-      const long r = static_cast<long>(j - lv.center) * lv.stride;
-      const long nn = static_cast<long>(n / 2);
-      if (((r % nn) + nn) % nn == 0)
-        baby[j] = KeySwitchExt(cc, ct);
-      else
-        baby[j] = EvalFastRotationExt(cc, ct, galois_keys_, static_cast<int>(r), digits.get(), true);
+  // every baby step in one launch (keyswitch_rotate_batch): the digits and c0 are read from HBM
+  // once for the level, not once per rotation; baby j at babies + j 2 QlP n
+  const size_t baby_words = 2 * QlP * n;
+  DeviceBuffer<uint64_t> babies(static_cast<size_t>(lv.g) * baby_words, s);
+  {
+    const RnsTool& rt = cc.get_context_data(ct.chain_index()).gpu_rns_tool();
+    phx::KsRotateBatchArgs ba;
+    ba.digits = digits.get();
+    ba.entries = static_cast<const phx::KsBatchEntry*>(baby_table(cc, lv, QlP));
+    ba.count = static_cast<uint32_t>(lv.g);
+    ba.qp = cc.mod_QP().q;
+    ba.qp_barrett = cc.mod_QP().barrett;
+    ba.ct = ct.data();
+    ba.pmod = rt.bigP_mod_q();
+    ba.pmod_shoup = rt.bigP_mod_q_shoup();
+    ba.out = babies.get();
+    ba.ql = static_cast<uint32_t>(Ql);
+    ba.qlp = static_cast<uint32_t>(QlP);
+    ba.size_q = static_cast<uint32_t>(cc.size_Q());
+    ba.size_p = static_cast<uint32_t>(cc.size_P());
+    ba.beta = static_cast<uint32_t>(rt.beta());
+    hip_ok(phx::keyswitch_rotate_batch(ba, n, s), "linear transform baby steps");
+    static const bool shapes = std::getenv("PHX_BOOT_TRACE") != nullptr;
+    if (shapes)
+      std::fprintf(stderr, "[lt] chain %zu Ql %zu beta %zu D %d g %d b %d\n", lv.chain, Ql, rt.beta(), lv.D, lv.g, lv.b);
+    size_t rotations = 0;
+    for (int j = 0; j < lv.g; ++j) {
+      const long r = static_cast<long>(j - lv.center) * lv.stride, nn = static_cast<long>(n / 2);
+      rotations += ((r % nn) + nn) % nn != 0;
     }
-  });
-  for (auto& b : baby) b.retag(s);  // read and freed on this stream from here on
+    traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP * rotations, n));
+    // the digits and c0 read, the baby steps written
+    traffic::ciphertexts(traffic::limb_bytes(rt.beta() * QlP + Ql + 2 * QlP * static_cast<size_t>(lv.g), n));
+  }
   digits.release();
   // every giant step's inner sum in one launch
   std::vector<PhantomCiphertext> inner(lv.b);
@@ -710,7 +756,7 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
   la.pts = lv.d_pts.get();
   la.q = cc.mod_QP().q;
   la.barrett = cc.mod_QP().barrett;
-  for (int j = 0; j < lv.g; ++j) la.baby[j] = baby[j].data();
+  for (int j = 0; j < lv.g; ++j) la.baby[j] = babies.get() + static_cast<size_t>(j) * baby_words;
   for (int i = 0; i < lv.b; ++i) {
     inner[i].resize(2, QlP, n, s, false);
     inner[i].set_chain_index(ct.chain_index());
@@ -727,7 +773,7 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
     traffic::plaintexts(traffic::limb_bytes(nz * QlP, n));
     traffic::ciphertexts(traffic::limb_bytes(2 * QlP * static_cast<size_t>(lv.g + lv.b), n));
   }
-  baby.clear();
+  babies.release();
   // giant steps accumulate in the extended basis (one moddown at the end), spread over the
   // context's streams (giant i on chain i mod k); inner[] (main-stream buffers) lives until all
   // chains have joined

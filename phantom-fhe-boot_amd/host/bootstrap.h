@@ -150,6 +150,11 @@ class FHECKKSRNS {
   std::vector<double> cheb_;
   int giant_streams_ = 3;  // PHX_BOOT_GIANT_STREAMS: concurrent giant-step chains per level (profiles/r01/giant_streams_sweep.txt)
   mutable LeafTableCache leaf_tables_;
+  // per linear-transform level: the device table of its baby steps (phx::KsBatchEntry as raw
+  // words) and the host copy it was uploaded from (re-uploaded when keys or tables move)
+  mutable std::mutex baby_mu_;
+  mutable std::map<const void*, std::pair<std::vector<uint64_t>, DeviceBuffer<uint64_t>>> baby_tables_;
+  const void* baby_table(const PhantomContext& cc, const LTLevel& lv, size_t QlP) const;
   PhantomRelinKey mul_key_;
   PhantomGaloisKey galois_keys_;  // fused keys
 };

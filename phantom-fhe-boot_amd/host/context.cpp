@@ -1,11 +1,13 @@
 #include "context.h"
 
+#include <algorithm>
 #include <stdexcept>
 #include <thread>
 
 #include "hip_check.h"
 #include "numth.h"
 #include "../csrc/ntt.h"
+#include "../csrc/rns.h"
 
 namespace phantom {
 
@@ -84,11 +86,15 @@ const uint32_t* PhantomContext::galois_perm(uint32_t elt) const {
   if (it != perms_.end()) return it->second.get();
   if (!(elt & 1) || elt >= 2 * n_) throw std::invalid_argument("invalid Galois element");
   const int logn = arith::log2_exact(n_);
-  std::vector<uint32_t> perm(n_);
+  std::vector<uint32_t> perm(n_);  // [n] permutation, then [n / bsz] block inverse
   for (uint32_t j = 0; j < n_; ++j) {
     const uint64_t idx = ((2ull * j + 1) * elt) % (2ull * n_);
     perm[arith::reverse_bits(j, logn)] = arith::reverse_bits(static_cast<uint32_t>(idx >> 1), logn);
   }
+  // + the block inverse (galois_block_inv): output block ob reads source block perm[ob bsz] / bsz
+  const uint32_t bsz = static_cast<uint32_t>(std::min<size_t>(n_, phx::kGaloisBlock)), nb = static_cast<uint32_t>(n_) / bsz;
+  perm.resize(n_ + nb);
+  for (uint32_t ob = 0; ob < nb; ++ob) perm[n_ + perm[static_cast<size_t>(ob) * bsz] / bsz] = ob;
   DeviceBuffer<uint32_t> d;
   d.upload(perm, stream_.s);
   return perms_.emplace(elt, std::move(d)).first->second.get();

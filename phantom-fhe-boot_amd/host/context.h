@@ -151,6 +151,9 @@ class PhantomContext {
   // NTT-form polynomial (PrecomputeAutoMapKernel, src/util.cu:941-958; the reference rebuilds it
   // on every call).  Built once per context, so every table lives on the context's device.
   const uint32_t* galois_perm(uint32_t elt) const;
+  // its block inverse: source block sb (min(n, phx::kGaloisBlock) consecutive indices) is read by
+  // output block galois_block_inv(elt)[sb] (n / min(n, kGaloisBlock) entries)
+  const uint32_t* galois_block_inv(uint32_t elt) const { return galois_perm(elt) + n_; }
   // NTT(X^power) over the first L key moduli ([L][n]), cached per context
   const uint64_t* monomial_ntt(uint32_t power, size_t L) const;
 

@@ -62,6 +62,8 @@ _SIGS = {
     "phantom_keyswitch_ext": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_fast_rotation_ext": (ctypes.c_int, [vp, sz, vp, vp, ctypes.POINTER(vp), sz, ctypes.c_uint32, ctypes.c_int,
                                                  vp, vp]),
+    "phantom_fast_rotation_ext_batch": (ctypes.c_int, [vp, sz, vp, vp, ctypes.POINTER(ctypes.POINTER(vp)), sz,
+                                                       ctypes.POINTER(ctypes.c_uint32), sz, ctypes.POINTER(vp), vp]),
     "phantom_rotate_ext_accumulate": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, ctypes.c_uint32, vp,
                                                      ctypes.c_int, vp]),
     "phantom_tensor_lin": (ctypes.c_int, [vp, sz, vp, vp, vp, vp, vp, sz, vp, vp]),

@@ -12,6 +12,8 @@ against the CPU oracle (oracle/oracle.c, which restates the reference functions 
 
 Operands are uniform random residues (parity is a property of the arithmetic, not of key or
 ciphertext structure)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -99,6 +101,49 @@ def test_fast_rotation_ext(c4, rng, chain, elt_kind, add_first):
     O.lib().or_fast_rotation_ext(O.P(c0), O.P(digits), O.ptrs(keys), elt, add_first, O.P(want), N, len(ql),
                                  c4.size_Q, c4.size_P, O.P(O.arr(c4.moduli)))
     assert np.array_equal(to_host(dout), want)
+
+
+@pytest.mark.parametrize("shape,chain,count,identity_at", [("c4", 1, 9, 4), ("c4", 3, 4, None), ("c4", 17, 32, 16),
+                                                             ("n512", 1, 7, 2)])
+def test_fast_rotation_ext_batch(c4, rng, shape, chain, count, identity_at):
+    """one launch of `count` baby steps == the per-rotation EvalFastRotationExt / KeySwitchExt
+    (c4: full 1024-index blocks, beta 3 / 2; n512: the any-size kernel, beta 4)"""
+    if shape == "c4":
+        ctx, n, size_p = c4, N, SIZE_P
+    else:
+        n, size_p = 512, 2
+        ctx = PA.Context(n, O.coeff_modulus_create(n, [50] * 10), size_p)
+    ql = ctx.ql(chain)
+    em = _ext_mods(ctx, chain)
+    beta = -(-len(ql) // size_p)
+    rand = lambda mods, polys=1: np.concatenate([O.random_limbs(rng, n, mods) for _ in range(polys)])
+    ct = rand(ql, 2)
+    digits = rand(em, beta)
+    elts = [pow(5, 3 * k + 1, 2 * n) for k in range(count)]
+    elts[-1] = 2 * n - 1  # a conjugation among the rotations
+    dnum = -(-ctx.size_Q // size_p)
+    distinct = []  # host memory: three key sets shared round robin
+    for _ in range(3):
+        keys = [rand(ctx.moduli, 2) for _ in range(dnum)]
+        distinct.append((keys, [to_dev(k) for k in keys]))
+    keysets = [distinct[k % 3] for k in range(count)]
+    dct, ddig = to_dev(ct), to_dev(digits)
+    douts = [to_dev(np.full(2 * len(em) * n, 5, dtype=np.uint64)) for _ in range(count)]
+    key_arrays = [None if k == identity_at else _vp(keysets[k][1]) for k in range(count)]
+    kk = (ctypes.POINTER(ctypes.c_void_p) * count)(*[ctypes.cast(a, ctypes.POINTER(ctypes.c_void_p)) if a is not None
+                                                     else None for a in key_arrays])
+    el = (ctypes.c_uint32 * count)(*elts)
+    PA.check(_lib().phantom_fast_rotation_ext_batch(ctx.handle, chain, ptr(dct), ptr(ddig), kk, dnum, el, count,
+                                                    _vp(douts), stream()))
+    mods = O.P(O.arr(ctx.moduli))
+    for k in range(count):
+        want = np.zeros(2 * len(em) * n, dtype=np.uint64)
+        if k == identity_at:
+            O.lib().or_keyswitch_ext(O.P(ct), O.P(want), n, len(ql), ctx.size_Q, ctx.size_P, mods)
+        else:
+            O.lib().or_fast_rotation_ext(O.P(ct), O.P(digits), O.ptrs(keysets[k][0]), elts[k], 1, O.P(want), n,
+                                         len(ql), ctx.size_Q, ctx.size_P, mods)
+        assert np.array_equal(to_host(douts[k]), want), k
 
 
 @pytest.mark.parametrize("chain,accumulate", [(2, 0), (2, 1)])
