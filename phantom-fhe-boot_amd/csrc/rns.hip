@@ -322,12 +322,26 @@ __global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32
   }
 }
 
+// blockIdx.y = limb l (digit l / alpha: one scalar division per block), blockIdx.x = a chunk of
+// kCopyPairs pairs of that limb; every load of a thread issued before its stores
+constexpr int kCopyPairs = 4 * kBlock;
 __global__ __launch_bounds__(kBlock) void modup_copy_kernel(const uint64_t* c2, uint64_t* tmu, uint32_t log_n,
-                                                            size_t pairs, size_t size_qlp_n, size_t alpha_n) {
-  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
-    const size_t e = 2 * i;
-    const size_t beta = e / alpha_n;
-    *reinterpret_cast<u64x2*>(tmu + beta * size_qlp_n + e) = ld2(c2 + e);
+                                                            size_t size_qlp_n, uint32_t alpha) {
+  const uint32_t l = blockIdx.y, digit = l / alpha;
+  const size_t base = ((size_t)l << log_n) + (size_t)blockIdx.x * 2 * kCopyPairs;
+  const size_t limb_end = (size_t)(l + 1) << log_n;
+  const uint64_t* src = c2 + base;
+  uint64_t* dst = tmu + digit * size_qlp_n + base;
+  u64x2 v[kCopyPairs / kBlock];
+#pragma unroll
+  for (int r = 0; r < kCopyPairs / kBlock; ++r) {
+    const size_t e = 2 * ((size_t)r * kBlock + threadIdx.x);
+    if (base + e < limb_end) v[r] = ld2(src + e);
+  }
+#pragma unroll
+  for (int r = 0; r < kCopyPairs / kBlock; ++r) {
+    const size_t e = 2 * ((size_t)r * kBlock + threadIdx.x);
+    if (base + e < limb_end) *reinterpret_cast<u64x2*>(dst + e) = v[r];
   }
 }
 
@@ -799,9 +813,10 @@ hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s) {
 
 hipError_t modup_copy_digits(const uint64_t* c2, uint64_t* t_mod_up, size_t n, size_t size_ql, size_t size_qlp,
                              size_t alpha, hipStream_t s) {
-  const size_t pairs = n * size_ql / 2;
-  modup_copy_kernel<<<grid_for(pairs), kBlock, 0, s>>>(c2, t_mod_up, __builtin_ctzll(n), pairs, size_qlp * n,
-                                                       alpha * n);
+  if (size_ql == 0) return hipSuccess;
+  if (alpha == 0 || n < 2) return hipErrorInvalidValue;
+  const dim3 grid(static_cast<uint32_t>((n / 2 + kCopyPairs - 1) / kCopyPairs), static_cast<uint32_t>(size_ql));
+  modup_copy_kernel<<<grid, kBlock, 0, s>>>(c2, t_mod_up, __builtin_ctzll(n), size_qlp * n, static_cast<uint32_t>(alpha));
   return hipGetLastError();
 }
 

@@ -3,7 +3,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r02v
-timeout -k 10 600 python -u -m pytest tests/test_gpu_bootk.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r02v/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_bootk.py tests/test_gpu_ckks.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r02v/pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/r02v/pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 ./phantom-fhe-boot_amd/bin/bootstrapping_example boot 16 5 > gpurun_out/r02v/boot.log 2>&1 || { tail -5 gpurun_out/r02v/boot.log; exit 1; }
 tail -4 gpurun_out/r02v/boot.log
