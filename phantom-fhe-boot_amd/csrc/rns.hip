@@ -34,6 +34,12 @@ dim3 poly_grid(size_t work_items, size_t polys) {
 using u64x2 = ulonglong2;
 
 __device__ __forceinline__ u64x2 ld2(const uint64_t* p) { return *reinterpret_cast<const u64x2*>(p); }
+// streamed-once operands (keys): nontemporal 16-byte load
+__device__ __forceinline__ u64x2 ld2_nt(const uint64_t* p) {
+  typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+  const v2u64 v = __builtin_nontemporal_load(reinterpret_cast<const v2u64*>(p));
+  return make_ulonglong2(v.x, v.y);
+}
 __device__ __forceinline__ void st2(uint64_t* p, uint64_t a, uint64_t b) {
   *reinterpret_cast<u64x2*>(p) = make_ulonglong2(a, b);
 }
@@ -549,8 +555,8 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchArgs
 #pragma unroll
       for (int p = 0; p < PP; ++p) {
         const size_t j = j0 + 2 * (threadIdx.x + p * kBlock);
-        k0[p][b] = ld2(key + kbase + j);
-        k1[p][b] = ld2(key + qp_n + kbase + j);
+        k0[p][b] = ld2_nt(key + kbase + j);
+        k1[p][b] = ld2_nt(key + qp_n + kbase + j);
       }
     }
   };
