@@ -591,8 +591,8 @@ __global__ __launch_bounds__(CBLOCK, BCV ? 2 : kWavesPerEU) void ntt_col(KArgs a
         for (int j = 0; j < E; ++j) store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, v[j]);  // lazy [0, 8q)
       } else {
         const uint64_t ni = a.n_inv[tr.row], nis = a.n_inv_shoup[tr.row];
-        const bool scaled = a.scale != nullptr;
-        const uint64_t sc = scaled ? a.scale[tr.buf_limb] : 0, scs = scaled ? a.scale_shoup[tr.buf_limb] : 0;
+        const uint64_t sc = a.scale ? a.scale[tr.buf_limb] : 1, scs = a.scale ? a.scale_shoup[tr.buf_limb] : 0;
+        const bool scaled = sc != 1;  // (a scale of 1 is the identity on canonical values)
 #pragma unroll
         for (int j = 0; j < E; ++j) {
           uint64_t y = mul_shoup(v[j], ni, nis, lc.q);

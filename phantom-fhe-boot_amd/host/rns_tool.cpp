@@ -33,6 +33,7 @@ void DeviceBaseConverter::init(const std::vector<uint64_t>& in, const std::vecto
   d_ibase.upload(in, s);
   d_obase.upload(out, s);
   d_obase_barrett.upload(ob, s);
+  qhat_inv_host = qinv;
   d_qhat_inv.upload(qinv, s);
   d_qhat_inv_shoup.upload(qinvs, s);
   d_qhat_mod_p.upload(qhat, s);
@@ -123,6 +124,21 @@ RnsTool::RnsTool(size_t n, const std::vector<uint64_t>& qp, size_t size_P, size_
   d_partQlHatInv_.upload(hatinv, s);
   d_partQlHatInv_shoup_.upload(hatinvs, s);
   p_to_ql_.init(base_P_, base_Ql_, s);
+  {
+    // moddown_modup's INTT over Ql u P: 1 on Ql (the finish reads those limbs as they are),
+    // qHat_p^-1 on P (the P -> Ql conversion's prescale)
+    std::vector<uint64_t> sc(base_Ql_.size() + size_P_), scs(sc.size());
+    for (size_t i = 0; i < base_Ql_.size(); ++i) {
+      sc[i] = 1;
+      scs[i] = shoup(1, base_Ql_[i]);
+    }
+    for (size_t i = 0; i < size_P_; ++i) {
+      sc[base_Ql_.size() + i] = p_to_ql_.qhat_inv_host[i];
+      scs[base_Ql_.size() + i] = shoup(sc[base_Ql_.size() + i], base_P_[i]);
+    }
+    d_mm_scale_.upload(sc, s);
+    d_mm_scale_shoup_.upload(scs, s);
+  }
   if (size_Ql >= 2) {
     std::vector<uint64_t> ib{base_Ql_.back()};
     ib.insert(ib.end(), base_P_.begin(), base_P_.end());
@@ -242,10 +258,10 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
   pm.first_a = 0;
   pm.first_b = (int)size_Q_;
   const bool fused = fused_bconv_ok(size_P_) && polys <= (size_t)phx::kMaxBconvPolys;
-  // with the fused conversion the INTT also applies the converter's qHat^-1 (bconv's prescale)
-  hip_ok(phx::ntt_inverse(ntt, cp, cp, pm.batched(np, size_QlP * n_, size_QlP * n_),
-                          fused ? p_to_ql_.d_qhat_inv.get() : nullptr, fused ? p_to_ql_.d_qhat_inv_shoup.get() : nullptr,
-                          s),
+  // the INTT also applies the converter's qHat^-1 (the conversion's prescale, otherwise redone
+  // by every output group of the conversion)
+  hip_ok(phx::ntt_inverse(ntt, cp, cp, pm.batched(np, size_QlP * n_, size_QlP * n_), p_to_ql_.d_qhat_inv.get(),
+                          p_to_ql_.d_qhat_inv_shoup.get(), s),
          "moddown INTT(P)");
   uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, polys * size_Ql * n_);
   // NTT(delta) with the finish (cx - delta) P^-1 (+ ct) as its epilogue
@@ -270,7 +286,7 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
     hip_ok(phx::ntt_forward_bconv(ntt, delta, dm, bcv, epi, s), "moddown bconv + NTT + finish");
     return;
   }
-  phx::BconvArgs ba = p_to_ql_.args(cp, delta, true);
+  phx::BconvArgs ba = p_to_ql_.args(cp, delta, false);
   ba.polys = np;
   ba.in_stride = size_QlP * n_;
   ba.out_stride = size_Ql * n_;
@@ -286,9 +302,9 @@ void RnsTool::moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTabl
   all.split = (int)size_Ql;
   all.first_a = 0;
   all.first_b = (int)size_Q_;
-  hip_ok(phx::ntt_inverse(ntt, c1, c1, all, nullptr, nullptr, s), "moddown-modup INTT");
+  hip_ok(phx::ntt_inverse(ntt, c1, c1, all, d_mm_scale_.get(), d_mm_scale_shoup_.get(), s), "moddown-modup INTT");
   uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, size_Ql * n_);
-  hip_ok(phx::bconv(p_to_ql_.args(c1 + size_Ql * n_, delta, true), n_, s), "moddown-modup bconv P");
+  hip_ok(phx::bconv(p_to_ql_.args(c1 + size_Ql * n_, delta, false), n_, s), "moddown-modup bconv P");
   uint64_t* t_cks = ws_->get(s, Workspace::kModupInv, size_Ql * n_);
   phx::ModdownModupConsts k{d_Ql_.get(), d_bigPInv_mod_q_.get(), d_bigPInv_mod_q_shoup_.get(), d_partQlHatInv_.get(),
                             d_partQlHatInv_shoup_.get()};
@@ -313,8 +329,7 @@ void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables&
   dm.first_b = (int)size_Q_;
   const bool fused = fused_bconv_ok(1 + size_P_) && polys <= (size_t)phx::kMaxBconvPolys;
   hip_ok(phx::ntt_inverse(ntt, dropped, dropped, dm.batched(np, size_QlP * n_, size_QlP * n_),
-                          fused ? pq_to_ql1_.d_qhat_inv.get() : nullptr,
-                          fused ? pq_to_ql1_.d_qhat_inv_shoup.get() : nullptr, s),
+                          pq_to_ql1_.d_qhat_inv.get(), pq_to_ql1_.d_qhat_inv_shoup.get(), s),
          "moddown-rescale INTT");
   uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, polys * Ln * n_);
   phx::NttEpilogue epi;
@@ -337,7 +352,7 @@ void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables&
     hip_ok(phx::ntt_forward_bconv(ntt, delta, om, bcv, epi, s), "moddown-rescale bconv + NTT + finish");
     return;
   }
-  phx::BconvArgs ba = pq_to_ql1_.args(dropped, delta, true);
+  phx::BconvArgs ba = pq_to_ql1_.args(dropped, delta, false);
   ba.polys = np;
   ba.in_stride = size_QlP * n_;
   ba.out_stride = Ln * n_;

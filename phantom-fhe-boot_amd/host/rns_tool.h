@@ -19,6 +19,7 @@ struct DeviceBaseConverter {
   std::vector<uint64_t> ibase, obase;
   DeviceBuffer<uint64_t> d_ibase, d_obase, d_obase_barrett;
   DeviceBuffer<uint64_t> d_qhat_inv, d_qhat_inv_shoup;  // [ibase] (qHat_i^-1 mod q_i)
+  std::vector<uint64_t> qhat_inv_host;
   DeviceBuffer<uint64_t> d_qhat_mod_p;                  // [ibase][obase]
   void init(const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, hipStream_t s);
   phx::BconvArgs args(const uint64_t* in, uint64_t* out, bool prescale) const;
@@ -81,6 +82,7 @@ class RnsTool {
   DeviceBuffer<uint64_t> d_Ql_, d_Ql_barrett_, d_QlP_, d_QlP_barrett_;
   // key switching
   DeviceBuffer<uint64_t> d_partQlHatInv_, d_partQlHatInv_shoup_;
+  DeviceBuffer<uint64_t> d_mm_scale_, d_mm_scale_shoup_;  // moddown_modup's INTT scale over Ql u P
   // the base conversion can run as the forward NTT's column-pass prologue (ntt.h BconvPrologue):
   // 2-D transform sizes and at most 15 input limbs; opt-in (PHX_FUSED_BCONV=1), see rns_tool.cpp
   bool fused_bconv_ok(size_t ibase) const;
