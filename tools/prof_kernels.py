@@ -8,7 +8,7 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "phantom-fhe-boot_amd", "py"))
+sys.path.insert(0, os.environ.get("PHX_PY", os.path.join(ROOT, "phantom-fhe-boot_amd", "py")))  # PHX_PY: a variant build
 import torch  # noqa: E402
 import phantom_amd as PA  # noqa: E402
 
