@@ -132,6 +132,14 @@ int phantom_modup(const phantom_context *ctx, size_t chain_index, const uint64_t
 /* key_switch_inner_prod (include/evaluate.cuh:27-29, src/eval_key_switch.cu:88-109) */
 int phantom_keyswitch_inner_prod(const phantom_context *ctx, size_t chain_index, const uint64_t *t_mod_up,
                                  const uint64_t *const *key_digits, size_t dnum, uint64_t *cx, hipStream_t stream);
+/* DBaseConverter::bConv_BEHZ (src/rns_bconv.cu:212-229; bconv_mult_unroll2_kernel :40-69 and
+ * bconv_matmul_unroll2_kernel :143-179): dst[j] = sum_i [src_i * qHat_i^-1]_{q_i} * (qHat_i mod p_j)
+ * mod p_j for coefficient-form src [ibase_size][n] -> dst [obase_size][n] (device arrays); ibase /
+ * obase are host arrays of moduli.  prescale = 0 skips the [x * qHat^-1] step (src already scaled,
+ * as the key-switch drivers pass it).  Builds the converter's tables and synchronizes `stream`
+ * before returning (a test / one-off entry; the drivers keep converters per level). */
+int phantom_fast_bconv(const uint64_t *ibase, size_t ibase_size, const uint64_t *obase, size_t obase_size,
+                       const uint64_t *src, uint64_t *dst, size_t n, int prescale, hipStream_t stream);
 /* DRNSTool::moddown_from_NTT (src/rns_bconv.cu:791-843): cx_i [L+P][n] NTT form (P limbs clobbered)
  * -> out [L][n] = (cx_i - NTT(bconv(INTT(cx_i|P)))) * P^-1 */
 int phantom_moddown_from_ntt(const phantom_context *ctx, size_t chain_index, uint64_t *cx_i, uint64_t *out,

@@ -13,6 +13,7 @@
 #include "../host/context.h"
 #include "../host/evaluate.h"
 #include "../host/numth.h"
+#include "../host/rns_tool.h"
 #include "../host/serialize.h"
 #include "phantom_amd.h"
 #include "rns.h"
@@ -140,6 +141,20 @@ int phantom_keyswitch_inner_prod(const phantom_context* ctx, size_t chain_index,
     const auto& pc = *ctx->ctx;
     return from_hip(phx::keyswitch_inner_prod(t_mod_up, evk, cx, pc.mod_QP().q, pc.mod_QP().barrett, pc.poly_degree(),
                                               rt.size_Ql(), pc.size_Q(), pc.size_P(), rt.beta(), stream));
+  });
+}
+
+int phantom_fast_bconv(const uint64_t* ibase, size_t ibase_size, const uint64_t* obase, size_t obase_size,
+                       const uint64_t* src, uint64_t* dst, size_t n, int prescale, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (!ibase || !obase || !src || !dst || ibase_size == 0 || obase_size == 0 || n == 0 || n % 2 != 0)
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "fast_bconv: empty or odd-sized input");
+    phantom::DeviceBaseConverter conv;
+    conv.init(std::vector<uint64_t>(ibase, ibase + ibase_size), std::vector<uint64_t>(obase, obase + obase_size), stream);
+    const hipError_t e = phx::bconv(conv.args(src, dst, prescale != 0), n, stream);
+    if (e != hipSuccess) return from_hip(e);
+    // the converter's tables are freed on return
+    return from_hip(hipStreamSynchronize(stream));
   });
 }
 

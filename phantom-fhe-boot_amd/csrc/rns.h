@@ -77,8 +77,27 @@ struct BconvArgs {
   const uint64_t* job_qhat_mod_p[kMaxJobs] = {};
   const uint64_t* job_obase[kMaxJobs] = {};
   const uint64_t* job_obase_barrett[kMaxJobs] = {};
+  // Matrix-core form (bconv_mfma_tables): with these set, ibase <= 16, obase <= 64 and n a
+  // multiple of 16, the conversion runs as int8 MFMA products (rns.hip, bconv_mfma_kernel)
+  const void* mfma_frag = nullptr;       // A fragments, bconv_mfma_frag_bytes(ibase, obase) bytes
+  const uint64_t* mfma_rows = nullptr;   // [16 * ceil(obase / 16)][2] = {p_j, bits of double(1 / p_j)}
+  const void* job_mfma_frag[kMaxJobs] = {};
+  const uint64_t* job_mfma_rows[kMaxJobs] = {};
 };
 hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s);
+
+// Matrix-core base conversion tables.  The conversion y_j = sum_s t_s c_sj mod p_j runs as int8
+// MFMA products: with m_{s,a,j} = c_sj 256^a mod p_j and t_s = sum_a d_{s,a} 256^a (signed base-256
+// digits d in [-128, 128)), y_j = sum_b 256^b T_bj (mod p_j) with T_bj = sum_{s,a} d_{s,a} e_b(m_{s,a,j})
+// (e_b: signed digit b), 8 int8 GEMMs with K = 8 ibase.  The host precomputes the A fragments of
+// v_mfma_i32_16x16x64_i8: [jb][b][kstep][lane][16 bytes], lane (r, g) = (lane & 15, lane >> 4)
+// holding row j = 16 jb + r, bytes i <-> (limb s = 8 kstep + 2 g + i / 8, digit a = i % 8).
+constexpr int kBconvMfmaMaxIbase = 16;
+constexpr int kBconvMfmaMaxObase = 64;
+size_t bconv_mfma_frag_bytes(int ibase, int obase);
+// fills frag (bconv_mfma_frag_bytes) and rows from qhat_mod_p [ibase][obase] and obase (host arrays)
+void bconv_mfma_tables(const uint64_t* qhat_mod_p, const uint64_t* obase, int ibase, int obase_size, uint8_t* frag,
+                       uint64_t* rows);
 
 // ---- hybrid key switching -------------------------------------------------------------
 // modup_copy_partQl_kernel (src/rns_bconv.cu:522-528): t_mod_up[beta][qlp] gets the digit's own

@@ -4,6 +4,8 @@
 #include "rns.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <vector>
 
 #include "arith.h"
 
@@ -12,7 +14,7 @@ namespace {
 
 constexpr int kBlock = 256;
 
-int grid_for(size_t work_items) {
+int num_cus() {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -20,6 +22,11 @@ int grid_for(size_t work_items) {
     cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ? p.multiProcessorCount
                                                                                               : 256;
   }
+  return cus;
+}
+
+int grid_for(size_t work_items) {
+  const int cus = num_cus();
   const size_t blocks = (work_items + kBlock - 1) / kBlock;
   return static_cast<int>(std::max<size_t>(1, std::min<size_t>(blocks, static_cast<size_t>(cus) * 8)));
 }
@@ -192,6 +199,8 @@ __device__ __forceinline__ void bconv_select_job(BconvArgs& a) {
         a.qhat_mod_p = a.job_qhat_mod_p[k];
         a.obase = a.job_obase[k];
         a.obase_barrett = a.job_obase_barrett[k];
+        a.mfma_frag = a.job_mfma_frag[k];
+        a.mfma_rows = a.job_mfma_rows[k];
       }
     a.skip_at += d * a.skip_step;
   }
@@ -325,6 +334,181 @@ __global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32
     }
     const int oj = j < a.skip_at ? j : j + a.skip_len;
     st2(a.out + (size_t)oj * n + 2 * i, out[0], out[1]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Base conversion on the matrix cores (rns.h, bconv_mfma_tables).  Inputs t < 2^61 become signed
+// base-256 digits with one add and one xor: (t + 0x80..80) ^ 0x80..80 holds bytes d_a + 128 ^ 128
+// = d_a as int8, sum_a d_a 256^a = t.  For a tile of 16 coefficients (the MFMA's columns) and 16
+// output limbs (its rows), the 8 products T_b = A_b . D (v_mfma_i32_16x16x64_i8, K = 64 per
+// kstep: 8 limbs x 8 digits) are exact int32 sums of at most 128 products of magnitude <= 2^14,
+// so |T_b| <= 2^21, and
+//   y = sum_b T_b 256^b = sum_{s,a} d_{s,a} m_{s,a}       (|y| <= 2^14 p, congruent to the result)
+// is rebuilt from four int32 pairs (T_0 + 256 T_1 ...) as its low 64 bits (wrapping adds) and
+// an FP32 estimate of y / p; q = rint(estimate) is the nearest quotient (|error| ~2^-8), so y - q p
+// lies in [-p/2, p/2] and one conditional add of p makes it canonical.  Per output element this
+// is about 32 VALU instructions instead of the 60 v_mad_u64_u32 of the 30-bit-split form.
+//
+// The conversion is then bound by its data movement, and what sets that is the reads in flight:
+// measured (tools/variants, profiles/r02/bconv_mfma/), the same kernel with its products or its
+// reassembly removed ran at the same speed while it kept one tile of loads in flight per wave.
+// So: workgroups stage the job's A fragments (<= 64 KB) in LDS once; each wave owns whole
+// 16-coefficient tiles (every 16-row block, NJB of them), keeps the inputs of the next TWO tiles
+// in flight, and stores through a raw buffer resource (rows past obase are dropped by the range
+// check instead of a branch, so the store count is static and the loop's vmcnt waits never wait
+// for stores).
+// ---------------------------------------------------------------------------------------
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+#ifndef PHX_BCONV_MFMA_WAVES
+#define PHX_BCONV_MFMA_WAVES 8
+#endif
+constexpr int kMfmaWaves = PHX_BCONV_MFMA_WAVES;  // waves per workgroup; two workgroups per CU
+constexpr int kMfmaMaxJB = kBconvMfmaMaxObase / 16;
+constexpr uint32_t kDropRow = 0x80000000u;  // byte offset of output rows past obase
+constexpr int kBufferWord3 = 0x00020000;    // raw buffer resource word 3 (gfx9: 32-bit data format)
+constexpr int kStoreSc1 = 16;               // write-through output stores (sc1): 27.3 -> 25.8 us mean, nt 27.6
+
+__device__ __forceinline__ uint64_t signed_digits(uint64_t t) {
+  constexpr uint64_t k80 = 0x8080808080808080ull;
+  return (t + k80) ^ k80;
+}
+
+template <int KT, int NJB, bool PRE>
+__global__ __launch_bounds__(kMfmaWaves * 64) __attribute__((amdgpu_waves_per_eu(kMfmaWaves / 2, kMfmaWaves / 2)))
+void bconv_mfma_kernel(BconvArgs a, uint32_t n) {
+  __shared__ v4i frag[NJB * 8 * KT * 64];
+  // per output row j: p_j, quotient factors, {p_j as P0 + 2^32 P1 with P0 a signed 32-bit value,
+  // byte offset of the row in a.out}
+  __shared__ uint64_t row_p[NJB * 16];
+  __shared__ float4 row_f[NJB * 16];  // {2^48, 2^32, 2^16, 1} / p_j
+  __shared__ uint4 row_m[NJB * 16];
+  bconv_select_job(a);
+  a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial (or digit)
+  a.out += blockIdx.z * a.out_stride;
+  const int ib = a.ibase_size, ob = a.obase_size;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t c = lane & 15, g = lane >> 4;
+  const uint32_t tiles = n / 16, step = gridDim.x * kMfmaWaves;
+  uint32_t tile = blockIdx.x * kMfmaWaves + wave;
+  // this lane's input limbs: s = 8 t + 2 g + u.  Loads are unconditional: limbs past ib read limb
+  // ib - 1 (zeroed when converted) and tiles past the end read the last tile
+  auto load = [&](uint64_t (&x)[KT][2], uint32_t tl) {
+    const uint64_t* src = a.in + min(tl, tiles - 1) * 16 + c;
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int s = min(8 * t + 2 * static_cast<int>(g) + u, ib - 1);
+        x[t][u] = __builtin_nontemporal_load(src + (size_t)s * n);
+      }
+  };
+  uint64_t xa[KT][2], xb[KT][2];
+  load(xa, tile);  // in flight while the tables are staged
+  load(xb, tile + step);
+  {
+    const v4i* gf = static_cast<const v4i*>(a.mfma_frag);
+    constexpr int kWords = NJB * 8 * KT * 64, kPer = (kWords + kMfmaWaves * 64 - 1) / (kMfmaWaves * 64);
+    v4i tmp[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = threadIdx.x + i * kMfmaWaves * 64;
+      if (e < kWords) tmp[i] = gf[e];
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = threadIdx.x + i * kMfmaWaves * 64;
+      if (e < kWords) frag[e] = tmp[i];
+    }
+    for (int e = threadIdx.x; e < NJB * 16; e += kMfmaWaves * 64) {
+      const uint64_t p = a.mfma_rows[2 * e];
+      const double inv = __longlong_as_double(static_cast<long long>(a.mfma_rows[2 * e + 1]));
+      row_p[e] = p;
+      row_f[e] = make_float4(static_cast<float>(inv * 281474976710656.0), static_cast<float>(inv * 4294967296.0),
+                             static_cast<float>(inv * 65536.0), static_cast<float>(inv));
+      const int oj = e < a.skip_at ? e : e + a.skip_len;
+      const uint32_t p0 = lo32(p), p1 = hi32(p) + (p0 >> 31);  // p = (int32)p0 + 2^32 p1
+      row_m[e] = make_uint4(p0, p1, e < ob ? static_cast<uint32_t>(oj) * n * 8u : kDropRow, 0u);
+    }
+  }
+  __syncthreads();
+  if (tile >= tiles) return;  // no barrier below
+  // the output rows as a raw buffer (<= kDropRow bytes, checked by the launcher)
+  const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      a.out, 0, static_cast<int>(static_cast<uint32_t>(ob + max(a.skip_len, 0)) * n * 8u), kBufferWord3);
+
+  // convert one tile (its inputs in x, which is then refilled with the tile two steps ahead)
+  auto convert = [&](uint64_t (&x)[KT][2], uint32_t tl) {
+    v4i bf[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      uint64_t d[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int s = 8 * t + 2 * static_cast<int>(g) + u;
+        uint64_t v = x[t][u];
+        if constexpr (PRE) {
+          const int sc = min(s, ib - 1);
+          v = mul_shoup(v, a.qhat_inv[sc], a.qhat_inv_shoup[sc], a.ibase[sc]);
+        }
+        d[u] = s < ib ? signed_digits(v) : 0;  // limbs past ib: zero digits (their A bytes are 0 too)
+      }
+      bf[t] = v4i{(int)lo32(d[0]), (int)hi32(d[0]), (int)lo32(d[1]), (int)hi32(d[1])};
+    }
+    load(x, tl + 2 * step);
+    const uint32_t k = tl * 16 + c;
+#pragma unroll
+    for (int jb = 0; jb < NJB; ++jb) {
+      __builtin_amdgcn_sched_barrier(0);  // one row block at a time (hoisting the next block's LDS reads spills)
+      v4i acc[8];
+#pragma unroll
+      for (int b = 0; b < 8; ++b)  // the first product takes an inline-constant zero accumulator
+        acc[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(frag[(jb * 8 + b) * KT * 64 + lane], bf[0], v4i{0, 0, 0, 0}, 0,
+                                                       0, 0);
+#pragma unroll
+      for (int t = 1; t < KT; ++t)
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+          acc[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(frag[((jb * 8 + b) * KT + t) * 64 + lane], bf[t], acc[b], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = jb * 16 + 4 * static_cast<int>(g) + r;
+        const int lo_a = acc[0][r] + acc[1][r] * 256, lo_b = acc[2][r] + acc[3][r] * 256;
+        const int hi_a = acc[4][r] + acc[5][r] * 256, hi_b = acc[6][r] + acc[7][r] * 256;
+        // low 64 bits of y: (hi_a 2^32 + hi_b 2^48) only touch the high word
+        const uint32_t w = static_cast<uint32_t>(hi_a) + (static_cast<uint32_t>(hi_b) << 16);
+        const uint64_t L = static_cast<uint64_t>(static_cast<int64_t>(lo_a)) +
+                           (static_cast<uint64_t>(static_cast<int64_t>(lo_b)) << 16) + (static_cast<uint64_t>(w) << 32);
+        // nearest quotient in FP32 from per-row factors f = {2^48, 2^32, 2^16, 1} / p: the
+        // quotient is below 2^15 and every term below ~2^15, so its error is ~2^-8 < 1/2
+        const float4 f = row_f[j];
+        const uint4 rm = row_m[j];
+        const uint64_t p = row_p[j];
+        const int qt = static_cast<int>(__builtin_rintf(
+            __builtin_fmaf(static_cast<float>(hi_b), f.x,
+                           __builtin_fmaf(static_cast<float>(hi_a), f.y,
+                                          __builtin_fmaf(static_cast<float>(lo_b), f.z, static_cast<float>(lo_a) * f.w)))));
+        // y = L - qt p (mod 2^64) with p = P0 + 2^32 P1: one v_mad_i64_i32 and a high-word
+        // subtract; y lies in [-p/2, p/2] (qt is the nearest quotient): one conditional add of p
+        const int64_t tq = static_cast<int64_t>(-qt) * static_cast<int64_t>(static_cast<int32_t>(rm.x)) +
+                           static_cast<int64_t>(L);
+        int64_t y = static_cast<int64_t>(static_cast<uint64_t>(tq) -
+                                         (static_cast<uint64_t>(static_cast<uint32_t>(qt) * rm.y) << 32));
+        y += static_cast<int64_t>(p) & (y >> 63);
+        // rows past ob sit at kDropRow, past the buffer's range: the store is dropped
+        const v2u yv = {lo32(static_cast<uint64_t>(y)), hi32(static_cast<uint64_t>(y))};
+        __builtin_amdgcn_raw_buffer_store_b64(yv, out_rsrc, rm.z + k * 8u, 0, kStoreSc1);
+      }
+    }
+  };
+  for (;;) {  // two tiles per trip: the input buffers alternate without register moves
+    convert(xa, tile);
+    tile += step;
+    if (tile >= tiles) break;
+    convert(xb, tile);
+    tile += step;
+    if (tile >= tiles) break;
   }
 }
 
@@ -795,11 +979,90 @@ hipError_t tensor_prod_2x2(const uint64_t* ct1, const uint64_t* ct2, uint64_t* o
   return hipGetLastError();
 }
 
+size_t bconv_mfma_frag_bytes(int ibase, int obase) {
+  return static_cast<size_t>((obase + 15) / 16) * 8 * ((ibase + 7) / 8) * 64 * 16;
+}
+
+void bconv_mfma_tables(const uint64_t* qhat_mod_p, const uint64_t* obase, int ibase, int obase_size, uint8_t* frag,
+                       uint64_t* rows) {
+  using u128h = unsigned __int128;
+  constexpr uint64_t k80 = 0x8080808080808080ull;
+  const int njb = (obase_size + 15) / 16, kt = (ibase + 7) / 8;
+  // signed base-256 digits of m_{s,a,j} = c_sj 256^a mod p_j, packed in a uint64 each
+  std::vector<uint64_t> sd((size_t)ibase * 8 * obase_size);
+  for (int s = 0; s < ibase; ++s)
+    for (int dig = 0; dig < 8; ++dig)
+      for (int j = 0; j < obase_size; ++j) {
+        const uint64_t p = obase[j];
+        const uint64_t m =
+            static_cast<uint64_t>((static_cast<u128h>(qhat_mod_p[(size_t)s * obase_size + j] % p) << (8 * dig)) % p);
+        sd[((size_t)s * 8 + dig) * obase_size + j] = (m + k80) ^ k80;
+      }
+  // A fragment of v_mfma_i32_16x16x64_i8: lane (r, g) = (lane & 15, lane >> 4) holds row r and
+  // bytes i = 0..15 of K slots 16 g + i <-> (limb 8 t + 2 g + i / 8, digit i % 8); the B fragment
+  // (the kernel's inputs) uses the same K order
+  for (int jb = 0; jb < njb; ++jb)
+    for (int b = 0; b < 8; ++b)
+      for (int t = 0; t < kt; ++t)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int i = 0; i < 16; ++i) {
+            const int j = jb * 16 + (lane & 15), s = 8 * t + 2 * (lane >> 4) + i / 8, dig = i % 8;
+            const uint8_t v = j < obase_size && s < ibase
+                                  ? static_cast<uint8_t>(sd[((size_t)s * 8 + dig) * obase_size + j] >> (8 * b))
+                                  : 0;
+            frag[((((size_t)jb * 8 + b) * kt + t) * 64 + lane) * 16 + i] = v;
+          }
+  for (int j = 0; j < njb * 16; ++j) {
+    const double inv = j < obase_size ? 1.0 / static_cast<double>(obase[j]) : 0.0;
+    uint64_t bits;
+    static_assert(sizeof(bits) == sizeof(inv), "double");
+    __builtin_memcpy(&bits, &inv, sizeof(bits));
+    rows[2 * j] = j < obase_size ? obase[j] : 0;
+    rows[2 * j + 1] = bits;
+  }
+}
+
+namespace {
+bool mfma_bconv_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PHX_BCONV_MFMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+}  // namespace
+
 hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s) {
   if (a.ibase_size <= 0 || a.ibase_size > kMaxIbase || a.obase_size <= 0) return hipErrorInvalidValue;
   const uint32_t pairs = static_cast<uint32_t>(n / 2);
   if (a.polys < 1) return hipErrorInvalidValue;
   if (a.jobs > 1 && (a.jobs != a.polys || a.jobs > BconvArgs::kMaxJobs)) return hipErrorInvalidValue;
+  bool mfma = mfma_bconv_enabled() && a.ibase_size <= kBconvMfmaMaxIbase && a.obase_size <= kBconvMfmaMaxObase &&
+              n >= 16 && n % 16 == 0 &&
+              static_cast<size_t>(a.obase_size + std::max(0, a.skip_len)) * n * 8 <= kDropRow;
+  if (a.jobs > 1)
+    for (int d = 0; d < a.jobs; ++d) mfma = mfma && a.job_mfma_frag[d] && a.job_mfma_rows[d];
+  else
+    mfma = mfma && a.mfma_frag && a.mfma_rows;
+  if (mfma) {
+    // two workgroups per CU over all polynomials, each wave looping over 16-column tiles
+    const uint32_t tiles = static_cast<uint32_t>(n / 16);
+    const uint32_t want = std::max<uint32_t>(1, static_cast<uint32_t>(2 * num_cus() / a.polys));
+    const dim3 g(std::min<uint32_t>((tiles + kMfmaWaves - 1) / kMfmaWaves, want), 1, a.polys);
+    const bool pre = a.qhat_inv != nullptr;
+    const uint32_t nn = static_cast<uint32_t>(n);
+    const int kt = (a.ibase_size + 7) / 8, njb = (a.obase_size + 15) / 16;
+#define PHX_BCONV_MFMA_LAUNCH(KT, NJB)                                                             \
+  if (kt == KT && njb == NJB) {                                                                    \
+    if (pre) bconv_mfma_kernel<KT, NJB, true><<<g, kMfmaWaves * 64, 0, s>>>(a, nn);                \
+    else bconv_mfma_kernel<KT, NJB, false><<<g, kMfmaWaves * 64, 0, s>>>(a, nn);                   \
+    return hipGetLastError();                                                                      \
+  }
+    PHX_BCONV_MFMA_LAUNCH(1, 1) PHX_BCONV_MFMA_LAUNCH(1, 2) PHX_BCONV_MFMA_LAUNCH(1, 3) PHX_BCONV_MFMA_LAUNCH(1, 4)
+    PHX_BCONV_MFMA_LAUNCH(2, 1) PHX_BCONV_MFMA_LAUNCH(2, 2) PHX_BCONV_MFMA_LAUNCH(2, 3) PHX_BCONV_MFMA_LAUNCH(2, 4)
+#undef PHX_BCONV_MFMA_LAUNCH
+    return hipErrorInvalidValue;
+  }
   const dim3 g(((pairs + kBlock - 1) / kBlock) * ((a.obase_size + kBconvJ - 1) / kBconvJ), 1, a.polys);
   const bool pre = a.qhat_inv != nullptr;
   switch (a.ibase_size) {

@@ -37,6 +37,13 @@ void DeviceBaseConverter::init(const std::vector<uint64_t>& in, const std::vecto
   d_qhat_inv.upload(qinv, s);
   d_qhat_inv_shoup.upload(qinvs, s);
   d_qhat_mod_p.upload(qhat, s);
+  if (I <= (size_t)phx::kBconvMfmaMaxIbase && O <= (size_t)phx::kBconvMfmaMaxObase) {
+    std::vector<uint8_t> frag(phx::bconv_mfma_frag_bytes((int)I, (int)O));
+    std::vector<uint64_t> rows(2 * 16 * ((O + 15) / 16));
+    phx::bconv_mfma_tables(qhat.data(), out.data(), (int)I, (int)O, frag.data(), rows.data());
+    d_mfma_frag.upload(frag, s);
+    d_mfma_rows.upload(rows, s);
+  }
 }
 
 phx::BconvArgs DeviceBaseConverter::args(const uint64_t* in, uint64_t* out, bool prescale) const {
@@ -51,6 +58,8 @@ phx::BconvArgs DeviceBaseConverter::args(const uint64_t* in, uint64_t* out, bool
   a.obase_barrett = d_obase_barrett.get();
   a.ibase_size = static_cast<int>(ibase.size());
   a.obase_size = static_cast<int>(obase.size());
+  a.mfma_frag = d_mfma_frag.get();
+  a.mfma_rows = d_mfma_rows.get();
   return a;
 }
 
@@ -188,6 +197,8 @@ void RnsTool::digit_bconv(const uint64_t* t_cks, uint64_t* t_mod_up, hipStream_t
       a.job_qhat_mod_p[d] = c.d_qhat_mod_p.get();
       a.job_obase[d] = c.d_obase.get();
       a.job_obase_barrett[d] = c.d_obase_barrett.get();
+      a.job_mfma_frag[d] = c.d_mfma_frag.get();
+      a.job_mfma_rows[d] = c.d_mfma_rows.get();
     }
     hip_ok(phx::bconv(a, n_, s), "digit bconv");
   }

@@ -21,6 +21,9 @@ struct DeviceBaseConverter {
   DeviceBuffer<uint64_t> d_qhat_inv, d_qhat_inv_shoup;  // [ibase] (qHat_i^-1 mod q_i)
   std::vector<uint64_t> qhat_inv_host;
   DeviceBuffer<uint64_t> d_qhat_mod_p;                  // [ibase][obase]
+  // matrix-core form of the conversion (rns.h bconv_mfma_tables), empty when the shape has none
+  DeviceBuffer<uint8_t> d_mfma_frag;
+  DeviceBuffer<uint64_t> d_mfma_rows;
   void init(const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, hipStream_t s);
   phx::BconvArgs args(const uint64_t* in, uint64_t* out, bool prescale) const;
 };

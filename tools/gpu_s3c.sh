@@ -1,0 +1,11 @@
+# MFMA base conversion: parity + C3 kernel traces for grid variants
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out/s3c
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ckks.py tests/test_gpu_bootk.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/s3c/pytest.log 2>&1
+rc=$?; tail -3 gpurun_out/s3c/pytest.log; [ $rc -eq 0 ] || exit $rc
+cd /tmp
+for v in "PHX_BCONV_MFMA_WG=2" "PHX_BCONV_MFMA_WG=4"; do
+  env $v MODE=c3 timeout -k 10 200 rocprofv3 --kernel-trace -d $GRAFT_REPO_ROOT/gpurun_out/s3c/$v -o c3 -- python3 $GRAFT_REPO_ROOT/tools/prof_kernels.py > $GRAFT_REPO_ROOT/gpurun_out/s3c/$v.log 2>&1 || exit 1
+done
