@@ -384,6 +384,7 @@ void bconv_mfma_kernel(BconvArgs a, uint32_t n) {
   __shared__ uint64_t row_p[NJB * 16];
   __shared__ float4 row_f[NJB * 16];  // {2^48, 2^32, 2^16, 1} / p_j
   __shared__ uint4 row_m[NJB * 16];
+  __shared__ ulonglong4 pre_c[PRE ? kBconvMfmaMaxIbase : 1];  // {q_s, qHat_s^-1, its Shoup quotient}
   bconv_select_job(a);
   a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial (or digit)
   a.out += blockIdx.z * a.out_stride;
@@ -421,6 +422,10 @@ void bconv_mfma_kernel(BconvArgs a, uint32_t n) {
       const int e = threadIdx.x + i * kMfmaWaves * 64;
       if (e < kWords) frag[e] = tmp[i];
     }
+    if constexpr (PRE)
+      if (threadIdx.x < static_cast<uint32_t>(ib))
+        pre_c[threadIdx.x] = make_ulonglong4(a.ibase[threadIdx.x], a.qhat_inv[threadIdx.x],
+                                             a.qhat_inv_shoup[threadIdx.x], 0);
     for (int e = threadIdx.x; e < NJB * 16; e += kMfmaWaves * 64) {
       const uint64_t p = a.mfma_rows[2 * e];
       const double inv = __longlong_as_double(static_cast<long long>(a.mfma_rows[2 * e + 1]));
@@ -449,8 +454,8 @@ void bconv_mfma_kernel(BconvArgs a, uint32_t n) {
         const int s = 8 * t + 2 * static_cast<int>(g) + u;
         uint64_t v = x[t][u];
         if constexpr (PRE) {
-          const int sc = min(s, ib - 1);
-          v = mul_shoup(v, a.qhat_inv[sc], a.qhat_inv_shoup[sc], a.ibase[sc]);
+          const int sc = min(s, ib - 1);  // per-limb constants from LDS: global loads here would
+          v = mul_shoup(v, pre_c[sc].y, pre_c[sc].z, pre_c[sc].x);  // join the loop's vmcnt waits
         }
         d[u] = s < ib ? signed_digits(v) : 0;  // limbs past ib: zero digits (their A bytes are 0 too)
       }
