@@ -124,6 +124,19 @@ hipError_t ntt_forward_bconv(const NttTables& t, uint64_t* out, const LimbMap& m
 hipError_t ntt_inverse(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                        const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream);
 
+// Inverse NTT that also copies its (NTT-form) input: the first pass stores every loaded input
+// limb l (buffer limb index) unchanged at copy + (l / alpha) * digit_stride + l * n as well.  This
+// is modup's modup_copy_partQl_kernel (src/rns_bconv.cu:522-528) folded into its INTT
+// (nwt_2d_radix8_backward_scale): the copy no longer re-reads c2.  2-D sizes (n >= 2^10) only.
+struct NttCopy {
+  uint64_t* out = nullptr;
+  size_t digit_stride = 0;  // elements between digits
+  int alpha = 1;            // limbs per digit
+};
+hipError_t ntt_inverse_copy(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
+                            const uint64_t* scale, const uint64_t* scale_shoup, const NttCopy& copy,
+                            hipStream_t stream);
+
 // The 1-D radix-2 path (fnwt_1d / inwt_1d, include/ntt.cuh:157-169, src/ntt/ntt_1d.cu): one
 // workgroup per limb, the limb in LDS; n = 2^3 .. 2^11.  ntt_forward / ntt_inverse use it for
 // n < 2^10; these entry points force it (the reference's test_nwt_1d covers n = 2^8 .. 2^11).

@@ -301,6 +301,7 @@ struct KArgs {
   size_t bcast_stride;
   NttEpilogue epi;            // forward epilogue (see ntt.h), row pass only
   BconvPrologue bcv;          // forward base-conversion prologue (see ntt.h), column pass only
+  NttCopy copy;               // inverse: the row pass also stores its input here (see ntt.h)
 };
 
 // y: processed-limb index over the batch -> polynomial, buffer limb within it, table row
@@ -639,6 +640,15 @@ __device__ __forceinline__ void row_load(uint64_t (&x)[E], const uint64_t* src) 
   for (int j = 0; j < E; ++j) x[j] = __builtin_nontemporal_load(src + j * Sub<S2_LOG>::T);
 }
 
+// inverse row pass with NttCopy: the loaded input limb stored unchanged into its digit's slot
+template <int S2_LOG>
+__device__ __forceinline__ void row_copy(const KArgs& a, const TileRef& tr, const uint64_t (&x)[E]) {
+  uint64_t* dst = a.copy.out + (size_t)(tr.buf_limb / a.copy.alpha) * a.copy.digit_stride +
+                  (size_t)tr.buf_limb * a.n + tr.k;
+#pragma unroll
+  for (int j = 0; j < E; ++j) store_wt(dst + j * Sub<S2_LOG>::T, x[j]);
+}
+
 // The epilogue form holds its operands (EpiOperands) through the butterflies: two waves per SIMD
 // give it the registers to do so without spilling (168 VGPRs at three waves spilled 47).
 template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false>
@@ -675,6 +685,7 @@ __global__ __launch_bounds__(BLOCK, EPI ? 2 : kWavesPerEU) void ntt_row(KArgs a)
     uint64_t x[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) x[j] = xn[j];
+    if (!FWD && a.copy.out) row_copy<S2_LOG>(a, tr, x);  // workgroup-uniform branch
     const LimbCtx lc = limb_ctx(a, tr.row);
     uint64_t* dst = a.out + tr.off;
     uint32_t rn = 0;
@@ -922,7 +933,7 @@ template <int S1_LOG, int S2_LOG>
 hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const LimbMap& map, bool inverse,
                   const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream,
                   const uint64_t* bcast = nullptr, size_t bcast_stride = 0, const NttEpilogue& epi = NttEpilogue{},
-                  const BconvPrologue* bcv = nullptr) {
+                  const BconvPrologue* bcv = nullptr, const NttCopy& copy = NttCopy{}) {
   const int per_poly = map.num_limbs - (map.skip_end - map.skip_begin);
   if (per_poly <= 0 || map.polys <= 0) return hipSuccess;
   const int limbs = per_poly * map.polys;
@@ -941,6 +952,7 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   a.bcast = bcast; a.bcast_stride = bcast_stride;
   a.epi = epi;
   if (bcv) a.bcv = *bcv;
+  if (inverse) a.copy = copy;
   if (a.map.in_stride == 0) a.map.in_stride = (size_t)map.num_limbs * tb.n;
   if (a.map.out_stride == 0) a.map.out_stride = (size_t)map.num_limbs * tb.n;
   constexpr int S1 = 1 << S1_LOG, S2 = 1 << S2_LOG;
@@ -972,6 +984,7 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
     hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false>), grid_r, block_r, 0, stream, a);
     a.in = out;
     a.map.in_stride = a.map.out_stride;
+    a.copy = NttCopy{};  // the row pass made the copy
     hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false>), grid_c, block_c, 0, stream, a);
   }
   return hipGetLastError();
@@ -980,11 +993,11 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
 hipError_t dispatch(const NttTables& tb, const uint64_t* in, uint64_t* out, const LimbMap& map, bool inverse,
                     const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream,
                     const uint64_t* bcast = nullptr, size_t bcast_stride = 0, const NttEpilogue& epi = NttEpilogue{},
-                    const BconvPrologue* bcv = nullptr) {
+                    const BconvPrologue* bcv = nullptr, const NttCopy& copy = NttCopy{}) {
 #define PHX_NTT_CASE(LOGN, A, B) \
-  case LOGN: return launch<A, B>(tb, in, out, map, inverse, scale, scale_shoup, stream, bcast, bcast_stride, epi, bcv);
+  case LOGN: return launch<A, B>(tb, in, out, map, inverse, scale, scale_shoup, stream, bcast, bcast_stride, epi, bcv, copy);
   if (tb.log_n < 10) {
-    if (bcv) return hipErrorNotSupported;
+    if (bcv || copy.out) return hipErrorNotSupported;
     return launch_1d(tb, in, out, map, inverse, scale, scale_shoup, stream, bcast, bcast_stride, epi);
   }
   switch (tb.log_n) {
@@ -1023,6 +1036,13 @@ hipError_t ntt_forward_bconv(const NttTables& t, uint64_t* out, const LimbMap& m
 hipError_t ntt_inverse(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                        const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream) {
   return dispatch(t, in, out, map, true, scale, scale_shoup, stream);
+}
+
+hipError_t ntt_inverse_copy(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
+                            const uint64_t* scale, const uint64_t* scale_shoup, const NttCopy& copy,
+                            hipStream_t stream) {
+  if (!copy.out || copy.alpha < 1 || in == out) return hipErrorInvalidValue;
+  return dispatch(t, in, out, map, true, scale, scale_shoup, stream, nullptr, 0, NttEpilogue{}, nullptr, copy);
 }
 
 hipError_t ntt_1d_forward(const NttTables& t, uint64_t* inout, const LimbMap& map, hipStream_t stream) {

@@ -214,10 +214,22 @@ void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables
   const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_, alpha = size_P_;
   uint64_t* t_cks = ws_->get(s, Workspace::kModupInv, size_Ql * n_);
   // INTT(c2) * partQlHatInv (nwt_2d_radix8_backward_scale)
-  hip_ok(phx::ntt_inverse(ntt, c2, t_cks, phx::LimbMap::contiguous((int)size_Ql, 0), d_partQlHatInv_.get(),
-                          d_partQlHatInv_shoup_.get(), s),
-         "modup INTT");
-  hip_ok(phx::modup_copy_digits(c2, t_mod_up, n_, size_Ql, size_QlP, alpha, s), "modup copy");
+  // and the digits' own limbs (modup_copy_partQl_kernel) stored by the INTT's first pass, which
+  // reads c2 anyway
+  if (n_ >= 1024) {
+    phx::NttCopy cp;
+    cp.out = t_mod_up;
+    cp.digit_stride = size_QlP * n_;
+    cp.alpha = (int)alpha;
+    hip_ok(phx::ntt_inverse_copy(ntt, c2, t_cks, phx::LimbMap::contiguous((int)size_Ql, 0), d_partQlHatInv_.get(),
+                                 d_partQlHatInv_shoup_.get(), cp, s),
+           "modup INTT + copy");
+  } else {
+    hip_ok(phx::ntt_inverse(ntt, c2, t_cks, phx::LimbMap::contiguous((int)size_Ql, 0), d_partQlHatInv_.get(),
+                            d_partQlHatInv_shoup_.get(), s),
+           "modup INTT");
+    hip_ok(phx::modup_copy_digits(c2, t_mod_up, n_, size_Ql, size_QlP, alpha, s), "modup copy");
+  }
   // per digit: the complement limbs = NTT(bconv(digit)), every limb but the digit's own
   // (include_special_mod_exclude_range); the full digits in one launch (digit b skips
   // [b alpha, (b + 1) alpha)), a short last digit apart.  At n >= 2^10 the conversion is the
