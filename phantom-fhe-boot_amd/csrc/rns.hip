@@ -361,6 +361,9 @@ __global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32
 // ---------------------------------------------------------------------------------------
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+#ifndef PHX_BCONV_CONTIG
+#define PHX_BCONV_CONTIG 0
+#endif
 #ifndef PHX_BCONV_MFMA_WAVES
 #define PHX_BCONV_MFMA_WAVES 8
 #endif
@@ -391,8 +394,16 @@ void bconv_mfma_kernel(BconvArgs a, uint32_t n) {
   const int ib = a.ibase_size, ob = a.obase_size;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t c = lane & 15, g = lane >> 4;
-  const uint32_t tiles = n / 16, step = gridDim.x * kMfmaWaves;
+  const uint32_t tiles = n / 16;
+#if PHX_BCONV_CONTIG  // experiment: each wave owns a contiguous run of tiles
+  const uint32_t nwaves = gridDim.x * kMfmaWaves, per = (tiles + nwaves - 1) / nwaves, step = 1;
+  uint32_t tile = (blockIdx.x * kMfmaWaves + wave) * per;
+  const uint32_t tile_end = min(tile + per, tiles);
+#else
+  const uint32_t step = gridDim.x * kMfmaWaves;
   uint32_t tile = blockIdx.x * kMfmaWaves + wave;
+  const uint32_t tile_end = tiles;
+#endif
   // this lane's input limbs: s = 8 t + 2 g + u.  Loads are unconditional: limbs past ib read limb
   // ib - 1 (zeroed when converted) and tiles past the end read the last tile
   auto load = [&](uint64_t (&x)[KT][2], uint32_t tl) {
@@ -438,7 +449,7 @@ void bconv_mfma_kernel(BconvArgs a, uint32_t n) {
     }
   }
   __syncthreads();
-  if (tile >= tiles) return;  // no barrier below
+  if (tile >= tile_end) return;  // no barrier below
   // the output rows as a raw buffer (<= kDropRow bytes, checked by the launcher)
   const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
       a.out, 0, static_cast<int>(static_cast<uint32_t>(ob + max(a.skip_len, 0)) * n * 8u), kBufferWord3);
@@ -510,10 +521,10 @@ void bconv_mfma_kernel(BconvArgs a, uint32_t n) {
   for (;;) {  // two tiles per trip: the input buffers alternate without register moves
     convert(xa, tile);
     tile += step;
-    if (tile >= tiles) break;
+    if (tile >= tile_end) break;
     convert(xb, tile);
     tile += step;
-    if (tile >= tiles) break;
+    if (tile >= tile_end) break;
   }
 }
 
