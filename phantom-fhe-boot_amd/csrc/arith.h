@@ -120,6 +120,61 @@ __device__ __forceinline__ uint64_t mulhi_approx(uint64_t a, uint64_t s) {
   return static_cast<uint64_t>(a1) * s1 + h;
 }
 
+#ifndef PHX_INT_NOCARRY
+#define PHX_INT_NOCARRY 1
+#endif
+
+#if PHX_INT_NOCARRY
+// Carry-free forms.  A 64-bit subtraction compiles to v_sub_co / v_subb_co with the borrow in
+// VCC, and gfx950 needs wait states (s_nop) between the VCC write and the VCC read; a csub adds
+// a 64-bit compare and two v_cndmask behind another VCC hazard.  Here every constant subtraction
+// is an addition of the negated constant in one v_lshl_add_u64 (shift 0), and csub selects with
+// a sign mask (ashr + and) instead of VCC.  Same integers, so bit-identical results.
+__device__ __forceinline__ uint64_t add64(uint64_t a, uint64_t b) {
+  uint64_t r;
+  asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// hides that v is a negation, so x + v is not canonicalised back into a subtraction
+__device__ __forceinline__ uint64_t opaque(uint64_t v) {
+  asm("" : "+v"(v));
+  return v;
+}
+// x - m if that is >= 0 else x, for x, m < 2^63, given nm = -m mod 2^64
+__device__ __forceinline__ uint64_t csub_n(uint64_t x, uint64_t m, uint64_t nm) {
+  const uint64_t t = add64(x, nm);
+  const uint32_t s = static_cast<uint32_t>(static_cast<int32_t>(hi32(t)) >> 31);
+  return add64(t, (static_cast<uint64_t>(hi32(m) & s) << 32) | (lo32(m) & s));
+}
+// a w mod q in [0, 4q) (as mul_shoup_lazy4 below), given nq = -q mod 2^64: a w + Q' (-q)
+__device__ __forceinline__ uint64_t mul_shoup_lazy4(uint64_t a, uint64_t w, uint64_t ws, uint64_t q) {
+  return a * w + mulhi_approx(a, ws) * opaque(0 - q);
+}
+
+// forward CT butterfly: x, y in [0, 8q) -> [0, 8q)
+__device__ __forceinline__ void ct_bfly8(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
+  const uint64_t q4 = q << 2;
+  const uint64_t t = mul_shoup_lazy4(y, w, ws, q);
+  const uint64_t u = csub_n(x, q4, opaque(0 - q4));
+  x = add64(u, t);
+  y = u + q4 - t;
+}
+
+// inverse GS butterfly: x, y in [0, 4q) -> [0, 4q)
+__device__ __forceinline__ void gs_bfly4(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
+  const uint64_t q4 = q << 2;
+  const uint64_t d = x + q4 - y;
+  x = csub_n(add64(x, y), q4, opaque(0 - q4));
+  y = mul_shoup_lazy4(d, w, ws, q);
+}
+
+// [0, 8q) -> [0, q)
+__device__ __forceinline__ uint64_t reduce8(uint64_t v, uint64_t q) {
+  v = csub_n(v, q << 2, opaque(0 - (q << 2)));
+  v = csub_n(v, q << 1, opaque(0 - (q << 1)));
+  return csub_n(v, q, opaque(0 - q));
+}
+#else
 // a w mod q in [0, 4q) for any a < 2^64, w < q, ws = floor(w 2^64 / q)
 __device__ __forceinline__ uint64_t mul_shoup_lazy4(uint64_t a, uint64_t w, uint64_t ws, uint64_t q) {
   return a * w - mulhi_approx(a, ws) * q;
@@ -144,5 +199,7 @@ __device__ __forceinline__ void gs_bfly4(uint64_t& x, uint64_t& y, uint64_t w, u
 
 // [0, 8q) -> [0, q)
 __device__ __forceinline__ uint64_t reduce8(uint64_t v, uint64_t q) { return csub(csub(csub(v, q << 2), q << 1), q); }
+
+#endif  // PHX_INT_NOCARRY
 
 }  // namespace phx
