@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <sstream>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -95,6 +96,42 @@ static void example_ckks_enc(PhantomContext& context, double scale) {
   correctness = true;
   for (size_t i = 0; i < slot_count; i++) correctness &= eq(result[i], input[i]);
   require(correctness, "Asymmetric encryption error");
+}
+
+// seed-compressed symmetric ciphertexts (include/ciphertext.h:227-318): save_symmetric writes c0
+// and the seed of c1, load_symmetric regenerates c1 bit for bit; the loaded ciphertext decrypts
+// to the message, and the asymmetric / 3-polynomial cases throw as in the reference
+static void example_ckks_save_symmetric(PhantomContext& context, double scale) {
+  PhantomSecretKey secret_key(context);
+  PhantomPublicKey public_key = secret_key.gen_publickey(context);
+  PhantomCKKSEncoder encoder(context);
+  std::vector<cplx> input = random_msg(encoder.slot_count()), result;
+  PhantomPlaintext plain;
+  encoder.encode(context, input, scale, plain);
+  PhantomCiphertext sym;
+  secret_key.encrypt_symmetric(context, plain, sym);
+  std::stringstream ss;
+  sym.save_symmetric(ss);
+  const size_t words = sym.coeff_modulus_size() * sym.poly_modulus_degree();
+  require(ss.str().size() == 58 + words * 8 + PhantomCiphertext::kSeedBytes, "save_symmetric size");
+  PhantomCiphertext loaded;
+  loaded.load_symmetric(context, ss);
+  require(loaded.to_host(context.stream()) == sym.to_host(context.stream()), "load_symmetric: c0 || c1 differ");
+  require(loaded.chain_index() == sym.chain_index() && loaded.scale() == sym.scale(), "load_symmetric header");
+  secret_key.decrypt(context, loaded, plain);
+  encoder.decode(context, plain, result);
+  bool correctness = true;
+  for (size_t i = 0; i < input.size(); i++) correctness &= eq(result[i], input[i]);
+  require(correctness, "seed-compressed ciphertext decrypt error");
+  PhantomCiphertext asym;
+  public_key.encrypt_asymmetric(context, plain, asym);
+  bool threw = false;
+  try {
+    asym.save_symmetric(ss);
+  } catch (const std::runtime_error&) {
+    threw = true;
+  }
+  require(threw, "save_symmetric of an asymmetric ciphertext must throw");
 }
 
 static void example_ckks_add(PhantomContext& context, double scale) {
@@ -325,6 +362,7 @@ int main(int argc, char** argv) {
     PhantomContext context(parms);
     run("ckks_enc", alpha, [&] { example_ckks_enc(context, scale); });
     run("ckks_add", alpha, [&] { example_ckks_add(context, scale); });
+    run("ckks_save_symmetric", alpha, [&] { example_ckks_save_symmetric(context, scale); });
     run("ckks_mul_plain", alpha, [&] { example_ckks_mul_plain(context, scale); });
     run("ckks_mul", alpha, [&] { example_ckks_mul(context, scale); });
     run("ckks_rotation", alpha, [&] { example_ckks_rotation(context, scale); });

@@ -3,6 +3,9 @@
 #include <algorithm>
 #include <stdexcept>
 
+#include "../csrc/ntt.h"
+#include "hip_check.h"
+#include "keys.h"
 #include "serialize.h"
 
 namespace phantom {
@@ -75,6 +78,62 @@ void PhantomCiphertext::load(const PhantomContext& ctx, std::istream& is) {
   is_asymmetric_ = h.is_asymmetric;
 }
 
+void PhantomCiphertext::save_symmetric(std::ostream& os) const {
+  if (is_asymmetric_) throw std::runtime_error("Asymmetric ciphertext does not have seed.");
+  if (size_ != 2) throw std::runtime_error("This method is only for 2-polynomial ciphertext.");
+  if (seed_.size() != kSeedBytes) throw std::runtime_error("ciphertext was not made by encrypt_symmetric");
+  ser::CiphertextHeader h;
+  h.chain_index = chain_index_;
+  h.size = size_;
+  h.poly_modulus_degree = n_;
+  h.coeff_modulus_size = L_;
+  h.scale = scale_;
+  h.correction_factor = correction_factor_;
+  h.noise_scale_deg = noise_scale_deg_;
+  h.is_ntt_form = is_ntt_form_;
+  h.is_asymmetric = is_asymmetric_;
+  const hipStream_t s = StreamScope::current() ? StreamScope::current() : data_.stream();
+  std::vector<uint64_t> c0(L_ * n_);
+  PHX_CHECK(hipMemcpyAsync(c0.data(), data_.get(), c0.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  PHX_CHECK(hipStreamSynchronize(s));
+  ser::write_ciphertext_header(os, h);
+  os.write(reinterpret_cast<const char*>(c0.data()), static_cast<std::streamsize>(c0.size() * sizeof(uint64_t)));
+  os.write(reinterpret_cast<const char*>(seed_.data()), static_cast<std::streamsize>(seed_.size()));
+  if (!os) throw std::runtime_error("ciphertext write failed");
+}
+
+void PhantomCiphertext::load_symmetric(const PhantomContext& ctx, std::istream& is) {
+  ser::CiphertextHeader h;
+  ser::read_ciphertext_header(is, h);
+  if (h.is_asymmetric) throw std::runtime_error("Asymmetric ciphertext does not have seed.");
+  if (h.size != 2) throw std::runtime_error("This method is only for 2-polynomial ciphertext.");
+  check_ciphertext_header(ctx, h);
+  if (h.coeff_modulus_size != ctx.get_context_data(1).coeff_modulus_size())
+    throw std::runtime_error("Only support ciphertext without modulus switching.");
+  const size_t words = h.coeff_modulus_size * h.poly_modulus_degree;
+  std::vector<uint64_t> c0(words);
+  std::vector<uint8_t> seed(kSeedBytes);
+  is.read(reinterpret_cast<char*>(c0.data()), static_cast<std::streamsize>(words * sizeof(uint64_t)));
+  is.read(reinterpret_cast<char*>(seed.data()), static_cast<std::streamsize>(seed.size()));
+  if (!is) throw std::runtime_error("truncated seed-compressed ciphertext");
+  const hipStream_t s = ctx.stream();
+  resize(2, h.coeff_modulus_size, h.poly_modulus_degree, s, false);
+  PHX_CHECK(hipMemcpyAsync(data_.get(), c0.data(), words * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  sample_uniform_seeded(ctx, seed.data(), data_.get() + words, h.coeff_modulus_size);
+  if (!h.is_ntt_form)
+    hip_ok(phx::ntt_inverse(ctx.gpu_rns_tables(), data_.get() + words, data_.get() + words,
+                            phx::LimbMap::contiguous(static_cast<int>(h.coeff_modulus_size), 0), nullptr, nullptr, s),
+           "c1 INTT");
+  PHX_CHECK(hipStreamSynchronize(s));
+  chain_index_ = h.chain_index;
+  scale_ = h.scale;
+  correction_factor_ = h.correction_factor;
+  noise_scale_deg_ = h.noise_scale_deg;
+  is_ntt_form_ = h.is_ntt_form;
+  is_asymmetric_ = false;
+  seed_ = std::move(seed);
+}
+
 void PhantomPlaintext::save(std::ostream& os, hipStream_t s) const {
   ser::PlaintextHeader h;
   h.chain_index = chain_index_;
@@ -139,6 +198,7 @@ void PhantomCiphertext::copy_from(const PhantomCiphertext& o) {
   noise_scale_deg_ = o.noise_scale_deg_;
   is_ntt_form_ = o.is_ntt_form_;
   is_asymmetric_ = o.is_asymmetric_;
+  seed_ = o.seed_;
   sf_ = o.sf_;
   sf_big_ = o.sf_big_;
   const size_t count = size_ * L_ * n_;

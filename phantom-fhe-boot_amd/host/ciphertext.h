@@ -16,6 +16,7 @@ namespace phantom {
 
 class PhantomCiphertext {
  public:
+  static constexpr size_t kSeedBytes = 64;  // prng_seed_byte_count (include/host/globals.h:20-21)
   PhantomCiphertext() = default;
   PhantomCiphertext(PhantomCiphertext&& o) noexcept { *this = std::move(o); }
   // moves leave the source empty (sizes zeroed with the buffer)
@@ -30,6 +31,7 @@ class PhantomCiphertext {
       noise_scale_deg_ = o.noise_scale_deg_;
       is_ntt_form_ = o.is_ntt_form_;
       is_asymmetric_ = o.is_asymmetric_;
+      seed_ = std::move(o.seed_);
       data_ = std::move(o.data_);
       sf_ = std::move(o.sf_);
       sf_big_ = std::move(o.sf_big_);
@@ -71,6 +73,17 @@ class PhantomCiphertext {
   void save(std::ostream& os) const;
   void load(const PhantomContext& ctx, std::istream& is);
   bool is_asymmetric() const { return is_asymmetric_; }
+  // Seed-compressed symmetric ciphertexts (include/ciphertext.h:227-318): c0 and the 64-byte
+  // seed of c1 = a instead of c1 itself.  encrypt_symmetric draws `a` from a fresh public seed
+  // that the ciphertext keeps; load_symmetric regenerates c1 from it (ChaCha20 keystream, so the
+  // bytes of c1 differ from the reference's Salsa20 expansion of the same seed).  Same errors as
+  // the reference: asymmetric ciphertexts, size != 2, and (load) a chain below the first data
+  // level throw std::runtime_error.  Like the reference, save_symmetric trusts that c1 is still
+  // the seed's expansion (an in-place operation on c1 makes the saved form stale).
+  void save_symmetric(std::ostream& os) const;
+  void load_symmetric(const PhantomContext& ctx, std::istream& is);
+  const std::vector<uint8_t>& seed() const { return seed_; }
+  void set_seed(std::vector<uint8_t> s) { seed_ = std::move(s); }
   // hand the buffer to stream `s` (DeviceBuffer::set_stream): after a concurrent section, for a
   // result made on a side stream that the joining stream uses from now on
   void retag(hipStream_t s) { data_.set_stream(s); }
@@ -95,6 +108,7 @@ class PhantomCiphertext {
   size_t noise_scale_deg_ = 1;
   bool is_ntt_form_ = true;
   bool is_asymmetric_ = false;
+  std::vector<uint8_t> seed_;  // prng_seed_byte_count (64) bytes after encrypt_symmetric, else empty
   DeviceBuffer<uint64_t> data_;
   std::vector<double> sf_, sf_big_;
 };

@@ -147,6 +147,15 @@ void sample_uniform_poly(const PhantomContext& ctx, RandomStream& rng, uint64_t*
          "sample uniform");
 }
 
+void sample_uniform_seeded(const PhantomContext& ctx, const uint8_t* seed, uint64_t* dst, size_t L) {
+  phx::ChaChaKey k;
+  std::memcpy(k.k, seed, sizeof(k.k));
+  uint64_t nonce = 0;
+  for (int i = 7; i >= 0; --i) nonce = (nonce << 8) | seed[32 + i];
+  hip_ok(phx::sample_uniform(dst, ctx.mod_QP().q, ctx.mod_QP().barrett, ctx.poly_degree(), L, k, nonce, ctx.stream()),
+         "sample uniform (seeded)");
+}
+
 void sample_error_poly_ntt(const PhantomContext& ctx, RandomStream& rng, uint64_t* dst, size_t L) {
   hip_ok(phx::sample_cbd(dst, ctx.mod_QP().q, ctx.poly_degree(), L, rng.key(), rng.next_draw(), ctx.stream()),
          "sample e");
@@ -199,11 +208,14 @@ void PhantomSecretKey::init_powers(const PhantomContext& ctx) {
 }
 
 void PhantomSecretKey::encrypt_zero_raw(const PhantomContext& ctx, uint64_t* c0, uint64_t* c1, size_t L,
-                                        const uint64_t* enc_key) const {
+                                        const uint64_t* enc_key, const uint8_t* a_seed) const {
   const size_t n = ctx.poly_degree();
   hipStream_t s = ctx.stream();
   DeviceBuffer<uint64_t> e(L * n, s);
-  sample_uniform_poly(ctx, rng_, c1, L);  // uniform in NTT form is uniform
+  if (a_seed)
+    sample_uniform_seeded(ctx, a_seed, c1, L);
+  else
+    sample_uniform_poly(ctx, rng_, c1, L);  // uniform in NTT form is uniform
   sample_error_poly_ntt(ctx, rng_, e.get(), L);
   const phx::ModView m = ctx.mod_QP();
   hip_ok(phx::poly_mul_add(c1, enc_key ? enc_key : s_.get(), e.get(), c0, m, n, L, s), "a*s+e");
@@ -335,7 +347,11 @@ void PhantomSecretKey::encrypt_symmetric(const PhantomContext& ctx, const Phanto
   out.set_correction_factor(1);
   out.SetNoiseScaleDeg(1);
   out.set_asymmetric(false);
-  encrypt_zero_raw(ctx, out.data(), out.data() + L * n, L);
+  // a public seed for a (save_symmetric writes it instead of c1): one draw of this key's stream
+  std::vector<uint8_t> seed(PhantomCiphertext::kSeedBytes);
+  rng_.host_words(reinterpret_cast<uint64_t*>(seed.data()), seed.size() / sizeof(uint64_t));
+  encrypt_zero_raw(ctx, out.data(), out.data() + L * n, L, nullptr, seed.data());
+  out.set_seed(std::move(seed));
   hip_ok(phx::poly_add(out.data(), plain.data(), out.data(), ctx.mod_QP(), n, L, s), "m - (a s + e)");
   PHX_CHECK(hipStreamSynchronize(s));
 }

@@ -168,8 +168,9 @@ class PhantomSecretKey {
   void init_powers(const PhantomContext& ctx);
   // symmetric encryption of zero over the first L limbs of Q u P under enc_key (default s):
   // (-(a s + e), a), NTT form
+  // a_seed: take a from sample_uniform_seeded(a_seed) instead of this key's stream
   void encrypt_zero_raw(const PhantomContext& ctx, uint64_t* c0, uint64_t* c1, size_t L,
-                        const uint64_t* enc_key = nullptr) const;
+                        const uint64_t* enc_key = nullptr, const uint8_t* a_seed = nullptr) const;
   mutable RandomStream rng_;
   bool deterministic_ = false;
   std::vector<int8_t> coeffs_;
@@ -185,6 +186,9 @@ uint32_t galois_elt_from_step(int step, size_t n);
 // draws of a ChaCha20 stream into device polynomials over the first L limbs of Q u P
 // (the reference's sample_uniform_poly / sample_error_poly / sample_ternary_poly, src/prng.cu)
 void sample_uniform_poly(const PhantomContext& ctx, RandomStream& rng, uint64_t* dst, size_t L);
+// uniform `a` of a seed-compressed symmetric ciphertext from its public 64-byte seed: the ChaCha20
+// keystream under key = seed[0..32) and draw nonce = seed[32..40) (little endian)
+void sample_uniform_seeded(const PhantomContext& ctx, const uint8_t* seed, uint64_t* dst, size_t L);
 // centered-binomial error, returned in NTT form
 void sample_error_poly_ntt(const PhantomContext& ctx, RandomStream& rng, uint64_t* dst, size_t L);
 // ternary polynomial, returned in NTT form

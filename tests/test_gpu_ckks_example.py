@@ -3,7 +3,8 @@
 PhantomSecretKey(context) + gen_publickey, encode/decode, encrypt_symmetric / encrypt_asymmetric,
 add / sub, multiply_plain, the x*y*x HomMul with relinearize_inplace / rescale_to_next_inplace /
 mod_switch_to_next_inplace, EvalRotateKeyGen + EvalRotateFused / EvalConjFused, and the
-small-parameter apply_galois_inplace — each checked with the reference's own rule (every slot
+small-parameter apply_galois_inplace, and the seed-compressed save_symmetric /
+load_symmetric round trip — each checked with the reference's own rule (every slot
 within 1e-3, 3_ckks.cu:19,33-41).  Keys come from the OS entropy path (no test seed)."""
 import json
 import os
@@ -15,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "phantom-fhe-boot_amd", "bin", "ckks_example")
-EXAMPLES = ["ckks_enc", "ckks_add", "ckks_mul_plain", "ckks_mul", "ckks_rotation"]
+EXAMPLES = ["ckks_enc", "ckks_add", "ckks_save_symmetric", "ckks_mul_plain", "ckks_mul", "ckks_rotation"]
 
 
 @pytest.mark.parametrize("alpha", [15, 1, 3])
