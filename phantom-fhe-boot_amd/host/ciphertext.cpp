@@ -34,6 +34,7 @@ void PhantomCiphertext::resize(size_t size, size_t L, size_t n, hipStream_t s, b
   size_ = size;
   L_ = L;
   n_ = n;
+  seed_.clear();  // a reshaped ciphertext is no longer the expansion of an encryption seed
 }
 
 void PhantomCiphertext::save(std::ostream& os) const {

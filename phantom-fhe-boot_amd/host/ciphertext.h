@@ -78,8 +78,9 @@ class PhantomCiphertext {
   // that the ciphertext keeps; load_symmetric regenerates c1 from it (ChaCha20 keystream, so the
   // bytes of c1 differ from the reference's Salsa20 expansion of the same seed).  Same errors as
   // the reference: asymmetric ciphertexts, size != 2, and (load) a chain below the first data
-  // level throw std::runtime_error.  Like the reference, save_symmetric trusts that c1 is still
-  // the seed's expansion (an in-place operation on c1 makes the saved form stale).
+  // level throw std::runtime_error.  resize() drops the seed (every operation that writes a new
+  // result through it); like the reference, in-place operations that keep the shape (add,
+  // multiply_plain) leave it, so save_symmetric is meant for fresh encryptions.
   void save_symmetric(std::ostream& os) const;
   void load_symmetric(const PhantomContext& ctx, std::istream& is);
   const std::vector<uint8_t>& seed() const { return seed_; }
