@@ -118,6 +118,11 @@ size_t phantom_context_coeff_modulus_size(const phantom_context *ctx, size_t cha
  * ct1, ct2 are [2][L][n] at chain_index, out [3][L][n] (out may alias ct1's storage if sized for 3) */
 int phantom_multiply(const phantom_context *ctx, size_t chain_index, const uint64_t *ct1, const uint64_t *ct2,
                      uint64_t *out, hipStream_t stream);
+/* tensor_square_2x2_rns_poly (src/polymath.cu:538-582), the branch bgv_ckks_multiply takes when both
+ * operands are the same ciphertext (src/evaluate.cu:443-450): ct [2][L][n] -> out [3][L][n] =
+ * (c0^2, 2 c0 c1, c1^2); out may alias ct's storage if sized for 3 */
+int phantom_square(const phantom_context *ctx, size_t chain_index, const uint64_t *ct, uint64_t *out,
+                   hipStream_t stream);
 /* relinearize_inplace (src/evaluate.cu:1552-1589) -> keyswitch_inplace (src/eval_key_switch.cu:112-212):
  * ct is [3][L][n]; on return its first two polys hold the relinearized ciphertext.
  * key_digits: host array of dnum device pointers, each a [2][size_QP][n] key digit. */

@@ -367,9 +367,20 @@ void or_tensor_prod_2x2(const uint64_t *ct1, const uint64_t *ct2, uint64_t *out,
     }
 }
 
-/* tensor_square_2x2_rns_poly (src/polymath.cu:538-582) */
+/* tensor_square_2x2_rns_poly (src/polymath.cu:538-582): d0 = c0^2, d1 = (c0 c1 << 1) reduced as
+ * one 128-bit value (:559-562; 2 c0 c1 < 2^123 for q < 2^61), d2 = c1^2.  out may alias ct. */
 void or_tensor_square_2x2(const uint64_t *ct, uint64_t *out, size_t n, size_t L, const uint64_t *moduli) {
-    or_tensor_prod_2x2(ct, ct, out, n, L, moduli);
+    const size_t s = n * L;
+    for (size_t l = 0; l < L; l++) {
+        uint64_t q = moduli[l];
+        for (size_t k = 0; k < n; k++) {
+            size_t i = l * n + k;
+            uint64_t c0 = ct[i], c1 = ct[s + i];
+            out[i] = or_mulmod(c0, c0, q);
+            out[s + i] = (uint64_t)((((u128)c0 * c1) << 1) % q);
+            out[2 * s + i] = or_mulmod(c1, c1, q);
+        }
+    }
 }
 
 /* ------------------------------------------------------------------ */

@@ -104,6 +104,14 @@ int phantom_multiply(const phantom_context* ctx, size_t chain_index, const uint6
   });
 }
 
+int phantom_square(const phantom_context* ctx, size_t chain_index, const uint64_t* ct, uint64_t* out,
+                   hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& rt = tool(ctx, chain_index);
+    return from_hip(phx::tensor_square_2x2(ct, out, ctx->ctx->mod_QP(), ctx->ctx->poly_degree(), rt.size_Ql(), stream));
+  });
+}
+
 int phantom_keyswitch(const phantom_context* ctx, size_t chain_index, uint64_t* ct, const uint64_t* c2,
                       const uint64_t* const* key_digits, size_t dnum, hipStream_t stream) {
   PHX_CAPI_GUARD({

@@ -32,6 +32,16 @@ hipError_t poly_negate(const uint64_t* a, uint64_t* out, ModView m, size_t n, si
                        size_t polys = 1);
 hipError_t poly_mul(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
                     hipStream_t s, size_t polys = 1, size_t b_stride = kContiguous);
+// out = sum of the polynomials in[0 .. count) (add_many_rns_poly, src/polymath.cu): each operand
+// is read once; `polys` polynomials per operand, operand i's polynomial y at in[i] + y * stride
+constexpr int kAddManyMax = 16;
+struct AddManyArgs {
+  const uint64_t* in[kAddManyMax];
+  int count = 0;
+  bool accumulate = false;  // out += sum (chunks of more than kAddManyMax operands)
+};
+hipError_t poly_add_many(const AddManyArgs& a, uint64_t* out, ModView m, size_t n, size_t L, hipStream_t s,
+                         size_t polys, size_t stride);
 // out = a * b + c
 hipError_t poly_mul_add(const uint64_t* a, const uint64_t* b, const uint64_t* c, uint64_t* out, ModView m,
                         size_t n, size_t L, hipStream_t s);
@@ -45,6 +55,9 @@ hipError_t poly_add_scalar(const uint64_t* a, const uint64_t* scalar, uint64_t* 
 // (tensor_prod_2x2_rns_poly, src/polymath.cu:501-536).  out may alias ct1.
 hipError_t tensor_prod_2x2(const uint64_t* ct1, const uint64_t* ct2, uint64_t* out, ModView m, size_t n, size_t L,
                            hipStream_t s);
+// (c0, c1)^2 -> (c0^2, 2 c0 c1, c1^2) (tensor_square_2x2_rns_poly, src/polymath.cu:538-582); ct is
+// [2][L][n], out [3][L][n], out may alias ct
+hipError_t tensor_square_2x2(const uint64_t* ct, uint64_t* out, ModView m, size_t n, size_t L, hipStream_t s);
 
 // ---- base conversion ------------------------------------------------------------------
 // Fast base conversion (bconv_mult + bconv_matmul, src/rns_bconv.cu:40-179, 455-485):

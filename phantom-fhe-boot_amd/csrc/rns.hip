@@ -86,6 +86,23 @@ struct MulOp {
   }
 };
 
+// out (+)= sum_i in[i]; blockIdx.y: polynomial
+__global__ __launch_bounds__(kBlock) void add_many_kernel(AddManyArgs a, uint64_t* out, ModView m, uint32_t log_n,
+                                                          size_t pairs, size_t stride) {
+  const size_t poff = blockIdx.y * stride;
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint64_t q = m.q[e >> log_n];
+    u64x2 acc = a.accumulate ? ld2(out + poff + e) : ld2(a.in[0] + poff + e);
+    for (int k = a.accumulate ? 0 : 1; k < a.count; ++k) {
+      const u64x2 x = ld2(a.in[k] + poff + e);
+      acc.x = add_mod(acc.x, x.x, q);
+      acc.y = add_mod(acc.y, x.y, q);
+    }
+    st2(out + poff + e, acc.x, acc.y);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void negate_kernel(const uint64_t* __restrict__ a, uint64_t* out, ModView m,
                                                         uint32_t log_n, size_t pairs) {
   a += blockIdx.y * 2 * pairs;  // blockIdx.y: polynomial
@@ -154,6 +171,25 @@ __global__ __launch_bounds__(kBlock) void tensor_kernel(const uint64_t* ct1, con
     const uint64_t d2x = mul_mod(a1.x, b1.x, q, r0, r1), d2y = mul_mod(a1.y, b1.y, q, r0, r1);
     st2(out + e, d0x, d0y);
     st2(out + stride + e, barrett_reduce_128(c1x, q, r0, r1), barrett_reduce_128(c1y, q, r0, r1));
+    st2(out + 2 * stride + e, d2x, d2y);
+  }
+}
+
+// squaring (tensor_square_2x2_rns_poly, src/polymath.cu:538-582): d0 = a0^2, d1 = 2 a0 a1,
+// d2 = a1^2 — 2 polynomials read instead of 4.  out may alias ct (each lane reads its own
+// elements before writing them).
+__global__ __launch_bounds__(kBlock) void tensor_square_kernel(const uint64_t* ct, uint64_t* out, ModView m,
+                                                               uint32_t log_n, size_t pairs, size_t stride) {
+  for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
+    const size_t e = 2 * i;
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const uint64_t q = m.q[l], r0 = m.barrett[2 * l], r1 = m.barrett[2 * l + 1];
+    const u64x2 a0 = ld2(ct + e), a1 = ld2(ct + stride + e);
+    const uint64_t px = mul_mod(a0.x, a1.x, q, r0, r1), py = mul_mod(a0.y, a1.y, q, r0, r1);
+    const uint64_t d0x = mul_mod(a0.x, a0.x, q, r0, r1), d0y = mul_mod(a0.y, a0.y, q, r0, r1);
+    const uint64_t d2x = mul_mod(a1.x, a1.x, q, r0, r1), d2y = mul_mod(a1.y, a1.y, q, r0, r1);
+    st2(out + e, d0x, d0y);
+    st2(out + stride + e, add_mod(px, px, q), add_mod(py, py, q));
     st2(out + 2 * stride + e, d2x, d2y);
   }
 }
@@ -944,6 +980,14 @@ hipError_t poly_add(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView
   return hipGetLastError();
 }
 
+hipError_t poly_add_many(const AddManyArgs& a, uint64_t* out, ModView m, size_t n, size_t L, hipStream_t s,
+                         size_t polys, size_t stride) {
+  if (a.count < 1 || a.count > kAddManyMax) return hipErrorInvalidValue;
+  const size_t pairs = n * L / 2;
+  add_many_kernel<<<poly_grid(pairs, polys), kBlock, 0, s>>>(a, out, m, __builtin_ctzll(n), pairs, stride);
+  return hipGetLastError();
+}
+
 hipError_t poly_sub(const uint64_t* a, const uint64_t* b, uint64_t* out, ModView m, size_t n, size_t L,
                     hipStream_t s, size_t polys, size_t b_stride) {
   const size_t pairs = n * L / 2;
@@ -992,6 +1036,12 @@ hipError_t tensor_prod_2x2(const uint64_t* ct1, const uint64_t* ct2, uint64_t* o
                            hipStream_t s) {
   const size_t pairs = n * L / 2;
   tensor_kernel<<<grid_for(pairs), kBlock, 0, s>>>(ct1, ct2, out, m, __builtin_ctzll(n), pairs, n * L);
+  return hipGetLastError();
+}
+
+hipError_t tensor_square_2x2(const uint64_t* ct, uint64_t* out, ModView m, size_t n, size_t L, hipStream_t s) {
+  const size_t pairs = n * L / 2;
+  tensor_square_kernel<<<grid_for(pairs), kBlock, 0, s>>>(ct, out, m, __builtin_ctzll(n), pairs, n * L);
   return hipGetLastError();
 }
 

@@ -218,6 +218,78 @@ int main(int argc, char** argv) {
     return g_ok ? 0 : 1;
   }
 
+  if (mode == "flex") {
+    // the reference's FLEXIBLEAUTO surface (include/evaluate.cuh:270-452) with the ciphertext's
+    // PreComputeScale factors, as bootstrapping_example.cu:146-148 obtains them
+    PhantomRelinKey rlk = sk.gen_relinkey(ctx);
+    ct.PreComputeScale(ctx, scale);
+    const std::vector<double> sfR = ct.getScalingFactorsReal(), sfB = ct.getScalingFactorsRealBig();
+    auto want_of = [&](auto f) {
+      std::vector<std::complex<double>> w(slots);
+      for (size_t j = 0; j < slots; ++j) w[j] = f(x[j]);
+      return w;
+    };
+    const auto sq = want_of([](double v) { return v * v; });
+    PhantomCiphertext m = EvalMultAuto(ctx, ct, ct, rlk, sfR, sfB);
+    report("flex_mult_auto", max_abs_err(decrypt_decode(ctx, sk, enc, m), sq), 1e-5, m.chain_index());
+    PhantomCiphertext s2 = EvalSquare(ctx, ct, rlk, sfR, sfB);
+    report("flex_square", max_abs_err(decrypt_decode(ctx, sk, enc, s2), sq), 1e-5, s2.chain_index());
+    const bool degs = m.GetNoiseScaleDeg() == 2 && s2.GetNoiseScaleDeg() == 2;
+    report("flex_degrees", degs ? 0.0 : 1.0, 0.5, m.chain_index());
+    // same level, degrees 2 and 1; then across levels (rescaled product + fresh input)
+    PhantomCiphertext a1 = EvalAddAuto(ctx, m, ct, sfR, sfB);
+    const auto sq_plus = want_of([](double v) { return v * v + v; });
+    report("flex_add_auto_degree", max_abs_err(decrypt_decode(ctx, sk, enc, a1), sq_plus), 1e-5, a1.chain_index());
+    PhantomCiphertext r1 = ModReduce(ctx, m, 1);
+    PhantomCiphertext a2 = EvalAddAuto(ctx, ct, r1, sfR, sfB);
+    report("flex_add_auto_levels", max_abs_err(decrypt_decode(ctx, sk, enc, a2), sq_plus), 1e-5, a2.chain_index());
+    PhantomCiphertext d2 = EvalSubAuto(ctx, r1, ct, sfR, sfB);
+    report("flex_sub_auto_levels", max_abs_err(decrypt_decode(ctx, sk, enc, d2), want_of([](double v) { return v * v - v; })),
+           1e-5, d2.chain_index());
+    PhantomCiphertext c1 = EvalAddConst(ctx, ct, -2.5, sfR, sfB);
+    report("flex_add_const", max_abs_err(decrypt_decode(ctx, sk, enc, c1), want_of([](double v) { return v - 2.5; })), 1e-6,
+           c1.chain_index());
+    PhantomCiphertext c2 = EvalAddConst(ctx, m, 3.0, sfR, sfB);
+    report("flex_add_const_degree2", max_abs_err(decrypt_decode(ctx, sk, enc, c2), want_of([](double v) { return v * v + 3.0; })),
+           1e-5, c2.chain_index());
+    PhantomCiphertext mc = EvalMultConst(ctx, m, 0.25, sfR);  // lazily rescales m first
+    report("flex_mult_const_lazy", max_abs_err(decrypt_decode(ctx, sk, enc, mc), want_of([](double v) { return 0.25 * v * v; })),
+           1e-5, mc.chain_index());
+    {
+      PhantomPlaintext pp;
+      std::vector<double> half(slots, 0.5);
+      enc.encode(ctx, half, scale, pp, 1);
+      PhantomCiphertext mp = ct;
+      EvalMultAutoInplace(ctx, mp, pp, sfR, sfB);
+      report("flex_mult_plain_auto", max_abs_err(decrypt_decode(ctx, sk, enc, mp), want_of([](double v) { return 0.5 * v; })),
+             1e-5, mp.chain_index());
+    }
+    // Chebyshev series on [1, 5]: degree 4 (the linear method) and 30 (the fused recursion),
+    // against the host value of the same interpolant; levels consumed reported
+    for (uint32_t deg : {4u, 30u}) {
+      auto f = [](double t) { return std::sin(t) / t; };
+      const std::vector<double> co = EvalChebyshevCoefficients(f, 1.0, 5.0, deg);
+      PhantomCiphertext cs = EvalChebyshevFunction(f, ctx, rlk, ct, 1.0, 5.0, deg, sfR, sfB);
+      const auto host = want_of([&](double v) {
+        const double y = (2.0 * v - 6.0) / 4.0;
+        double t0 = 1.0, t1 = y, acc = co[0] / 2 + co[1] * y;
+        for (size_t k = 2; k < co.size(); ++k) {
+          const double t2 = 2.0 * y * t1 - t0;
+          acc += co[k] * t2;
+          t0 = t1;
+          t1 = t2;
+        }
+        return acc;
+      });
+      const size_t used = cs.chain_index() - ct.chain_index() + (cs.GetNoiseScaleDeg() > 1 ? 1 : 0);
+      std::printf("{\"chebyshev_degree\": %u, \"levels_used\": %zu}\n", deg, used);
+      report(deg == 4 ? "flex_chebyshev_linear" : "flex_chebyshev_ps", max_abs_err(decrypt_decode(ctx, sk, enc, cs), host),
+             1e-4, cs.chain_index());
+    }
+    std::printf("{\"done\": \"flex\", \"ok\": %s}\n", g_ok ? "true" : "false");
+    return g_ok ? 0 : 1;
+  }
+
   if (mode == "ops") {
     PhantomGaloisKey gk = sk.create_galois_keys_fused(
         ctx, {FindAutomorphismIndex2nComplex(1, N), FindAutomorphismIndex2nComplex(-3, N), static_cast<uint32_t>(2 * N - 1)});

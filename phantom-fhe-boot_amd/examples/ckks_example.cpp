@@ -13,6 +13,7 @@
 //   Default: 15.  Prints one JSON line per example; exit status 0 iff all pass.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <complex>
 #include <cstdio>
@@ -281,6 +282,130 @@ static void example_ckks_rotation(PhantomContext& context, double scale) {
   require(correctness, "Homomorphic conjugate error");
 }
 
+// the rest of include/evaluate.cuh's CKKS surface (round 3): add_many, add/sub_plain, the squaring
+// branch of multiply (bit-identical to the product of two copies), multiply_and_relin, plaintext
+// mod_switch_to(_next), hoisting_inplace, rotations composed from their non-adjacent form, and the
+// seed-compressed save's validity after in-place operations; each decrypted with the 1e-3 rule
+static void example_ckks_api(PhantomContext& context, double scale) {
+  PhantomSecretKey secret_key(context);
+  PhantomCKKSEncoder encoder(context);
+  const size_t slots = encoder.slot_count(), n = context.poly_degree();
+  std::vector<cplx> a = random_msg(slots), b = random_msg(slots), c = random_msg(slots), out;
+  PhantomPlaintext pa, pb, pc;
+  encoder.encode(context, a, scale, pa);
+  encoder.encode(context, b, scale, pb);
+  encoder.encode(context, c, scale, pc);
+  PhantomCiphertext ca = secret_key.encrypt_symmetric(context, pa), cb = secret_key.encrypt_symmetric(context, pb),
+                    cc = secret_key.encrypt_symmetric(context, pc);
+  auto check = [&](const PhantomCiphertext& ct, const std::vector<cplx>& want, const char* what) {
+    PhantomPlaintext p = secret_key.decrypt(context, ct);
+    encoder.decode(context, p, out);
+    for (size_t i = 0; i < want.size(); ++i)
+      if (!eq(out[i], want[i]) || std::fabs(out[i].imag() - want[i].imag()) >= EPSINON) throw std::logic_error(what);
+  };
+  // add_many
+  std::vector<PhantomCiphertext> many = {ca, cb, cc};
+  PhantomCiphertext sum;
+  add_many(context, many, sum);
+  std::vector<cplx> want(slots);
+  for (size_t i = 0; i < slots; ++i) want[i] = a[i] + b[i] + c[i];
+  check(sum, want, "add_many error");
+  // add_plain / sub_plain
+  PhantomCiphertext t = sub_plain(context, add_plain(context, ca, pb), pc);
+  for (size_t i = 0; i < slots; ++i) want[i] = a[i] + b[i] - c[i];
+  check(t, want, "add_plain / sub_plain error");
+  // squaring kernel == product of two copies, bit for bit; then relinearize + rescale
+  PhantomCiphertext sq = ca;
+  multiply_inplace(context, sq, sq);
+  PhantomCiphertext copy = ca;
+  PhantomCiphertext prod = multiply(context, ca, copy);
+  require(sq.to_host(context.stream()) == prod.to_host(context.stream()), "square differs from the product");
+  PhantomRelinKey relin_key = secret_key.gen_relinkey(context);
+  PhantomCiphertext ab = multiply_and_relin(context, ca, cb, relin_key);
+  rescale_to_next_inplace(context, ab);
+  for (size_t i = 0; i < slots; ++i) want[i] = a[i] * b[i];
+  check(ab, want, "multiply_and_relin error");
+  PhantomCiphertext a2 = multiply_and_relin(context, ca, ca, relin_key);
+  rescale_to_next_inplace(context, a2);
+  for (size_t i = 0; i < slots; ++i) want[i] = a[i] * a[i];
+  check(a2, want, "multiply_and_relin (square) error");
+  // plaintext modulus switching: c at the product's level times the product
+  PhantomPlaintext pc1 = mod_switch_to_next(context, pc);
+  require(pc1.chain_index() == ab.chain_index() && pc1.coeff_modulus_size() == ab.coeff_modulus_size(),
+          "plaintext mod_switch_to_next level");
+  PhantomPlaintext pc3 = mod_switch_to(context, pc, pc.chain_index() + 3);
+  require(pc3.chain_index() == pc.chain_index() + 3, "plaintext mod_switch_to level");
+  PhantomCiphertext abc = ab;
+  pc1.set_scale(ab.scale());
+  add_plain_inplace(context, abc, pc1);
+  for (size_t i = 0; i < slots; ++i) want[i] = a[i] * b[i] + c[i] * (scale / ab.scale());
+  check(abc, want, "plaintext mod_switch add error");
+  bool threw = false;
+  try {
+    PhantomPlaintext top = pc;
+    mod_switch_to_inplace(context, top, 0);
+  } catch (const std::invalid_argument&) {
+    threw = true;
+  }
+  require(threw, "plaintext mod_switch_to a higher level must throw");
+  // rotations: hoisting over {1, 2}, and a rotation by 3 composed from its NAF {-1, 4}
+  std::vector<uint32_t> elts;
+  for (int st : {1, 2, 4, -1}) elts.push_back(galois_elt_from_step(st, n));
+  PhantomGaloisKey galois_keys = secret_key.create_galois_keys(context, elts);
+  PhantomCiphertext h = hoisting(context, ca, galois_keys, {1, 2});
+  for (size_t i = 0; i < slots; ++i) want[i] = a[(i + 1) % slots] + a[(i + 2) % slots];
+  check(h, want, "hoisting error");
+  PhantomCiphertext r3 = rotate(context, ca, 3, galois_keys);
+  for (size_t i = 0; i < slots; ++i) want[i] = a[(i + 3) % slots];
+  check(r3, want, "rotation by 3 (NAF) error");
+  threw = false;
+  try {
+    PhantomCiphertext r8 = rotate(context, ca, 8, galois_keys);
+  } catch (const std::invalid_argument&) {
+    threw = true;
+  }
+  require(threw, "a missing power-of-two key must throw");
+  // seed-compressed save after in-place operations: add_plain keeps c1 (the seed stays valid),
+  // a rotation or multiply_plain rewrites it (save_symmetric must refuse)
+  {
+    PhantomCiphertext s1 = ca;
+    add_plain_inplace(context, s1, pb);
+    std::stringstream ss;
+    s1.save_symmetric(ss);
+    PhantomCiphertext l1;
+    l1.load_symmetric(context, ss);
+    for (size_t i = 0; i < slots; ++i) want[i] = a[i] + b[i];
+    check(l1, want, "seed-compressed save after add_plain");
+    for (int op = 0; op < 2; ++op) {
+      PhantomCiphertext s2 = ca;
+      if (op == 0) rotate_inplace(context, s2, 1, galois_keys);
+      else multiply_plain_inplace(context, s2, pb);
+      threw = false;
+      try {
+        std::stringstream s3;
+        s2.save_symmetric(s3);
+      } catch (const std::runtime_error&) {
+        threw = true;
+      }
+      require(threw, op == 0 ? "save_symmetric after a rotation must throw" : "save_symmetric after multiply_plain must throw");
+    }
+  }
+  // keys regenerated from one seed: same secret, independent encryption randomness
+  {
+    uint8_t seed[32];
+    for (int i = 0; i < 32; ++i) seed[i] = static_cast<uint8_t>(7 * i + 1);
+    PhantomSecretKey k1 = PhantomSecretKey::from_seed(context, seed), k2 = PhantomSecretKey::from_seed(context, seed);
+    require(k1.coefficients() == k2.coefficients(), "from_seed keys differ");
+    PhantomCiphertext e1 = k1.encrypt_symmetric(context, pa), e2 = k2.encrypt_symmetric(context, pa);
+    const std::vector<uint64_t> h1 = e1.to_host(context.stream()), h2 = e2.to_host(context.stream());
+    const size_t half = h1.size() / 2;
+    require(!std::equal(h1.begin() + half, h1.end(), h2.begin() + half), "from_seed replicas share encryption randomness");
+    PhantomPlaintext d = k2.decrypt(context, e1);
+    encoder.decode(context, d, out);
+    for (size_t i = 0; i < slots; ++i) require(eq(out[i], a[i]), "from_seed replica cannot decrypt");
+  }
+}
+
 static void example_ckks_small_param() {
   EncryptionParameters parms(scheme_type::ckks);
   const size_t N = 1 << 13;
@@ -366,6 +491,7 @@ int main(int argc, char** argv) {
     run("ckks_mul_plain", alpha, [&] { example_ckks_mul_plain(context, scale); });
     run("ckks_mul", alpha, [&] { example_ckks_mul(context, scale); });
     run("ckks_rotation", alpha, [&] { example_ckks_rotation(context, scale); });
+    run("ckks_api", alpha, [&] { example_ckks_api(context, scale); });
   }
   run("ckks_small_param", 1, [&] { example_ckks_small_param(); });
   std::printf("{\"done\": \"ckks_example\", \"ok\": %s}\n", all ? "true" : "false");

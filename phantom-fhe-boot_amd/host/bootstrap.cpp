@@ -145,11 +145,18 @@ int ceil_log2(int x) {
   return r;
 }
 
+// the split p = q T_m + r of a degree-d series (d > kLeafDegree): the largest power of two m
+// with 2m <= d, halved when d is itself a power of two so that q is never a constant
+int cheb_split(int d) {
+  int m = 1;
+  while (2 * m <= d) m *= 2;
+  return m == d ? m / 2 : m;
+}
+
 // depth (levels consumed) of evaluating a degree-d series with the recursion below
 int cheb_depth(int d) {
   if (d <= kLeafDegree) return (d <= 1 ? 0 : ceil_log2(d)) + 1;
-  int m = 1;
-  while (2 * m <= d) m *= 2;
+  const int m = cheb_split(d);
   return std::max(std::max(cheb_depth(d - m), ceil_log2(m)) + 1, cheb_depth(m - 1));
 }
 
@@ -238,9 +245,8 @@ struct ChebEvaluator {
       node->c.resize(d + 1);
       return node;
     }
-    int m = 1;
-    while (2 * m <= d) m *= 2;
-    // c_i T_i = c_i (2 T_m T_(i-m) - T_(2m-i)) for m < i <= d; i = m gives T_m T_0
+    const int m = cheb_split(d);
+    // c_i T_i = c_i (2 T_m T_(i-m) - T_(2m-i)) for m < i <= d (<= 2m); i = m gives T_m T_0
     std::vector<double> q(d - m + 1, 0.0), r(c.begin(), c.begin() + m);
     q[0] = c[m];
     for (int i = m + 1; i <= d; ++i) {
@@ -269,7 +275,7 @@ struct ChebEvaluator {
     std::map<size_t, std::vector<Node*>> by_level;
     for (Node* lf : leaves) {
       const int d = static_cast<int>(lf->c.size()) - 1;
-      if (d < 1) throw std::invalid_argument("constant Chebyshev leaf");
+      if (d < 1) continue;  // a constant remainder: combine() folds it into its parent's product
       size_t lvl = 0;
       for (int i = 1; i <= d; ++i) lvl = std::max(lvl, level_of(get(i)));
       by_level[lvl].push_back(lf);
@@ -324,12 +330,14 @@ struct ChebEvaluator {
   PhantomCiphertext combine(Node* node) {
     if (!node->m) return std::move(node->v);
     PhantomCiphertext qv = combine(node->q.get());
-    PhantomCiphertext rv = combine(node->r.get());
+    PhantomCiphertext rv = (node->r->m || node->r->c.size() > 1) ? combine(node->r.get()) : PhantomCiphertext();
     // q T_m + r: r joins the product before its rescale when it is not deeper than it
     const size_t lvl = std::max(level_of(qv), level_of(get(node->m)));
     PhantomCiphertext tmp;
     const PhantomCiphertext& x = AtLevel(cc, qv, lvl, sf, tmp);
     const PhantomCiphertext& y = aligned(node->m, lvl);
+    if (!node->r->m && node->r->c.size() <= 1)  // constant remainder
+      return MulAddRescale(cc, x, y, rlk, 1, {}, node->r->c.empty() ? 0.0 : node->r->c[0]);
     if (level_of(rv) <= lvl) return MulAddRescale(cc, x, y, rlk, 1, {{&rv, 1.0}}, 0.0);
     PhantomCiphertext res = MulAddRescale(cc, x, y, rlk, 1, {}, 0.0);
     EvalAddAutoInplace(cc, res, rv, sf);
@@ -346,6 +354,31 @@ struct ChebEvaluator {
 };
 
 }  // namespace
+
+PhantomCiphertext EvalChebyshevSeriesPS(const PhantomContext& ctx, const PhantomRelinKey& rlk, const PhantomCiphertext& x,
+                                        const std::vector<double>& coeffs, double a, double b,
+                                        const std::vector<double>& sf, const std::vector<double>& sfBig) {
+  size_t d = coeffs.size() ? coeffs.size() - 1 : 0;
+  while (d > 0 && coeffs[d] == 0.0) --d;
+  if (d < 2) return EvalChebyshevSeriesLinear(ctx, rlk, x, {coeffs.at(0), d ? coeffs[1] : 0.0}, a, b, sf, sfBig);
+  // y = (2 x - a - b) / (b - a) at degree 1 (as EvalChebyshevSeriesLinear's T_1, src/evaluate.cu:3195-3207)
+  PhantomCiphertext y = x;
+  const bool unit = std::fabs(a + 1.0) < 1e-10 && std::fabs(b - 1.0) < 1e-10;
+  if (!unit) {
+    EvalMultConstInplace(ctx, y, 2.0 / (b - a), sf);
+    EvalAddConstInPlaceWrap(ctx, y, -1.0 - 2.0 * a / (b - a), sf, sfBig);
+  }
+  if (y.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(ctx, y, 1);
+  // the reference's series adds c_0 / 2; the evaluator's p = sum c_k T_k takes c_0 as is
+  std::vector<double> c(coeffs.begin(), coeffs.begin() + static_cast<long>(d) + 1);
+  c[0] *= 0.5;
+  LeafTableCache tables;
+  ChebEvaluator ev{ctx, rlk, sf, tables, {}, {}, {}};
+  ev.T.emplace(1, std::move(y));
+  PhantomCiphertext r = ev.eval(c);
+  PHX_CHECK(hipStreamSynchronize(ctx.stream()));  // the leaf tables die with this frame
+  return r;
+}
 
 // ======================================================================================
 // concurrent chains: task(0) on this thread's stream, task(i) from worker thread i on stream i
@@ -453,7 +486,22 @@ FHECKKSRNS::FHECKKSRNS(PhantomCKKSEncoder& encoder) : encoder_(encoder) {
   if (const char* e = std::getenv("PHX_BOOT_GIANT_STREAMS")) giant_streams_ = std::max(1, std::atoi(e));
 }
 
+// GetDepthByDegree (src/util.cu:44-71): the reference's Paterson-Stockmeyer depth of a degree-d
+// Chebyshev series, its affine map included
+static uint32_t reference_series_depth(int d) {
+  static const int bounds[] = {5, 6, 14, 28, 60, 120, 248, 496, 1008, 2032};
+  if (d < 5 || d > 2031) throw std::invalid_argument("Polynomial degree is supported from 5 to 2031 inclusive");
+  uint32_t depth = 3;
+  for (int b : bounds)
+    if (d >= b) ++depth;
+  return depth;
+}
+
 uint32_t FHECKKSRNS::GetBootstrapDepth(const std::vector<uint32_t>& levelBudget) {
+  return levelBudget.at(0) + levelBudget.at(1) + reference_series_depth(kChebDegree) + R_UNIFORM;
+}
+
+uint32_t FHECKKSRNS::GetBootstrapDepthTight(const std::vector<uint32_t>& levelBudget) {
   return levelBudget.at(0) + levelBudget.at(1) + static_cast<uint32_t>(cheb_depth(kChebDegree)) + R_UNIFORM;
 }
 
@@ -610,18 +658,24 @@ void FHECKKSRNS::EvalBootstrapSetup(const PhantomContext& cc, const std::vector<
   std::reverse(dec_sizes.begin(), dec_sizes.end());
   const size_t depth_enc = enc_sizes.size(), depth_dec = dec_sizes.size();
   const size_t depth_mod = static_cast<size_t>(cheb_depth(kChebDegree)) + R_UNIFORM;
-  if (1 + depth_enc + depth_mod + depth_dec > cc.size_Q())
+  // reference layout: the raise lands on the level the reference's extra Chebyshev level would
+  // have consumed, so the output chain index is the reference's
+  const size_t own = depth_enc + depth_mod + depth_dec;
+  const size_t ref = depth_enc + depth_dec + reference_series_depth(kChebDegree) + R_UNIFORM;
+  raise_level_ = tight_levels_ || ref < own ? 0 : ref - own;
+  if (1 + raise_level_ + own > cc.size_Q())
     throw std::invalid_argument("not enough levels in the modulus chain for bootstrapping");
   // the sparse partial sum multiplies the coefficients it keeps by N / (2 slots)
   const double gap = static_cast<double>(N / 2) / slots;
   Precom pc;
   pc.slots = slots;
   // CoeffToSlot: slots become (t_lo + i t_hi) / (2 q0 K) (the conjugate split doubles them)
-  build_levels(cc, true, enc_sizes, sf_.at(0) / (2.0 * gap * q0 * K_UNIFORM), 1, slots, dim1.size() > 0 ? dim1[0] : 0,
-               pc.enc);
-  // SlotToCoeff: from (t0_lo + i t0_hi) / q0 back to the message at the raise scale sf[0]
-  build_levels(cc, false, dec_sizes, q0 / sf_.at(0), 1 + depth_enc + depth_mod, slots, dim1.size() > 1 ? dim1[1] : 0,
-               pc.dec);
+  const double s_raise = sf_.at(raise_level_);
+  build_levels(cc, true, enc_sizes, s_raise / (2.0 * gap * q0 * K_UNIFORM), 1 + raise_level_, slots,
+               dim1.size() > 0 ? dim1[0] : 0, pc.enc);
+  // SlotToCoeff: from (t0_lo + i t0_hi) / q0 back to the message at the raise scale
+  build_levels(cc, false, dec_sizes, q0 / s_raise, 1 + raise_level_ + depth_enc + depth_mod, slots,
+               dim1.size() > 1 ? dim1[1] : 0, pc.dec);
   precom_[slots] = std::move(pc);
   const double args[2] = {static_cast<double>(K_UNIFORM), static_cast<double>(R_UNIFORM)};
   cheb_ = boot::chebyshev_coefficients(boot::scaled_cosine, args, kChebDegree);
@@ -860,13 +914,14 @@ PhantomCiphertext FHECKKSRNS::RaiseWithCorrection(const PhantomCiphertext& in, c
   if (ct.coeff_modulus_size() < 2) throw std::invalid_argument("bootstrapping needs an input with at least two limbs");
   // scale the message down by 2^-correction and land on scale sf[0] (AdjustCiphertext)
   const double qdrop = static_cast<double>(cc.get_context_data(ct.chain_index()).moduli().back());
-  const double k = std::ldexp(1.0, -static_cast<int>(correction_)) * qdrop * sf_.at(0) / ct.scale();
+  const double s_raise = sf_.at(raise_level_);
+  const double k = std::ldexp(1.0, -static_cast<int>(correction_)) * qdrop * s_raise / ct.scale();
   mult_by_real_integer_inplace(cc, ct, k);
   ct.SetNoiseScaleDeg(2);
   EvalModReduceInPlace(cc, ct, 1);
-  ct.set_scale(sf_.at(0));
+  ct.set_scale(s_raise);
   mod_switch_to_inplace(cc, ct, cc.size_Q());  // limb q0 only
-  return RaiseMod(cc, ct);
+  return RaiseMod(cc, ct, 1 + raise_level_);
 }
 
 // PHX_BOOT_TRACE=1: synchronise and report after every bootstrap stage (debugging aid)

@@ -73,13 +73,14 @@ class FHECKKSRNS {
                           const std::vector<double>& sf, uint32_t correctionFactor = 0, uint32_t slots = 0,
                           const std::vector<uint32_t>& dim1 = {0, 0});
   // the reference's argument list (scalingFactorsRealBig is accepted for drop-in calls; this engine
-  // derives everything it needs from scalingFactorsReal)
+  // derives everything it needs from scalingFactorsReal; `precompute` = false is not supported:
+  // the linear-transform plaintexts are always precomputed)
   void EvalBootstrapSetup(const PhantomContext& cc, const std::vector<uint32_t>& levelBudget, double scale,
                           const std::vector<double>& sf, const std::vector<double>& sf_big,
                           const std::vector<uint32_t>& dim1 = {0, 0}, uint32_t slots = 0,
                           uint32_t correctionFactor = 0, bool precompute = true) {
     (void)sf_big;
-    (void)precompute;
+    if (!precompute) throw std::invalid_argument("EvalBootstrapSetup: precompute = false is not supported");
     EvalBootstrapSetup(cc, levelBudget, scale, sf, correctionFactor, slots, dim1);
   }
   // EvalBootstrapKeyGen / EvalMultKeyGen (bootstrap.cu:566-841): fused rotation keys for the
@@ -107,7 +108,16 @@ class FHECKKSRNS {
   // ModRaise input preparation (AdjustCiphertext, bootstrap.cu:1131-1155) + RaiseMod
   PhantomCiphertext RaiseWithCorrection(const PhantomCiphertext& ct, const PhantomContext& cc) const;
 
+  // GetBootstrapDepth (bootstrap.cu:595-604): the reference's level budget, levelBudget[0] +
+  // levelBudget[1] + GetMultiplicativeDepthByCoeffVector(88) (8, util.cu:44-58) + R (6) = 18 for
+  // {2, 2}.  This engine's own evaluation needs one level less (the Chebyshev recursion folds the
+  // affine map, GetBootstrapDepthTight = 17); by default a bootstrap still lands on the
+  // reference's output level (the raise starts one level down), so a caller's level bookkeeping
+  // after EvalBootstrap is the reference's.  UseTightLevels(true) before EvalBootstrapSetup keeps
+  // the extra level instead.
   static uint32_t GetBootstrapDepth(const std::vector<uint32_t>& levelBudget);
+  static uint32_t GetBootstrapDepthTight(const std::vector<uint32_t>& levelBudget);
+  void UseTightLevels(bool tight) { tight_levels_ = tight; }
   // rotations (slot offsets) whose keys a bootstrap with `numSlots` slots needs
   std::vector<int> rotation_indices(uint32_t numSlots = 0) const;
   // chain index of a bootstrap's output
@@ -146,6 +156,8 @@ class FHECKKSRNS {
   std::vector<double> sf_;
   std::vector<uint32_t> budget_;
   uint32_t correction_ = 0;
+  bool tight_levels_ = false;
+  size_t raise_level_ = 0;  // the level ModRaise lands on (reference layout: the spare level)
   std::map<uint32_t, Precom> precom_;
   std::vector<double> cheb_;
   int giant_streams_ = 3;  // PHX_BOOT_GIANT_STREAMS: concurrent giant-step chains per level (profiles/r01/giant_streams_sweep.txt)

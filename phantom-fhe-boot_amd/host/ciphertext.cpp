@@ -35,6 +35,24 @@ void PhantomCiphertext::resize(size_t size, size_t L, size_t n, hipStream_t s, b
   L_ = L;
   n_ = n;
   seed_.clear();  // a reshaped ciphertext is no longer the expansion of an encryption seed
+  seed_fp_.clear();
+}
+
+// 8 words of every limb of c1, at coefficient positions k * n / 8
+std::vector<uint64_t> PhantomCiphertext::c1_fingerprint(hipStream_t s) const {
+  constexpr size_t kPerLimb = 8;
+  std::vector<uint64_t> fp(kPerLimb * L_);
+  if (size_ < 2 || !data_ || n_ < kPerLimb) return fp;
+  const size_t stride = n_ / kPerLimb;
+  PHX_CHECK(hipMemcpy2DAsync(fp.data(), sizeof(uint64_t), data_.get() + L_ * n_, stride * sizeof(uint64_t),
+                             sizeof(uint64_t), fp.size(), hipMemcpyDeviceToHost, s));
+  PHX_CHECK(hipStreamSynchronize(s));
+  return fp;
+}
+
+void PhantomCiphertext::set_seed(std::vector<uint8_t> seed, hipStream_t s) {
+  seed_ = std::move(seed);
+  seed_fp_ = c1_fingerprint(s);
 }
 
 void PhantomCiphertext::save(std::ostream& os) const {
@@ -83,6 +101,9 @@ void PhantomCiphertext::save_symmetric(std::ostream& os) const {
   if (is_asymmetric_) throw std::runtime_error("Asymmetric ciphertext does not have seed.");
   if (size_ != 2) throw std::runtime_error("This method is only for 2-polynomial ciphertext.");
   if (seed_.size() != kSeedBytes) throw std::runtime_error("ciphertext was not made by encrypt_symmetric");
+  const hipStream_t s = StreamScope::current() ? StreamScope::current() : data_.stream();
+  if (c1_fingerprint(s) != seed_fp_)
+    throw std::runtime_error("ciphertext c1 was modified after encrypt_symmetric; its seed no longer describes it");
   ser::CiphertextHeader h;
   h.chain_index = chain_index_;
   h.size = size_;
@@ -93,7 +114,6 @@ void PhantomCiphertext::save_symmetric(std::ostream& os) const {
   h.noise_scale_deg = noise_scale_deg_;
   h.is_ntt_form = is_ntt_form_;
   h.is_asymmetric = is_asymmetric_;
-  const hipStream_t s = StreamScope::current() ? StreamScope::current() : data_.stream();
   std::vector<uint64_t> c0(L_ * n_);
   PHX_CHECK(hipMemcpyAsync(c0.data(), data_.get(), c0.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   PHX_CHECK(hipStreamSynchronize(s));
@@ -132,7 +152,7 @@ void PhantomCiphertext::load_symmetric(const PhantomContext& ctx, std::istream& 
   noise_scale_deg_ = h.noise_scale_deg;
   is_ntt_form_ = h.is_ntt_form;
   is_asymmetric_ = false;
-  seed_ = std::move(seed);
+  set_seed(std::move(seed), s);
 }
 
 void PhantomPlaintext::save(std::ostream& os, hipStream_t s) const {
@@ -200,6 +220,7 @@ void PhantomCiphertext::copy_from(const PhantomCiphertext& o) {
   is_ntt_form_ = o.is_ntt_form_;
   is_asymmetric_ = o.is_asymmetric_;
   seed_ = o.seed_;
+  seed_fp_ = o.seed_fp_;
   sf_ = o.sf_;
   sf_big_ = o.sf_big_;
   const size_t count = size_ * L_ * n_;
@@ -224,6 +245,18 @@ void PhantomCiphertext::from_host(const PhantomContext& ctx, size_t chain_index,
   if (v.size() != size_ * L_ * n_) throw std::invalid_argument("ciphertext data size mismatch");
   PHX_CHECK(hipMemcpyAsync(data_.get(), v.data(), v.size() * sizeof(uint64_t), hipMemcpyHostToDevice, s));
   PHX_CHECK(hipStreamSynchronize(s));
+}
+
+void PhantomPlaintext::copy_from(const PhantomPlaintext& o) {
+  chain_index_ = o.chain_index_;
+  n_ = o.n_;
+  L_ = o.L_;
+  noise_scale_deg_ = o.noise_scale_deg_;
+  scale_ = o.scale_;
+  const size_t count = L_ * n_;
+  hipStream_t s = StreamScope::current() ? StreamScope::current() : o.data_.stream();
+  data_.allocate(count, s);
+  if (count) PHX_CHECK(hipMemcpyAsync(data_.get(), o.data_.get(), count * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
 }
 
 void PhantomPlaintext::resize(const PhantomContext& ctx, size_t chain_index, hipStream_t s) {

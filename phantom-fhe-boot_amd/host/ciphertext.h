@@ -32,6 +32,7 @@ class PhantomCiphertext {
       is_ntt_form_ = o.is_ntt_form_;
       is_asymmetric_ = o.is_asymmetric_;
       seed_ = std::move(o.seed_);
+      seed_fp_ = std::move(o.seed_fp_);
       data_ = std::move(o.data_);
       sf_ = std::move(o.sf_);
       sf_big_ = std::move(o.sf_big_);
@@ -78,13 +79,16 @@ class PhantomCiphertext {
   // that the ciphertext keeps; load_symmetric regenerates c1 from it (ChaCha20 keystream, so the
   // bytes of c1 differ from the reference's Salsa20 expansion of the same seed).  Same errors as
   // the reference: asymmetric ciphertexts, size != 2, and (load) a chain below the first data
-  // level throw std::runtime_error.  resize() drops the seed (every operation that writes a new
-  // result through it); like the reference, in-place operations that keep the shape (add,
-  // multiply_plain) leave it, so save_symmetric is meant for fresh encryptions.
+  // level throw std::runtime_error.  The seed describes c1 only while c1 is its expansion:
+  // resize() drops it, and set_seed records a fingerprint of c1 (words sampled from every limb)
+  // that save_symmetric re-reads, so a ciphertext whose c1 an in-place operation rewrote (rotate,
+  // relinearize, add of a ciphertext, multiply_plain) throws instead of writing a stale seed;
+  // operations that leave c1 alone (add_plain, sub_plain) keep the seed valid.
   void save_symmetric(std::ostream& os) const;
   void load_symmetric(const PhantomContext& ctx, std::istream& is);
   const std::vector<uint8_t>& seed() const { return seed_; }
-  void set_seed(std::vector<uint8_t> s) { seed_ = std::move(s); }
+  // c1 must already hold the seed's expansion (synchronises stream `s`)
+  void set_seed(std::vector<uint8_t> seed, hipStream_t s);
   // hand the buffer to stream `s` (DeviceBuffer::set_stream): after a concurrent section, for a
   // result made on a side stream that the joining stream uses from now on
   void retag(hipStream_t s) { data_.set_stream(s); }
@@ -103,6 +107,7 @@ class PhantomCiphertext {
 
  private:
   void copy_from(const PhantomCiphertext& o);
+  std::vector<uint64_t> c1_fingerprint(hipStream_t s) const;
   size_t chain_index_ = 0, size_ = 0, n_ = 0, L_ = 0;
   double scale_ = 1.0;
   uint64_t correction_factor_ = 1;
@@ -110,6 +115,7 @@ class PhantomCiphertext {
   bool is_ntt_form_ = true;
   bool is_asymmetric_ = false;
   std::vector<uint8_t> seed_;  // prng_seed_byte_count (64) bytes after encrypt_symmetric, else empty
+  std::vector<uint64_t> seed_fp_;  // c1_fingerprint() when seed_ was set
   DeviceBuffer<uint64_t> data_;
   std::vector<double> sf_, sf_big_;
 };
@@ -123,6 +129,15 @@ void check_ciphertext_header(const PhantomContext& ctx, const ser::CiphertextHea
 
 class PhantomPlaintext {
  public:
+  PhantomPlaintext() = default;
+  PhantomPlaintext(PhantomPlaintext&&) noexcept = default;
+  PhantomPlaintext& operator=(PhantomPlaintext&&) noexcept = default;
+  // deep device copy (on this thread's stream, else the source's)
+  PhantomPlaintext(const PhantomPlaintext& o) { copy_from(o); }
+  PhantomPlaintext& operator=(const PhantomPlaintext& o) {
+    if (this != &o) copy_from(o);
+    return *this;
+  }
   uint64_t* data() const { return data_.get(); }
   size_t chain_index() const { return chain_index_; }
   size_t coeff_modulus_size() const { return L_; }
@@ -130,6 +145,7 @@ class PhantomPlaintext {
   double scale() const { return scale_; }
   bool is_ntt_form() const { return true; }
   void set_scale(double s) { scale_ = s; }
+  void set_chain_index(size_t c) { chain_index_ = c; }
   size_t GetNoiseScaleDeg() const { return noise_scale_deg_; }
   void SetNoiseScaleDeg(size_t d) { noise_scale_deg_ = d; }
   void resize(const PhantomContext& ctx, size_t chain_index, hipStream_t s);
@@ -141,6 +157,7 @@ class PhantomPlaintext {
   void load(const PhantomContext& ctx, std::istream& is);
 
  private:
+  void copy_from(const PhantomPlaintext& o);
   size_t chain_index_ = 0, n_ = 0, L_ = 0;
   size_t noise_scale_deg_ = 1;
   double scale_ = 1.0;

@@ -91,11 +91,63 @@ void MultByIntegerInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, uint
   if (static_cast<uint64_t>(static_cast<double>(k)) != k) throw std::invalid_argument("integer not exact in double");
 }
 
-void EvalMultConstInplace(const PhantomContext& ctx, PhantomCiphertext& ct, double c, const std::vector<double>& sf) {
-  const double f = sf.at(level_of(ct));
-  mult_by_real_integer_inplace(ctx, ct, c * f);
+// GetElementForEvalMult (src/evaluate.cu:2332-2412): round(operand * sf[level]) as residues, the
+// reference's exact integer path (a 125-bit window rounded half up, then scaled back by powers of 2)
+std::vector<uint64_t> GetElementForEvalMult(const PhantomContext& ctx, const PhantomCiphertext& ct, double operand,
+                                            const std::vector<double>& sf) {
+  const auto& mods = ctx.get_context_data(ct.chain_index()).moduli();
+  const double scFactor = sf.at(ct.chain_index() - 1);
+  int32_t logApprox = 0;
+  const double res = std::fabs(operand * scFactor);
+  if (res > 0) {
+    const int32_t logSF = static_cast<int32_t>(std::ceil(std::log2(res)));
+    logApprox = logSF - std::min<int32_t>(logSF, 125);
+  }
+  const double approxFactor = std::pow(2.0, logApprox);
+  using i128 = __int128;
+  const i128 large = static_cast<i128>(operand / approxFactor * scFactor + 0.5);
+  std::vector<uint64_t> f(mods.size());
+  for (size_t i = 0; i < mods.size(); ++i) {
+    const i128 r = large % static_cast<i128>(mods[i]);
+    f[i] = static_cast<uint64_t>(r < 0 ? r + static_cast<i128>(mods[i]) : r);
+  }
+  while (logApprox > 0) {  // times 2^logApprox, 60 bits at a time
+    const int32_t step = std::min<int32_t>(logApprox, 60);
+    for (size_t i = 0; i < mods.size(); ++i) f[i] = mul_mod(f[i], (uint64_t(1) << step) % mods[i], mods[i]);
+    logApprox -= step;
+  }
+  return f;
+}
+
+// ct *= per-limb residues `r` (Shoup constants in the kernel arguments when they fit)
+static void mult_by_residues(const PhantomContext& ctx, PhantomCiphertext& ct, const std::vector<uint64_t>& r) {
+  const auto& mods = ctx.get_context_data(ct.chain_index()).moduli();
+  const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size();
+  traffic::ciphertexts(traffic::limb_bytes(2 * ct.size() * L, n));
+  if (L <= static_cast<size_t>(phx::kMaxScalarLimbs)) {
+    phx::LimbScalars c;
+    for (size_t l = 0; l < L; ++l) {
+      c.v[l] = r[l];
+      c.vs[l] = shoup(r[l], mods[l]);
+    }
+    hip_ok(phx::mul_scalar_v(ct.data(), c, ct.data(), ctx.mod_QP().q, n, L, ctx.stream(), ct.size()), "mult const");
+    return;
+  }
+  Scalars sc = upload_scalars(r, mods, ctx.stream());
+  hip_ok(phx::poly_mul_scalar(ct.data(), sc.v.get(), sc.vs.get(), ct.data(), ctx.mod_QP(), n, L, ctx.stream(),
+                              ct.size()),
+         "mult const");
+}
+
+void EvalMultConstInplaceCore(const PhantomContext& ctx, PhantomCiphertext& ct, double c, const std::vector<double>& sf) {
+  mult_by_residues(ctx, ct, GetElementForEvalMult(ctx, ct, c, sf));
   ct.SetNoiseScaleDeg(ct.GetNoiseScaleDeg() + 1);
-  ct.set_scale(ct.scale() * f);
+  ct.set_scale(ct.scale() * sf.at(level_of(ct)));
+}
+
+void EvalMultConstInplace(const PhantomContext& ctx, PhantomCiphertext& ct, double c, const std::vector<double>& sf) {
+  if (ct.GetNoiseScaleDeg() == 2) EvalModReduceInPlace(ctx, ct, 1);  // include/evaluate.cuh:317-326
+  EvalMultConstInplaceCore(ctx, ct, c, sf);
 }
 
 void EvalAddConstInplace(const PhantomContext& ctx, PhantomCiphertext& ct, double c) {
@@ -346,12 +398,14 @@ PhantomCiphertext EvalMultRescale(const PhantomContext& ctx, const PhantomCipher
   return RelinearizeRescale(ctx, d, rlk);
 }
 
-PhantomCiphertext RaiseMod(const PhantomContext& ctx, const PhantomCiphertext& ct) {
-  const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size(), Q = ctx.size_Q();
+PhantomCiphertext RaiseMod(const PhantomContext& ctx, const PhantomCiphertext& ct, size_t chain_index) {
+  if (chain_index < 1 || chain_index >= ctx.total_parm_size()) throw std::invalid_argument("invalid chain index");
+  const size_t n = ctx.poly_degree(), L = ct.coeff_modulus_size();
+  const size_t Q = ctx.get_context_data(chain_index).coeff_modulus_size();
   hipStream_t s = ctx.stream();
   DeviceBuffer<uint64_t> c(n, s);
   PhantomCiphertext out;
-  out.resize(ctx, 1, 2, s, false);
+  out.resize(ctx, chain_index, 2, s, false);
   for (size_t i = 0; i < 2; ++i) {
     // limb q0 to coefficient form
     hip_ok(phx::ntt_inverse(ctx.gpu_rns_tables(), ct.data() + i * L * n, c.get(), phx::LimbMap::contiguous(1, 0),

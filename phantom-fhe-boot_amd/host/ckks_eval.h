@@ -12,6 +12,7 @@
 
 #include <complex>
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "ciphertext.h"
@@ -31,8 +32,26 @@ void ScalarResidues(const PhantomContext& ctx, size_t chain, double k, uint64_t*
 void mult_by_real_integer_inplace(const PhantomContext& ctx, PhantomCiphertext& ct, double k);
 // MultByIntegerInPlace (src/evaluate.cu:3942-3970)
 void MultByIntegerInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, uint64_t k);
-// EvalMultConstInplace (src/evaluate.cu:2299-2412): times round(c * sf[level]), degree + 1
+// GetElementForEvalMult (src/evaluate.cu:2332-2412): residues of round(c * sf[level]) as the
+// reference rounds it (125-bit window, half up)
+std::vector<uint64_t> GetElementForEvalMult(const PhantomContext& ctx, const PhantomCiphertext& ct, double c,
+                                            const std::vector<double>& sf);
+// EvalMultConstInplaceCore (src/evaluate.cu:2299-2330): times round(c * sf[level]), degree + 1,
+// scale times sf[level]
+void EvalMultConstInplaceCore(const PhantomContext& ctx, PhantomCiphertext& ct, double c, const std::vector<double>& sf);
+// EvalMultConstInplace (include/evaluate.cuh:317-326): a degree-2 input is rescaled first (the
+// lazy rescale that lets bootstrapping_example.cu:150-153 call it 25 times in a row), then Core
 void EvalMultConstInplace(const PhantomContext& ctx, PhantomCiphertext& ct, double c, const std::vector<double>& sf);
+inline PhantomCiphertext EvalMultConst(const PhantomContext& ctx, const PhantomCiphertext& ct, double c,
+                                       const std::vector<double>& sf) {
+  PhantomCiphertext d = ct;
+  EvalMultConstInplace(ctx, d, c, sf);
+  return d;
+}
+inline PhantomCiphertext EvalMultConstCore(const PhantomContext& ctx, const PhantomCiphertext& ct, double c,
+                                           const std::vector<double>& sf) {
+  return EvalMultConst(ctx, ct, c, sf);
+}
 // add the constant c to every slot (c * scale on the constant coefficient)
 void EvalAddConstInplace(const PhantomContext& ctx, PhantomCiphertext& ct, double c);
 // MultByMonomialInPlace (src/evaluate.cu:2505-2554): times X^power (slots times zeta^(power 5^j))
@@ -78,8 +97,8 @@ PhantomCiphertext EvalMultRescale(const PhantomContext& ctx, const PhantomCipher
                                   const PhantomRelinKey& rlk, const std::vector<double>& sf);
 
 // RaiseMod (src/evaluate.cu:2459-2503): limb q0 of a ciphertext -> the full chain Q (chain 1),
-// centered lift; NTT form in and out.
-PhantomCiphertext RaiseMod(const PhantomContext& ctx, const PhantomCiphertext& ct);
+// or the leading limbs of chain `chain_index`; centered lift; NTT form in and out.
+PhantomCiphertext RaiseMod(const PhantomContext& ctx, const PhantomCiphertext& ct, size_t chain_index = 1);
 
 // ---- hoisted rotations (src/evaluate.cu:3631-3940) ------------------------------------
 // EvalFastRotationPrecompute: modup of c1, [beta][size_QlP][n]
@@ -126,5 +145,96 @@ inline void EvalConjFused(const PhantomContext& ctx, const PhantomGaloisKey& fus
 
 // Galois element of a slot rotation (FindAutomorphismIndex2nComplex, src/util.cu:908-935)
 uint32_t FindAutomorphismIndex2nComplex(int index, size_t n);
+
+// ---- the reference's FLEXIBLEAUTO surface (include/evaluate.cuh:270-452; host/flexauto.cpp) ----
+// sf = getScalingFactorsReal(), sfBig = getScalingFactorsRealBig() (PreComputeScale).  These keep
+// the reference's degree bookkeeping: products are left at degree 2 and rescaled lazily.
+// ModReduce (src/evaluate.cu:2284-2297): a rescaled copy (levels > 1 rescales that many times;
+// the reference rescales the same input repeatedly, i.e. once)
+PhantomCiphertext ModReduce(const PhantomContext& ctx, const PhantomCiphertext& ct, size_t levels);
+// ModSwitchLevelInPlace (include/evaluate.cuh:304-312): drop `levels` limbs, degree kept
+void ModSwitchLevelInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, size_t levels);
+// AdjustLevelsAndDepthInPlace (src/evaluate.cu:2611-2779): the lower operand is brought to the
+// other's level, degree and scale
+void AdjustLevelsAndDepthInPlace(const PhantomContext& ctx, PhantomCiphertext& c1, PhantomCiphertext& c2,
+                                 const std::vector<double>& sf, const std::vector<double>& sfBig);
+// EvalMultAuto (src/evaluate.cu:2794-2811): adjust, rescale degree-2 operands, multiply + relin;
+// the result has degree deg1 + deg2 (not rescaled)
+PhantomCiphertext EvalMultAuto(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
+                               const PhantomRelinKey& rlk, const std::vector<double>& sf,
+                               const std::vector<double>& sfBig);
+// EvalMultAutoInplace with a plaintext (src/evaluate.cu:2813-2825) and EvalMultBroadcast (:2827-2854)
+void EvalMultAutoInplace(const PhantomContext& ctx, PhantomCiphertext& ct, const PhantomPlaintext& pt,
+                         const std::vector<double>& sf, const std::vector<double>& sfBig);
+void EvalMultBroadcast(const PhantomContext& ctx, PhantomCiphertext& ct, const PhantomCiphertext& single);
+// EvalSquare (src/evaluate.cu:3611-3629): squaring kernel + relin, degree doubled
+PhantomCiphertext EvalSquare(const PhantomContext& ctx, const PhantomCiphertext& ct, const PhantomRelinKey& rlk,
+                             const std::vector<double>& sf, const std::vector<double>& sfBig);
+inline void EvalSquareInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, const PhantomRelinKey& rlk,
+                              const std::vector<double>& sf, const std::vector<double>& sfBig) {
+  ct = EvalSquare(ctx, ct, rlk, sf, sfBig);
+}
+// EvalAddAutoInplace / EvalSubAutoInplace with the reference's adjustment (src/evaluate.cu:2856-2873)
+void EvalAddAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b,
+                        const std::vector<double>& sf, const std::vector<double>& sfBig);
+void EvalSubAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b,
+                        const std::vector<double>& sf, const std::vector<double>& sfBig);
+inline PhantomCiphertext EvalAddAuto(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
+                                     const std::vector<double>& sf, const std::vector<double>& sfBig) {
+  PhantomCiphertext d = a;
+  EvalAddAutoInplace(ctx, d, b, sf, sfBig);
+  return d;
+}
+inline PhantomCiphertext EvalSubAuto(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
+                                     const std::vector<double>& sf, const std::vector<double>& sfBig) {
+  PhantomCiphertext d = a;
+  EvalSubAutoInplace(ctx, d, b, sf, sfBig);
+  return d;
+}
+// GetElementForEvalAddOrSub / EvalAddConstInPlace / EvalSubConstInPlace (src/evaluate.cu:2894-2996):
+// the constant at scale sf[level]^degree added to c0; operand >= 0 (EvalAddConstInPlaceWrap
+// dispatches on the sign, include/evaluate.cuh:425-443)
+std::vector<uint64_t> GetElementForEvalAddOrSub(const PhantomContext& ctx, const PhantomCiphertext& ct, double operand,
+                                                const std::vector<double>& sf, const std::vector<double>& sfBig);
+void EvalAddConstInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, double operand, const std::vector<double>& sf,
+                         const std::vector<double>& sfBig);
+void EvalSubConstInPlace(const PhantomContext& ctx, PhantomCiphertext& ct, double operand, const std::vector<double>& sf,
+                         const std::vector<double>& sfBig);
+void EvalAddConstInPlaceWrap(const PhantomContext& ctx, PhantomCiphertext& ct, double operand,
+                             const std::vector<double>& sf, const std::vector<double>& sfBig);
+inline PhantomCiphertext EvalAddConst(const PhantomContext& ctx, const PhantomCiphertext& ct, double operand,
+                                      const std::vector<double>& sf, const std::vector<double>& sfBig) {
+  PhantomCiphertext d = ct;
+  EvalAddConstInPlaceWrap(ctx, d, operand, sf, sfBig);
+  return d;
+}
+// ConvertToEval / ConvertToCoeff (src/evaluate.cu:2556-2609): NTT / INTT of every polynomial
+void ConvertToEval(const PhantomContext& ctx, PhantomCiphertext& ct);
+void ConvertToCoeff(const PhantomContext& ctx, PhantomCiphertext& ct);
+// EvalChebyshevCoefficients (src/evaluate.cu:3585-3609): degree + 1 coefficients of func on [a, b]
+// (coefficient 0 not halved)
+std::vector<double> EvalChebyshevCoefficients(const std::function<double(double)>& func, double a, double b,
+                                              uint32_t degree);
+// EvalChebyshevSeries (src/evaluate.cu:3176-3186): sum c_k T_k((2x - a - b) / (b - a)) with c_0
+// halved.  Degree < 5: the reference's linear method (EvalChebyshevSeriesLinear, :3188-3262);
+// otherwise this engine's fused p = q T_m + r recursion (the bootstrap's EvalMod evaluator,
+// host/bootstrap.cpp) after the affine map.  Depth: 1 (affine map, skipped on [-1, 1]) + the
+// recursion's depth; e.g. degree 88 consumes 8 levels, as the reference's Paterson-Stockmeyer.
+PhantomCiphertext EvalChebyshevSeries(const PhantomContext& ctx, const PhantomRelinKey& rlk, const PhantomCiphertext& x,
+                                      const std::vector<double>& coeffs, double a, double b,
+                                      const std::vector<double>& sf, const std::vector<double>& sfBig);
+PhantomCiphertext EvalChebyshevSeriesLinear(const PhantomContext& ctx, const PhantomRelinKey& rlk,
+                                            const PhantomCiphertext& x, const std::vector<double>& coeffs, double a,
+                                            double b, const std::vector<double>& sf, const std::vector<double>& sfBig);
+PhantomCiphertext EvalChebyshevSeriesPS(const PhantomContext& ctx, const PhantomRelinKey& rlk, const PhantomCiphertext& x,
+                                        const std::vector<double>& coeffs, double a, double b,
+                                        const std::vector<double>& sf, const std::vector<double>& sfBig);
+// EvalChebyshevFunction (include/evaluate.cuh:381-388)
+inline PhantomCiphertext EvalChebyshevFunction(const std::function<double(double)>& func, const PhantomContext& ctx,
+                                               const PhantomRelinKey& rlk, const PhantomCiphertext& ct, double a,
+                                               double b, uint32_t degree, const std::vector<double>& sf,
+                                               const std::vector<double>& sfBig) {
+  return EvalChebyshevSeries(ctx, rlk, ct, EvalChebyshevCoefficients(func, a, b, degree), a, b, sf, sfBig);
+}
 
 }  // namespace phantom

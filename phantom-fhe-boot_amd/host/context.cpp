@@ -49,10 +49,10 @@ PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t s
 
   ws_ = std::make_unique<Workspace>();
   ntt_ = std::make_unique<DeviceNttTables>(n_, qp_, s);
-  data_.push_back(std::make_unique<ContextData>(0, qp_));
+  data_.push_back(std::make_unique<ContextData>(0, qp_, &params_));
   for (size_t c = 1; c <= size_Q_; ++c) {
     std::vector<uint64_t> ql(qp_.begin(), qp_.begin() + (size_Q_ - (c - 1)));
-    data_.push_back(std::make_unique<ContextData>(c, ql));
+    data_.push_back(std::make_unique<ContextData>(c, ql, &params_));
   }
   // per-level RNS tools (host constant generation is O(L^2) per level; run levels in parallel)
   std::vector<std::unique_ptr<RnsTool>> tools(size_Q_ + 1);

@@ -8,6 +8,7 @@
 #include <memory>
 #include <mutex>
 #include <utility>
+#include <stdexcept>
 #include <vector>
 
 #include "modulus.h"
@@ -45,8 +46,15 @@ class EncryptionParameters {
 // further index drops the last data prime (src/context.cu:133-159).
 class ContextData {
  public:
-  ContextData(size_t chain_index, std::vector<uint64_t> moduli) : chain_index_(chain_index), moduli_(std::move(moduli)) {}
+  ContextData(size_t chain_index, std::vector<uint64_t> moduli, const EncryptionParameters* parms = nullptr)
+      : chain_index_(chain_index), moduli_(std::move(moduli)), parms_(parms) {}
   size_t chain_index() const { return chain_index_; }
+  // the context's EncryptionParameters (key level Q u P; the reference's per-level parms carry the
+  // level's moduli, which moduli() gives here)
+  const EncryptionParameters& parms() const {
+    if (!parms_) throw std::logic_error("context data without parameters");
+    return *parms_;
+  }
   const std::vector<uint64_t>& moduli() const { return moduli_; }
   size_t coeff_modulus_size() const { return moduli_.size(); }
   const RnsTool& gpu_rns_tool() const { return *rns_tool_; }
@@ -56,6 +64,7 @@ class ContextData {
  private:
   size_t chain_index_;
   std::vector<uint64_t> moduli_;
+  const EncryptionParameters* parms_;
   std::unique_ptr<RnsTool> rns_tool_;
 };
 

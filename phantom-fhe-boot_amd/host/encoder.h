@@ -35,6 +35,10 @@ class PhantomCKKSEncoder {
   // every block of sparse_slots slots, i.e. the plaintext is m'(X^(N / (2 sparse_slots))), the form
   // a sparse bootstrap expects.  set_sparse_encode takes the subring dimension 2 * sparse_slots.
   void set_sparse_encode(size_t subring_degree) { sparse_slots_ = subring_degree / 2; }
+  void set_sparse_encode(const EncryptionParameters& parms, size_t subring_degree) {
+    (void)parms;
+    set_sparse_encode(subring_degree);
+  }
   void encode_sparse(const PhantomContext& ctx, const std::vector<double>& values, double scale, PhantomPlaintext& out,
                      size_t chain_index = 1) const;
   void encode_sparse(const PhantomContext& ctx, const std::vector<std::complex<double>>& values, double scale,

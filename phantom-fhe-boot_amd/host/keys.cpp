@@ -93,7 +93,7 @@ PhantomSecretKey PhantomSecretKey::load(const PhantomContext& ctx, std::istream&
   if (power < 1 || n != ctx.poly_degree() || limbs != ctx.size_QP())
     throw std::invalid_argument("secret key does not match the context");
   v.resize(n * limbs);  // s itself; higher powers are recomputed
-  PhantomSecretKey k;  // fresh entropy-seeded stream
+  PhantomSecretKey k;  // fresh entropy-seeded streams
   hipStream_t s = ctx.stream();
   k.s_.upload(v, s);
   k.init_powers(ctx);
@@ -177,11 +177,13 @@ PhantomSecretKey PhantomSecretKey::for_testing(const PhantomContext& ctx, uint64
 PhantomSecretKey PhantomSecretKey::from_seed(const PhantomContext& ctx, const uint8_t seed[32]) {
   phx::ChaChaKey k;
   std::memcpy(k.k, seed, sizeof(k.k));
-  return PhantomSecretKey(ctx, RandomStream::from_key(k), true);
+  // the seed fixes the key material only; encryptions draw from fresh OS entropy so that replicas
+  // of one key owner never share an (a, e) pair
+  return PhantomSecretKey(ctx, RandomStream::from_key(k), false);
 }
 
-PhantomSecretKey::PhantomSecretKey(const PhantomContext& ctx, RandomStream rng, bool deterministic)
-    : rng_(rng), deterministic_(deterministic) {
+PhantomSecretKey::PhantomSecretKey(const PhantomContext& ctx, RandomStream rng, bool reproducible_encryption)
+    : rng_(rng), reproducible_(reproducible_encryption) {
   const size_t n = ctx.poly_degree();
   // ternary s (sample_ternary_poly): one 64-bit keystream word per coefficient, mod 3
   std::vector<uint64_t> w(n);
@@ -197,6 +199,9 @@ PhantomSecretKey::PhantomSecretKey(const PhantomContext& ctx, RandomStream rng, 
                           ctx.stream()),
          "sk NTT");
   init_powers(ctx);
+  // for_testing: encryptions follow from the seed too (a child of the key stream); otherwise they
+  // come from a stream keyed from the OS CSPRNG, independent of the key seed
+  enc_rng_ = reproducible_ ? rng_.derive() : RandomStream();
 }
 
 void PhantomSecretKey::init_powers(const PhantomContext& ctx) {
@@ -207,16 +212,16 @@ void PhantomSecretKey::init_powers(const PhantomContext& ctx) {
   PHX_CHECK(hipStreamSynchronize(s));
 }
 
-void PhantomSecretKey::encrypt_zero_raw(const PhantomContext& ctx, uint64_t* c0, uint64_t* c1, size_t L,
-                                        const uint64_t* enc_key, const uint8_t* a_seed) const {
+void PhantomSecretKey::encrypt_zero_raw(const PhantomContext& ctx, RandomStream& rng, uint64_t* c0, uint64_t* c1,
+                                        size_t L, const uint64_t* enc_key, const uint8_t* a_seed) const {
   const size_t n = ctx.poly_degree();
   hipStream_t s = ctx.stream();
   DeviceBuffer<uint64_t> e(L * n, s);
   if (a_seed)
     sample_uniform_seeded(ctx, a_seed, c1, L);
   else
-    sample_uniform_poly(ctx, rng_, c1, L);  // uniform in NTT form is uniform
-  sample_error_poly_ntt(ctx, rng_, e.get(), L);
+    sample_uniform_poly(ctx, rng, c1, L);  // uniform in NTT form is uniform
+  sample_error_poly_ntt(ctx, rng, e.get(), L);
   const phx::ModView m = ctx.mod_QP();
   hip_ok(phx::poly_mul_add(c1, enc_key ? enc_key : s_.get(), e.get(), c0, m, n, L, s), "a*s+e");
   hip_ok(phx::poly_negate(c0, c0, m, n, L, s), "-(a*s+e)");
@@ -236,7 +241,7 @@ PhantomKSwitchKey PhantomSecretKey::make_kswitch_key(const PhantomContext& ctx, 
     DeviceBuffer<uint64_t> key(2 * QP * n, s);
     uint64_t* b = key.get();
     uint64_t* a = key.get() + QP * n;
-    encrypt_zero_raw(ctx, b, a, QP, enc_key);
+    encrypt_zero_raw(ctx, rng_, b, a, QP, enc_key);
     // + P * new_key on this digit's primes (multiply_temp_mod_and_add_rns_poly)
     const size_t l0 = d * alpha, l1 = std::min(Q, l0 + alpha);
     phx::ModView sub{mqp.q + l0, mqp.barrett + 2 * l0};
@@ -349,11 +354,10 @@ void PhantomSecretKey::encrypt_symmetric(const PhantomContext& ctx, const Phanto
   out.set_asymmetric(false);
   // a public seed for a (save_symmetric writes it instead of c1): one draw of this key's stream
   std::vector<uint8_t> seed(PhantomCiphertext::kSeedBytes);
-  rng_.host_words(reinterpret_cast<uint64_t*>(seed.data()), seed.size() / sizeof(uint64_t));
-  encrypt_zero_raw(ctx, out.data(), out.data() + L * n, L, nullptr, seed.data());
-  out.set_seed(std::move(seed));
+  enc_rng_.host_words(reinterpret_cast<uint64_t*>(seed.data()), seed.size() / sizeof(uint64_t));
+  encrypt_zero_raw(ctx, enc_rng_, out.data(), out.data() + L * n, L, nullptr, seed.data());
   hip_ok(phx::poly_add(out.data(), plain.data(), out.data(), ctx.mod_QP(), n, L, s), "m - (a s + e)");
-  PHX_CHECK(hipStreamSynchronize(s));
+  out.set_seed(std::move(seed), s);  // synchronises s
 }
 
 void PhantomSecretKey::decrypt(const PhantomContext& ctx, const PhantomCiphertext& ct, PhantomPlaintext& out) const {
@@ -375,9 +379,9 @@ PhantomPublicKey PhantomSecretKey::gen_publickey(const PhantomContext& ctx) cons
   const size_t n = ctx.poly_degree(), QP = ctx.size_QP();
   pk.pk_.resize(ctx, 0, 2, ctx.stream(), false);
   pk.pk_.set_ntt_form(true);
-  encrypt_zero_raw(ctx, pk.pk_.data(), pk.pk_.data() + QP * n, QP);
+  encrypt_zero_raw(ctx, rng_, pk.pk_.data(), pk.pk_.data() + QP * n, QP);  // key material
   // the encryptor's own stream: fresh entropy, or derived for reproducible tests
-  pk.rng_ = deterministic_ ? rng_.derive() : RandomStream();
+  pk.rng_ = reproducible_ ? enc_rng_.derive() : RandomStream();
   PHX_CHECK(hipStreamSynchronize(ctx.stream()));
   return pk;
 }

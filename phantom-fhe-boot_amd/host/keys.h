@@ -110,8 +110,10 @@ class PhantomSecretKey {
   explicit PhantomSecretKey(const PhantomContext& ctx);
   // reproducible key for tests only: every draw (s, errors, uniform halves) follows from `seed`
   static PhantomSecretKey for_testing(const PhantomContext& ctx, uint64_t seed);
-  // key and every later draw derived from a 256-bit secret seed: replicas of one key owner (the
-  // ranks of a multi-GPU job) regenerate identical keys from a shared seed instead of moving them
+  // key material (s, public key, relin / Galois keys) derived from a 256-bit secret seed: replicas
+  // of one key owner (the ranks of a multi-GPU job) regenerate identical keys from a shared seed
+  // instead of moving them.  Encryptions still draw from fresh OS entropy, so two replicas' k-th
+  // encryptions share no randomness.
   static PhantomSecretKey from_seed(const PhantomContext& ctx, const uint8_t seed[32]);
   PhantomSecretKey(PhantomSecretKey&&) = default;
   PhantomSecretKey& operator=(PhantomSecretKey&&) = default;
@@ -163,16 +165,17 @@ class PhantomSecretKey {
                                      const uint64_t* enc_key = nullptr);
 
  private:
-  PhantomSecretKey(const PhantomContext& ctx, RandomStream rng, bool deterministic);
+  PhantomSecretKey(const PhantomContext& ctx, RandomStream rng, bool reproducible_encryption);
   PhantomSecretKey() = default;
   void init_powers(const PhantomContext& ctx);
   // symmetric encryption of zero over the first L limbs of Q u P under enc_key (default s):
   // (-(a s + e), a), NTT form
   // a_seed: take a from sample_uniform_seeded(a_seed) instead of this key's stream
-  void encrypt_zero_raw(const PhantomContext& ctx, uint64_t* c0, uint64_t* c1, size_t L,
+  void encrypt_zero_raw(const PhantomContext& ctx, RandomStream& rng, uint64_t* c0, uint64_t* c1, size_t L,
                         const uint64_t* enc_key = nullptr, const uint8_t* a_seed = nullptr) const;
-  mutable RandomStream rng_;
-  bool deterministic_ = false;
+  // rng_: key material; enc_rng_: encryption draws (OS entropy unless for_testing)
+  mutable RandomStream rng_, enc_rng_;
+  bool reproducible_ = false;
   std::vector<int8_t> coeffs_;
   DeviceBuffer<uint64_t> s_, s2_;
 };

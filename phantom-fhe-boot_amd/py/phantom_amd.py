@@ -38,6 +38,7 @@ _SIGS = {
     "phantom_context_destroy": (ctypes.c_int, [vp]),
     "phantom_context_coeff_modulus_size": (sz, [vp, sz]),
     "phantom_multiply": (ctypes.c_int, [vp, sz, vp, vp, vp, vp]),
+    "phantom_square": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_relinearize": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, vp]),
     "phantom_keyswitch": (ctypes.c_int, [vp, sz, vp, vp, ctypes.POINTER(vp), sz, vp]),
     "phantom_modup": (ctypes.c_int, [vp, sz, vp, vp, vp]),

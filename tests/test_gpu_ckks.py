@@ -68,6 +68,30 @@ def test_multiply(request, rng, fixture, chain):
     assert np.array_equal(to_host(dout), want)
 
 
+@pytest.mark.parametrize("fixture,chain", [("c3", 1), ("small", 1), ("small", 5)])
+def test_square(request, rng, fixture, chain):
+    """tensor_square_2x2_rns_poly (src/polymath.cu:538-582), out of place and in place"""
+    ctx = request.getfixturevalue(fixture)
+    ql = ctx.ql(chain)
+    a = _rand_ct(rng, ctx, chain, 2)
+    # extreme residues: q - 1 and 0 in the first limb
+    a[: ctx.n // 2] = ql[0] - 1
+    a[ctx.n // 2: ctx.n] = 0
+    want = np.zeros(3 * len(ql) * ctx.n, dtype=np.uint64)
+    O.lib().or_tensor_square_2x2(O.P(a), O.P(want), ctx.n, len(ql), O.P(O.arr(ql)))
+    da = to_dev(a)
+    dout = to_dev(np.zeros(3 * len(ql) * ctx.n, dtype=np.uint64))
+    PA.check(_lib().phantom_square(ctx.handle, chain, ptr(da), ptr(dout), stream()))
+    assert np.array_equal(to_host(dout), want)
+    dio = to_dev(np.concatenate([a, np.zeros(len(ql) * ctx.n, dtype=np.uint64)]))
+    PA.check(_lib().phantom_square(ctx.handle, chain, ptr(dio), ptr(dio), stream()))
+    assert np.array_equal(to_host(dio), want)
+    # the square is the product with itself
+    prod = np.zeros_like(want)
+    O.lib().or_tensor_prod_2x2(O.P(a), O.P(a), O.P(prod), ctx.n, len(ql), O.P(O.arr(ql)))
+    assert np.array_equal(prod, want)
+
+
 @pytest.mark.parametrize("fixture,chain", [("c3", 1), ("small", 1), ("small", 2), ("small", 6)])
 def test_modup(request, rng, fixture, chain):
     ctx = request.getfixturevalue(fixture)

@@ -4,7 +4,10 @@ PhantomSecretKey(context) + gen_publickey, encode/decode, encrypt_symmetric / en
 add / sub, multiply_plain, the x*y*x HomMul with relinearize_inplace / rescale_to_next_inplace /
 mod_switch_to_next_inplace, EvalRotateKeyGen + EvalRotateFused / EvalConjFused, and the
 small-parameter apply_galois_inplace, and the seed-compressed save_symmetric /
-load_symmetric round trip — each checked with the reference's own rule (every slot
+load_symmetric round trip, and (ckks_api) the rest of include/evaluate.cuh's CKKS surface: add_many,
+add/sub_plain, the squaring branch of multiply (bit-identical to the product of two copies),
+multiply_and_relin, plaintext mod_switch_to(_next), hoisting_inplace, NAF-composed rotations,
+save_symmetric refusing a rewritten c1, from_seed keys with independent encryption randomness — each checked with the reference's own rule (every slot
 within 1e-3, 3_ckks.cu:19,33-41).  Keys come from the OS entropy path (no test seed)."""
 import json
 import os
@@ -16,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "phantom-fhe-boot_amd", "bin", "ckks_example")
-EXAMPLES = ["ckks_enc", "ckks_add", "ckks_save_symmetric", "ckks_mul_plain", "ckks_mul", "ckks_rotation"]
+EXAMPLES = ["ckks_enc", "ckks_add", "ckks_save_symmetric", "ckks_mul_plain", "ckks_mul", "ckks_rotation", "ckks_api"]
 
 
 @pytest.mark.parametrize("alpha", [15, 1, 3])

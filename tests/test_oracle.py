@@ -155,6 +155,27 @@ def test_tensor_product_formula(rng):
             assert int(out[2 * s + i]) == a1 * b1 % q
 
 
+def test_tensor_square_formula(rng):
+    """or_tensor_square_2x2 (polymath.cu:538-582) = the product with itself, exact, incl. q - 1"""
+    n = 32
+    mods = O.coeff_modulus_create(n, [60, 59, 50])
+    L = len(mods)
+    c = np.concatenate([O.random_limbs(rng, n, mods) for _ in range(2)])
+    c[:4] = mods[0] - 1
+    c[L * n: L * n + 4] = mods[0] - 1
+    out = np.zeros(3 * L * n, dtype=np.uint64)
+    O.lib().or_tensor_square_2x2(P(c), P(out), n, L, P(arr(mods)))
+    prod = np.zeros_like(out)
+    O.lib().or_tensor_prod_2x2(P(c), P(c), P(prod), n, L, P(arr(mods)))
+    assert np.array_equal(out, prod)
+    s = L * n
+    for l, q in enumerate(mods):
+        for k in range(n):
+            i = l * n + k
+            a0, a1 = int(c[i]), int(c[s + i])
+            assert int(out[s + i]) == 2 * a0 * a1 % q
+
+
 # --------------------------------------------------------------------------------------
 # base conversion, moddown, rescale
 # --------------------------------------------------------------------------------------
