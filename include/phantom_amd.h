@@ -285,6 +285,11 @@ int phantom_boot_encrypt(phantom_boot_session *s, const double *values, size_t c
                          uint8_t *dev_out, size_t stride, size_t *ct_bytes);
 /* size of one serialized bootstrap output */
 int phantom_boot_output_bytes(phantom_boot_session *s, size_t *bytes);
+/* the same sizes from the session parameters alone (host only, no GPU): one serialized input at
+ * chain_index, one serialized output, and the output's chain index */
+int phantom_boot_layout(int log_n, int depth, int special, const uint32_t *level_budget, uint32_t num_slots,
+                        uint32_t num_iterations, size_t chain_index, size_t *in_bytes, size_t *out_bytes,
+                        size_t *out_chain);
 /* EvalBootstrap of `count` serialized ciphertexts, `lanes` side by side (EvalBootstrapBatch) */
 int phantom_boot_run(phantom_boot_session *s, const uint8_t *dev_in, size_t in_stride, size_t count, uint8_t *dev_out,
                      size_t out_stride, int lanes);

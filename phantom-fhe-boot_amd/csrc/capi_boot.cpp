@@ -163,6 +163,26 @@ int phantom_boot_session_create(int log_n, int depth, int special, const uint32_
   });
 }
 
+int phantom_boot_layout(int log_n, int depth, int special, const uint32_t* level_budget, uint32_t num_slots,
+                        uint32_t num_iterations, size_t chain_index, size_t* in_bytes, size_t* out_bytes,
+                        size_t* out_chain) {
+  PHX_CAPI_GUARD({
+    if (!level_budget || !in_bytes || !out_bytes || !out_chain) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (log_n < 10 || log_n > 17 || depth < 1 || special < 1) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "bad parameters");
+    const size_t N = size_t(1) << log_n, size_Q = static_cast<size_t>(depth) + 1;
+    const uint32_t slots = num_slots ? num_slots : static_cast<uint32_t>(N / 2);
+    if (slots & (slots - 1)) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "slot count not a power of two");
+    if (chain_index < 1 || chain_index + 1 > size_Q) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "bad chain index");
+    const size_t oc = FHECKKSRNS::OutputChainIndex({level_budget[0], level_budget[1]},
+                                                   static_cast<uint32_t>(__builtin_ctz(slots)), num_iterations);
+    if (oc > size_Q) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "not enough levels for bootstrapping");
+    *in_bytes = ser::kCiphertextHeaderBytes + 2 * (size_Q - (chain_index - 1)) * N * 8;
+    *out_bytes = ser::kCiphertextHeaderBytes + 2 * (size_Q - (oc - 1)) * N * 8;
+    *out_chain = oc;
+    return PHANTOM_OK;
+  });
+}
+
 int phantom_boot_session_destroy(phantom_boot_session* s) {
   if (s) (void)hipDeviceSynchronize();
   delete s;

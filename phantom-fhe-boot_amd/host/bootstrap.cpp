@@ -690,6 +690,17 @@ const FHECKKSRNS::Precom& FHECKKSRNS::precom(uint32_t numSlots, const PhantomCon
   return it->second;
 }
 
+size_t FHECKKSRNS::OutputChainIndex(const std::vector<uint32_t>& levelBudget, uint32_t log_slots,
+                                    uint32_t numIterations, bool tight) {
+  if (log_slots < 1) throw std::invalid_argument("bad slot count");
+  const size_t enc = std::clamp<uint32_t>(levelBudget.at(0), 1, log_slots);
+  const size_t dec = std::clamp<uint32_t>(levelBudget.at(1), 1, log_slots);
+  const size_t own_mod = static_cast<size_t>(cheb_depth(kChebDegree)) + R_UNIFORM;
+  const size_t ref_mod = reference_series_depth(kChebDegree) + R_UNIFORM;
+  const size_t raise = tight || ref_mod < own_mod ? 0 : ref_mod - own_mod;
+  return 1 + raise + enc + own_mod + dec + (numIterations > 1 ? 1 : 0);
+}
+
 size_t FHECKKSRNS::output_chain_index(uint32_t numSlots, uint32_t numIterations) const {
   const uint32_t slots = numSlots ? numSlots : static_cast<uint32_t>(encoder_.slot_count());
   auto it = precom_.find(slots);

@@ -122,6 +122,10 @@ class FHECKKSRNS {
   std::vector<int> rotation_indices(uint32_t numSlots = 0) const;
   // chain index of a bootstrap's output
   size_t output_chain_index(uint32_t numSlots = 0, uint32_t numIterations = 1) const;
+  // the same from the parameters alone (no context, no setup): ModRaise lands on chain
+  // 1 + raise level, then CoeffToSlot, EvalMod and SlotToCoeff each consume their depth
+  static size_t OutputChainIndex(const std::vector<uint32_t>& levelBudget, uint32_t log_slots,
+                                 uint32_t numIterations = 1, bool tight = false);
   uint32_t correction_factor() const { return correction_; }
   const std::vector<double>& eval_mod_coefficients() const { return cheb_; }
   const std::vector<double>& scaling_factors() const { return sf_; }

@@ -75,6 +75,9 @@ _SIGS = {
     "phantom_eval_mod_coefficients": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp]),
     "phantom_boot_encrypt": (ctypes.c_int, [vp, vp, sz, sz, vp, sz, ctypes.POINTER(sz)]),
     "phantom_boot_output_bytes": (ctypes.c_int, [vp, ctypes.POINTER(sz)]),
+    "phantom_boot_layout": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_uint32,
+                                           ctypes.c_uint32, sz, ctypes.POINTER(sz), ctypes.POINTER(sz),
+                                           ctypes.POINTER(sz)]),
     "phantom_boot_run": (ctypes.c_int, [vp, vp, sz, sz, vp, sz, ctypes.c_int]),
     "phantom_boot_decrypt": (ctypes.c_int, [vp, vp, sz, vp]),
 }
@@ -192,6 +195,16 @@ class NttTables:
             pass
 
 
+def boot_layout(chain_index, log_n=16, depth=29, special=10, level_budget=(2, 2), num_slots=0, iterations=1):
+    """(input bytes at chain_index, output bytes, output chain index) of a bootstrap session's
+    serialized ciphertexts, computed on the host from the parameters (phantom_boot_layout)."""
+    lb = (ctypes.c_uint32 * 2)(*level_budget)
+    a, b, c = sz(0), sz(0), sz(0)
+    check(load().phantom_boot_layout(log_n, depth, special, lb, num_slots, iterations, chain_index,
+                                     ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+    return a.value, b.value, c.value
+
+
 class BootSession:
     """Owning handle of a phantom_boot_session (the SimpleBootstrapExample set-up; C4/C5)."""
 
@@ -208,6 +221,8 @@ class BootSession:
         self.n = 1 << log_n
         self.slots = num_slots or self.n // 2
         self.depth = depth
+        self.params = dict(log_n=log_n, depth=depth, special=special, level_budget=tuple(level_budget),
+                           num_slots=num_slots, iterations=iterations)
 
     def output_bytes(self):
         b = sz(0)
@@ -215,12 +230,14 @@ class BootSession:
         return b.value
 
     def input_bytes(self, chain_index):
-        return 58 + 2 * (self.depth + 1 - (chain_index - 1)) * self.n * 8
+        return boot_layout(chain_index, **self.params)[0]
 
     def encrypt(self, values, chain_index, dev_ptr, stride):
         """values: float64 [count, slots]; writes serialized ciphertexts at dev_ptr + i * stride."""
         import numpy as np
         v = np.ascontiguousarray(values, dtype=np.float64)
+        if v.ndim != 2 or v.shape[1] != self.slots:
+            raise ValueError(f"values must be [count, {self.slots}], got shape {v.shape}")
         b = sz(0)
         check(load().phantom_boot_encrypt(self.handle, v.ctypes.data, v.shape[0], chain_index, dev_ptr, stride,
                                           ctypes.byref(b)))
