@@ -64,8 +64,9 @@ def test_single_process_helpers_without_a_group():
 def test_c5_spawn_scatter_gather_two_ranks_gloo():
     """bench.py's C5 data path end to end on host buffers: shard.spawn_ranks starts 2 ranks with the
     rendezvous environment (what `bench.py --gpus 2` does without a launcher), rank 0 scatters
-    serialized ciphertexts, each rank transforms its slice, rank 0 gathers and verifies order and
-    contents (tests/c5_gloo_worker.py)."""
+    session-format serialized ciphertexts at the C5 shape (N = 2^16, chain 26 in, the session's
+    output chain out, strides from phantom_boot_layout), each rank checks and transforms its
+    slice, rank 0 gathers and verifies order and every byte (tests/c5_gloo_worker.py)."""
     import json
     import subprocess
     code = ("import sys; sys.path.insert(0, %r); import shard; "
@@ -74,4 +75,24 @@ def test_c5_spawn_scatter_gather_two_ranks_gloo():
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     rows = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
-    assert rows == [{"ok": True, "world": 2, "total": 12, "seed_bytes": 32}], (rows, out.stderr[-2000:])
+    assert len(rows) == 1 and rows[0]["ok"], (rows, out.stderr[-2000:])
+    # 5 input limbs, 12 output limbs (chain 19: the reference's output level) at N = 2^16
+    assert rows[0] == {"ok": True, "world": 2, "total": 4, "seed_bytes": 32, "in_bytes": 58 + 2 * 5 * 65536 * 8,
+                       "out_bytes": 58 + 2 * 12 * 65536 * 8, "out_chain": 19}, rows
+
+
+def test_c4_reference_bytes_by_hand():
+    """The C4 roofline denominator is the reference schedule's work, recomputed here term by term
+    (bench.c4_reference_bytes docstring): it depends on no engine counter."""
+    sys.path.insert(0, ROOT)
+    import bench
+    w = 8 * 65536
+    key = {2: 3 * 2 * 39, 3: 3 * 2 * 38, 4: 3 * 2 * 37, 7: 3 * 2 * 34, 11: 2 * 2 * 30, 12: 2 * 2 * 29,
+           13: 2 * 2 * 28, 14: 2 * 2 * 27, 15: 2 * 2 * 26, 16: 2 * 2 * 25, 17: 2 * 2 * 24, 18: 2 * 2 * 23}
+    keys = (70 * key[2] + 38 * key[3] + 70 * key[17] + 38 * key[18] + key[4] + 36 * key[7]
+            + 2 * sum(key[c] for c in range(11, 17))) * w
+    pts = (511 * 39 + 255 * 38 + 511 * 24 + 255 * 23) * w
+    cts = (2 * 5 + 2 * 12) * w
+    total, parts = bench.c4_reference_bytes()
+    assert parts == {"keys": keys, "plaintexts": pts, "ciphertexts": cts}
+    assert total == keys + pts + cts == 48196747264
