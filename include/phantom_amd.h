@@ -228,6 +228,11 @@ typedef struct phantom_ct_header {
 /* writes the header and data (host) to out[capacity]; *written = bytes (needed size when too small) */
 int phantom_ciphertext_serialize(const phantom_ct_header *h, const uint64_t *host_data, uint8_t *out,
                                  size_t capacity, size_t *written);
+/* PhantomGaloisKey::save (include/secretkey.h:195-205) of host words (host only, no GPU):
+ * host_keys = [count][dnum][2][size_QP][n]; writes count, then per key dnum and dnum key-level
+ * ciphertexts (chain 0, size 2, n, size_QP, scale 1, correction 1, degree 1, NTT form, symmetric) */
+int phantom_galois_key_serialize(size_t n, size_t size_QP, size_t dnum, size_t count, const uint64_t *host_keys,
+                                 uint8_t *out, size_t capacity, size_t *written);
 /* parses in[len]; copies the words to host_data[capacity_words] (may be null: header only);
  * *words = the ciphertext's word count */
 int phantom_ciphertext_deserialize(const uint8_t *in, size_t len, phantom_ct_header *h, uint64_t *host_data,
@@ -307,6 +312,13 @@ int phantom_chacha20_block(const uint32_t *key, uint64_t counter, uint64_t nonce
  *   PHANTOM_SAMPLE_CBD:     centered binomial 21+21 bits of 64-bit word k (sample_error_poly)
  *   PHANTOM_SAMPLE_TERNARY: 64-bit word k mod 3 minus 1 (sample_ternary_poly)
  * the last two write the same signed value to every limb (coefficient form). */
+/* the reference's Salsa20 block (src/prng.cu:17-140; host only): seed[64], nonce -> out[16] */
+int phantom_salsa20_block(const uint8_t *seed, uint64_t nonce, uint32_t *out);
+/* the reference's uniform expansion of a public 64-byte seed (sample_uniform_poly,
+ * src/prng.cu:164-197): `a` of a seed-compressed symmetric ciphertext, [coeff_modulus_size][n]
+ * over the first limbs of the key-level chain, bit for bit as the reference */
+int phantom_sample_uniform_seeded(const phantom_context *ctx, const uint8_t *seed, uint64_t *out,
+                                  size_t coeff_modulus_size, hipStream_t stream);
 #define PHANTOM_SAMPLE_UNIFORM 0
 #define PHANTOM_SAMPLE_CBD 1
 #define PHANTOM_SAMPLE_TERNARY 2

@@ -384,6 +384,82 @@ void or_tensor_square_2x2(const uint64_t *ct, uint64_t *out, size_t n, size_t L,
 }
 
 /* ------------------------------------------------------------------ */
+/* seed expansion of symmetric ciphertexts (src/prng.cu)                 */
+/* ------------------------------------------------------------------ */
+
+static uint32_t or_rotl32(uint32_t u, int c) { return (u << c) | (u >> (32 - c)); }
+
+/* the Salsa20 core (20 rounds + feed-forward), as the loop of salsa20_gpu (src/prng.cu:48-99) */
+void or_salsa20_core(const uint32_t in[16], uint32_t out[16]) {
+    uint32_t x[16];
+    for (int i = 0; i < 16; i++) x[i] = in[i];
+    for (int r = 0; r < 10; r++) {
+        /* columns */
+        x[4] ^= or_rotl32(x[0] + x[12], 7);  x[8] ^= or_rotl32(x[4] + x[0], 9);
+        x[12] ^= or_rotl32(x[8] + x[4], 13); x[0] ^= or_rotl32(x[12] + x[8], 18);
+        x[9] ^= or_rotl32(x[5] + x[1], 7);   x[13] ^= or_rotl32(x[9] + x[5], 9);
+        x[1] ^= or_rotl32(x[13] + x[9], 13); x[5] ^= or_rotl32(x[1] + x[13], 18);
+        x[14] ^= or_rotl32(x[10] + x[6], 7); x[2] ^= or_rotl32(x[14] + x[10], 9);
+        x[6] ^= or_rotl32(x[2] + x[14], 13); x[10] ^= or_rotl32(x[6] + x[2], 18);
+        x[3] ^= or_rotl32(x[15] + x[11], 7); x[7] ^= or_rotl32(x[3] + x[15], 9);
+        x[11] ^= or_rotl32(x[7] + x[3], 13); x[15] ^= or_rotl32(x[11] + x[7], 18);
+        /* rows */
+        x[1] ^= or_rotl32(x[0] + x[3], 7);   x[2] ^= or_rotl32(x[1] + x[0], 9);
+        x[3] ^= or_rotl32(x[2] + x[1], 13);  x[0] ^= or_rotl32(x[3] + x[2], 18);
+        x[6] ^= or_rotl32(x[5] + x[4], 7);   x[7] ^= or_rotl32(x[6] + x[5], 9);
+        x[4] ^= or_rotl32(x[7] + x[6], 13);  x[5] ^= or_rotl32(x[4] + x[7], 18);
+        x[11] ^= or_rotl32(x[10] + x[9], 7); x[8] ^= or_rotl32(x[11] + x[10], 9);
+        x[9] ^= or_rotl32(x[8] + x[11], 13); x[10] ^= or_rotl32(x[9] + x[8], 18);
+        x[12] ^= or_rotl32(x[15] + x[14], 7); x[13] ^= or_rotl32(x[12] + x[15], 9);
+        x[14] ^= or_rotl32(x[13] + x[12], 13); x[15] ^= or_rotl32(x[14] + x[13], 18);
+    }
+    for (int i = 0; i < 16; i++) out[i] = x[i] + in[i];
+}
+
+static uint32_t or_le32(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+/* one 64-byte block of salsa20_gpu(out, 64, nonce, seed, 64) (src/prng.cu:17-47): the state holds
+ * seed bytes 0..31 in words 0..7, the nonce in words 8..9 and seed bytes 32..55 in words 10..15
+ * (bytes 56..63 of the 64-byte seed are unused; no constants, no block counter) */
+void or_salsa20_block(const uint8_t seed[64], uint64_t nonce, uint32_t out[16]) {
+    uint32_t in[16];
+    for (int i = 0; i < 8; i++) in[i] = or_le32(seed + 4 * i);
+    in[8] = (uint32_t)nonce;
+    in[9] = (uint32_t)(nonce >> 32);
+    for (int i = 0; i < 6; i++) in[10 + i] = or_le32(seed + 32 + 4 * i);
+    or_salsa20_core(in, out);
+}
+
+/* sample_uniform_poly (src/prng.cu:164-197): thread tid < (n / 8) L fills out[8 tid .. 8 tid + 8)
+ * of limb tid / (n / 8) with the block of nonce tid read as 8 little-endian 64-bit words, each
+ * reduced mod q; a word above max_multiple = 2^64 - 1 - ((2^64 - 1) mod q) - 1 is rejected by
+ * replacing the WHOLE block with the one of nonce tid + tries n L (tries = 1, 2, ..) and
+ * continuing at the same word index */
+void or_sample_uniform_seeded(const uint8_t seed[64], const uint64_t *moduli, size_t n, size_t L, uint64_t *out) {
+    const size_t per = n >> 3;
+    for (size_t tid = 0; tid < per * L; tid++) {
+        const uint64_t q = moduli[tid / per];
+        const uint64_t maxr = ~(uint64_t)0;
+        const uint64_t max_multiple = maxr - maxr % q - 1;
+        uint32_t blk[16];
+        uint64_t tries = 0;
+        or_salsa20_block(seed, tid, blk);
+        tries++;
+        for (int index = 0; index < 8; index++) {
+            uint64_t r = (uint64_t)blk[2 * index] | ((uint64_t)blk[2 * index + 1] << 32);
+            while (r > max_multiple) {
+                or_salsa20_block(seed, tid + tries * n * L, blk);
+                tries++;
+                r = (uint64_t)blk[2 * index] | ((uint64_t)blk[2 * index + 1] << 32);
+            }
+            out[tid * 8 + index] = r % q;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
 /* base conversion                                                      */
 /* ------------------------------------------------------------------ */
 

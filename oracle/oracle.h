@@ -65,6 +65,10 @@ void or_poly_mul_scalar(const uint64_t *a, const uint64_t *scalars, uint64_t *ou
                         const uint64_t *moduli);
 void or_tensor_prod_2x2(const uint64_t *ct1, const uint64_t *ct2, uint64_t *out, size_t n, size_t L,
                         const uint64_t *moduli);
+/* the reference's Salsa20 generator (src/prng.cu:17-140) and uniform sampler (:164-197) */
+void or_salsa20_core(const uint32_t in[16], uint32_t out[16]);
+void or_salsa20_block(const uint8_t seed[64], uint64_t nonce, uint32_t out[16]);
+void or_sample_uniform_seeded(const uint8_t seed[64], const uint64_t *moduli, size_t n, size_t L, uint64_t *out);
 void or_tensor_square_2x2(const uint64_t *ct, uint64_t *out, size_t n, size_t L, const uint64_t *moduli);
 
 /* ---- base conversion (src/rns_bconv.cu:22-229, include/host/rns.h:135-199) ---- */

@@ -192,6 +192,28 @@ int phantom_moddown_rescale(const phantom_context* ctx, size_t chain_index, uint
   });
 }
 
+int phantom_galois_key_serialize(size_t n, size_t size_QP, size_t dnum, size_t count, const uint64_t* host_keys,
+                                 uint8_t* out, size_t capacity, size_t* written) {
+  PHX_CAPI_GUARD({
+    if (!written || (count && !host_keys)) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (dnum > 64) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "dnum too large");
+    const size_t digit = phantom::ser::checked_words(2, size_QP, n);
+    const size_t need = 8 + count * (8 + dnum * (phantom::ser::kCiphertextHeaderBytes + digit * sizeof(uint64_t)));
+    *written = need;
+    if (!out || capacity < need) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "output buffer too small");
+    std::ostringstream os;
+    phantom::ser::write_u64(os, count);
+    for (size_t k = 0; k < count; ++k) {
+      std::vector<const uint64_t*> d;
+      for (size_t i = 0; i < dnum; ++i) d.push_back(host_keys + (k * dnum + i) * digit);
+      phantom::ser::write_kswitch_key(os, n, size_QP, d);
+    }
+    const std::string b = os.str();
+    std::memcpy(out, b.data(), b.size());
+    return PHANTOM_OK;
+  });
+}
+
 int phantom_ciphertext_serialize(const phantom_ct_header* h, const uint64_t* host_data, uint8_t* out, size_t capacity,
                                  size_t* written) {
   PHX_CAPI_GUARD({

@@ -32,6 +32,24 @@ int phantom_chacha20_block(const uint32_t* key, uint64_t counter, uint64_t nonce
   return PHANTOM_OK;
 }
 
+int phantom_salsa20_block(const uint8_t* seed, uint64_t nonce, uint32_t* out) {
+  if (!seed || !out) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+  phx::salsa20_block(phx::salsa_seed(seed), nonce, out);
+  return PHANTOM_OK;
+}
+
+int phantom_sample_uniform_seeded(const phantom_context* ctx, const uint8_t* seed, uint64_t* out,
+                                  size_t coeff_modulus_size, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (!seed || !out) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    const phantom::PhantomContext& pc = phantom_capi_context(ctx);
+    if (coeff_modulus_size < 1 || coeff_modulus_size > pc.size_QP())
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "limb count exceeds the chain");
+    return from_hip(phx::sample_uniform_seeded(out, pc.mod_QP().q, pc.mod_QP().barrett, pc.poly_degree(),
+                                               coeff_modulus_size, phx::salsa_seed(seed), stream));
+  });
+}
+
 int phantom_sample_poly(const phantom_context* ctx, int kind, const uint32_t* key, uint64_t nonce, uint64_t* out,
                         size_t coeff_modulus_size, hipStream_t stream) {
   PHX_CAPI_GUARD({

@@ -8,6 +8,7 @@
 #include <cstdint>
 
 #include "chacha.h"
+#include "salsa.h"
 
 namespace phx {
 
@@ -15,6 +16,10 @@ namespace phx {
 // uniform: 128-bit keystream values reduced mod q[l] (one independent value per element)
 hipError_t sample_uniform(uint64_t* out, const uint64_t* q, const uint64_t* barrett, size_t n, size_t L,
                           const ChaChaKey& key, uint64_t nonce, hipStream_t s);
+// the reference's expansion of a public 64-byte seed into a uniform [L][n] polynomial
+// (sample_uniform_poly, src/prng.cu:164-197; salsa.h), bit for bit
+hipError_t sample_uniform_seeded(uint64_t* out, const uint64_t* q, const uint64_t* barrett, size_t n, size_t L,
+                                 const SalsaSeed& seed, hipStream_t s);
 // centered binomial e_k (21 + 21 bits, sigma ~3.24), the same e_k in every limb (coefficient form)
 hipError_t sample_cbd(uint64_t* out, const uint64_t* q, size_t n, size_t L, const ChaChaKey& key, uint64_t nonce,
                       hipStream_t s);

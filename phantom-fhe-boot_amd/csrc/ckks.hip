@@ -29,6 +29,38 @@ __global__ __launch_bounds__(kBlock) void uniform_kernel(uint64_t* out, const ui
   }
 }
 
+// the reference's uniform expansion of a public 64-byte seed (sample_uniform_poly,
+// src/prng.cu:164-197; salsa.h): thread t < (n / 8) L fills 8 coefficients of limb t / (n / 8)
+// from the block of nonce t, rejecting words above max_multiple by replacing the whole block
+// with the one of nonce t + tries n L.  barrett[2 l + 1] = floor(2^64 / q): the exact 64-bit
+// remainder of barrett_reduce_64.
+__global__ __launch_bounds__(kBlock) void uniform_salsa_kernel(uint64_t* out, const uint64_t* q,
+                                                               const uint64_t* barrett, uint32_t log_n, size_t L,
+                                                               SalsaSeed seed) {
+  const size_t per = (size_t(1) << log_n) >> 3, total = per * L, nl = L << log_n;
+  for (size_t t = blockIdx.x * (size_t)kBlock + threadIdx.x; t < total; t += (size_t)gridDim.x * kBlock) {
+    const size_t l = t / per;
+    const uint64_t ql = q[l], r1 = barrett[2 * l + 1];
+    const uint64_t max_multiple = ~uint64_t(0) - barrett_reduce_64(~uint64_t(0), ql, r1) - 1;
+    uint32_t w[16];
+    salsa20_block(seed, t, w);
+    uint64_t tries = 1;
+    uint64_t v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      uint64_t r = static_cast<uint64_t>(w[2 * i]) | (static_cast<uint64_t>(w[2 * i + 1]) << 32);
+      while (r > max_multiple) {
+        salsa20_block(seed, t + tries * nl, w);
+        ++tries;
+        r = static_cast<uint64_t>(w[2 * i]) | (static_cast<uint64_t>(w[2 * i + 1]) << 32);
+      }
+      v[i] = barrett_reduce_64(r, ql, r1);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) *reinterpret_cast<ulonglong2*>(out + 8 * t + i) = make_ulonglong2(v[i], v[i + 1]);
+  }
+}
+
 // small signed samples, one 64-bit word per coefficient k (block k / 8), the same value written
 // to every limb: MODE 0 centered binomial (21 + 21 bits, sigma = sqrt(10.5) ~ 3.24, as the
 // reference's sample_error_poly draws a CBD), MODE 1 ternary {-1, 0, 1} uniform (word mod 3,
@@ -333,6 +365,13 @@ hipError_t sample_uniform(uint64_t* out, const uint64_t* q, const uint64_t* barr
   if (n < 8 || (n & (n - 1))) return hipErrorInvalidValue;
   const size_t blocks = n * L / 4;
   uniform_kernel<<<grid_for(blocks), kBlock, 0, s>>>(out, q, barrett, __builtin_ctzll(n), blocks, key, nonce);
+  return hipGetLastError();
+}
+
+hipError_t sample_uniform_seeded(uint64_t* out, const uint64_t* q, const uint64_t* barrett, size_t n, size_t L,
+                                 const SalsaSeed& seed, hipStream_t s) {
+  if (n < 8 || (n & (n - 1))) return hipErrorInvalidValue;
+  uniform_salsa_kernel<<<grid_for(n / 8 * L), kBlock, 0, s>>>(out, q, barrett, __builtin_ctzll(n), L, seed);
   return hipGetLastError();
 }
 

@@ -363,9 +363,9 @@ int main(int argc, char** argv) {
         PHX_CHECK(hipMemcpy(hb.data(), rlk2.digit(i), hb.size() * 8, hipMemcpyDeviceToHost));
         same_key = ha == hb;
       }
-      gk.save(ctx, gs);
+      gk.save_with_elements(ctx, gs);  // fused keys: no reference format exists
       PhantomGaloisKey gk2;
-      gk2.load(ctx, gs);
+      gk2.load_with_elements(ctx, gs);
       sk.save(ctx, ss);
       PhantomSecretKey sk2 = PhantomSecretKey::load(ctx, ss);
       PhantomCiphertext rc = EvalRotateFused(ctx, c2, gk2, 1);

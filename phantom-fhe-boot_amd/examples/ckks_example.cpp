@@ -431,6 +431,67 @@ static void example_ckks_small_param() {
     if (!eq(input[i], output[i])) throw std::logic_error("error in example_ckks_small_param");
 }
 
+// PhantomGaloisKey::save / load in the reference's bytes (include/secretkey.h:195-220): the
+// context's default element list (get_elts_all: 2N - 1, then 5^(2^i), 5^(-2^i)), each key a relin
+// key record (dnum, then dnum key-level ciphertexts); parsed back field by field, reloaded, and a
+// rotation with the reloaded keys decrypts
+static void example_ckks_galois_key_layout() {
+  EncryptionParameters parms(scheme_type::ckks);
+  const size_t N = 1 << 12;
+  parms.set_poly_modulus_degree(N);
+  parms.set_special_modulus_size(2);
+  parms.set_coeff_modulus(CoeffModulus::Create(N, {60, 40, 40, 60, 60}));
+  PhantomContext context(parms);
+  PhantomSecretKey secret_key(context);
+  PhantomCKKSEncoder encoder(context);
+  PhantomGaloisKey gk = secret_key.create_galois_keys(context);
+  const std::vector<uint32_t> elts = context.key_galois_elts();
+  require(elts.size() == 1 + 2 * 11 && elts[0] == 2 * N - 1 && elts[1] == 5 && elts[3] == 25, "default element list");
+  std::stringstream ss;
+  gk.save(context, ss);
+  const std::string bytes = ss.str();
+  const size_t QP = 5, dnum = 2, ct_bytes = 58 + 2 * QP * N * 8;
+  require(bytes.size() == 8 + elts.size() * (8 + dnum * ct_bytes), "Galois key byte count");
+  auto u64_at = [&](size_t off) {
+    uint64_t v;
+    std::memcpy(&v, bytes.data() + off, 8);
+    return v;
+  };
+  require(u64_at(0) == elts.size(), "Galois key count field");
+  for (size_t k = 0; k < elts.size(); ++k) {
+    const size_t base = 8 + k * (8 + dnum * ct_bytes);
+    require(u64_at(base) == dnum, "relin key dnum field");
+    for (size_t d = 0; d < dnum; ++d) {
+      const size_t h = base + 8 + d * ct_bytes;
+      require(u64_at(h) == 0 && u64_at(h + 8) == 2 && u64_at(h + 16) == N && u64_at(h + 24) == QP,
+              "key digit header (chain 0, size 2, N, size_QP)");
+      std::vector<uint64_t> dev(2 * QP * N);
+      PHX_CHECK(hipMemcpy(dev.data(), gk.get(elts[k]).digit(d), dev.size() * 8, hipMemcpyDeviceToHost));
+      require(std::memcmp(dev.data(), bytes.data() + h + 58, dev.size() * 8) == 0, "key digit words");
+    }
+  }
+  PhantomGaloisKey loaded;
+  loaded.load(context, ss);
+  std::vector<cplx> x = random_msg(encoder.slot_count()), out;
+  PhantomPlaintext p;
+  encoder.encode(context, x, std::pow(2.0, 40), p);
+  PhantomCiphertext c = secret_key.encrypt_symmetric(context, p);
+  rotate_inplace(context, c, 2, loaded);
+  secret_key.decrypt(context, c, p);
+  encoder.decode(context, p, out);
+  for (size_t i = 0; i < x.size(); ++i) require(eq(out[i], x[(i + 2) % x.size()]), "rotation with reloaded Galois keys");
+  // a key set without the context's list cannot be written in the reference's format
+  PhantomGaloisKey partial = secret_key.create_galois_keys(context, {5});
+  bool threw = false;
+  try {
+    std::stringstream t;
+    partial.save(context, t);
+  } catch (const std::invalid_argument&) {
+    threw = true;
+  }
+  require(threw, "save of a partial key set must throw");
+}
+
 // 3_ckks.cu:761-818
 static EncryptionParameters params_for(int alpha, double& scale) {
   EncryptionParameters parms(scheme_type::ckks);
@@ -494,6 +555,7 @@ int main(int argc, char** argv) {
     run("ckks_api", alpha, [&] { example_ckks_api(context, scale); });
   }
   run("ckks_small_param", 1, [&] { example_ckks_small_param(); });
+  run("ckks_galois_key_layout", 2, [&] { example_ckks_galois_key_layout(); });
   std::printf("{\"done\": \"ckks_example\", \"ok\": %s}\n", all ? "true" : "false");
   return all ? 0 : 1;
 }

@@ -80,6 +80,20 @@ PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t s
   PHX_CHECK(hipStreamSynchronize(s));
 }
 
+std::vector<uint32_t> PhantomContext::key_galois_elts() const {
+  if (!params_.galois_elts().empty()) return params_.galois_elts();
+  const uint64_t m = 2 * static_cast<uint64_t>(n_);
+  std::vector<uint32_t> elts{static_cast<uint32_t>(m - 1)};
+  uint64_t pos = 5, neg = arith::inv_mod(5, m);
+  for (size_t i = 0; i + 1 < static_cast<size_t>(arith::log2_exact(n_)); ++i) {
+    elts.push_back(static_cast<uint32_t>(pos));
+    pos = pos * pos & (m - 1);
+    elts.push_back(static_cast<uint32_t>(neg));
+    neg = neg * neg & (m - 1);
+  }
+  return elts;
+}
+
 const uint32_t* PhantomContext::galois_perm(uint32_t elt) const {
   std::lock_guard<std::mutex> lk(cache_mu_);
   auto it = perms_.find(elt);

@@ -160,6 +160,10 @@ class PhantomContext {
   // NTT-form polynomial (PrecomputeAutoMapKernel, src/util.cu:941-958; the reference rebuilds it
   // on every call).  Built once per context, so every table lives on the context's device.
   const uint32_t* galois_perm(uint32_t elt) const;
+  // the Galois element list keys are indexed by (the reference's key_galois_tool_->galois_elts(),
+  // src/context.cu:231): the parameters' list, or when none was set PhantomGaloisTool::get_elts_all
+  // (src/galois.cu:41-65): 2N - 1, then 5^(2^i) and 5^(-2^i) for i < log2(N) - 1
+  std::vector<uint32_t> key_galois_elts() const;
   // its block inverse: source block sb (min(n, phx::kGaloisBlock) consecutive indices) is read by
   // output block galois_block_inv(elt)[sb] (n / min(n, kGaloisBlock) entries)
   const uint32_t* galois_block_inv(uint32_t elt) const { return galois_perm(elt) + n_; }

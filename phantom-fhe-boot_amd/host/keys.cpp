@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
+#include <string>
 
 #include "../csrc/ckks.h"
 #include "../csrc/ntt.h"
@@ -22,51 +23,60 @@ void PhantomKSwitchKey::adopt(std::vector<DeviceBuffer<uint64_t>>&& digits, hipS
 }
 
 void PhantomKSwitchKey::save(const PhantomContext& ctx, std::ostream& os) const {
-  const uint64_t dnum = digits_.size(), n = ctx.poly_degree(), QP = ctx.size_QP();
-  os.write(reinterpret_cast<const char*>(&dnum), sizeof(dnum));
-  std::vector<uint64_t> h(2 * QP * n);
-  for (const auto& d : digits_) {
-    PHX_CHECK(hipMemcpyAsync(h.data(), d.get(), h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx.stream()));
-    PHX_CHECK(hipStreamSynchronize(ctx.stream()));
-    ser::CiphertextHeader hd;
-    hd.chain_index = 0;
-    hd.size = 2;
-    hd.poly_modulus_degree = n;
-    hd.coeff_modulus_size = QP;
-    ser::write_ciphertext(os, hd, h.data());
+  const uint64_t n = ctx.poly_degree(), QP = ctx.size_QP();
+  std::vector<std::vector<uint64_t>> h(digits_.size(), std::vector<uint64_t>(2 * QP * n));
+  std::vector<const uint64_t*> ptrs;
+  for (size_t i = 0; i < digits_.size(); ++i) {
+    PHX_CHECK(hipMemcpyAsync(h[i].data(), digits_[i].get(), h[i].size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                             ctx.stream()));
+    ptrs.push_back(h[i].data());
   }
+  PHX_CHECK(hipStreamSynchronize(ctx.stream()));
+  ser::write_kswitch_key(os, n, QP, ptrs);
 }
 
 void PhantomKSwitchKey::load(const PhantomContext& ctx, std::istream& is) {
-  uint64_t dnum = 0;
-  is.read(reinterpret_cast<char*>(&dnum), sizeof(dnum));
-  if (!is || dnum > 64) throw std::runtime_error("bad key-switching key stream");
-  const uint64_t n = ctx.poly_degree(), QP = ctx.size_QP();
+  std::vector<std::vector<uint64_t>> v;
+  ser::read_kswitch_key(is, ctx.poly_degree(), ctx.size_QP(), v);
   std::vector<DeviceBuffer<uint64_t>> digits;
-  for (uint64_t i = 0; i < dnum; ++i) {
-    ser::CiphertextHeader hd;
-    std::vector<uint64_t> v;
-    ser::read_ciphertext(is, hd, v);
-    if (hd.size != 2 || hd.poly_modulus_degree != n || hd.coeff_modulus_size != QP)
-      throw std::invalid_argument("key-switching key does not match the context");
-    DeviceBuffer<uint64_t> d;
-    d.upload(v, ctx.stream());
-    digits.push_back(std::move(d));
+  for (const auto& d : v) {
+    DeviceBuffer<uint64_t> b;
+    b.upload(d, ctx.stream());
+    digits.push_back(std::move(b));
   }
   adopt(std::move(digits), ctx.stream());
 }
 
 void PhantomGaloisKey::save(const PhantomContext& ctx, std::ostream& os) const {
-  const uint64_t count = keys_.size();
-  os.write(reinterpret_cast<const char*>(&count), sizeof(count));
+  // the reference's layout: keys in the order of the context's Galois element list, no elements
+  const std::vector<uint32_t> elts = ctx.key_galois_elts();
+  for (uint32_t e : elts)
+    if (!has(e))
+      throw std::invalid_argument("PhantomGaloisKey lacks the key of Galois element " + std::to_string(e) +
+                                  " of the context's list (save_with_elements writes any key set)");
+  ser::write_u64(os, elts.size());
+  for (uint32_t e : elts) keys_.at(e).save(ctx, os);
+}
+
+void PhantomGaloisKey::load(const PhantomContext& ctx, std::istream& is) {
+  const std::vector<uint32_t> elts = ctx.key_galois_elts();
+  const uint64_t count = ser::read_u64(is);
+  if (count != elts.size())
+    throw std::invalid_argument("Galois key count does not match the context's Galois element list");
+  std::map<uint32_t, PhantomKSwitchKey> keys;
+  for (uint32_t e : elts) keys[e].load(ctx, is);
+  keys_ = std::move(keys);
+}
+
+void PhantomGaloisKey::save_with_elements(const PhantomContext& ctx, std::ostream& os) const {
+  ser::write_u64(os, keys_.size());
   for (const auto& kv : keys_) kv.second.save(ctx, os);
   for (const auto& kv : keys_) os.write(reinterpret_cast<const char*>(&kv.first), sizeof(uint32_t));
 }
 
-void PhantomGaloisKey::load(const PhantomContext& ctx, std::istream& is) {
-  uint64_t count = 0;
-  is.read(reinterpret_cast<char*>(&count), sizeof(count));
-  if (!is || count > (uint64_t(1) << 20)) throw std::runtime_error("bad Galois key stream");
+void PhantomGaloisKey::load_with_elements(const PhantomContext& ctx, std::istream& is) {
+  const uint64_t count = ser::read_u64(is);
+  if (count > (uint64_t(1) << 20)) throw std::runtime_error("bad Galois key stream");
   std::vector<PhantomKSwitchKey> ks(count);
   for (auto& k : ks) k.load(ctx, is);
   keys_.clear();
@@ -148,11 +158,8 @@ void sample_uniform_poly(const PhantomContext& ctx, RandomStream& rng, uint64_t*
 }
 
 void sample_uniform_seeded(const PhantomContext& ctx, const uint8_t* seed, uint64_t* dst, size_t L) {
-  phx::ChaChaKey k;
-  std::memcpy(k.k, seed, sizeof(k.k));
-  uint64_t nonce = 0;
-  for (int i = 7; i >= 0; --i) nonce = (nonce << 8) | seed[32 + i];
-  hip_ok(phx::sample_uniform(dst, ctx.mod_QP().q, ctx.mod_QP().barrett, ctx.poly_degree(), L, k, nonce, ctx.stream()),
+  hip_ok(phx::sample_uniform_seeded(dst, ctx.mod_QP().q, ctx.mod_QP().barrett, ctx.poly_degree(), L,
+                                    phx::salsa_seed(seed), ctx.stream()),
          "sample uniform (seeded)");
 }
 
@@ -286,16 +293,7 @@ PhantomGaloisKey PhantomSecretKey::create_galois_keys(const PhantomContext& ctx,
 }
 
 PhantomGaloisKey PhantomSecretKey::create_galois_keys(const PhantomContext& ctx) {
-  std::vector<uint32_t> elts = ctx.params().galois_elts();
-  if (elts.empty()) {
-    const size_t n = ctx.poly_degree();
-    for (size_t step = 1; step < n / 2; step <<= 1) {
-      elts.push_back(galois_elt_from_step(static_cast<int>(step), n));
-      elts.push_back(galois_elt_from_step(-static_cast<int>(step), n));
-    }
-    elts.push_back(static_cast<uint32_t>(2 * n - 1));
-  }
-  return create_galois_keys(ctx, elts);
+  return create_galois_keys(ctx, ctx.key_galois_elts());
 }
 
 PhantomGaloisKey PhantomSecretKey::EvalRotateKeyGen(const PhantomContext& ctx, const std::vector<int32_t>& index_list) {

@@ -58,12 +58,18 @@ class PhantomGaloisKey {
     for (auto& kv : other.keys_) keys_[kv.first] = std::move(kv.second);
     other.keys_.clear();
   }
-  // PhantomGaloisKey::save / load (include/secretkey.h:195-220): the number of keys, then each
-  // as a relin key.  The reference indexes keys by position in its galois_elts list; here the
-  // element itself is the key, so the count is followed by the elements (uint32_t each, in
-  // ascending order) after the keys
+  // PhantomGaloisKey::save / load (include/secretkey.h:195-220), the reference's bytes: the
+  // number of keys, then each as a relin key, in the order of the context's Galois element list
+  // (PhantomContext::key_galois_elts, the reference's key_galois_tool_ order), which is how the
+  // reference indexes them.  save throws std::invalid_argument if a key of that list is missing;
+  // load requires the stream's count to be the list's length.
   void save(const PhantomContext& ctx, std::ostream& os) const;
   void load(const PhantomContext& ctx, std::istream& is);
+  // any key set (e.g. the fused bootstrap keys, which the reference never serializes): the same
+  // records followed by the elements (uint32_t each, ascending)
+  void save_with_elements(const PhantomContext& ctx, std::ostream& os) const;
+  void load_with_elements(const PhantomContext& ctx, std::istream& is);
+  size_t size() const { return keys_.size(); }
 
  private:
   std::map<uint32_t, PhantomKSwitchKey> keys_;
@@ -130,9 +136,8 @@ class PhantomSecretKey {
   PhantomPublicKey gen_publickey(const PhantomContext& ctx) const;
   PhantomRelinKey gen_relinkey(const PhantomContext& ctx);
   PhantomGaloisKey create_galois_keys(const PhantomContext& ctx, const std::vector<uint32_t>& galois_elts);
-  // create_galois_keys(context) (src/secretkey.cu:534-570): the context's galois_elts, or when none
-  // were set, every rotation by +-2^i and the conjugation (PhantomGaloisTool::get_elts_all,
-  // include/galois.cuh:84-92)
+  // create_galois_keys(context) (src/secretkey.cu:532-572): keys for the context's Galois element
+  // list (PhantomContext::key_galois_elts)
   PhantomGaloisKey create_galois_keys(const PhantomContext& ctx);
   // keys for hoisted rotations (the reference's PhantomGaloisKeyFused): the key for element k
   // switches from s to s(X^(k^-1)), so the automorphism can be applied after the inner product
@@ -189,8 +194,9 @@ uint32_t galois_elt_from_step(int step, size_t n);
 // draws of a ChaCha20 stream into device polynomials over the first L limbs of Q u P
 // (the reference's sample_uniform_poly / sample_error_poly / sample_ternary_poly, src/prng.cu)
 void sample_uniform_poly(const PhantomContext& ctx, RandomStream& rng, uint64_t* dst, size_t L);
-// uniform `a` of a seed-compressed symmetric ciphertext from its public 64-byte seed: the ChaCha20
-// keystream under key = seed[0..32) and draw nonce = seed[32..40) (little endian)
+// uniform `a` of a seed-compressed symmetric ciphertext from its public 64-byte seed: the
+// reference's Salsa20 expansion (sample_uniform_poly, src/prng.cu:164-197; csrc/salsa.h), so the
+// compressed form interchanges with the reference's save_symmetric / load_symmetric
 void sample_uniform_seeded(const PhantomContext& ctx, const uint8_t* seed, uint64_t* dst, size_t L);
 // centered-binomial error, returned in NTT form
 void sample_error_poly_ntt(const PhantomContext& ctx, RandomStream& rng, uint64_t* dst, size_t L);

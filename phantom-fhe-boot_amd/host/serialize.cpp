@@ -106,6 +106,39 @@ void read_plaintext(std::istream& is, PlaintextHeader& h, std::vector<uint64_t>&
   get_words(is, data, h.words());
 }
 
+void write_u64(std::ostream& os, uint64_t v) { put(os, v); }
+
+uint64_t read_u64(std::istream& is) {
+  uint64_t v = 0;
+  get(is, v);
+  return v;
+}
+
+void write_kswitch_key(std::ostream& os, uint64_t n, uint64_t size_QP, const std::vector<const uint64_t*>& digits) {
+  put(os, static_cast<uint64_t>(digits.size()));
+  for (const uint64_t* d : digits) {
+    CiphertextHeader h;
+    h.chain_index = 0;
+    h.size = 2;
+    h.poly_modulus_degree = n;
+    h.coeff_modulus_size = size_QP;
+    write_ciphertext(os, h, d);
+  }
+}
+
+void read_kswitch_key(std::istream& is, uint64_t n, uint64_t size_QP, std::vector<std::vector<uint64_t>>& digits) {
+  uint64_t dnum = 0;
+  get(is, dnum);
+  if (dnum > 64) throw std::runtime_error("bad key-switching key stream");
+  digits.assign(dnum, {});
+  for (auto& d : digits) {
+    CiphertextHeader h;
+    read_ciphertext(is, h, d);
+    if (h.chain_index != 0 || h.size != 2 || h.poly_modulus_degree != n || h.coeff_modulus_size != size_QP)
+      throw std::invalid_argument("key-switching key does not match the context");
+  }
+}
+
 void write_secret_key(std::ostream& os, uint64_t max_power, uint64_t n, uint64_t limbs, const uint64_t* data) {
   put(os, max_power);
   put(os, n);

@@ -51,6 +51,14 @@ void read_ciphertext(std::istream& is, CiphertextHeader& h, std::vector<uint64_t
 void read_ciphertext_header(std::istream& is, CiphertextHeader& h);
 void write_plaintext(std::ostream& os, const PlaintextHeader& h, const uint64_t* data);
 void read_plaintext(std::istream& is, PlaintextHeader& h, std::vector<uint64_t>& data);
+// key-switching key (PhantomRelinKey::save, include/secretkey.h:130-141): dnum, then every digit
+// as a 2-polynomial key-level ciphertext (chain 0, size_QP limbs, scale 1, NTT form); digits[i]
+// points at [2][size_QP][n] host words
+void write_kswitch_key(std::ostream& os, uint64_t n, uint64_t size_QP, const std::vector<const uint64_t*>& digits);
+// the inverse; throws std::runtime_error / std::invalid_argument on a malformed or mismatched stream
+void read_kswitch_key(std::istream& is, uint64_t n, uint64_t size_QP, std::vector<std::vector<uint64_t>>& digits);
+void write_u64(std::ostream& os, uint64_t v);
+uint64_t read_u64(std::istream& is);
 void write_secret_key(std::ostream& os, uint64_t max_power, uint64_t n, uint64_t limbs, const uint64_t* data);
 void read_secret_key(std::istream& is, uint64_t& max_power, uint64_t& n, uint64_t& limbs, std::vector<uint64_t>& data);
 

@@ -75,6 +75,9 @@ _SIGS = {
     "phantom_eval_mod_coefficients": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp]),
     "phantom_boot_encrypt": (ctypes.c_int, [vp, vp, sz, sz, vp, sz, ctypes.POINTER(sz)]),
     "phantom_boot_output_bytes": (ctypes.c_int, [vp, ctypes.POINTER(sz)]),
+    "phantom_galois_key_serialize": (ctypes.c_int, [sz, sz, sz, sz, vp, vp, sz, vp]),
+    "phantom_salsa20_block": (ctypes.c_int, [vp, ctypes.c_uint64, vp]),
+    "phantom_sample_uniform_seeded": (ctypes.c_int, [vp, vp, vp, sz, vp]),
     "phantom_boot_layout": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_uint32,
                                            ctypes.c_uint32, sz, ctypes.POINTER(sz), ctypes.POINTER(sz),
                                            ctypes.POINTER(sz)]),

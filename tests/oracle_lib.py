@@ -13,6 +13,8 @@ ORACLE_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
 
 u64 = ctypes.c_uint64
 u64p = ctypes.POINTER(ctypes.c_uint64)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+u8p = ctypes.POINTER(ctypes.c_uint8)
 sz = ctypes.c_size_t
 
 _lib = None
@@ -47,6 +49,9 @@ def lib():
             "or_poly_mul": (None, [u64p, u64p, u64p, sz, sz, u64p]),
             "or_poly_mul_scalar": (None, [u64p, u64p, u64p, sz, sz, u64p]),
             "or_tensor_prod_2x2": (None, [u64p, u64p, u64p, sz, sz, u64p]),
+            "or_salsa20_core": (None, [u32p, u32p]),
+            "or_salsa20_block": (None, [ctypes.c_char_p, ctypes.c_uint64, u32p]),
+            "or_sample_uniform_seeded": (None, [ctypes.c_char_p, u64p, sz, sz, u64p]),
             "or_tensor_square_2x2": (None, [u64p, u64p, sz, sz, u64p]),
             "or_bconv": (None, [u64p, u64p, sz, u64p, sz, u64p, sz]),
             "or_modup": (None, [u64p, u64p, sz, u64p, sz, u64p, sz]),

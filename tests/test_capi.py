@@ -79,3 +79,73 @@ def test_numpy_chacha_matches_rfc8439_and_library():
     key = [0xDEADBEEF, 1, 2, 3, 4, 5, 6, 0xFFFFFFFF]
     for counter, nonce in [(0, 0), (7, 3), (2**32 + 5, 2**40 + 9)]:
         assert [int(x) for x in C.blocks(key, [counter], nonce)[0]] == _lib_block(key, counter, nonce)
+
+
+# ---- the reference's Salsa20 seed expansion (csrc/salsa.h, src/prng.cu:17-197) -----------------
+# The core is pinned to the example of Bernstein's Salsa20 specification (section 8: the Salsa20
+# hash of a 64-byte input); the reference's state layout and rejection sampler have no published
+# vector ("parity unpinned" beyond the core): the library and the oracle restate them separately.
+SALSA_SPEC_IN = bytes([211, 159, 13, 115, 76, 55, 82, 183, 3, 117, 222, 37, 191, 187, 234, 136, 49, 237, 179, 48, 1,
+                       106, 178, 219, 175, 199, 166, 48, 86, 16, 179, 207, 31, 240, 32, 63, 15, 83, 93, 161, 116, 147,
+                       48, 113, 238, 55, 204, 36, 79, 201, 235, 79, 3, 81, 156, 47, 203, 26, 244, 243, 88, 118, 104, 54])
+SALSA_SPEC_OUT = bytes([109, 42, 178, 168, 156, 240, 248, 238, 168, 196, 190, 203, 26, 110, 170, 154, 29, 29, 150, 26,
+                        150, 30, 235, 249, 190, 163, 251, 48, 69, 144, 51, 57, 118, 40, 152, 157, 180, 57, 27, 94, 107,
+                        42, 236, 35, 27, 111, 114, 114, 219, 236, 232, 135, 111, 155, 110, 18, 24, 232, 95, 158, 179, 19,
+                        48, 202])
+
+
+# NTT primes (= 1 mod 2^18) far from a power of two: the rejection path of the sampler is frequent
+SALSA_REJECT_PRIMES = [864691128459460609, 864691128461688833, 864691128466800641]
+
+
+def test_salsa20_core_matches_specification():
+    import ctypes
+    import numpy as np
+    import oracle_lib as O
+    inp = np.frombuffer(SALSA_SPEC_IN, dtype=np.uint32).copy()
+    out = np.zeros(16, dtype=np.uint32)
+    O.lib().or_salsa20_core(inp.ctypes.data_as(O.u32p), out.ctypes.data_as(O.u32p))
+    assert out.tobytes() == SALSA_SPEC_OUT
+    # the library's block = the core over the reference's state (seed words 0..7, nonce, 8..13)
+    lib = PA.load()
+    seed = bytes(range(64))
+    for nonce in (0, 1, 0x123456789ABCDEF):
+        got = (ctypes.c_uint32 * 16)()
+        PA.check(lib.phantom_salsa20_block(seed, nonce, got))
+        w = np.frombuffer(seed, dtype=np.uint32)
+        state = np.concatenate([w[:8], np.array([nonce & 0xFFFFFFFF, nonce >> 32], dtype=np.uint32), w[8:14]])
+        want = np.zeros(16, dtype=np.uint32)
+        O.lib().or_salsa20_core(state.ctypes.data_as(O.u32p), want.ctypes.data_as(O.u32p))
+        assert list(got) == want.tolist()
+        blk = np.zeros(16, dtype=np.uint32)
+        O.lib().or_salsa20_block(seed, nonce, blk.ctypes.data_as(O.u32p))
+        assert blk.tolist() == want.tolist()
+
+
+def test_seeded_uniform_oracle_rejects_and_reduces():
+    """or_sample_uniform_seeded (sample_uniform_poly): every value < q; with 60-bit primes words
+    above max_multiple occur with probability ((2^64 - 1) mod q + 1) / 2^64: ~2^-6 for these
+    primes 3 * 2^58 + k 2^17 + 1 (chain primes just below 2^b almost never reject), so the retry
+    path is exercised; one ordinary chain prime besides"""
+    import numpy as np
+    import oracle_lib as O
+    n = 1024
+    mods = SALSA_REJECT_PRIMES[:2] + O.coeff_modulus_create(n, [59])
+    seed = bytes((7 * i + 3) & 0xFF for i in range(64))
+    out = np.zeros(len(mods) * n, dtype=np.uint64)
+    O.lib().or_sample_uniform_seeded(seed, O.P(O.arr(mods)), n, len(mods), O.P(out))
+    for l, q in enumerate(mods):
+        assert (out[l * n:(l + 1) * n] < q).all()
+    # the first-try words, reduced: they differ from the output exactly where a retry happened
+    first = np.zeros_like(out)
+    retries = 0
+    for t in range(n // 8 * len(mods)):
+        blk = np.zeros(16, dtype=np.uint32)
+        O.lib().or_salsa20_block(seed, t, blk.ctypes.data_as(O.u32p))
+        words = blk.view(np.uint64)
+        q = mods[t // (n // 8)]
+        mm = (2**64 - 1) - (2**64 - 1) % q - 1
+        retries += int((words > np.uint64(mm)).any())
+        first[8 * t: 8 * t + 8] = words % np.uint64(q)
+    assert retries > 10
+    assert (first != out).sum() >= retries

@@ -276,3 +276,26 @@ def test_device_samplers_match_chacha20(kind):
         small = np.where(got[:n] > mods[0] // 2, got[:n].astype(np.float64) - mods[0], got[:n].astype(np.float64))
         assert np.abs(small).max() <= (21 if kind == 1 else 1)
     ctx.close()
+
+
+@pytest.mark.parametrize("log_n,which", [(12, "reject"), (16, "c4")])
+def test_sample_uniform_seeded_matches_reference_expansion(log_n, which):
+    """`a` of a seed-compressed symmetric ciphertext: the device expansion of a 64-byte seed
+    (phantom_sample_uniform_seeded, csrc/salsa.h) equals the oracle's restatement of the
+    reference's sample_uniform_poly (src/prng.cu:164-197) bit for bit — at primes where the
+    rejection path is frequent (3 * 2^58 + k 2^17 + 1) and on the C4 chain (40 limbs)."""
+    from test_capi import SALSA_REJECT_PRIMES
+    n = 1 << log_n
+    if which == "reject":
+        mods = SALSA_REJECT_PRIMES + O.coeff_modulus_create(n, [60])
+        ctx = PA.Context(n, mods, 1)
+    else:
+        mods = O.coeff_modulus_create(n, [60] + [59] * 29 + [60] * 10)
+        ctx = PA.Context(n, mods, 10)
+    L = len(mods) - (1 if which == "reject" else 0)
+    for seed in (bytes(range(64)), bytes((31 * i + 5) & 0xFF for i in range(64))):
+        dout = to_dev(np.zeros(L * n, dtype=np.uint64))
+        PA.check(_lib().phantom_sample_uniform_seeded(ctx.handle, seed, ptr(dout), L, stream()))
+        want = np.zeros(L * n, dtype=np.uint64)
+        O.lib().or_sample_uniform_seeded(seed, O.P(O.arr(mods[:L])), n, L, O.P(want))
+        assert np.array_equal(to_host(dout), want)

@@ -33,3 +33,5 @@ def test_3_ckks_examples(alpha):
     for name in EXAMPLES:
         assert got[name]["ok"] and got[name]["alpha"] == alpha, got[name]
     assert got["ckks_small_param"]["ok"], got["ckks_small_param"]
+    # PhantomGaloisKey::save / load in the reference's bytes (secretkey.h:195-220), parsed field by field
+    assert got["ckks_galois_key_layout"]["ok"], got["ckks_galois_key_layout"]

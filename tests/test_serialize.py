@@ -66,3 +66,35 @@ def test_short_buffers_are_rejected():
     # header only: parse without copying
     PA.check(lib.phantom_ciphertext_deserialize(blob, len(blob), ctypes.byref(back), None, 0, ctypes.byref(words)))
     assert words.value == data.size
+
+
+def test_galois_key_bytes_match_reference_layout():
+    """PhantomGaloisKey::save (include/secretkey.h:195-205): size_t count, then per key a
+    PhantomRelinKey record (:130-141): size_t dnum, then dnum PhantomPublicKey records, each the
+    key-level ciphertext pk_ (include/ciphertext.h:184-201) — packed here field by field."""
+    import ctypes
+    import struct
+
+    import numpy as np
+
+    import phantom_amd as PA
+    n, qp, dnum, count = 16, 3, 2, 3
+    rng = np.random.default_rng(9)
+    keys = rng.integers(0, 2**60, size=count * dnum * 2 * qp * n, dtype=np.uint64)
+    want = struct.pack("<Q", count)
+    for k in range(count):
+        want += struct.pack("<Q", dnum)
+        for d in range(dnum):
+            want += struct.pack("<QQQQdQQ??", 0, 2, n, qp, 1.0, 1, 1, True, False)
+            off = (k * dnum + d) * 2 * qp * n
+            want += keys[off: off + 2 * qp * n].tobytes()
+    lib = PA.load()
+    written = ctypes.c_size_t(0)
+    out = (ctypes.c_uint8 * len(want))()
+    PA.check(lib.phantom_galois_key_serialize(n, qp, dnum, count, keys.ctypes.data, out, len(want),
+                                              ctypes.byref(written)))
+    assert written.value == len(want) and bytes(out) == want
+    # a short buffer reports the size and fails
+    small = (ctypes.c_uint8 * 8)()
+    assert lib.phantom_galois_key_serialize(n, qp, dnum, count, keys.ctypes.data, small, 8, ctypes.byref(written)) != 0
+    assert written.value == len(want)
