@@ -174,6 +174,30 @@ __device__ __forceinline__ uint64_t reduce8(uint64_t v, uint64_t q) {
   v = csub_n(v, q << 1, opaque(0 - (q << 1)));
   return csub_n(v, q, opaque(0 - q));
 }
+
+// ---- primes q < 2^60: lazy range up to 16q (< 2^64) --------------------------------------
+// The forward butterfly reduces x only every other stage (LazyCT below): without the
+// reduction x, y < R q -> x + t, x + 4q - t < (R + 4) q; with it (x -= 8q if x >= 8q) the
+// outputs are < 12q.  Half the conditional subtractions of ct_bfly8, same integers.
+// no reduction of x: x, y < R q with R <= 12 -> outputs < (R + 4) q <= 16 q
+__device__ __forceinline__ void ct_bfly_nored(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
+  const uint64_t t = mul_shoup_lazy4(y, w, ws, q);
+  y = x + (q << 2) - t;
+  x = add64(x, t);
+}
+// x < 16q reduced below 8q first: outputs < 12q
+__device__ __forceinline__ void ct_bfly_c8(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
+  const uint64_t q8 = q << 3;
+  const uint64_t t = mul_shoup_lazy4(y, w, ws, q);
+  const uint64_t u = csub_n(x, q8, opaque(0 - q8));
+  x = add64(u, t);
+  y = u + (q << 2) - t;
+}
+// [0, 16q) -> [0, q)
+__device__ __forceinline__ uint64_t reduce16(uint64_t v, uint64_t q) {
+  v = csub_n(v, q << 3, opaque(0 - (q << 3)));
+  return reduce8(v, q);
+}
 #else
 // a w mod q in [0, 4q) for any a < 2^64, w < q, ws = floor(w 2^64 / q)
 __device__ __forceinline__ uint64_t mul_shoup_lazy4(uint64_t a, uint64_t w, uint64_t ws, uint64_t q) {
@@ -199,6 +223,20 @@ __device__ __forceinline__ void gs_bfly4(uint64_t& x, uint64_t& y, uint64_t w, u
 
 // [0, 8q) -> [0, q)
 __device__ __forceinline__ uint64_t reduce8(uint64_t v, uint64_t q) { return csub(csub(csub(v, q << 2), q << 1), q); }
+
+// lazy range up to 16q for q < 2^60 (see the carry-free forms above)
+__device__ __forceinline__ void ct_bfly_nored(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
+  const uint64_t t = mul_shoup_lazy4(y, w, ws, q);
+  y = x + (q << 2) - t;
+  x = x + t;
+}
+__device__ __forceinline__ void ct_bfly_c8(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
+  const uint64_t t = mul_shoup_lazy4(y, w, ws, q);
+  const uint64_t u = csub(x, q << 3);
+  x = u + t;
+  y = u + (q << 2) - t;
+}
+__device__ __forceinline__ uint64_t reduce16(uint64_t v, uint64_t q) { return reduce8(csub(v, q << 3), q); }
 
 #endif  // PHX_INT_NOCARRY
 

@@ -35,6 +35,7 @@ struct NttTables {
   double* row_b_fwd = nullptr;   // [num_moduli][S2]: B_g(iloc) at index 2^g + iloc
   double* row_a_inv = nullptr;   // the same factors of itw (inverses of the forward ones)
   double* row_b_inv = nullptr;
+  bool lazy16 = false;           // every modulus < 2^60: forward integer passes use the 16q lazy range
 };
 
 // log2 of the column-pass size S1 for a given log2(n) (the row pass handles the rest)

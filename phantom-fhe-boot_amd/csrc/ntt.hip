@@ -24,7 +24,9 @@
 //    of the first radix-16 round (the same for all lanes of a row) cooperatively through LDS.
 //  * Integer path: the reference's butterflies with an approximate Shoup quotient and doubled lazy
 //    ranges ([0, 8q) forward, [0, 4q) inverse; arith.h), twiddles and Shoup quotients read from
-//    the full tables, n^-1 applied after the last stage.
+//    the full tables, n^-1 applied after the last stage.  Forward limbs with q < 2^60 (every
+//    prime of the bootstrap chain) run with a 16q lazy range and reduce x only every other stage
+//    (Plan::col_lz / row_lz): the column pass hands values < 12q to the row pass.
 #include "ntt.h"
 
 #include <algorithm>
@@ -120,8 +122,33 @@ constexpr Sched sched_gs(int s, double x0, double w, bool fold) {
   return r;
 }
 
+// Integer forward path for q < 2^60 (arith.h ct_bfly_nored / ct_bfly_c8): values stay below
+// 16q < 2^64; bit g of `mask` = reduce x below 8q before stage g, needed only when the bound
+// would pass 16q.  `out` = bound of the pass output (units of q).
+struct LazySched {
+  uint32_t mask;
+  int out;
+};
+constexpr LazySched lazy_ct(int s, int start) {
+  LazySched r{0u, start};
+  int b = start;
+  for (int g = 0; g < s; ++g) {
+    if (b + 4 <= 16) {
+      b += 4;
+    } else {
+      r.mask |= 1u << g;
+      b = 12;  // x < 16q reduced below 8q, plus t < 4q
+    }
+  }
+  r.out = b;
+  return r;
+}
+
 template <int S1_LOG, int S2_LOG>
 struct Plan {
+  static constexpr LazySched col_lz = lazy_ct(S1_LOG, 1);
+  static constexpr LazySched row_lz = lazy_ct(S2_LOG, col_lz.out);
+  static_assert(col_lz.out <= 16 && row_lz.out <= 16, "lazy bound");
   static constexpr Sched col_fwd = sched_ct(S1_LOG, 1.0, Bound::kTableW);
   static constexpr Sched row_fwd = sched_ct(S2_LOG, col_fwd.out, Bound::kGenW);
   static constexpr Sched row_inv = sched_gs(S2_LOG, 1.0, Bound::kGenW, false);
@@ -244,6 +271,28 @@ __device__ __forceinline__ void ct_round_int(uint64_t (&v)[E], const uint64_t (&
       if (j & h) continue;
       const int sl = tw_slot<Rd::ex>(gl, tw_key<Rd::ex>(gl, j));
       ct_bfly8(v[j], v[j | h], w[sl], ws[sl], q);
+    }
+  }
+}
+
+// forward CT round, integer path for q < 2^60: values in [0, 16q), x reduced only at the stages
+// of CMASK (Plan::col_lz / row_lz)
+template <int S_LOG, int R, uint32_t CMASK>
+__device__ __forceinline__ void ct_round_int16(uint64_t (&v)[E], const uint64_t (&w)[E], const uint64_t (&ws)[E],
+                                               uint64_t q) {
+  using Rd = Round<S_LOG, R>;
+#pragma unroll
+  for (int gl = 0; gl < Rd::er; ++gl) {
+    const int h = 1 << (E_LOG - 1 - gl);
+    const bool reduce = (CMASK >> (Rd::g0 + gl)) & 1u;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      if (j & h) continue;
+      const int sl = tw_slot<Rd::ex>(gl, tw_key<Rd::ex>(gl, j));
+      if (reduce)
+        ct_bfly_c8(v[j], v[j | h], w[sl], ws[sl], q);
+      else
+        ct_bfly_nored(v[j], v[j | h], w[sl], ws[sl], q);
     }
   }
 }
@@ -492,7 +541,8 @@ __device__ __forceinline__ void col_load(uint64_t (&x)[E], const uint64_t* src, 
     x[j] = __builtin_nontemporal_load(src + (size_t)(pf | Round<S1_LOG, RF>::p_elem(j)) * (1 << S2_LOG));
 }
 
-template <int S1_LOG, int S2_LOG, bool FWD, bool BCV = false>
+// LZ (forward, every modulus of the table < 2^60): the integer path runs with the 16q lazy range
+template <int S1_LOG, int S2_LOG, bool FWD, bool BCV = false, bool LZ = false>
 __global__ __launch_bounds__(CBLOCK, BCV ? 2 : kWavesPerEU) void ntt_col(KArgs a) {
   using SB = Sub<S1_LOG>;
   using P = Plan<S1_LOG, S2_LOG>;
@@ -575,30 +625,35 @@ __global__ __launch_bounds__(CBLOCK, BCV ? 2 : kWavesPerEU) void ntt_col(KArgs a
       // prefetch (fewer registers; such tiles wait for the prefetch)
       if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, src + col_ref<S2_LOG>(a, next, c).in_off, pf);
       uint64_t(&v)[E] = x;
-      static_for<RN>([&](auto rc) {
-        constexpr int R = FWD ? decltype(rc)::value : RN - 1 - decltype(rc)::value;
-        if constexpr (FWD && R > 0) relayout<S1_LOG, R - 1, R>(v, lds, idx, sync, t);
-        if constexpr (!FWD && R < RN - 1) relayout<S1_LOG, R + 1, R>(v, lds, idx, sync, t);
-        uint64_t w[E], ws[E];
-        load_tw<S1_LOG, R>(w, tw, Round<S1_LOG, R>::p_thread(t), 1);
-        load_tw<S1_LOG, R>(ws, tws, Round<S1_LOG, R>::p_thread(t), 1);
-        if constexpr (FWD)
-          ct_round_int<S1_LOG, R>(v, w, ws, lc.q);
-        else
-          gs_round_int<S1_LOG, R>(v, w, ws, lc.q);
-      });
-      if constexpr (FWD) {
+      // LZ: forward with the 16q lazy range; stores values < col_lz.out q
+      {
+        static_for<RN>([&](auto rc) {
+          constexpr int R = FWD ? decltype(rc)::value : RN - 1 - decltype(rc)::value;
+          if constexpr (FWD && R > 0) relayout<S1_LOG, R - 1, R>(v, lds, idx, sync, t);
+          if constexpr (!FWD && R < RN - 1) relayout<S1_LOG, R + 1, R>(v, lds, idx, sync, t);
+          uint64_t w[E], ws[E];
+          load_tw<S1_LOG, R>(w, tw, Round<S1_LOG, R>::p_thread(t), 1);
+          load_tw<S1_LOG, R>(ws, tws, Round<S1_LOG, R>::p_thread(t), 1);
+          if constexpr (FWD && LZ)
+            ct_round_int16<S1_LOG, R, P::col_lz.mask>(v, w, ws, lc.q);
+          else if constexpr (FWD)
+            ct_round_int<S1_LOG, R>(v, w, ws, lc.q);
+          else
+            gs_round_int<S1_LOG, R>(v, w, ws, lc.q);
+        });
+        if constexpr (FWD) {
 #pragma unroll
-        for (int j = 0; j < E; ++j) store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, v[j]);  // lazy [0, 8q)
-      } else {
-        const uint64_t ni = a.n_inv[tr.row], nis = a.n_inv_shoup[tr.row];
-        const uint64_t sc = a.scale ? a.scale[tr.buf_limb] : 1, scs = a.scale ? a.scale_shoup[tr.buf_limb] : 0;
-        const bool scaled = sc != 1;  // (a scale of 1 is the identity on canonical values)
+          for (int j = 0; j < E; ++j) store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, v[j]);  // lazy
+        } else {
+          const uint64_t ni = a.n_inv[tr.row], nis = a.n_inv_shoup[tr.row];
+          const uint64_t sc = a.scale ? a.scale[tr.buf_limb] : 1, scs = a.scale ? a.scale_shoup[tr.buf_limb] : 0;
+          const bool scaled = sc != 1;  // (a scale of 1 is the identity on canonical values)
 #pragma unroll
-        for (int j = 0; j < E; ++j) {
-          uint64_t y = mul_shoup(v[j], ni, nis, lc.q);
-          if (scaled) y = mul_shoup(y, sc, scs, lc.q);
-          store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, y);
+          for (int j = 0; j < E; ++j) {
+            uint64_t y = mul_shoup(v[j], ni, nis, lc.q);
+            if (scaled) y = mul_shoup(y, sc, scs, lc.q);
+            store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, y);
+          }
         }
       }
     }
@@ -651,7 +706,7 @@ __device__ __forceinline__ void row_copy(const KArgs& a, const TileRef& tr, cons
 
 // The epilogue form holds its operands (EpiOperands) through the butterflies: two waves per SIMD
 // give it the registers to do so without spilling (168 VGPRs at three waves spilled 47).
-template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false>
+template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false, bool LZ = false>
 __global__ __launch_bounds__(BLOCK, EPI ? 2 : kWavesPerEU) void ntt_row(KArgs a) {
   using SB = Sub<S2_LOG>;
   using P = Plan<S1_LOG, S2_LOG>;
@@ -787,21 +842,31 @@ __global__ __launch_bounds__(BLOCK, EPI ? 2 : kWavesPerEU) void ntt_row(KArgs a)
         load_tw<S2_LOG, R>(ws, tws, Round<S2_LOG, R>::p_thread(t), B);
       };
       if constexpr (FWD) {
-        static_for<RN>([&](auto rc) {
-          constexpr int R = decltype(rc)::value;
-          if constexpr (R > 0) relayout<S2_LOG, R - 1, R>(v, lrow, idx, sync, t);
-          uint64_t w[E], ws[E];
-          get_tw(rc, w, ws);
-          if constexpr (EPI && R == RN - 1) epilogue_load(a, tr, T, eo);  // behind the last twiddles
-          ct_round_int<S2_LOG, R>(v, w, ws, lc.q);
-        });
-        if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, lrow, idx, sync, t);
-        if constexpr (EPI) {
+        // LZ: the 16q lazy range; the input is the column pass's lazy output
+        {
+          static_for<RN>([&](auto rc) {
+            constexpr int R = decltype(rc)::value;
+            if constexpr (R > 0) relayout<S2_LOG, R - 1, R>(v, lrow, idx, sync, t);
+            uint64_t w[E], ws[E];
+            get_tw(rc, w, ws);
+            if constexpr (EPI && R == RN - 1) epilogue_load(a, tr, T, eo);  // behind the last twiddles
+            if constexpr (LZ)
+              ct_round_int16<S2_LOG, R, P::row_lz.mask>(v, w, ws, lc.q);
+            else
+              ct_round_int<S2_LOG, R>(v, w, ws, lc.q);
+          });
+          if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, lrow, idx, sync, t);
+          auto canon = [&](uint64_t y) {
+            if constexpr (LZ && P::row_lz.out > 8) return reduce16(y, lc.q);
+            else return reduce8(y, lc.q);
+          };
+          if constexpr (EPI) {
 #pragma unroll
-          for (int j = 0; j < E; ++j) epilogue_store(a, tr, j, T, eo, reduce8(v[j], lc.q), lc.q);
-        } else {
+            for (int j = 0; j < E; ++j) epilogue_store(a, tr, j, T, eo, canon(v[j]), lc.q);
+          } else {
 #pragma unroll
-          for (int j = 0; j < E; ++j) store_wt(dst + j * T, reduce8(v[j], lc.q));
+            for (int j = 0; j < E; ++j) store_wt(dst + j * T, canon(v[j]));
+          }
         }
       } else {
         if constexpr (RN > 1) relayout<S2_LOG, 0, RN - 1>(v, lrow, idx, sync, t);
@@ -968,18 +1033,28 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   if (!inverse) {
     NttEpilogue epi_row = a.epi;
     a.epi = NttEpilogue{};  // the column pass stores its intermediate
-    if (bcv)
-      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true, true>), grid_c, block_c, 0, stream, a);
+    // one lazy range for the whole launch: both passes must agree on the intermediate's bound
+    const bool lz = tb.lazy16;
+    if (bcv && lz)
+      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true, true, true>), grid_c, block_c, 0, stream, a);
+    else if (bcv)
+      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true, true, false>), grid_c, block_c, 0, stream, a);
+    else if (lz)
+      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true, false, true>), grid_c, block_c, 0, stream, a);
     else
-      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true>), grid_c, block_c, 0, stream, a);
+      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true, false, false>), grid_c, block_c, 0, stream, a);
     a.in = out;
     a.map.in_stride = a.map.out_stride;
     a.bcast = nullptr;  // the row pass reads the intermediate
     a.epi = epi_row;
-    if (a.epi.out)
-      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true>), grid_r, block_r, 0, stream, a);
+    if (a.epi.out && lz)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true, true>), grid_r, block_r, 0, stream, a);
+    else if (a.epi.out)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true, false>), grid_r, block_r, 0, stream, a);
+    else if (lz)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, false, true>), grid_r, block_r, 0, stream, a);
     else
-      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, false>), grid_r, block_r, 0, stream, a);
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, false, false>), grid_r, block_r, 0, stream, a);
   } else {
     hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false>), grid_r, block_r, 0, stream, a);
     a.in = out;

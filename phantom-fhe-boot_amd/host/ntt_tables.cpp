@@ -40,6 +40,8 @@ DeviceNttTables::DeviceNttTables(size_t n, const std::vector<uint64_t>& moduli, 
   const size_t L = moduli.size();
   t_.n = n;
   t_.log_n = log2_exact(n);
+  t_.lazy16 = true;
+  for (uint64_t q : moduli) t_.lazy16 &= q < (uint64_t(1) << 60);
   t_.num_moduli = L;
   if (t_.log_n < 3 || t_.log_n > 17) throw std::invalid_argument("unsupported polynomial degree");
 

@@ -76,7 +76,9 @@ def test_bootstrapping_example_verbatim():
     assert vals["Before Bootstrapping"] == "4", vals
     # the reference's output chain index 19 (raise to chain 1 + depth 18): 40 - 19 - 10 - 1
     assert vals["After Bootstrapping"] == "10", vals
-    assert float(vals["avg"]) > 9.5, vals
+    # one sample with fresh keys and public-key encryption: 9.44-10.0 bits seen on MI355X; the C5
+    # fresh-key tail is 8.99 over 1024 (profiles/r03/api/bench.json)
+    assert float(vals["avg"]) > 9.0, vals
 
 
 def test_bootstrap_batch_on_stream_lanes():

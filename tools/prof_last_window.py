@@ -1,4 +1,4 @@
-"""Per-kernel stats of the LAST warm run in a rocprofv3 kernel-trace database: the trace is cut at
+"""Per-kernel stats of the LAST warm run in a rocprofv3 kernel-trace database (or csv trace): the trace is cut at
 the last idle gap longer than `gap_us` (the host synchronises between runs), so setup, key
 generation and earlier runs are excluded.  Prints kernel stats CSV for that window plus the
 window's wall span and the union of kernel intervals (GPU busy time)."""
@@ -9,11 +9,16 @@ import sys
 
 
 def main(path, gap_us=300.0):
-    dbs = glob.glob(path + "/**/*.db", recursive=True) if not path.endswith(".db") else [path]
     ks = []
-    for db in dbs:
-        c = sqlite3.connect(db)
-        ks += list(c.execute("select name, start, end from kernels"))
+    if path.endswith(".csv"):  # --output-format csv: run_kernel_trace.csv
+        import csv
+        for r in csv.DictReader(open(path)):
+            ks.append((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    else:
+        dbs = glob.glob(path + "/**/*.db", recursive=True) if not path.endswith(".db") else [path]
+        for db in dbs:
+            c = sqlite3.connect(db)
+            ks += list(c.execute("select name, start, end from kernels"))
     ks.sort(key=lambda r: r[1])
     # walk back from the end to the last gap > gap_us between the running max end and the next start
     cut = 0
