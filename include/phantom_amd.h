@@ -159,6 +159,11 @@ int phantom_moddown_from_ntt(const phantom_context *ctx, size_t chain_index, uin
  * chain_index (clobbered) -> out [polys][Ql-1][n]. */
 int phantom_moddown_modup(const phantom_context *ctx, size_t chain_index, uint64_t *cx_i, uint64_t *t_mod_up,
                           hipStream_t stream);
+/* phantom_moddown_modup over `count` independent polynomials in one launch per stage (the giant
+ * steps of one linear-transform level, src/bootstrap.cu:1335-1348): polynomial i at
+ * cx + i * cx_stride (elements, >= QlP n; clobbered), its digits at t_mod_up + i * beta * QlP * n. */
+int phantom_moddown_modup_batch(const phantom_context *ctx, size_t chain_index, uint64_t *cx, size_t count,
+                                size_t cx_stride, uint64_t *t_mod_up, hipStream_t stream);
 int phantom_moddown_rescale(const phantom_context *ctx, size_t chain_index, uint64_t *cx, uint64_t *out,
                             size_t polys, hipStream_t stream);
 /* ---- the bootstrap's own kernels (src/bootstrap.cu:1157-1405, src/evaluate.cu:2299-3940) ------

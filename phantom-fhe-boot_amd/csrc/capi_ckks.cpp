@@ -182,6 +182,15 @@ int phantom_moddown_modup(const phantom_context* ctx, size_t chain_index, uint64
   });
 }
 
+int phantom_moddown_modup_batch(const phantom_context* ctx, size_t chain_index, uint64_t* cx, size_t count,
+                                size_t cx_stride, uint64_t* t_mod_up, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (!cx || !t_mod_up || count == 0) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "empty batch");
+    tool(ctx, chain_index).moddown_modup(t_mod_up, cx, ctx->ctx->gpu_rns_tables(), stream, count, cx_stride);
+    return from_hip(hipGetLastError());
+  });
+}
+
 int phantom_moddown_rescale(const phantom_context* ctx, size_t chain_index, uint64_t* cx, uint64_t* out, size_t polys,
                             hipStream_t stream) {
   PHX_CAPI_GUARD({

@@ -87,6 +87,12 @@ struct BconvArgs {
   static constexpr int kMaxJobs = 8;
   int jobs = 1;
   int skip_step = 0;
+  // several independent batches of the same job set (the giant steps' modups): with period > 0,
+  // polynomial z runs job z % period at in + (z / period) in_outer + (z % period) in_stride (out
+  // likewise) and skips at skip_at + (z % period) skip_step; polys is a multiple of period
+  int period = 0;
+  size_t in_outer = 0;
+  size_t out_outer = 0;
   const uint64_t* job_qhat_mod_p[kMaxJobs] = {};
   const uint64_t* job_obase[kMaxJobs] = {};
   const uint64_t* job_obase_barrett[kMaxJobs] = {};
@@ -141,9 +147,12 @@ struct ModdownModupConsts {
   const uint64_t* hatinv;
   const uint64_t* hatinv_shoup;
 };
+// `polys` independent ones per launch: c1 at p c1_stride, t_mod_up at p mod_up_stride, delta and
+// t_cks contiguous [polys][size_ql][n]
 hipError_t moddown_modup_finish(const uint64_t* c1, const uint64_t* delta, const ModdownModupConsts& k,
                                 uint64_t* t_cks, uint64_t* t_mod_up, size_t n, size_t size_ql, size_t size_qlp,
-                                size_t alpha, hipStream_t s);
+                                size_t alpha, hipStream_t s, size_t polys = 1, size_t c1_stride = 0,
+                                size_t mod_up_stride = 0);
 
 // ---- automorphism ---------------------------------------------------------------------
 // apply_galois_ntt_permutation_direct (src/galois.cu:104-119): out[l][j] = in[l][perm[j]]

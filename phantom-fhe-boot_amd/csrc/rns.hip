@@ -227,7 +227,7 @@ constexpr int kBconvJ = PHX_BCONV_J;
 // the job of a multi-converter launch (BconvArgs::jobs): its matrix, output base and skip
 __device__ __forceinline__ void bconv_select_job(BconvArgs& a) {
   if (a.jobs > 1) {
-    const int d = blockIdx.z;
+    const int d = a.period ? static_cast<int>(blockIdx.z) % a.period : static_cast<int>(blockIdx.z);
     // constant indices only: a dynamic index would copy the kernel arguments to scratch
 #pragma unroll
     for (int k = 0; k < BconvArgs::kMaxJobs; ++k)
@@ -239,6 +239,19 @@ __device__ __forceinline__ void bconv_select_job(BconvArgs& a) {
         a.mfma_rows = a.job_mfma_rows[k];
       }
     a.skip_at += d * a.skip_step;
+  }
+}
+
+// blockIdx.z: polynomial (or digit; with a period, batch z / period of digit z % period)
+__device__ __forceinline__ void bconv_offsets(BconvArgs& a) {
+  const uint32_t z = blockIdx.z;
+  if (a.period) {
+    const uint32_t r = z % static_cast<uint32_t>(a.period), o = z / static_cast<uint32_t>(a.period);
+    a.in += r * a.in_stride + o * a.in_outer;
+    a.out += r * a.out_stride + o * a.out_outer;
+  } else {
+    a.in += z * a.in_stride;
+    a.out += z * a.out_stride;
   }
 }
 
@@ -279,8 +292,7 @@ __device__ __forceinline__ void bconv_inputs(const BconvArgs& a, uint64_t* tx, u
 
 __global__ __launch_bounds__(kBlock) void bconv_kernel(BconvArgs a, uint32_t n, uint32_t pairs, bool prescale) {
   bconv_select_job(a);
-  a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial (or digit)
-  a.out += blockIdx.z * a.out_stride;
+  bconv_offsets(a);
   const BconvBlock bb = bconv_block((pairs + kBlock - 1) / kBlock, (a.obase_size + kBconvJ - 1) / kBconvJ);
   const uint32_t i = bb.chunk * kBlock + threadIdx.x;
   if (i >= pairs) return;
@@ -320,8 +332,7 @@ __global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32
   __syncthreads();
   const uint32_t i = bb.chunk * kBlock + threadIdx.x;
   if (i >= pairs) return;
-  a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial (or digit)
-  a.out += blockIdx.z * a.out_stride;
+  bconv_offsets(a);
   uint32_t lo[2][IB], hi[2][IB];
   // every input load issued before any use (a branch between them would serialise them)
   u64x2 xin[IB];
@@ -425,8 +436,7 @@ void bconv_mfma_kernel(BconvArgs a, uint32_t n) {
   __shared__ uint4 row_m[NJB * 16];
   __shared__ ulonglong4 pre_c[PRE ? kBconvMfmaMaxIbase : 1];  // {q_s, qHat_s^-1, its Shoup quotient}
   bconv_select_job(a);
-  a.in += blockIdx.z * a.in_stride;  // blockIdx.z: polynomial (or digit)
-  a.out += blockIdx.z * a.out_stride;
+  bconv_offsets(a);
   const int ib = a.ibase_size, ob = a.obase_size;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t c = lane & 15, g = lane >> 4;
@@ -632,7 +642,13 @@ __global__ __launch_bounds__(kBlock) void ks_inner_kernel(const uint64_t* __rest
 __global__ __launch_bounds__(kBlock) void moddown_modup_finish_kernel(const uint64_t* c1, const uint64_t* delta,
                                                                       ModdownModupConsts k, uint64_t* t_cks,
                                                                       uint64_t* t_mod_up, uint32_t log_n, size_t pairs,
-                                                                      uint32_t alpha, size_t qlp_n) {
+                                                                      uint32_t alpha, size_t qlp_n, size_t c1_stride,
+                                                                      size_t mod_up_stride) {
+  // blockIdx.y: polynomial (c1 at y c1_stride, t_mod_up at y mod_up_stride, delta / t_cks [y][ql][n])
+  c1 += blockIdx.y * c1_stride;
+  delta += blockIdx.y * 2 * pairs;
+  t_cks += blockIdx.y * 2 * pairs;
+  t_mod_up += blockIdx.y * mod_up_stride;
   for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
     const size_t e = 2 * i;
     const uint32_t l = static_cast<uint32_t>(e >> log_n);
@@ -1102,7 +1118,9 @@ hipError_t bconv(const BconvArgs& a, size_t n, hipStream_t s) {
   if (a.ibase_size <= 0 || a.ibase_size > kMaxIbase || a.obase_size <= 0) return hipErrorInvalidValue;
   const uint32_t pairs = static_cast<uint32_t>(n / 2);
   if (a.polys < 1) return hipErrorInvalidValue;
-  if (a.jobs > 1 && (a.jobs != a.polys || a.jobs > BconvArgs::kMaxJobs)) return hipErrorInvalidValue;
+  if (a.period < 0 || (a.period && a.polys % a.period)) return hipErrorInvalidValue;
+  if (a.jobs > 1 && (a.jobs != (a.period ? a.period : a.polys) || a.jobs > BconvArgs::kMaxJobs))
+    return hipErrorInvalidValue;
   bool mfma = mfma_bconv_enabled() && a.ibase_size <= kBconvMfmaMaxIbase && a.obase_size <= kBconvMfmaMaxObase &&
               n >= 16 && n % 16 == 0 &&
               static_cast<size_t>(a.obase_size + std::max(0, a.skip_len)) * n * 8 <= kDropRow;
@@ -1168,10 +1186,12 @@ hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const*
 
 hipError_t moddown_modup_finish(const uint64_t* c1, const uint64_t* delta, const ModdownModupConsts& k,
                                 uint64_t* t_cks, uint64_t* t_mod_up, size_t n, size_t size_ql, size_t size_qlp,
-                                size_t alpha, hipStream_t s) {
+                                size_t alpha, hipStream_t s, size_t polys, size_t c1_stride, size_t mod_up_stride) {
   const size_t pairs = n * size_ql / 2;
-  moddown_modup_finish_kernel<<<grid_for(pairs), kBlock, 0, s>>>(c1, delta, k, t_cks, t_mod_up, __builtin_ctzll(n),
-                                                                 pairs, static_cast<uint32_t>(alpha), size_qlp * n);
+  if (polys < 1) return hipErrorInvalidValue;
+  moddown_modup_finish_kernel<<<poly_grid(pairs, polys), kBlock, 0, s>>>(
+      c1, delta, k, t_cks, t_mod_up, __builtin_ctzll(n), pairs, static_cast<uint32_t>(alpha), size_qlp * n, c1_stride,
+      mod_up_stride);
   return hipGetLastError();
 }
 

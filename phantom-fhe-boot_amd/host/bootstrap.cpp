@@ -482,9 +482,7 @@ const uint64_t* LeafTableCache::get(const std::vector<uint64_t>& table, hipStrea
   return it->second.get();
 }
 
-FHECKKSRNS::FHECKKSRNS(PhantomCKKSEncoder& encoder) : encoder_(encoder) {
-  if (const char* e = std::getenv("PHX_BOOT_GIANT_STREAMS")) giant_streams_ = std::max(1, std::atoi(e));
-}
+FHECKKSRNS::FHECKKSRNS(PhantomCKKSEncoder& encoder) : encoder_(encoder) {}
 
 // GetDepthByDegree (src/util.cu:44-71): the reference's Paterson-Stockmeyer depth of a degree-d
 // Chebyshev series, its affine map included
@@ -810,8 +808,15 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
     traffic::ciphertexts(traffic::limb_bytes(rt.beta() * QlP + Ql + 2 * QlP * static_cast<size_t>(lv.g), n));
   }
   digits.release();
-  // every giant step's inner sum in one launch
-  std::vector<PhantomCiphertext> inner(lv.b);
+  // every giant step's inner sum in one launch: giant 0 straight into the accumulator, giants
+  // 1 .. b-1 into one buffer [b - 1][2][QlP][n] so that their moddowns batch
+  const size_t ext_words = 2 * QlP * n;
+  const size_t G = static_cast<size_t>(lv.b - 1);
+  PhantomCiphertext acc;
+  acc.resize(2, QlP, n, s, false);
+  acc.set_chain_index(ct.chain_index());
+  acc.set_ntt_form(true);
+  DeviceBuffer<uint64_t> giants(std::max<size_t>(G, 1) * ext_words, s);
   phx::LtArgs la;
   la.g = lv.g;
   la.b = lv.b;
@@ -822,13 +827,8 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
   la.q = cc.mod_QP().q;
   la.barrett = cc.mod_QP().barrett;
   for (int j = 0; j < lv.g; ++j) la.baby[j] = babies.get() + static_cast<size_t>(j) * baby_words;
-  for (int i = 0; i < lv.b; ++i) {
-    inner[i].resize(2, QlP, n, s, false);
-    inner[i].set_chain_index(ct.chain_index());
-    inner[i].set_scale(ct.scale() * sf_.at(lv.chain - 1));
-    inner[i].SetNoiseScaleDeg(2);
-    la.out[i] = inner[i].data();
-  }
+  la.out[0] = acc.data();
+  for (size_t i = 1; i <= G; ++i) la.out[i] = giants.get() + (i - 1) * ext_words;
   hip_ok(phx::lt_bsgs(la, n, s), "linear transform inner products");
   {
     // the level's non-zero diagonals read once; the baby steps read and the inner sums written
@@ -839,26 +839,21 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
     traffic::ciphertexts(traffic::limb_bytes(2 * QlP * static_cast<size_t>(lv.g + lv.b), n));
   }
   babies.release();
-  // giant steps accumulate in the extended basis (one moddown at the end), spread over the
-  // context's streams (giant i on chain i mod k); inner[] (main-stream buffers) lives until all
-  // chains have joined
-  const int k = std::max(1, std::min(giant_streams_, lv.b));
-  std::vector<PhantomCiphertext> part(k);
-  part[0] = std::move(inner[0]);
-  run_parallel(cc, k, [&](int t) {
-    bool have = t == 0;
-    for (int i = t == 0 ? k : t; i < lv.b; i += k) {
-      EvalRotateExtAccumulate(cc, inner[i], galois_keys_, static_cast<int>(static_cast<long>(lv.g) * i * lv.stride),
-                              part[t], have);
-      have = true;
-    }
-  });
-  PhantomCiphertext acc = std::move(part[0]);
-  for (int t = 1; t < k; ++t) {
-    part[t].retag(s);
-    if (part[t].size()) EvalAddExtInPlace(cc, acc, part[t]);
+  if (G > 0) {
+    // giant steps accumulate in the extended basis (one moddown at the end).  Their c1's come down
+    // to Ql and into their modup digits in one batched pass (one launch per stage over all G,
+    // instead of G chains of small launches on concurrent streams, which a single launch over
+    // the same limbs beats: profiles/r03/giant_batch/), then each key switch + rotation adds into
+    // acc in turn
+    const RnsTool& rt = cc.get_context_data(ct.chain_index()).gpu_rns_tool();
+    const size_t dwords = rt.beta() * QlP * n;
+    DeviceBuffer<uint64_t> digits(G * dwords, s);
+    rt.moddown_modup(digits.get(), giants.get() + QlP * n, cc.gpu_rns_tables(), s, G, ext_words);
+    for (size_t i = 1; i <= G; ++i)
+      EvalRotateExtAccumulateDigits(cc, ct.chain_index(), giants.get() + (i - 1) * ext_words,
+                                    digits.get() + (i - 1) * dwords, galois_keys_,
+                                    static_cast<int>(static_cast<long>(lv.g) * static_cast<long>(i) * lv.stride), acc);
   }
-  inner.clear();
   acc.set_scale(ct.scale() * sf_.at(lv.chain - 1));
   acc.SetNoiseScaleDeg(2);
   // giant steps: each inner sum read once, the level's result written once
@@ -1053,14 +1048,23 @@ PhantomCiphertext FHECKKSRNS::bootstrap_once(const PhantomCiphertext& in, const 
     // launches that leave most of the GPU idle on their own)
     // enc_i (allocated on the main stream) stays alive until the main stream has joined
     PhantomCiphertext im;
-    run_parallel(cc, 2, [&](int t) {
+    auto half = [&](int t) {
       if (t == 0) {
         enc = eval_mod(enc, cc);
       } else {
         im = eval_mod(enc_i, cc);
         MultByMonomialInPlace(cc, im, M / 4);  // times i
       }
-    });
+    };
+    // PHX_EVALMOD_SERIAL=1: the halves one after the other on the main stream (measurement aid)
+    static const bool serial = std::getenv("PHX_EVALMOD_SERIAL") != nullptr;
+    if (serial) {
+      half(0);
+      trace(cc, "evalmod-re", enc);
+      half(1);
+    } else {
+      run_parallel(cc, 2, half);
+    }
     im.retag(cc.stream());
     trace(cc, "evalmod", enc);
     EvalAddAutoInplace(cc, enc, im, sf_);

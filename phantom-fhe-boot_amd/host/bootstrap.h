@@ -164,7 +164,6 @@ class FHECKKSRNS {
   size_t raise_level_ = 0;  // the level ModRaise lands on (reference layout: the spare level)
   std::map<uint32_t, Precom> precom_;
   std::vector<double> cheb_;
-  int giant_streams_ = 3;  // PHX_BOOT_GIANT_STREAMS: concurrent giant-step chains per level (profiles/r01/giant_streams_sweep.txt)
   mutable LeafTableCache leaf_tables_;
   // per linear-transform level: the device table of its baby steps (phx::KsBatchEntry as raw
   // words) and the host copy it was uploaded from (re-uploaded when keys or tables move)

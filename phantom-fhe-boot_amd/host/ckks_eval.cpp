@@ -481,6 +481,29 @@ PhantomCiphertext EvalFastAutomorphismExt(const PhantomContext& ctx, const Phant
   return out;
 }
 
+// inner product, + c0 (P-scaled, extended basis), permutation and accumulation in one pass
+static void rotate_ext_accumulate(const PhantomContext& ctx, const RnsTool& rt, const uint64_t* c0,
+                                  const uint64_t* digits, const PhantomGaloisKey& keys, uint32_t elt,
+                                  PhantomCiphertext& acc, bool accumulate) {
+  const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P();
+  phx::KsRotateArgs g;
+  g.digits = digits;
+  g.evk = keys.get(elt).public_keys_ptr();
+  g.qp = ctx.mod_QP().q;
+  g.qp_barrett = ctx.mod_QP().barrett;
+  g.c0 = c0;
+  g.out = acc.data();
+  g.perm = ctx.galois_perm(elt);
+  g.ql = static_cast<uint32_t>(Ql);
+  g.qlp = static_cast<uint32_t>(QlP);
+  g.size_q = static_cast<uint32_t>(ctx.size_Q());
+  g.size_p = static_cast<uint32_t>(ctx.size_P());
+  g.beta = static_cast<uint32_t>(rt.beta());
+  g.accumulate = accumulate;
+  hip_ok(phx::keyswitch_rotate(g, 2, n, ctx.stream()), "giant step key switch + permute + accumulate");
+  traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP, n));
+}
+
 void EvalRotateExtAccumulate(const PhantomContext& ctx, PhantomCiphertext& ext, const PhantomGaloisKey& keys,
                              int index, PhantomCiphertext& acc, bool accumulate) {
   const RnsTool& rt = ctx.get_context_data(ext.chain_index()).gpu_rns_tool();
@@ -499,23 +522,17 @@ void EvalRotateExtAccumulate(const PhantomContext& ctx, PhantomCiphertext& ext, 
     acc.SetNoiseScaleDeg(ext.GetNoiseScaleDeg());
     acc.set_ntt_form(true);
   }
-  // inner product, + c0 (P-scaled, extended basis), permutation and accumulation in one pass
-  phx::KsRotateArgs g;
-  g.digits = digits.get();
-  g.evk = keys.get(elt).public_keys_ptr();
-  g.qp = ctx.mod_QP().q;
-  g.qp_barrett = ctx.mod_QP().barrett;
-  g.c0 = ext.data();
-  g.out = acc.data();
-  g.perm = ctx.galois_perm(elt);
-  g.ql = static_cast<uint32_t>(Ql);
-  g.qlp = static_cast<uint32_t>(QlP);
-  g.size_q = static_cast<uint32_t>(ctx.size_Q());
-  g.size_p = static_cast<uint32_t>(ctx.size_P());
-  g.beta = static_cast<uint32_t>(rt.beta());
-  g.accumulate = accumulate;
-  hip_ok(phx::keyswitch_rotate(g, 2, n, s), "giant step key switch + permute + accumulate");
-  traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP, n));
+  rotate_ext_accumulate(ctx, rt, ext.data(), digits.get(), keys, elt, acc, accumulate);
+}
+
+void EvalRotateExtAccumulateDigits(const PhantomContext& ctx, size_t chain, const uint64_t* c0,
+                                   const uint64_t* digits, const PhantomGaloisKey& keys, int index,
+                                   PhantomCiphertext& acc) {
+  const RnsTool& rt = ctx.get_context_data(chain).gpu_rns_tool();
+  if (acc.size() != 2 || acc.coeff_modulus_size() != rt.size_Ql() + ctx.size_P())
+    throw std::invalid_argument("not an extended-basis accumulator");
+  rotate_ext_accumulate(ctx, rt, c0, digits, keys, FindAutomorphismIndex2nComplex(index, ctx.poly_degree()), acc,
+                        true);
 }
 
 PhantomCiphertext EvalFastRotationExt(const PhantomContext& ctx, const PhantomCiphertext& ct,

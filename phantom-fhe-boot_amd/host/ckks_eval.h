@@ -119,6 +119,12 @@ PhantomCiphertext EvalFastAutomorphismExt(const PhantomContext& ctx, const Phant
 // accumulate = false initialises acc.
 void EvalRotateExtAccumulate(const PhantomContext& ctx, PhantomCiphertext& ext, const PhantomGaloisKey& fused_keys,
                              int index, PhantomCiphertext& acc, bool accumulate);
+// its key switch alone, from digits already computed (RnsTool::moddown_modup of c1, batched over
+// the giant steps of a level): acc (+)= rotation of (c0 + KeySwitch(digits)); c0 [QlP][n] is the
+// extended ciphertext's first polynomial at chain index `chain`.  acc must be initialised.
+void EvalRotateExtAccumulateDigits(const PhantomContext& ctx, size_t chain, const uint64_t* c0,
+                                   const uint64_t* digits, const PhantomGaloisKey& fused_keys, int index,
+                                   PhantomCiphertext& acc);
 // KeySwitchExt: (c0, c1) -> P * (c0, c1) in the extended basis
 PhantomCiphertext KeySwitchExt(const PhantomContext& ctx, const PhantomCiphertext& ct);
 // KeySwitchDown: extended -> Ql (moddown of both polynomials); `ext` is consumed (its P limbs

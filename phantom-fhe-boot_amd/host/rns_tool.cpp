@@ -180,18 +180,24 @@ bool RnsTool::fused_bconv_ok(size_t ibase) const {
 // every digit's conversion to its complement of QlP (digit b: t_cks limbs [b alpha, b alpha + part)
 // -> t_mod_up[b], skipping the digit's own limbs); the full digits in one launch (one converter
 // per blockIdx.z), a short last digit apart
-void RnsTool::digit_bconv(const uint64_t* t_cks, uint64_t* t_mod_up, hipStream_t s) const {
-  const size_t size_QlP = base_Ql_.size() + size_P_, alpha = size_P_, beta = converters_.size();
+void RnsTool::digit_bconv(const uint64_t* t_cks, uint64_t* t_mod_up, hipStream_t s, size_t count) const {
+  const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_, alpha = size_P_, beta = converters_.size();
   const size_t full = digit_size_.back() == alpha ? beta : beta - 1;
   for (size_t b0 = 0; b0 < full; b0 += phx::BconvArgs::kMaxJobs) {
     const size_t cnt = std::min<size_t>(phx::BconvArgs::kMaxJobs, full - b0);
     phx::BconvArgs a = converters_[b0].args(t_cks + digit_start_[b0] * n_, t_mod_up + b0 * size_QlP * n_, false);
     a.skip_at = (int)digit_start_[b0];
     a.skip_len = (int)alpha;
-    a.polys = a.jobs = (int)cnt;
+    a.jobs = (int)cnt;
+    a.polys = (int)(cnt * count);
     a.in_stride = alpha * n_;
     a.out_stride = size_QlP * n_;
     a.skip_step = (int)alpha;
+    if (count > 1) {
+      a.period = (int)cnt;
+      a.in_outer = size_Ql * n_;
+      a.out_outer = beta * size_QlP * n_;
+    }
     for (size_t d = 0; d < cnt; ++d) {
       const DeviceBaseConverter& c = converters_[b0 + d];
       a.job_qhat_mod_p[d] = c.d_qhat_mod_p.get();
@@ -206,6 +212,9 @@ void RnsTool::digit_bconv(const uint64_t* t_cks, uint64_t* t_mod_up, hipStream_t
     phx::BconvArgs a = converters_[full].args(t_cks + digit_start_[full] * n_, t_mod_up + full * size_QlP * n_, false);
     a.skip_at = (int)digit_start_[full];
     a.skip_len = (int)digit_size_[full];
+    a.polys = (int)count;
+    a.in_stride = size_Ql * n_;
+    a.out_stride = beta * size_QlP * n_;
     hip_ok(phx::bconv(a, n_, s), "digit bconv (short digit)");
   }
 }
@@ -317,24 +326,34 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
   hip_ok(phx::ntt_forward_fused(ntt, delta, delta, dm, nullptr, 0, epi, s), "moddown NTT + finish");
 }
 
-void RnsTool::moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTables& ntt, hipStream_t s) const {
-  const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_, alpha = size_P_;
+void RnsTool::moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTables& ntt, hipStream_t s, size_t count,
+                            size_t c1_stride) const {
+  const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_, alpha = size_P_, beta = converters_.size();
   if (size_P_ == 0) throw std::invalid_argument("no special primes");
+  if (count < 1 || (count > 1 && c1_stride < size_QlP * n_)) throw std::invalid_argument("moddown_modup: bad batch");
+  const int nc = static_cast<int>(count);
   phx::LimbMap all;
   all.num_limbs = (int)size_QlP;
   all.split = (int)size_Ql;
   all.first_a = 0;
   all.first_b = (int)size_Q_;
-  hip_ok(phx::ntt_inverse(ntt, c1, c1, all, d_mm_scale_.get(), d_mm_scale_shoup_.get(), s), "moddown-modup INTT");
-  uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, size_Ql * n_);
-  hip_ok(phx::bconv(p_to_ql_.args(c1 + size_Ql * n_, delta, false), n_, s), "moddown-modup bconv P");
-  uint64_t* t_cks = ws_->get(s, Workspace::kModupInv, size_Ql * n_);
+  hip_ok(phx::ntt_inverse(ntt, c1, c1, all.batched(nc, c1_stride, c1_stride), d_mm_scale_.get(),
+                          d_mm_scale_shoup_.get(), s),
+         "moddown-modup INTT");
+  uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, count * size_Ql * n_);
+  phx::BconvArgs ba = p_to_ql_.args(c1 + size_Ql * n_, delta, false);
+  ba.polys = nc;
+  ba.in_stride = c1_stride;
+  ba.out_stride = size_Ql * n_;
+  hip_ok(phx::bconv(ba, n_, s), "moddown-modup bconv P");
+  uint64_t* t_cks = ws_->get(s, Workspace::kModupInv, count * size_Ql * n_);
   phx::ModdownModupConsts k{d_Ql_.get(), d_bigPInv_mod_q_.get(), d_bigPInv_mod_q_shoup_.get(), d_partQlHatInv_.get(),
                             d_partQlHatInv_shoup_.get()};
-  hip_ok(phx::moddown_modup_finish(c1, delta, k, t_cks, t_mod_up, n_, size_Ql, size_QlP, alpha, s),
+  hip_ok(phx::moddown_modup_finish(c1, delta, k, t_cks, t_mod_up, n_, size_Ql, size_QlP, alpha, s, count, c1_stride,
+                                   beta * size_QlP * n_),
          "moddown-modup finish");
-  digit_bconv(t_cks, t_mod_up, s);
-  hip_ok(phx::ntt_forward(ntt, t_mod_up, t_mod_up, all.batched((int)converters_.size()), s), "moddown-modup NTT");
+  digit_bconv(t_cks, t_mod_up, s, count);
+  hip_ok(phx::ntt_forward(ntt, t_mod_up, t_mod_up, all.batched(nc * (int)beta), s), "moddown-modup NTT");
 }
 
 void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables& ntt, hipStream_t s,

@@ -54,7 +54,10 @@ class RnsTool {
   // [beta][size_QlP][n] = modup(round(c1 / P)).  The subtraction happens in the coefficient
   // domain: one INTT over Ql u P and one NTT over every digit replace moddown's INTT(P) + NTT(Ql)
   // and modup's INTT(Ql) + NTT(digits).  c1 is clobbered.
-  void moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTables& ntt, hipStream_t s) const;
+  // `count` independent ones in one launch per stage (the giant steps of a linear-transform
+  // level): c1 of job i at c1 + i c1_stride, its digits at t_mod_up + i beta QlP n
+  void moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTables& ntt, hipStream_t s, size_t count = 1,
+                     size_t c1_stride = 0) const;
   // moddown fused with the following rescale: cx [polys][size_QlP][n] NTT form holds P x (a
   // ciphertext at this level, scale S); out [polys][size_Ql - 1][n] = round(cx / (P q_last)),
   // the ciphertext rescaled to the next level (scale S / q_last).  One INTT over the 1 + size_P
@@ -89,7 +92,8 @@ class RnsTool {
   // the base conversion can run as the forward NTT's column-pass prologue (ntt.h BconvPrologue):
   // 2-D transform sizes and at most 15 input limbs; opt-in (PHX_FUSED_BCONV=1), see rns_tool.cpp
   bool fused_bconv_ok(size_t ibase) const;
-  void digit_bconv(const uint64_t* t_cks, uint64_t* t_mod_up, hipStream_t s) const;
+  // `count` batches: t_cks [count][Ql][n] -> t_mod_up [count][beta][QlP][n]
+  void digit_bconv(const uint64_t* t_cks, uint64_t* t_mod_up, hipStream_t s, size_t count = 1) const;
   std::vector<DeviceBaseConverter> converters_;  // digit beta: part -> complement of QlP
   std::vector<size_t> digit_start_, digit_size_;
   DeviceBaseConverter p_to_ql_;

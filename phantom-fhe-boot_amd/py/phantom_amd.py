@@ -46,6 +46,7 @@ _SIGS = {
     "phantom_moddown_from_ntt": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_fast_bconv": (ctypes.c_int, [u64p, sz, u64p, sz, vp, vp, sz, ctypes.c_int, vp]),
     "phantom_moddown_modup": (ctypes.c_int, [vp, sz, vp, vp, vp]),
+    "phantom_moddown_modup_batch": (ctypes.c_int, [vp, sz, vp, sz, sz, vp, vp]),
     "phantom_ciphertext_serialize": (ctypes.c_int, [vp, vp, vp, sz, vp]),
     "phantom_ciphertext_deserialize": (ctypes.c_int, [vp, sz, vp, vp, sz, vp]),
     "phantom_moddown_rescale": (ctypes.c_int, [vp, sz, vp, vp, sz, vp]),

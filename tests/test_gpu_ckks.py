@@ -155,6 +155,30 @@ def test_moddown_modup_fused(request, rng, fixture, chain):
     assert np.array_equal(to_host(dout), want)
 
 
+@pytest.mark.parametrize("fixture,chain", [("c3", 1), ("c3", 30), ("small", 2), ("small", 5)])
+def test_moddown_modup_batch(request, rng, fixture, chain):
+    """The giant steps' batched moddown∘modup (3 polynomials at a padded stride, full and short
+    digits) equals modup(moddown(cx_i)) of each polynomial bit for bit."""
+    ctx = request.getfixturevalue(fixture)
+    ql, p = ctx.ql(chain), ctx.moduli[ctx.size_Q:]
+    qlp = len(ql) + len(p)
+    beta, count, stride = -(-len(ql) // ctx.size_P), 3, 2 * (len(ql) + len(p)) * ctx.n
+    cxs = [O.random_limbs(rng, ctx.n, ql + p) for _ in range(count)]
+    buf = np.zeros(count * stride, dtype=np.uint64)
+    for i, cx in enumerate(cxs):
+        buf[i * stride:i * stride + cx.size] = cx
+    d = to_dev(buf)
+    dout = to_dev(np.zeros(count * beta * qlp * ctx.n, dtype=np.uint64))
+    PA.check(_lib().phantom_moddown_modup_batch(ctx.handle, chain, ptr(d), count, stride, ptr(dout), stream()))
+    got = to_host(dout).reshape(count, -1)
+    for i, cx in enumerate(cxs):
+        down = np.zeros(len(ql) * ctx.n, dtype=np.uint64)
+        O.lib().or_moddown_from_ntt(O.P(cx.copy()), O.P(down), ctx.n, O.P(O.arr(ql)), len(ql), O.P(O.arr(p)), len(p))
+        want = np.zeros(beta * qlp * ctx.n, dtype=np.uint64)
+        O.lib().or_modup(O.P(down), O.P(want), ctx.n, O.P(O.arr(ql)), len(ql), O.P(O.arr(p)), len(p))
+        assert np.array_equal(got[i], want), i
+
+
 @pytest.mark.parametrize("fixture,chain", [("c3", 1), ("c3", 30), ("small", 1), ("small", 5)])
 def test_moddown_rescale_fused(request, rng, fixture, chain):
     """moddown + rescale as one division by P q_last = moddown_from_NTT with {q_last} u P as the
