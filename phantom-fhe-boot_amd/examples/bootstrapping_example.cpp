@@ -388,7 +388,28 @@ int main(int argc, char** argv) {
 
   FHECKKSRNS boot(enc);
   t0 = now_ms();
-  boot.EvalBootstrapSetup(ctx, levelBudget, scale, sf);
+  if (mode == "deferred") {
+    // the reference's argument list (bootstrap.cu:15-18) with precompute = false: the level
+    // structure now, the linear-transform plaintexts at the first EvalBootstrap.  A
+    // scalingFactorsRealBig that is not the squares of scalingFactorsReal is refused.
+    std::vector<double> sf_big(sf.size() - 1);
+    for (size_t k = 0; k < sf_big.size(); ++k) sf_big[k] = sf[k] * sf[k];
+    bool threw = false;
+    try {
+      std::vector<double> bad = sf_big;
+      bad[3] *= 1.5;
+      FHECKKSRNS b2(enc);
+      b2.EvalBootstrapSetup(ctx, levelBudget, scale, sf, bad);
+    } catch (const std::invalid_argument&) {
+      threw = true;
+    }
+    report("sf_big_mismatch_refused", threw ? 0.0 : 1.0, 0.5, 0);
+    boot.EvalBootstrapSetup(ctx, levelBudget, scale, sf, sf_big, {0, 0}, 0, 0, false);
+    report("deferred_not_encoded", boot.precomputed() ? 1.0 : 0.0, 0.5, 0);
+    report("sf_big_kept", boot.scaling_factors_big() == sf_big ? 0.0 : 1.0, 0.5, 0);
+  } else {
+    boot.EvalBootstrapSetup(ctx, levelBudget, scale, sf);
+  }
   PHX_CHECK(hipDeviceSynchronize());
   const double setup_ms = now_ms() - t0;
   t0 = now_ms();
@@ -462,6 +483,7 @@ int main(int argc, char** argv) {
               ct.chain_index(), out.chain_index(),
               levels_after, (unsigned long long)tk, (unsigned long long)tp, (unsigned long long)tc);
   g_ok &= bits_avg > 9.85;
+  if (mode == "deferred") report("deferred_encoded_by_bootstrap", boot.precomputed() ? 0.0 : 1.0, 0.5, out.chain_index());
   std::printf("{\"done\": \"boot\", \"ok\": %s}\n", g_ok ? "true" : "false");
   return g_ok ? 0 : 1;
 }

@@ -503,9 +503,12 @@ uint32_t FHECKKSRNS::GetBootstrapDepthTight(const std::vector<uint32_t>& levelBu
   return levelBudget.at(0) + levelBudget.at(1) + static_cast<uint32_t>(cheb_depth(kChebDegree)) + R_UNIFORM;
 }
 
-void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const std::vector<int>& sizes,
-                              double constant, size_t first_chain, uint32_t slots, uint32_t dim1,
-                              std::vector<LTLevel>& out) const {
+void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const LevelArgs& args, uint32_t slots,
+                              std::vector<LTLevel>& out, bool encode) const {
+  const std::vector<int>& sizes = args.sizes;
+  const double constant = args.constant;
+  const size_t first_chain = args.first_chain;
+  const uint32_t dim1 = args.dim1;
   const size_t n = cc.poly_degree() / 2;  // slots of the ring
   const size_t ns = slots;                // slots of the (sub)problem: n = full packing
   const int logslots = arith::log2_exact(ns);
@@ -572,6 +575,11 @@ void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const s
     }
     lv.b = (lv.D + lv.g - 1) / lv.g;
     lv.chain = first_chain + gi;
+    if (lv.g > phx::kLtMaxG || lv.b > phx::kLtMaxB) throw std::invalid_argument("linear transform level too large");
+    if (!encode) {
+      out.push_back(std::move(lv));
+      continue;
+    }
     const double scale = sf_.at(lv.chain - 1);
     lv.pts.resize(lv.D);
     // the level's diagonals: their host encodings (FFT + exact RNS rounding) run on host threads,
@@ -622,7 +630,6 @@ void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const s
       ptrs[u] = lv.zero.get();
     }
     lv.d_pts.upload(ptrs, cc.stream());
-    if (lv.g > phx::kLtMaxG || lv.b > phx::kLtMaxB) throw std::invalid_argument("linear transform level too large");
     out.push_back(std::move(lv));
   }
 }
@@ -631,6 +638,38 @@ void FHECKKSRNS::EvalBootstrapSetup(const PhantomContext& cc, const std::vector<
                                     const std::vector<double>& sf, uint32_t correctionFactor, uint32_t slots_in,
                                     const std::vector<uint32_t>& dim1) {
   (void)scale;
+  sf_big_.assign(sf.empty() ? 0 : sf.size() - 1, 0.0);
+  for (size_t k = 0; k < sf_big_.size(); ++k) sf_big_[k] = sf[k] * sf[k];
+  setup(cc, levelBudget, sf, correctionFactor, slots_in, dim1, true);
+}
+
+void FHECKKSRNS::EvalBootstrapSetup(const PhantomContext& cc, const std::vector<uint32_t>& levelBudget, double scale,
+                                    const std::vector<double>& sf, const std::vector<double>& sf_big,
+                                    const std::vector<uint32_t>& dim1, uint32_t slots, uint32_t correctionFactor,
+                                    bool precompute) {
+  (void)scale;
+  // FLEXIBLEAUTO: m_scalingFactorsRealBig[k] = m_scalingFactorsReal[k]^2 (ciphertext.h:357-365)
+  if (sf.empty() || sf_big.size() + 1 != sf.size())
+    throw std::invalid_argument("EvalBootstrapSetup: scalingFactorsRealBig must have one entry less than scalingFactorsReal");
+  for (size_t k = 0; k < sf_big.size(); ++k) {
+    const double want = sf[k] * sf[k];
+    if (!(std::fabs(sf_big[k] - want) <= 1e-12 * want))
+      throw std::invalid_argument("EvalBootstrapSetup: scalingFactorsRealBig[" + std::to_string(k) +
+                                  "] is not scalingFactorsReal[" + std::to_string(k) + "]^2 (FLEXIBLEAUTO)");
+  }
+  sf_big_ = sf_big;
+  setup(cc, levelBudget, sf, correctionFactor, slots, dim1, precompute);
+}
+
+bool FHECKKSRNS::precomputed(uint32_t numSlots) const {
+  std::lock_guard<std::mutex> lk(precom_mu_);
+  auto it = precom_.find(numSlots ? numSlots : static_cast<uint32_t>(encoder_.slot_count()));
+  return it != precom_.end() && it->second.encoded;
+}
+
+void FHECKKSRNS::setup(const PhantomContext& cc, const std::vector<uint32_t>& levelBudget,
+                       const std::vector<double>& sf, uint32_t correctionFactor, uint32_t slots_in,
+                       const std::vector<uint32_t>& dim1, bool precompute) {
   sf_ = sf;
   budget_ = levelBudget;
   const size_t N = cc.poly_degree();
@@ -669,23 +708,39 @@ void FHECKKSRNS::EvalBootstrapSetup(const PhantomContext& cc, const std::vector<
   pc.slots = slots;
   // CoeffToSlot: slots become (t_lo + i t_hi) / (2 q0 K) (the conjugate split doubles them)
   const double s_raise = sf_.at(raise_level_);
-  build_levels(cc, true, enc_sizes, s_raise / (2.0 * gap * q0 * K_UNIFORM), 1 + raise_level_, slots,
-               dim1.size() > 0 ? dim1[0] : 0, pc.enc);
+  pc.enc_args = {enc_sizes, s_raise / (2.0 * gap * q0 * K_UNIFORM), 1 + raise_level_, dim1.size() > 0 ? dim1[0] : 0};
   // SlotToCoeff: from (t0_lo + i t0_hi) / q0 back to the message at the raise scale
-  build_levels(cc, false, dec_sizes, q0 / s_raise, 1 + raise_level_ + depth_enc + depth_mod, slots,
-               dim1.size() > 1 ? dim1[1] : 0, pc.dec);
-  precom_[slots] = std::move(pc);
+  pc.dec_args = {dec_sizes, q0 / s_raise, 1 + raise_level_ + depth_enc + depth_mod, dim1.size() > 1 ? dim1[1] : 0};
+  pc.encoded = precompute;
+  build_levels(cc, true, pc.enc_args, slots, pc.enc, precompute);
+  build_levels(cc, false, pc.dec_args, slots, pc.dec, precompute);
+  {
+    std::lock_guard<std::mutex> lk(precom_mu_);
+    precom_[slots] = std::move(pc);
+  }
   const double args[2] = {static_cast<double>(K_UNIFORM), static_cast<double>(R_UNIFORM)};
   cheb_ = boot::chebyshev_coefficients(boot::scaled_cosine, args, kChebDegree);
 }
 
 const FHECKKSRNS::Precom& FHECKKSRNS::precom(uint32_t numSlots, const PhantomContext& cc) const {
   const uint32_t slots = numSlots ? numSlots : static_cast<uint32_t>(cc.poly_degree() / 2);
+  std::lock_guard<std::mutex> lk(precom_mu_);
   auto it = precom_.find(slots);
   if (it == precom_.end())
     throw std::invalid_argument("Precomputations for " + std::to_string(slots) +
                                 " slots were not generated: call EvalBootstrapSetup and then EvalBootstrapKeyGen");
-  return it->second;
+  Precom& pc = const_cast<Precom&>(it->second);
+  if (!pc.encoded) {
+    // deferred (precompute = false): encode the plaintexts of the same level structure now, once
+    // (a std::map node is stable, and concurrent callers wait on precom_mu_)
+    std::vector<LTLevel> enc, dec;
+    build_levels(cc, true, pc.enc_args, slots, enc, true);
+    build_levels(cc, false, pc.dec_args, slots, dec, true);
+    pc.enc = std::move(enc);
+    pc.dec = std::move(dec);
+    pc.encoded = true;
+  }
+  return pc;
 }
 
 size_t FHECKKSRNS::OutputChainIndex(const std::vector<uint32_t>& levelBudget, uint32_t log_slots,

@@ -72,17 +72,17 @@ class FHECKKSRNS {
   void EvalBootstrapSetup(const PhantomContext& cc, const std::vector<uint32_t>& levelBudget, double scale,
                           const std::vector<double>& sf, uint32_t correctionFactor = 0, uint32_t slots = 0,
                           const std::vector<uint32_t>& dim1 = {0, 0});
-  // the reference's argument list (scalingFactorsRealBig is accepted for drop-in calls; this engine
-  // derives everything it needs from scalingFactorsReal; `precompute` = false is not supported:
-  // the linear-transform plaintexts are always precomputed)
+  // the reference's argument list (bootstrap.cu:15-18).  scalingFactorsRealBig must be the
+  // FLEXIBLEAUTO squares of scalingFactorsReal (ciphertext.h:357-365; PreComputeScale makes them
+  // so): other values throw std::invalid_argument instead of being ignored, and the factors are
+  // kept (scaling_factors_big()).  precompute = false sets up the level structure (what
+  // EvalBootstrapKeyGen needs, as the reference's m_paramsEnc / m_paramsDec) and defers the
+  // linear-transform plaintexts to the first EvalBootstrap of that slot count (the reference
+  // skips them, bootstrap.cu:87, and would then bootstrap with empty transforms).
   void EvalBootstrapSetup(const PhantomContext& cc, const std::vector<uint32_t>& levelBudget, double scale,
                           const std::vector<double>& sf, const std::vector<double>& sf_big,
                           const std::vector<uint32_t>& dim1 = {0, 0}, uint32_t slots = 0,
-                          uint32_t correctionFactor = 0, bool precompute = true) {
-    (void)sf_big;
-    if (!precompute) throw std::invalid_argument("EvalBootstrapSetup: precompute = false is not supported");
-    EvalBootstrapSetup(cc, levelBudget, scale, sf, correctionFactor, slots, dim1);
-  }
+                          uint32_t correctionFactor = 0, bool precompute = true);
   // EvalBootstrapKeyGen / EvalMultKeyGen (bootstrap.cu:566-841): fused rotation keys for the
   // baby/giant steps, the sparse partial sums and conjugation, and the relinearization key.
   void EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext& cc, uint32_t numSlots = 0);
@@ -129,6 +129,10 @@ class FHECKKSRNS {
   uint32_t correction_factor() const { return correction_; }
   const std::vector<double>& eval_mod_coefficients() const { return cheb_; }
   const std::vector<double>& scaling_factors() const { return sf_; }
+  const std::vector<double>& scaling_factors_big() const { return sf_big_; }
+  // whether the linear-transform plaintexts of a slot count are encoded (false between a
+  // precompute = false setup and the first bootstrap)
+  bool precomputed(uint32_t numSlots = 0) const;
 
   static constexpr uint32_t K_UNIFORM = 512;  // bound on |I| of the raised plaintext t = m + q0 I
   static constexpr uint32_t R_UNIFORM = 6;    // double-angle iterations
@@ -145,20 +149,33 @@ class FHECKKSRNS {
     DeviceBuffer<uint64_t> zero;                        // the zero plaintext absent diagonals point at
   };
   // the precomputation of one slot count (the reference's CKKSBootstrapPrecom)
+  // the arguments of one direction's build_levels, kept for a deferred encoding
+  struct LevelArgs {
+    std::vector<int> sizes;
+    double constant = 1.0;
+    size_t first_chain = 1;
+    uint32_t dim1 = 0;
+  };
   struct Precom {
     uint32_t slots = 0;
     std::vector<LTLevel> enc, dec;
+    bool encoded = true;  // false: level structure only (precompute = false)
+    LevelArgs enc_args, dec_args;
   };
-  void build_levels(const PhantomContext& cc, bool encode_dir, const std::vector<int>& group_sizes, double constant,
-                    size_t first_chain, uint32_t slots, uint32_t dim1, std::vector<LTLevel>& out) const;
+  void setup(const PhantomContext& cc, const std::vector<uint32_t>& levelBudget, const std::vector<double>& sf,
+             uint32_t correctionFactor, uint32_t slots, const std::vector<uint32_t>& dim1, bool precompute);
+  // encode = false: the levels' structure (g, b, stride, center, chain) without their plaintexts
+  void build_levels(const PhantomContext& cc, bool encode_dir, const LevelArgs& args, uint32_t slots,
+                    std::vector<LTLevel>& out, bool encode) const;
   const Precom& precom(uint32_t numSlots, const PhantomContext& cc) const;
   PhantomCiphertext apply_level(const PhantomContext& cc, const PhantomCiphertext& ct, const LTLevel& lv) const;
   PhantomCiphertext eval_mod(const PhantomCiphertext& ct, const PhantomContext& cc) const;
   PhantomCiphertext bootstrap_once(const PhantomCiphertext& ct, const PhantomContext& cc, const Precom& pc) const;
 
   PhantomCKKSEncoder& encoder_;
-  std::vector<double> sf_;
+  std::vector<double> sf_, sf_big_;
   std::vector<uint32_t> budget_;
+  mutable std::mutex precom_mu_;  // deferred encodings
   uint32_t correction_ = 0;
   bool tight_levels_ = false;
   size_t raise_level_ = 0;  // the level ModRaise lands on (reference layout: the spare level)

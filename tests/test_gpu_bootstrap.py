@@ -44,6 +44,21 @@ def test_full_bootstrap_precision_and_levels():
     assert boot["levels_after"] == 11, boot
 
 
+def test_deferred_setup_reference_arguments():
+    """EvalBootstrapSetup with the reference's argument list (bootstrap.cu:15-18): a
+    scalingFactorsRealBig that is not sf^2 is refused; precompute = false keeps the level structure
+    (the keys are generated from it) and the first EvalBootstrap encodes the plaintexts."""
+    rc, lines, err = _run("deferred", "16", "1", timeout=115)
+    assert rc == 0, (lines, err)
+    checks = {l["check"]: l for l in lines if "check" in l}
+    for name in ["sf_big_mismatch_refused", "deferred_not_encoded", "sf_big_kept", "deferred_encoded_by_bootstrap"]:
+        assert checks[name]["ok"], checks[name]
+    setup = [l for l in lines if l.get("stage") == "setup"][0]
+    assert setup["setup_ms"] < 400, setup  # no plaintexts encoded (a full setup takes 1.2-1.5 s)
+    boot = [l for l in lines if l.get("stage") == "bootstrap"][0]
+    assert boot["avg_bits"] > 9.85 and boot["levels_after"] == 11, boot
+
+
 def test_flexibleauto_surface():
     """EvalMultAuto / EvalSquare / EvalAddAuto / EvalSubAuto / EvalAddConst / EvalMultConst (lazy) /
     EvalMultAutoInplace with a plaintext / EvalChebyshevFunction (degree 4: the reference's linear
