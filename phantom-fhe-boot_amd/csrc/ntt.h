@@ -88,6 +88,13 @@ hipError_t ntt_forward(const NttTables& t, const uint64_t* in, uint64_t* out, co
 //    epi.out[p][i][k] = (epi.c[p][i][k] - y) * w[i] (+ epi.out[p][i][k] when accumulate), mod q:
 //    the rescale / moddown finish (src/rns.cu:1141-1158, src/ntt/ntt_moddown.cu:199-214).
 // Polynomial p of c / out starts at p * c_stride / p * out_stride (elements).
+//  - key-switch form (ks_beta > 0, the moddown of a key switch): c is not read; its value is the
+//    key-switch inner product of the Ql limbs formed in the epilogue,
+//      c[p][i][k] = sum_{d < ks_beta} tmu[d][i][k] * evk[d][p][i][k]  mod q_i
+//    (src/eval_key_switch.cu:26-85 for limbs i < size_Ql), so the inner product's Ql half never
+//    makes an HBM round trip (tmu: digit stride tmu_stride; evk: device array of ks_beta digit
+//    pointers, polynomial stride evk_poly_stride; the buffer limbs must be the first Ql limbs).
+constexpr int kMaxKsBeta = 4;
 struct NttEpilogue {
   const uint64_t* c = nullptr;
   size_t c_stride = 0;
@@ -96,6 +103,11 @@ struct NttEpilogue {
   const uint64_t* w = nullptr;   // per buffer limb
   const uint64_t* ws = nullptr;  // Shoup quotients
   bool accumulate = false;
+  int ks_beta = 0;
+  const uint64_t* tmu = nullptr;
+  size_t tmu_stride = 0;
+  const uint64_t* const* evk = nullptr;
+  size_t evk_poly_stride = 0;
 };
 hipError_t ntt_forward_fused(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                              const uint64_t* bcast, size_t bcast_stride, const NttEpilogue& epi, hipStream_t stream);

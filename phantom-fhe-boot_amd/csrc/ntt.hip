@@ -188,6 +188,23 @@ __device__ __forceinline__ void load_tw(W (&w)[E], const W* __restrict__ tab, ui
   }
 }
 
+// A twiddle from its Shoup quotient alone.  ws = floor(w 2^64 / q) with 0 < w < q and q prime:
+// w 2^64 = ws q + rem with 0 < rem < q < 2^64, so floor(ws q / 2^64) = w - 1 exactly.  (Every
+// table twiddle is a power of a root of unity, never 0.)
+__device__ __forceinline__ uint64_t w_from_shoup(uint64_t ws, uint64_t q) { return __umul64hi(ws, q) + 1; }
+
+template <int S_LOG, int R>
+__device__ __forceinline__ void w_from_shoup_round(uint64_t (&w)[E], const uint64_t (&ws)[E], uint64_t q) {
+  using Rd = Round<S_LOG, R>;
+#pragma unroll
+  for (int gl = 0; gl < Rd::er; ++gl)
+#pragma unroll
+    for (int key = 0; key < (1 << (gl + Rd::ex)); ++key) {
+      const int s = tw_slot<Rd::ex>(gl, key);
+      w[s] = w_from_shoup(ws[s], q);
+    }
+}
+
 // row-pass FP64 twiddles generated per lane: tw = A[g] * Btab[2^g + iloc] (unreduced, |tw| <= kGenW q)
 template <int S_LOG, int R>
 __device__ __forceinline__ void gen_tw_row(double (&w)[E], const double* __restrict__ A,
@@ -397,20 +414,40 @@ __device__ __forceinline__ uint32_t rpad(uint32_t p) { return p + (p >> 4); }
 __device__ __forceinline__ uint32_t cidx(uint32_t p, uint32_t c) { return p * COLS + c + (p >> 4) * COLS; }
 
 // ---------------------------------------------------------------------------------------
-// Launch structure.  Default (PHX_NTT_PERSIST = 0): one tile per workgroup, the grid covers
-// every tile and all of it is resident at once (2.75 waves per SIMD at [44][65536]).  Every
-// twiddle load of a tile is issued right after its data loads, so no twiddle round trip sits
-// between two butterfly rounds.  PHX_NTT_PERSIST = P > 0 builds a persistent variant instead:
-// P workgroups per CU loop over tiles and issue the NEXT tile's loads before computing the
-// current one (twiddle loads first: vector-memory loads retire in order).  Measured on MI355X
-// (profiles/r01/ntt_variants.txt) the persistent forms are slower at this size (tile counts do
-// not divide evenly over the CUs), so they stay a tuning knob.
+// Launch structure: one tile per workgroup, the grid covers every tile and all of it is resident
+// at once (2.75 waves per SIMD at [44][65536]).  Every twiddle load of a tile is issued right
+// after its data loads, so no twiddle round trip sits between two butterfly rounds.  (Persistent
+// grids that prefetch the next tile were measured slower in round 1, profiles/r01/ntt_variants.txt,
+// and were removed.)
 // ---------------------------------------------------------------------------------------
-#ifndef PHX_NTT_PERSIST
-#define PHX_NTT_PERSIST 0  // workgroups per CU (0: one tile per workgroup, grid = all tiles)
+// PHX_NTT_STAMP = 1 (diagnostic builds only, tools/ntt_timeline.py): every wave of the forward
+// passes records s_memrealtime (100 MHz, chip-wide) at entry, when its data has arrived, after
+// its butterflies, after its stores are issued and once they are complete, plus HW_ID / XCC_ID,
+// into g_ntt_stamps[slot][8] (column pass slots from 0, row pass slots from kStampRow).
+#ifndef PHX_NTT_STAMP
+#define PHX_NTT_STAMP 0
 #endif
-constexpr int kWavesPerEU = PHX_NTT_PERSIST > 0 ? PHX_NTT_PERSIST : PHX_NTT_WAVES_PER_EU;
-constexpr bool kPrefetch = PHX_NTT_PERSIST > 0;
+#if PHX_NTT_STAMP
+constexpr int kStampSlots = 32768, kStampRow = 16384;
+__device__ uint64_t g_ntt_stamps[kStampSlots * 8];
+__device__ __forceinline__ void stamp_now(int slot, int i, bool wait) {
+  if (wait) __builtin_amdgcn_s_waitcnt(0);
+  const uint64_t t = __builtin_amdgcn_s_memrealtime();
+  if (slot < kStampSlots && (threadIdx.x & 63) == 0) {
+    g_ntt_stamps[slot * 8 + i] = t;
+    if (i == 0) {
+      g_ntt_stamps[slot * 8 + 5] = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID
+      g_ntt_stamps[slot * 8 + 6] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
+    }
+  }
+}
+#define PHX_STAMP(slot, i, wait) stamp_now(slot, i, wait)
+#else
+#define PHX_STAMP(slot, i, wait) ((void)0)
+#endif
+#ifndef PHX_ROW_TWD
+#define PHX_ROW_TWD 1  // integer row pass: 1 = later rounds derive w from ws, 2 = and load them up front
+#endif
 
 struct TileRef {
   int buf_limb, row, poly;
@@ -445,6 +482,68 @@ __device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr
   store_wt(o, v);
 }
 
+// Key-switch epilogue (NttEpilogue::ks_beta > 0): out = (sum_d tmu[d] evk[d][p] mod q - y) w
+// (+ out), the inner product of eval_key_switch.cu:26-85 (128-bit sums, one Barrett-128 per
+// element) formed where the moddown finish consumes it.  KC elements at a time; the next group's
+// loads are issued before the current group's products.
+template <int T>
+__device__ __forceinline__ void ks_epilogue(const KArgs& a, const TileRef& tr, const uint64_t (&y)[E], uint64_t q,
+                                            uint64_t r0, uint64_t r1) {
+  constexpr int KC = 4, NC = E / KC;
+  const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
+  const int beta = __builtin_amdgcn_readfirstlane(a.epi.ks_beta);
+  const bool acc_out = a.epi.accumulate;
+  const uint64_t* tm = a.epi.tmu + e;
+  const uint64_t* kp[kMaxKsBeta];
+#pragma unroll
+  for (int d = 0; d < kMaxKsBeta; ++d) kp[d] = d < beta ? a.epi.evk[d] + tr.poly * a.epi.evk_poly_stride + e : tm;
+  uint64_t* o = a.epi.out + tr.poly * a.epi.out_stride + e;
+  const uint64_t w = a.epi.w[tr.buf_limb], ws = a.epi.ws[tr.buf_limb];
+  uint64_t tb[2][kMaxKsBeta][KC], kb[2][kMaxKsBeta][KC], ob[2][KC];
+  auto load = [&](int c, int s) {
+#pragma unroll
+    for (int d = 0; d < kMaxKsBeta; ++d) {
+      if (d < beta) {
+#pragma unroll
+        for (int i = 0; i < KC; ++i) {
+          tb[s][d][i] = __builtin_nontemporal_load(tm + d * a.epi.tmu_stride + (c * KC + i) * T);
+          kb[s][d][i] = __builtin_nontemporal_load(kp[d] + (c * KC + i) * T);
+        }
+      }
+    }
+    if (acc_out) {
+#pragma unroll
+      for (int i = 0; i < KC; ++i) ob[s][i] = __builtin_nontemporal_load(o + (c * KC + i) * T);
+    }
+  };
+  load(0, 0);
+  static_for<NC>([&](auto cc) {
+    constexpr int c = decltype(cc)::value, s = c & 1;
+    if constexpr (c + 1 < NC) load(c + 1, s ^ 1);
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      u128 acc{0, 0};
+#pragma unroll
+      for (int d = 0; d < kMaxKsBeta; ++d)
+        if (d < beta) add128(acc, mul_wide(tb[s][d][i], kb[s][d][i]));
+      uint64_t v = mul_shoup(sub_mod(barrett_reduce_128(acc, q, r0, r1), y[c * KC + i], q), w, ws, q);
+      if (acc_out) v = add_mod(v, ob[s][i], q);
+      store_wt(o + (c * KC + i) * T, v);
+    }
+  });
+}
+
+// Row-pass block order of the key-switch epilogue: the polynomials' blocks of one row group are
+// dealt to one XCD back to back (blocks b and b + 8 share an XCD under round-robin placement;
+// speed only, any placement is correct), so the second polynomial reads tmu from that XCD's L2.
+__device__ __forceinline__ int ks_row_block(const KArgs& a, int b, int waves, int groups) {
+  const int polys = a.map.polys;
+  if (polys < 2 || (a.limbs_per_poly * groups) % waves != 0) return b;
+  const int per = a.limbs_per_poly * groups / waves;  // blocks per polynomial
+  if (per % 8 != 0 || (int)gridDim.x != polys * per) return b;
+  const int x = b % 8, k = b / 8;
+  return (k % polys) * per + (k / polys) * 8 + x;
+}
 
 // Base-conversion prologue (ntt.h BconvPrologue): the tile's 16 elements of output limb j are
 // sum_s in[s][k] * mat[s][j] mod q, in two halves of 8 elements; per half the input loads of 4
@@ -542,41 +641,31 @@ __device__ __forceinline__ void col_load(uint64_t (&x)[E], const uint64_t* src, 
 }
 
 // LZ (forward, every modulus of the table < 2^60): the integer path runs with the 16q lazy range
-template <int S1_LOG, int S2_LOG, bool FWD, bool BCV = false, bool LZ = false>
-__global__ __launch_bounds__(CBLOCK, BCV ? 2 : kWavesPerEU) void ntt_col(KArgs a) {
+template <int S1_LOG>
+constexpr int col_lds_words() { return (Sub<S1_LOG>::S + Sub<S1_LOG>::S / 16) * COLS; }
+
+// One column tile (the calling workgroup's threads tid < NT; `lds`: col_lds_words words).
+template <int S1_LOG, int S2_LOG, bool FWD, bool BCV, bool LZ>
+__device__ __forceinline__ void col_tile(const KArgs& a, int tile, uint64_t* lds, [[maybe_unused]] int sslot) {
   using SB = Sub<S1_LOG>;
   using P = Plan<S1_LOG, S2_LOG>;
-  constexpr int T = SB::T, S2 = 1 << S2_LOG, NT = COLS * T, CT = S2 / COLS, RN = SB::ROUNDS;
+  constexpr int T = SB::T, S2 = 1 << S2_LOG, NT = COLS * T, RN = SB::ROUNDS;
   constexpr int RF = FWD ? 0 : RN - 1;  // first round executed
   constexpr int RL = FWD ? RN - 1 : 0;  // last round executed
   static_assert(NT <= CBLOCK, "column tile too large");
-  __shared__ uint64_t lds[(SB::S + SB::S / 16) * COLS];
-
   const uint32_t tid = threadIdx.x;
-  if (tid >= NT) return;  // no barrier below involves the idle threads' absence (NT is a multiple of 64)
   const uint32_t c = tid % COLS, t = tid / COLS;
-  const int ntiles = a.limbs * CT;
   auto idx = [c](uint32_t p) { return cidx(p, c); };
   auto sync = [] { __syncthreads(); };
   const uint32_t pf = Round<S1_LOG, RF>::p_thread(t), pl = Round<S1_LOG, RL>::p_thread(t);
-
-  int tile = BCV ? bcv_tile<S2_LOG>(a, blockIdx.x) : blockIdx.x;  // workgroup-uniform
-  if (tile >= ntiles) return;
-  uint64_t xn[E];
   const uint64_t* src = a.bcast ? a.bcast : a.in;
-  if constexpr (!BCV) col_load<S1_LOG, S2_LOG, RF>(xn, src + col_ref<S2_LOG>(a, tile, c).in_off, pf);
-  for (;;) {
+  {
     const TileRef tr = col_ref<S2_LOG>(a, tile, c);
-    const int next = tile + gridDim.x;
-    const bool more = kPrefetch && next < ntiles;
     uint64_t x[E];
+    if constexpr (!BCV) col_load<S1_LOG, S2_LOG, RF>(x, src + tr.in_off, pf);
     const LimbCtx lc = limb_ctx(a, tr.row);
-    if constexpr (BCV) {
+    if constexpr (BCV)
       bconv_prologue<S1_LOG, S2_LOG, RF>(x, a, tile, tr, pf, lc.q, a.barrett[2 * tr.row], a.barrett[2 * tr.row + 1]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < E; ++j) x[j] = xn[j];
-    }
     uint64_t* dst = a.out + tr.off;
     if (FWD && !BCV && a.bcast) {  // prologue: the broadcast limb reduced mod this limb's prime
       const uint64_t r1 = a.barrett[2 * tr.row + 1];
@@ -590,18 +679,21 @@ __global__ __launch_bounds__(CBLOCK, BCV ? 2 : kWavesPerEU) void ntt_col(KArgs a
         constexpr int R = decltype(rc)::value;
         load_tw<S1_LOG, R>(w[R], tab, Round<S1_LOG, R>::p_thread(t), 1);
       });
-      if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, src + col_ref<S2_LOG>(a, next, c).in_off, pf);
       double v[E];
 #pragma unroll
       for (int j = 0; j < E; ++j) v[j] = FWD ? u52_to_f64(x[j]) : as_f64(x[j]);
       if constexpr (FWD) {
+        if constexpr (!BCV) PHX_STAMP(sslot, 1, true);
         static_for<RN>([&](auto rc) {
           constexpr int R = decltype(rc)::value;
           if constexpr (R > 0) relayout<S1_LOG, R - 1, R>(v, reinterpret_cast<double*>(lds), idx, sync, t);
           ct_round_f64<S1_LOG, R, P::col_fwd.mask>(v, w[R], lc.qd, lc.qinv);
         });
+        if constexpr (!BCV) PHX_STAMP(sslot, 2, false);
 #pragma unroll
         for (int j = 0; j < E; ++j) store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, as_bits(v[j]));
+        if constexpr (!BCV) PHX_STAMP(sslot, 3, false);
+        if constexpr (!BCV) PHX_STAMP(sslot, 4, true);
       } else {
         double c0 = tab[0], c1 = tab[1];
         if (a.scale) {
@@ -621,12 +713,11 @@ __global__ __launch_bounds__(CBLOCK, BCV ? 2 : kWavesPerEU) void ntt_col(KArgs a
     } else {
       const uint64_t* tw = a.tw + (size_t)tr.row * a.n;
       const uint64_t* tws = a.tws + (size_t)tr.row * a.n;
-      // integer path (primes >= 2^50): twiddles and Shoup quotients per round, after the
-      // prefetch (fewer registers; such tiles wait for the prefetch)
-      if (kPrefetch && more) col_load<S1_LOG, S2_LOG, RF>(xn, src + col_ref<S2_LOG>(a, next, c).in_off, pf);
+      // integer path (primes >= 2^50): twiddles and Shoup quotients per round
       uint64_t(&v)[E] = x;
       // LZ: forward with the 16q lazy range; stores values < col_lz.out q
       {
+        if constexpr (FWD && !BCV) PHX_STAMP(sslot, 1, true);
         static_for<RN>([&](auto rc) {
           constexpr int R = FWD ? decltype(rc)::value : RN - 1 - decltype(rc)::value;
           if constexpr (FWD && R > 0) relayout<S1_LOG, R - 1, R>(v, lds, idx, sync, t);
@@ -642,8 +733,11 @@ __global__ __launch_bounds__(CBLOCK, BCV ? 2 : kWavesPerEU) void ntt_col(KArgs a
             gs_round_int<S1_LOG, R>(v, w, ws, lc.q);
         });
         if constexpr (FWD) {
+          if constexpr (!BCV) PHX_STAMP(sslot, 2, false);
 #pragma unroll
           for (int j = 0; j < E; ++j) store_wt(dst + (size_t)(pl | Round<S1_LOG, RL>::p_elem(j)) * S2, v[j]);  // lazy
+          if constexpr (!BCV) PHX_STAMP(sslot, 3, false);
+          if constexpr (!BCV) PHX_STAMP(sslot, 4, true);
         } else {
           const uint64_t ni = a.n_inv[tr.row], nis = a.n_inv_shoup[tr.row];
           const uint64_t sc = a.scale ? a.scale[tr.buf_limb] : 1, scs = a.scale ? a.scale_shoup[tr.buf_limb] : 0;
@@ -657,10 +751,19 @@ __global__ __launch_bounds__(CBLOCK, BCV ? 2 : kWavesPerEU) void ntt_col(KArgs a
         }
       }
     }
-    if (!more) break;
-    tile = next;
-    sync();  // the next tile's first LDS writes must not overtake this tile's last reads
   }
+}
+
+template <int S1_LOG, int S2_LOG, bool FWD, bool BCV = false, bool LZ = false>
+__global__ __launch_bounds__(CBLOCK, BCV ? 2 : PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) {
+  constexpr int NT = COLS * Sub<S1_LOG>::T, CT = (1 << S2_LOG) / COLS;
+  __shared__ uint64_t lds[col_lds_words<S1_LOG>()];
+  if (threadIdx.x >= NT) return;  // no barrier involves the idle threads' absence (NT is a multiple of 64)
+  const int tile = BCV ? bcv_tile<S2_LOG>(a, blockIdx.x) : blockIdx.x;  // workgroup-uniform
+  if (tile >= a.limbs * CT) return;
+  [[maybe_unused]] const int sslot = blockIdx.x * (CBLOCK / 64) + threadIdx.x / 64;
+  if constexpr (FWD && !BCV) PHX_STAMP(sslot, 0, false);
+  col_tile<S1_LOG, S2_LOG, FWD, BCV, LZ>(a, tile, lds, sslot);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -704,47 +807,40 @@ __device__ __forceinline__ void row_copy(const KArgs& a, const TileRef& tr, cons
   for (int j = 0; j < E; ++j) store_wt(dst + j * Sub<S2_LOG>::T, x[j]);
 }
 
-// The epilogue form holds its operands (EpiOperands) through the butterflies: two waves per SIMD
-// give it the registers to do so without spilling (168 VGPRs at three waves spilled 47).
-template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false, bool LZ = false>
-__global__ __launch_bounds__(BLOCK, EPI ? 2 : kWavesPerEU) void ntt_row(KArgs a) {
+template <int S1_LOG, int S2_LOG>
+struct RowShape {
+  static constexpr int S1 = 1 << S1_LOG, S2 = 1 << S2_LOG, T = Sub<S2_LOG>::T, RW = cmin(64 / T, S1);
+  static constexpr int RSTR = S2 + S2 / 16, WAVES = BLOCK / 64;
+  static constexpr int GROUPS = S1 / RW;  // row groups (wave items) per limb
+  static constexpr int LDS_WORDS = WAVES * RW * RSTR, TW0 = WAVES * RW * 16;
+};
+
+// One row item (the calling wave's RW rows; lds: RowShape::LDS_WORDS words, tw0: RowShape::TW0).
+template <int S1_LOG, int S2_LOG, bool FWD, bool EPI, bool LZ, bool KS>
+__device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds, double* tw0,
+                                         [[maybe_unused]] int sslot) {
   using SB = Sub<S2_LOG>;
   using P = Plan<S1_LOG, S2_LOG>;
-  constexpr int S1 = 1 << S1_LOG, S2 = SB::S, T = SB::T, RW = cmin(64 / T, S1), RSTR = S2 + S2 / 16, RN = SB::ROUNDS;
-  constexpr int WAVES = BLOCK / 64;
-  constexpr int GROUPS = S1 / RW;           // row groups per limb
+  using RS = RowShape<S1_LOG, S2_LOG>;
+  constexpr int S1 = RS::S1, S2 = RS::S2, T = RS::T, RW = RS::RW, RSTR = RS::RSTR, RN = SB::ROUNDS;
   constexpr int ER0 = Round<S2_LOG, 0>::er;  // stages of round 0 (its twiddles are row-uniform)
   constexpr int K0 = ((1 << ER0) - 1 + T - 1) / T;  // round-0 twiddles made per lane
   static_assert(Round<S2_LOG, 0>::ex == 0, "round 0 must be a full radix-16 round");
-  __shared__ uint64_t lds[WAVES * RW * RSTR];
-  __shared__ double tw0[WAVES * RW * 16];
-
   const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
   const uint32_t lr = lane / T, t = lane % T;
   uint64_t* lrow = lds + (wave * RW + lr) * RSTR;
   double* trow = tw0 + (wave * RW + lr) * 16;
-  const int nitems = a.limbs * GROUPS;
-  const int step = gridDim.x * WAVES;
   auto idx = [](uint32_t p) { return rpad(p); };
   auto sync = [] { __builtin_amdgcn_wave_barrier(); };
-
-  int item = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + wave);
-  if (item >= nitems) return;  // no workgroup barrier in this kernel
   uint32_t r;
-  uint64_t xn[E];
-  row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, item, lr, t, r).in_off);
-  for (;;) {
+  {
     const TileRef tr = row_ref<S1_LOG, S2_LOG>(a, item, lr, t, r);
-    const int next = item + step;
-    const bool more = kPrefetch && next < nitems;
     uint64_t x[E];
-#pragma unroll
-    for (int j = 0; j < E; ++j) x[j] = xn[j];
+    row_load<S2_LOG>(x, a.in + tr.in_off);
     if (!FWD && a.copy.out) row_copy<S2_LOG>(a, tr, x);  // workgroup-uniform branch
     const LimbCtx lc = limb_ctx(a, tr.row);
     uint64_t* dst = a.out + tr.off;
-    uint32_t rn = 0;
-    EpiOperands eo;
+    [[maybe_unused]] EpiOperands eo;
     if (lc.f64) {
       const double* A = a.row_a + ((size_t)tr.row * S1 + r) * 16;
       const double* Bt = a.row_b + (size_t)tr.row * S2;
@@ -775,8 +871,7 @@ __global__ __launch_bounds__(BLOCK, EPI ? 2 : kWavesPerEU) void ntt_row(KArgs a)
           }
         }
       });
-      if (kPrefetch && more) row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, next, lr, t, rn).in_off);
-      if constexpr (FWD && EPI) epilogue_load(a, tr, T, eo);
+      if constexpr (FWD && EPI && !KS) epilogue_load(a, tr, T, eo);
 #pragma unroll
       for (int k = 0; k < K0; ++k) {
         const uint32_t e = t + 1 + T * k;
@@ -803,6 +898,7 @@ __global__ __launch_bounds__(BLOCK, EPI ? 2 : kWavesPerEU) void ntt_row(KArgs a)
         }
       };
       if constexpr (FWD) {
+        if constexpr (!EPI) PHX_STAMP(sslot, 1, true);
         static_for<RN>([&](auto rc) {
           constexpr int R = decltype(rc)::value;
           if constexpr (R > 0) relayout<S2_LOG, R - 1, R>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
@@ -811,12 +907,20 @@ __global__ __launch_bounds__(BLOCK, EPI ? 2 : kWavesPerEU) void ntt_row(KArgs a)
           ct_round_f64<S2_LOG, R, P::row_fwd.mask>(v, w, lc.qd, lc.qinv);
         });
         if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
-        if constexpr (EPI) {
+        if constexpr (!EPI) PHX_STAMP(sslot, 2, false);
+        if constexpr (KS) {
+          uint64_t y[E];
+#pragma unroll
+          for (int j = 0; j < E; ++j) y[j] = f64_to_canonical(v[j], lc.qd, lc.qinv);
+          ks_epilogue<T>(a, tr, y, lc.q, a.barrett[2 * tr.row], a.barrett[2 * tr.row + 1]);
+        } else if constexpr (EPI) {
 #pragma unroll
           for (int j = 0; j < E; ++j) epilogue_store(a, tr, j, T, eo, f64_to_canonical(v[j], lc.qd, lc.qinv), lc.q);
         } else {
 #pragma unroll
           for (int j = 0; j < E; ++j) store_wt(dst + j * T, f64_to_canonical(v[j], lc.qd, lc.qinv));
+          PHX_STAMP(sslot, 3, false);
+          PHX_STAMP(sslot, 4, true);
         }
       } else {
         if constexpr (RN > 1) relayout<S2_LOG, 0, RN - 1>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
@@ -834,22 +938,43 @@ __global__ __launch_bounds__(BLOCK, EPI ? 2 : kWavesPerEU) void ntt_row(KArgs a)
       const uint32_t B = (1u << S1_LOG) + r;
       const uint64_t* tw = a.tw + (size_t)tr.row * a.n;
       const uint64_t* tws = a.tws + (size_t)tr.row * a.n;
-      if (kPrefetch && more) row_load<S2_LOG>(xn, a.in + row_ref<S1_LOG, S2_LOG>(a, next, lr, t, rn).in_off);
       uint64_t(&v)[E] = x;
+      // PHX_ROW_TWD: rounds after the first (whose twiddles are row-uniform: one broadcast line)
+      // read only the Shoup quotients and derive w (w_from_shoup): half the row pass's twiddle
+      // bytes (the (S1 + row)-indexed tables are ~2x the data).  2: those loads are issued up
+      // front with the tile, so no twiddle round trip sits between two rounds.
+      [[maybe_unused]] uint64_t wsr[RN][E];
+      if constexpr (PHX_ROW_TWD == 2) {
+        static_for<RN>([&](auto rc) {
+          constexpr int R = decltype(rc)::value;
+          if constexpr (R > 0) load_tw<S2_LOG, R>(wsr[R], tws, Round<S2_LOG, R>::p_thread(t), B);
+        });
+      }
       auto get_tw = [&](auto rc, uint64_t (&w)[E], uint64_t (&ws)[E]) {
         constexpr int R = decltype(rc)::value;
-        load_tw<S2_LOG, R>(w, tw, Round<S2_LOG, R>::p_thread(t), B);
-        load_tw<S2_LOG, R>(ws, tws, Round<S2_LOG, R>::p_thread(t), B);
+        if constexpr (PHX_ROW_TWD == 0 || R == 0) {
+          load_tw<S2_LOG, R>(w, tw, Round<S2_LOG, R>::p_thread(t), B);
+          load_tw<S2_LOG, R>(ws, tws, Round<S2_LOG, R>::p_thread(t), B);
+        } else {
+          if constexpr (PHX_ROW_TWD == 2) {
+#pragma unroll
+            for (int s = 0; s < E; ++s) ws[s] = wsr[R][s];
+          } else {
+            load_tw<S2_LOG, R>(ws, tws, Round<S2_LOG, R>::p_thread(t), B);
+          }
+          w_from_shoup_round<S2_LOG, R>(w, ws, lc.q);
+        }
       };
       if constexpr (FWD) {
         // LZ: the 16q lazy range; the input is the column pass's lazy output
         {
+          if constexpr (!EPI) PHX_STAMP(sslot, 1, true);
           static_for<RN>([&](auto rc) {
             constexpr int R = decltype(rc)::value;
             if constexpr (R > 0) relayout<S2_LOG, R - 1, R>(v, lrow, idx, sync, t);
             uint64_t w[E], ws[E];
             get_tw(rc, w, ws);
-            if constexpr (EPI && R == RN - 1) epilogue_load(a, tr, T, eo);  // behind the last twiddles
+            if constexpr (EPI && !KS && R == RN - 1) epilogue_load(a, tr, T, eo);  // behind the last twiddles
             if constexpr (LZ)
               ct_round_int16<S2_LOG, R, P::row_lz.mask>(v, w, ws, lc.q);
             else
@@ -860,12 +985,20 @@ __global__ __launch_bounds__(BLOCK, EPI ? 2 : kWavesPerEU) void ntt_row(KArgs a)
             if constexpr (LZ && P::row_lz.out > 8) return reduce16(y, lc.q);
             else return reduce8(y, lc.q);
           };
-          if constexpr (EPI) {
+          if constexpr (KS) {
+            uint64_t y[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j) y[j] = canon(v[j]);
+            ks_epilogue<T>(a, tr, y, lc.q, a.barrett[2 * tr.row], a.barrett[2 * tr.row + 1]);
+          } else if constexpr (EPI) {
 #pragma unroll
             for (int j = 0; j < E; ++j) epilogue_store(a, tr, j, T, eo, canon(v[j]), lc.q);
           } else {
+            PHX_STAMP(sslot, 2, false);
 #pragma unroll
             for (int j = 0; j < E; ++j) store_wt(dst + j * T, canon(v[j]));
+            PHX_STAMP(sslot, 3, false);
+            PHX_STAMP(sslot, 4, true);
           }
         }
       } else {
@@ -881,10 +1014,28 @@ __global__ __launch_bounds__(BLOCK, EPI ? 2 : kWavesPerEU) void ntt_row(KArgs a)
         for (int j = 0; j < E; ++j) store_wt(dst + j * T, v[j]);  // [0, 4q), column pass follows
       }
     }
-    if (!more) break;
-    item = next;
-    sync();  // trow / lrow of the next item are rewritten
   }
+}
+
+// The epilogue form holds its operands (EpiOperands) through the butterflies: two waves per SIMD
+// give it the registers to do so without spilling (168 VGPRs at three waves spilled 47).
+// KS: the epilogue is the key-switch form (ks_epilogue; EPI must be set too).
+template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false, bool LZ = false, bool KS = false>
+__global__ __launch_bounds__(BLOCK, EPI ? 2 : PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) {
+  using RS = RowShape<S1_LOG, S2_LOG>;
+  __shared__ uint64_t lds[RS::LDS_WORDS];
+  __shared__ double tw0[RS::TW0];
+  const int wave = threadIdx.x / 64;
+  const int blk = KS ? ks_row_block(a, blockIdx.x, RS::WAVES, RS::GROUPS) : (int)blockIdx.x;
+  const int item = __builtin_amdgcn_readfirstlane(blk * RS::WAVES + wave);
+  if (item >= a.limbs * RS::GROUPS) return;  // no workgroup barrier in this kernel
+#if PHX_NTT_STAMP
+  const int sslot = kStampRow + blockIdx.x * RS::WAVES + wave;
+#else
+  const int sslot = 0;
+#endif
+  if constexpr (FWD && !EPI) PHX_STAMP(sslot, 0, false);
+  row_item<S1_LOG, S2_LOG, FWD, EPI, LZ, KS>(a, item, lds, tw0, sslot);
 }
 // ---------------------------------------------------------------------------------------
 // 1-D path for small transforms, n = 2^8 .. 2^11 (the reference's radix-2 fnwt_1d / inwt_1d,
@@ -956,6 +1107,20 @@ __global__ __launch_bounds__(1024) void ntt_1d(KArgs a) {
   }
 }
 
+#if PHX_NTT_STAMP
+}  // namespace
+}  // namespace phx
+extern "C" int phantom_debug_ntt_stamps(void* dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(phx::g_ntt_stamps), bytes);
+}
+extern "C" int phantom_debug_ntt_stamps_clear() {
+  static uint64_t zeros[phx::kStampSlots * 8];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(phx::g_ntt_stamps), zeros, sizeof(zeros));
+}
+namespace phx {
+namespace {
+#endif
+
 hipError_t launch_1d(const NttTables& tb, const uint64_t* in, uint64_t* out, const LimbMap& map, bool inverse,
                      const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream, const uint64_t* bcast,
                      size_t bcast_stride, const NttEpilogue& epi) {
@@ -979,19 +1144,6 @@ hipError_t launch_1d(const NttTables& tb, const uint64_t* in, uint64_t* out, con
   if (inverse) hipLaunchKernelGGL(ntt_1d<false>, grid, block, 0, stream, a);
   else hipLaunchKernelGGL(ntt_1d<true>, grid, block, 0, stream, a);
   return hipGetLastError();
-}
-
-// compute units of the current device (cached per device id)
-int num_cus() {
-  static int cache[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cache[dev] == 0) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    cache[dev] = v;
-  }
-  return cache[dev];
 }
 
 template <int S1_LOG, int S2_LOG>
@@ -1025,9 +1177,7 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   const int col_tiles = limbs * (S2 / COLS);
   const int row_items = limbs * (S1 / RW);
   const int row_groups = (row_items + BLOCK / 64 - 1) / (BLOCK / 64);
-  // persistent grids: at most PHX_NTT_PERSIST workgroups per CU, each loops over tiles
-  const int cap = PHX_NTT_PERSIST > 0 ? num_cus() * PHX_NTT_PERSIST : 1 << 30;
-  const dim3 grid_c(std::min(col_tiles, cap)), grid_r(std::min(row_groups, cap));
+  const dim3 grid_c(col_tiles), grid_r(row_groups);
   // column tiles of small transforms need fewer than BLOCK threads (rounded up to a wavefront)
   const dim3 block_c(std::max(64, COLS * Sub<S1_LOG>::T)), block_r(BLOCK);
   if (!inverse) {
@@ -1047,7 +1197,11 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
     a.map.in_stride = a.map.out_stride;
     a.bcast = nullptr;  // the row pass reads the intermediate
     a.epi = epi_row;
-    if (a.epi.out && lz)
+    if (a.epi.out && a.epi.ks_beta > 0 && lz)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true, true, true>), grid_r, block_r, 0, stream, a);
+    else if (a.epi.out && a.epi.ks_beta > 0)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true, false, true>), grid_r, block_r, 0, stream, a);
+    else if (a.epi.out && lz)
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true, true>), grid_r, block_r, 0, stream, a);
     else if (a.epi.out)
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true, false>), grid_r, block_r, 0, stream, a);

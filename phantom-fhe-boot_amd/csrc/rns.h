@@ -126,7 +126,9 @@ hipError_t modup_copy_digits(const uint64_t* c2, uint64_t* t_mod_up, size_t n, s
 // key_switch_inner_prod_c2_and_evk (src/eval_key_switch.cu:26-85).  evk: device array of
 // beta pointers to [2][size_QP][n] key digits; modulus/barrett over the full QP chain.
 // Optional addend: cx[t][l] += P c[t][l] for the Ql limbs (c [2][size_ql][n], P mod q_l with
-// Shoup quotients), i.e. the P-scaled extended form of (c0, c1) + KeySwitch(c2).
+// Shoup quotients), i.e. the P-scaled extended form of (c0, c1) + KeySwitch(c2).  first_limb:
+// only limbs [first_limb, size_ql + size_p) are formed (first_limb = size_ql: the P half, when the
+// moddown's NTT epilogue forms the Ql half itself, ntt.h NttEpilogue::ks_beta).
 struct KsAddend {
   const uint64_t* c = nullptr;
   const uint64_t* pmod = nullptr;
@@ -135,7 +137,7 @@ struct KsAddend {
 hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const* evk, uint64_t* cx,
                                 const uint64_t* qp_mod, const uint64_t* qp_barrett, size_t n, size_t size_ql,
                                 size_t size_q, size_t size_p, size_t beta, hipStream_t s,
-                                const KsAddend& add = KsAddend{});
+                                const KsAddend& add = KsAddend{}, size_t first_limb = 0);
 // Coefficient-domain moddown whose result goes straight into a modup (a giant-step rotation of
 // an extended-basis ciphertext): c1 and delta [size_ql][n] coefficient form,
 //   y = (c1 - delta) P^-1 mod q_l -> t_mod_up[l / alpha][l]  (the digit's own limb)

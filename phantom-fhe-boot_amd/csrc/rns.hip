@@ -602,9 +602,9 @@ __global__ __launch_bounds__(kBlock) void ks_inner_kernel(const uint64_t* __rest
                                                           const uint64_t* qp, const uint64_t* qpb, uint32_t log_n,
                                                           size_t pairs, uint32_t size_ql, uint32_t size_q,
                                                           size_t size_qlp_n, size_t size_qp_n, uint32_t beta,
-                                                          KsAddend add) {
+                                                          KsAddend add, size_t first) {
   for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kBlock) {
-    const size_t e = 2 * i;
+    const size_t e = first + 2 * i;
     const uint32_t nid = static_cast<uint32_t>(e >> log_n);
     const uint32_t twr = nid >= size_ql ? size_q + (nid - size_ql) : nid;
     const size_t kk = e & ((size_t(1) << log_n) - 1);
@@ -1175,12 +1175,15 @@ hipError_t modup_copy_digits(const uint64_t* c2, uint64_t* t_mod_up, size_t n, s
 
 hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const* evk, uint64_t* cx,
                                 const uint64_t* qp_mod, const uint64_t* qp_barrett, size_t n, size_t size_ql,
-                                size_t size_q, size_t size_p, size_t beta, hipStream_t s, const KsAddend& add) {
+                                size_t size_q, size_t size_p, size_t beta, hipStream_t s, const KsAddend& add,
+                                size_t first_limb) {
   const size_t size_qlp = size_ql + size_p;
-  const size_t pairs = n * size_qlp / 2;
+  if (first_limb > size_qlp || (add.c && first_limb > 0)) return hipErrorInvalidValue;
+  const size_t pairs = n * (size_qlp - first_limb) / 2;
+  if (pairs == 0) return hipSuccess;
   ks_inner_kernel<<<grid_for(pairs), kBlock, 0, s>>>(t_mod_up, evk, cx, qp_mod, qp_barrett, __builtin_ctzll(n), pairs,
                                                     (uint32_t)size_ql, (uint32_t)size_q, size_qlp * n,
-                                                    (size_q + size_p) * n, (uint32_t)beta, add);
+                                                    (size_q + size_p) * n, (uint32_t)beta, add, first_limb * n);
   return hipGetLastError();
 }
 

@@ -279,7 +279,7 @@ void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables
 }
 
 void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx::NttTables& ntt, hipStream_t s,
-                          size_t polys) const {
+                          size_t polys, const uint64_t* tmu, const uint64_t* const* evk) const {
   // every stage runs once over all `polys` polynomials (ct [polys][Ql][n], cx [polys][QlP][n])
   const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_;
   const int np = static_cast<int>(polys);
@@ -305,6 +305,14 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
   epi.w = d_bigPInv_mod_q_.get();
   epi.ws = d_bigPInv_mod_q_shoup_.get();
   epi.accumulate = accumulate;
+  if (tmu) {
+    if (beta() > (size_t)phx::kMaxKsBeta) throw std::invalid_argument("moddown_add: too many key-switch digits");
+    epi.ks_beta = (int)beta();
+    epi.tmu = tmu;
+    epi.tmu_stride = size_QlP * n_;
+    epi.evk = evk;
+    epi.evk_poly_stride = size_QP() * n_;
+  }
   const phx::LimbMap dm = phx::LimbMap::contiguous((int)size_Ql, 0).batched(np);
   if (fused) {
     phx::BconvPrologue bcv;

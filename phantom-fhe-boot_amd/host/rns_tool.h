@@ -46,9 +46,11 @@ class RnsTool {
   void modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables& ntt, hipStream_t s) const;
   // moddown_from_NTT (src/rns_bconv.cu:791-843) fused with add_to_ct_kernel, for `polys`
   // polynomials at once: cx is [polys][size_QlP][n] NTT form (its P limbs are clobbered);
-  // ct [polys][size_Ql][n] (+)= moddown(cx).
+  // ct [polys][size_Ql][n] (+)= moddown(cx).  With tmu/evk (a key switch's t_mod_up and key
+  // digits, polys = 2): only the P limbs of cx are read; its Ql limbs, the inner product
+  // sum_d tmu[d] evk[d][p], are formed in the finish's epilogue (ntt.h NttEpilogue::ks_beta).
   void moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx::NttTables& ntt, hipStream_t s,
-                   size_t polys = 1) const;
+                   size_t polys = 1, const uint64_t* tmu = nullptr, const uint64_t* const* evk = nullptr) const;
   // moddown of an extended-basis polynomial fused with the modup of its result (giant-step
   // rotations): c1 [size_QlP][n] NTT form holding P x (a polynomial over Ql) -> t_mod_up
   // [beta][size_QlP][n] = modup(round(c1 / P)).  The subtraction happens in the coefficient
