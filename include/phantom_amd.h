@@ -128,6 +128,13 @@ int phantom_square(const phantom_context *ctx, size_t chain_index, const uint64_
  * key_digits: host array of dnum device pointers, each a [2][size_QP][n] key digit. */
 int phantom_relinearize(const phantom_context *ctx, size_t chain_index, uint64_t *ct,
                         const uint64_t *const *key_digits, size_t dnum, hipStream_t stream);
+/* relinearize_inplace followed by rescale_to_next_inplace (src/evaluate.cu:1552-1589, 1591-1647) as
+ * ONE division by P q_last (the bootstrap's EvalMult + ModReduce path): ct3 [3][L][n] at
+ * chain_index -> out [2][L-1][n]; the inner product's first L-1 limbs are formed inside the
+ * finish (NTT epilogue).  Equals moddown_from_NTT with {q_last} u P as the special basis applied
+ * to the P-scaled extended (c0, c1) + KeySwitch(c2). */
+int phantom_relinearize_rescale(const phantom_context *ctx, size_t chain_index, const uint64_t *ct3, uint64_t *out,
+                                const uint64_t *const *key_digits, size_t dnum, hipStream_t stream);
 /* keyswitch_inplace core: ct [2][L][n] += KeySwitch(c2 [L][n]) */
 int phantom_keyswitch(const phantom_context *ctx, size_t chain_index, uint64_t *ct, const uint64_t *c2,
                       const uint64_t *const *key_digits, size_t dnum, hipStream_t stream);

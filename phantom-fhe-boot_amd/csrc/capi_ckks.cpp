@@ -10,6 +10,7 @@
 
 #include "../host/buffer.h"
 #include "../host/capi_internal.h"
+#include "../host/ckks_eval.h"
 #include "../host/context.h"
 #include "../host/evaluate.h"
 #include "../host/numth.h"
@@ -129,6 +130,17 @@ int phantom_relinearize(const phantom_context* ctx, size_t chain_index, uint64_t
     const auto& rt = tool(ctx, chain_index);
     const size_t L = rt.size_Ql(), n = ctx->ctx->poly_degree();
     return phantom_keyswitch(ctx, chain_index, ct, ct + 2 * L * n, key_digits, dnum, stream);
+  });
+}
+
+int phantom_relinearize_rescale(const phantom_context* ctx, size_t chain_index, const uint64_t* ct3, uint64_t* out,
+                                const uint64_t* const* key_digits, size_t dnum, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& rt = tool(ctx, chain_index);
+    auto* c = const_cast<phantom_context*>(ctx);
+    const uint64_t* const* evk = c->device_key_array(key_digits, dnum, rt.beta());
+    phantom::relinearize_rescale_raw(*ctx->ctx, chain_index, ct3, out, evk, stream);
+    return from_hip(hipGetLastError());
   });
 }
 

@@ -108,6 +108,12 @@ struct NttEpilogue {
   size_t tmu_stride = 0;
   const uint64_t* const* evk = nullptr;
   size_t evk_poly_stride = 0;
+  // optional addend of the key-switch form (rns.h KsAddend): c[p][i][k] += P_i * add_c[p][i][k]
+  // (add_c polynomial stride add_stride), the P-scaled (c0, c1) of a relinearize + rescale
+  const uint64_t* add_c = nullptr;
+  size_t add_stride = 0;
+  const uint64_t* pmod = nullptr;
+  const uint64_t* pmod_shoup = nullptr;
 };
 hipError_t ntt_forward_fused(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                              const uint64_t* bcast, size_t bcast_stride, const NttEpilogue& epi, hipStream_t stream);

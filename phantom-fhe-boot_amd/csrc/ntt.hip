@@ -499,6 +499,8 @@ __device__ __forceinline__ void ks_epilogue(const KArgs& a, const TileRef& tr, c
   for (int d = 0; d < kMaxKsBeta; ++d) kp[d] = d < beta ? a.epi.evk[d] + tr.poly * a.epi.evk_poly_stride + e : tm;
   uint64_t* o = a.epi.out + tr.poly * a.epi.out_stride + e;
   const uint64_t w = a.epi.w[tr.buf_limb], ws = a.epi.ws[tr.buf_limb];
+  const uint64_t* ad = a.epi.add_c ? a.epi.add_c + tr.poly * a.epi.add_stride + e : nullptr;
+  const uint64_t pm = ad ? a.epi.pmod[tr.buf_limb] : 0, pms = ad ? a.epi.pmod_shoup[tr.buf_limb] : 0;
   uint64_t tb[2][kMaxKsBeta][KC], kb[2][kMaxKsBeta][KC], ob[2][KC];
   auto load = [&](int c, int s) {
 #pragma unroll
@@ -514,6 +516,9 @@ __device__ __forceinline__ void ks_epilogue(const KArgs& a, const TileRef& tr, c
     if (acc_out) {
 #pragma unroll
       for (int i = 0; i < KC; ++i) ob[s][i] = __builtin_nontemporal_load(o + (c * KC + i) * T);
+    } else if (ad) {  // (the two are never both set: accumulate is the relinearize form)
+#pragma unroll
+      for (int i = 0; i < KC; ++i) ob[s][i] = __builtin_nontemporal_load(ad + (c * KC + i) * T);
     }
   };
   load(0, 0);
@@ -526,7 +531,9 @@ __device__ __forceinline__ void ks_epilogue(const KArgs& a, const TileRef& tr, c
 #pragma unroll
       for (int d = 0; d < kMaxKsBeta; ++d)
         if (d < beta) add128(acc, mul_wide(tb[s][d][i], kb[s][d][i]));
-      uint64_t v = mul_shoup(sub_mod(barrett_reduce_128(acc, q, r0, r1), y[c * KC + i], q), w, ws, q);
+      uint64_t cx = barrett_reduce_128(acc, q, r0, r1);
+      if (ad) cx = add_mod(cx, mul_shoup(ob[s][i], pm, pms, q), q);
+      uint64_t v = mul_shoup(sub_mod(cx, y[c * KC + i], q), w, ws, q);
       if (acc_out) v = add_mod(v, ob[s][i], q);
       store_wt(o + (c * KC + i) * T, v);
     }

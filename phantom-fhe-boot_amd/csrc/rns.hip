@@ -1178,7 +1178,7 @@ hipError_t keyswitch_inner_prod(const uint64_t* t_mod_up, const uint64_t* const*
                                 size_t size_q, size_t size_p, size_t beta, hipStream_t s, const KsAddend& add,
                                 size_t first_limb) {
   const size_t size_qlp = size_ql + size_p;
-  if (first_limb > size_qlp || (add.c && first_limb > 0)) return hipErrorInvalidValue;
+  if (first_limb > size_qlp) return hipErrorInvalidValue;
   const size_t pairs = n * (size_qlp - first_limb) / 2;
   if (pairs == 0) return hipSuccess;
   ks_inner_kernel<<<grid_for(pairs), kBlock, 0, s>>>(t_mod_up, evk, cx, qp_mod, qp_barrett, __builtin_ctzll(n), pairs,

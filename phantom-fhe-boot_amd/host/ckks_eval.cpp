@@ -298,27 +298,50 @@ void EvalSubAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const P
   sub_inplace(ctx, a, AtLevel(ctx, b, target, sf, tmp));
 }
 
-PhantomCiphertext RelinearizeRescale(const PhantomContext& ctx, const PhantomCiphertext& d, const PhantomRelinKey& rlk) {
-  if (d.size() != 3) throw std::invalid_argument("destination_size must be 3");
-  const RnsTool& rt = ctx.get_context_data(d.chain_index()).gpu_rns_tool();
+void relinearize_rescale_raw(const PhantomContext& ctx, size_t chain_index, const uint64_t* d3, uint64_t* out,
+                             const uint64_t* const* evk, hipStream_t s) {
+  if (chain_index < 1 || chain_index + 1 >= ctx.total_parm_size())
+    throw std::invalid_argument("end of modulus switching chain reached");
+  const RnsTool& rt = ctx.get_context_data(chain_index).gpu_rns_tool();
   const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P(), beta = rt.beta();
-  if (d.chain_index() + 1 >= ctx.total_parm_size()) throw std::invalid_argument("end of modulus switching chain reached");
-  hipStream_t s = ctx.stream();
   uint64_t* t_mod_up = rt.workspace().get(s, Workspace::kKsModup, beta * QlP * n);
-  rt.modup(t_mod_up, d.data() + 2 * Ql * n, ctx.gpu_rns_tables(), s);
+  rt.modup(t_mod_up, d3 + 2 * Ql * n, ctx.gpu_rns_tables(), s);
   uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * QlP * n);
   phx::KsAddend add;
-  add.c = d.data();
+  add.c = d3;
   add.pmod = rt.bigP_mod_q();
   add.pmod_shoup = rt.bigP_mod_q_shoup();
-  hip_ok(phx::keyswitch_inner_prod(t_mod_up, rlk.public_keys_ptr(), cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, Ql,
-                                   ctx.size_Q(), ctx.size_P(), beta, s, add),
+  // the inner product's dropped limbs (q_last, P) here; its first Ql - 1 limbs inside the finish
+  // (NTT epilogue, ntt.h NttEpilogue::ks_beta), so they make no HBM round trip (PHX_KS_EPI=0: off)
+  const bool fuse = ks_epilogue_enabled() && beta <= (size_t)phx::kMaxKsBeta && n >= 1024 && Ql >= 2;
+  hip_ok(phx::keyswitch_inner_prod(t_mod_up, evk, cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, Ql, ctx.size_Q(),
+                                   ctx.size_P(), beta, s, add, fuse ? Ql - 1 : 0),
          "relinearize inner product");
+  phx::NttEpilogue ks;
+  if (fuse) {
+    ks.ks_beta = (int)beta;
+    ks.tmu = t_mod_up;
+    ks.tmu_stride = QlP * n;
+    ks.evk = evk;
+    ks.evk_poly_stride = ctx.size_QP() * n;
+    ks.add_c = d3;
+    ks.add_stride = Ql * n;
+    ks.pmod = rt.bigP_mod_q();
+    ks.pmod_shoup = rt.bigP_mod_q_shoup();
+  }
   traffic::keys(traffic::limb_bytes(beta * 2 * QlP, n));
   traffic::ciphertexts(traffic::limb_bytes(3 * Ql + 2 * (Ql - 1), n));  // d read, the rescaled result written
+  rt.moddown_rescale(out, cx, ctx.gpu_rns_tables(), s, 2, fuse ? &ks : nullptr);
+}
+
+PhantomCiphertext RelinearizeRescale(const PhantomContext& ctx, const PhantomCiphertext& d, const PhantomRelinKey& rlk) {
+  if (d.size() != 3) throw std::invalid_argument("destination_size must be 3");
+  if (d.chain_index() + 1 >= ctx.total_parm_size()) throw std::invalid_argument("end of modulus switching chain reached");
+  const RnsTool& rt = ctx.get_context_data(d.chain_index()).gpu_rns_tool();
+  hipStream_t s = ctx.stream();
   PhantomCiphertext out;
   out.resize(ctx, d.chain_index() + 1, 2, s, false);
-  rt.moddown_rescale(out.data(), cx, ctx.gpu_rns_tables(), s, 2);
+  relinearize_rescale_raw(ctx, d.chain_index(), d.data(), out.data(), rlk.public_keys_ptr(), s);
   out.set_ntt_form(true);
   out.set_scale(d.scale() / static_cast<double>(rt.base_Ql().back()));
   out.set_correction_factor(d.correction_factor());

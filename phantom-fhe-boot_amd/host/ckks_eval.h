@@ -79,6 +79,10 @@ void EvalSubAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const P
 // relinearize a 3-polynomial product and rescale it in one key-switch: (c0, c1) + KS(c2) is formed
 // P-scaled in the extended basis and divided by P q_last at once (RnsTool::moddown_rescale)
 PhantomCiphertext RelinearizeRescale(const PhantomContext& ctx, const PhantomCiphertext& d3, const PhantomRelinKey& rlk);
+// the same on raw device buffers: d3 [3][Ql][n] at chain_index -> out [2][Ql - 1][n];
+// evk: device array of the relinearization key's digit pointers
+void relinearize_rescale_raw(const PhantomContext& ctx, size_t chain_index, const uint64_t* d3, uint64_t* out,
+                             const uint64_t* const* evk, hipStream_t s);
 // KeySwitchDown followed by a rescale, as one division by P q_last
 PhantomCiphertext KeySwitchDownRescale(const PhantomContext& ctx, PhantomCiphertext& ext);
 // rescale(relinearize(factor a b + sum_t coeff_t t + constant)) with one key switch: every term

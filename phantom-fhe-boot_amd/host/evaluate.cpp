@@ -13,6 +13,14 @@
 
 namespace phantom {
 
+bool ks_epilogue_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PHX_KS_EPI");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, const uint64_t* c2,
                    const uint64_t* const* evk, hipStream_t s) {
   if (ctx.size_P() == 0) throw std::invalid_argument("key switching requires special primes");
@@ -26,11 +34,7 @@ void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, 
   uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * size_QlP * n);
   // the inner product's P limbs here; its Ql limbs inside the moddown finish (NTT epilogue), so
   // they make no HBM round trip (PHX_KS_EPI=0: the whole inner product in one kernel, as before)
-  static const bool ks_epi = [] {
-    const char* e = std::getenv("PHX_KS_EPI");
-    return !(e && e[0] == '0');
-  }();
-  const bool fuse = ks_epi && beta <= (size_t)phx::kMaxKsBeta && n >= 1024;
+  const bool fuse = ks_epilogue_enabled() && beta <= (size_t)phx::kMaxKsBeta && n >= 1024;
   hip_ok(phx::keyswitch_inner_prod(t_mod_up, evk, cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, size_Ql,
                                    ctx.size_Q(), ctx.size_P(), beta, s, phx::KsAddend{}, fuse ? size_Ql : 0),
          "keyswitch inner product");

@@ -14,6 +14,9 @@ namespace phantom {
 void keyswitch_inplace(const PhantomContext& ctx, PhantomCiphertext& encrypted, const uint64_t* c2,
                        const uint64_t* const* evk);
 // the same on raw device buffers: ct is [2][size_Ql][n] at `chain_index`, c2 [size_Ql][n]
+// whether key switches form the Ql half of their inner product inside the moddown finish (the NTT
+// epilogue, ntt.h NttEpilogue::ks_beta); PHX_KS_EPI=0 turns it off (the separate kernel)
+bool ks_epilogue_enabled();
 void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, const uint64_t* c2,
                    const uint64_t* const* evk, hipStream_t s);
 

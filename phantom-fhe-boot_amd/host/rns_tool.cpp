@@ -365,7 +365,7 @@ void RnsTool::moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTabl
 }
 
 void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables& ntt, hipStream_t s,
-                              size_t polys) const {
+                              size_t polys, const phx::NttEpilogue* ks) const {
   const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_;
   if (size_Ql < 2 || size_P_ == 0) throw std::invalid_argument("end of modulus switching chain reached");
   const size_t Ln = size_Ql - 1;
@@ -389,6 +389,18 @@ void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables&
   epi.out_stride = Ln * n_;
   epi.w = d_PQinv_.get();
   epi.ws = d_PQinv_shoup_.get();
+  if (ks) {
+    if (ks->ks_beta > phx::kMaxKsBeta) throw std::invalid_argument("moddown_rescale: too many key-switch digits");
+    epi.ks_beta = ks->ks_beta;
+    epi.tmu = ks->tmu;
+    epi.tmu_stride = ks->tmu_stride;
+    epi.evk = ks->evk;
+    epi.evk_poly_stride = ks->evk_poly_stride;
+    epi.add_c = ks->add_c;
+    epi.add_stride = ks->add_stride;
+    epi.pmod = ks->pmod;
+    epi.pmod_shoup = ks->pmod_shoup;
+  }
   const phx::LimbMap om = phx::LimbMap::contiguous((int)Ln, 0).batched(np);
   if (fused) {
     phx::BconvPrologue bcv;

@@ -65,8 +65,10 @@ class RnsTool {
   // the ciphertext rescaled to the next level (scale S / q_last).  One INTT over the 1 + size_P
   // dropped limbs, one base conversion, one NTT and one finish instead of a moddown (INTT P,
   // NTT Ql) followed by a rescale (INTT 1, NTT Ql - 1).  cx's dropped limbs are clobbered.
+  // With `ks` (polys = 2, a key switch's t_mod_up / key digits / P-scaled addend): only the dropped
+  // limbs of cx are read; its first size_Ql - 1 limbs are formed in the finish's epilogue.
   void moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables& ntt, hipStream_t s,
-                       size_t polys = 1) const;
+                       size_t polys = 1, const phx::NttEpilogue* ks = nullptr) const;
   // divide_and_round_q_last_ntt (src/rns.cu:1160-1184): in [polys][size_Ql][n] -> out
   // [polys][size_Ql-1][n], NTT form.  `in` is not modified.
   void rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const phx::NttTables& ntt,

@@ -40,6 +40,7 @@ _SIGS = {
     "phantom_multiply": (ctypes.c_int, [vp, sz, vp, vp, vp, vp]),
     "phantom_square": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_relinearize": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, vp]),
+    "phantom_relinearize_rescale": (ctypes.c_int, [vp, sz, vp, vp, ctypes.POINTER(vp), sz, vp]),
     "phantom_keyswitch": (ctypes.c_int, [vp, sz, vp, vp, ctypes.POINTER(vp), sz, vp]),
     "phantom_modup": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_keyswitch_inner_prod": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, vp, vp]),

@@ -216,6 +216,46 @@ def test_relinearize(request, rng, fixture, chain):
     assert np.array_equal(got[:2 * L * ctx.n], want[:2 * L * ctx.n])
 
 
+@pytest.mark.parametrize("fixture,chain", [("c3", 1), ("c3", 30), ("small", 1), ("small", 5)])
+def test_relinearize_rescale(request, rng, fixture, chain):
+    """The bootstrap's EvalMult + ModReduce key switch (include/phantom_amd.h
+    phantom_relinearize_rescale): the P-scaled (c0, c1) + KeySwitch(c2), divided by P q_last at
+    once, with the inner product's first L-1 limbs formed in the finish's epilogue; bit-exact vs
+    the oracle's inner product + addend + moddown_from_NTT over the special basis {q_last} u P."""
+    ctx = request.getfixturevalue(fixture)
+    ql, p = ctx.ql(chain), ctx.moduli[ctx.size_Q:]
+    L, n = len(ql), ctx.n
+    ct = _rand_ct(rng, ctx, chain, 3)
+    keys, dkeys = _keys(rng, ctx)
+    d = to_dev(ct)
+    dout = to_dev(np.zeros(2 * (L - 1) * n, dtype=np.uint64))
+    kp = PA.ptr_array([ptr(k) for k in dkeys])
+    PA.check(_lib().phantom_relinearize_rescale(ctx.handle, chain, ptr(d), ptr(dout), kp, len(dkeys), stream()))
+    beta = -(-L // ctx.size_P)
+    qlp = list(ql) + list(p)
+    tmu = np.zeros(beta * len(qlp) * n, dtype=np.uint64)
+    O.lib().or_modup(O.P(ct[2 * L * n:].copy()), O.P(tmu), n, O.P(O.arr(ql)), L, O.P(O.arr(p)), len(p))
+    cx = np.zeros(2 * len(qlp) * n, dtype=np.uint64)
+    O.lib().or_keyswitch_inner_prod(O.P(tmu), _oracle_keys(keys), O.P(cx), n, L, ctx.size_Q, ctx.size_P, beta,
+                                    O.P(O.arr(ctx.moduli)))
+    P = 1
+    for v in p:
+        P *= int(v)
+    pmod = O.arr([P % int(q) for q in ql])
+    want = []
+    for t in range(2):
+        c = cx[t * len(qlp) * n:(t + 1) * len(qlp) * n].copy()
+        scaled = np.zeros(L * n, dtype=np.uint64)
+        O.lib().or_poly_mul_scalar(O.P(ct[t * L * n:(t + 1) * L * n].copy()), O.P(pmod), O.P(scaled), n, L,
+                                   O.P(O.arr(ql)))
+        O.lib().or_poly_add(O.P(c[:L * n].copy()), O.P(scaled), O.P(c[:L * n]), n, L, O.P(O.arr(ql)))
+        w = np.zeros((L - 1) * n, dtype=np.uint64)
+        O.lib().or_moddown_from_ntt(O.P(c), O.P(w), n, O.P(O.arr(ql[:-1])), L - 1, O.P(O.arr([ql[-1]] + list(p))),
+                                    len(p) + 1)
+        want.append(w)
+    assert np.array_equal(to_host(dout), np.concatenate(want))
+
+
 @pytest.mark.parametrize("fixture,chain", [("c3", 1), ("c3", 44), ("small", 1), ("small", 6)])
 def test_rescale(request, rng, fixture, chain):
     ctx = request.getfixturevalue(fixture)
