@@ -5,6 +5,9 @@
 One step = forward NTT followed by inverse NTT of one [44][65536] uint64 batch that is
 already resident in HBM.  Each step uses the next buffer of a ring whose total size
 (> 256 MiB) exceeds the Infinity Cache, so every forward transform reads its input from HBM.
+The steps' batches are independent and are dealt round-robin to --c2-streams HIP streams (3), so
+the transforms of one batch fill another's launch ramp and store tail; `single_stream` reports
+the same steps on one stream.
 value = algorithmic bytes (16 B per coefficient per transform, the convention of the
 reference's benchmark/ntt_bench.cu:96-97) of all steps on all ranks / max-over-ranks time.
 
@@ -321,6 +324,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--c2-streams", type=int, default=3, help="C2: HIP streams the independent batches are dealt to")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 (mult+relin+rescale) leg")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (bootstrap latency) leg")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (sharded bootstrap batch) leg")
@@ -350,37 +354,53 @@ def main():
     mods = PA.coeff_modulus_create(N, C3_BITS)[:L]
     tables = PA.NttTables(N, mods)
 
+    # the steps (independent batches) are dealt round-robin to `c2_streams` HIP streams, so one
+    # batch's transforms fill the launch ramp and store tail of another's (a pass waits ~2 us for
+    # its first data and drains its stores for ~3 us: profiles/r03/ntt_experiments/); a buffer of
+    # the ring always stays on one stream (nbuf is a multiple of the stream count)
+    K = max(1, args.c2_streams)
     nbuf = max(2, RING_BYTES // (8 * N * L) + 1)
+    nbuf = -(-nbuf // K) * K
     rng = np.random.default_rng(0x5EED + rank)
     base = np.concatenate([rng.integers(0, q, size=N, dtype=np.uint64) for q in mods])
     ring = [torch.from_numpy(base.view(np.int64)).cuda() for _ in range(nbuf)]
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
+    lanes = [torch.cuda.Stream() for _ in range(K)]
+    for ls in lanes:
+        ls.wait_stream(stream)
 
-    def step(i, ev=None):
+    def step(i, ev=None, k=None):
         d = ring[i % nbuf].data_ptr()
+        st = stream if k is None else lanes[i % k]
+        h = st.cuda_stream
         if ev is not None:
-            ev[0].record(stream)
-        PA.check(lib.phantom_nwt_forward_inplace(d, tables.handle, L, 0, sh))
+            ev[0].record(st)
+        PA.check(lib.phantom_nwt_forward_inplace(d, tables.handle, L, 0, h))
         if ev is not None:
-            ev[1].record(stream)
-        PA.check(lib.phantom_nwt_backward_inplace(d, tables.handle, L, 0, sh))
+            ev[1].record(st)
+        PA.check(lib.phantom_nwt_backward_inplace(d, tables.handle, L, 0, h))
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    def timed(k):
+        for i in range(args.warmup):
+            step(i, k=k)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(i, k=k)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
 
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(K)
+    elapsed_1 = timed(1) if K > 1 else elapsed  # the same steps on one stream, for reference
+    for ls in lanes:
+        stream.wait_stream(ls)
 
     # forward-NTT launch duration for the roofline: HIP events on the launch stream around
     # `steps` back-to-back forward transforms over the buffer ring (average per launch), and,
@@ -396,8 +416,8 @@ def main():
     torch.cuda.synchronize()
     fwd_ms = fa.elapsed_time(fb) / args.steps
     fwd_ms_isolated = float(np.mean([a.elapsed_time(b) for a, b in events]))
-    elapsed, fwd_ms, fwd_ms_isolated = max_over_ranks(dist if world > 1 else None,
-                                                      [elapsed, fwd_ms, fwd_ms_isolated], "cuda")
+    elapsed, elapsed_1, fwd_ms, fwd_ms_isolated = max_over_ranks(
+        dist if world > 1 else None, [elapsed, elapsed_1, fwd_ms, fwd_ms_isolated], "cuda")
 
     c5 = None
     if not args.no_c5:
@@ -406,6 +426,7 @@ def main():
 
     # parity spot-check of the last buffer state is done by tests/; here just sanity
     value = job_throughput(2 * BYTES_PER_TRANSFORM * args.steps, world, elapsed) / 1e9
+    value_1 = job_throughput(2 * BYTES_PER_TRANSFORM * args.steps, world, elapsed_1) / 1e9
     achieved = BYTES_PER_TRANSFORM / (fwd_ms * 1e-3) / 1e9
 
     if rank == 0:
@@ -428,8 +449,10 @@ def main():
                 "limbs": L,
                 "batch_per_rank": 1,
                 "buffer_ring": nbuf,
-                "parallelism": f"replicas x{world} (independent batches per rank)",
+                "streams_per_rank": K,
+                "parallelism": f"replicas x{world} (independent batches per rank, dealt to {K} HIP streams)",
             },
+            "single_stream": {"value": round(value_1, 2), "ms_per_step": round(elapsed_1 / args.steps * 1e3, 5)},
             "roofline": {
                 "bound": "hbm",
                 "kernel": "forward NTT (ntt_col_pass + ntt_row_pass)",
@@ -437,6 +460,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "job_frac": round(value / world / HBM_PEAK_GBS, 4),
                 "fwd_ms": round(fwd_ms, 5),
                 "fwd_ms_isolated": round(fwd_ms_isolated, 5),
                 "traffic": pmc_traffic(),
