@@ -94,7 +94,7 @@ hipError_t ntt_forward(const NttTables& t, const uint64_t* in, uint64_t* out, co
 //    (src/eval_key_switch.cu:26-85 for limbs i < size_Ql), so the inner product's Ql half never
 //    makes an HBM round trip (tmu: digit stride tmu_stride; evk: device array of ks_beta digit
 //    pointers, polynomial stride evk_poly_stride; the buffer limbs must be the first Ql limbs).
-constexpr int kMaxKsBeta = 4;
+constexpr int kMaxKsBeta = 3;  // digits of the key-switch form (C3: 3, the C4 chain: <= 3)
 struct NttEpilogue {
   const uint64_t* c = nullptr;
   size_t c_stride = 0;

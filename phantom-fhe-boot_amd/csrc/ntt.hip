@@ -482,44 +482,39 @@ __device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr
   store_wt(o, v);
 }
 
-// Key-switch epilogue (NttEpilogue::ks_beta > 0): out = (sum_d tmu[d] evk[d][p] mod q - y) w
-// (+ out), the inner product of eval_key_switch.cu:26-85 (128-bit sums, one Barrett-128 per
-// element) formed where the moddown finish consumes it.  KC elements at a time; the next group's
-// loads are issued before the current group's products.
-template <int T>
-__device__ __forceinline__ void ks_epilogue(const KArgs& a, const TileRef& tr, const uint64_t (&y)[E], uint64_t q,
-                                            uint64_t r0, uint64_t r1) {
+// Key-switch epilogue (NttEpilogue::ks_beta > 0): out = (sum_d tmu[d] evk[d][p] (+ P add) mod q
+// - y) w (+ out), the inner product of eval_key_switch.cu:26-85 (128-bit sums, one Barrett-128
+// per element) formed where the moddown finish consumes it.  KC elements at a time; the next
+// group's loads are issued before the current group's products.  BETA is a template parameter
+// and every load is unconditional (the third operand stream is `out` when accumulating, else the
+// addend, else a harmless re-read of tmu), so the compiler can count the loads in flight
+// (s_waitcnt vmcnt(N)) instead of draining them all (vmcnt(0)) before every group.
+template <int T, int BETA>
+__device__ __forceinline__ void ks_epilogue_b(const KArgs& a, const TileRef& tr, const uint64_t (&y)[E], uint64_t q,
+                                              uint64_t r0, uint64_t r1) {
   constexpr int KC = 4, NC = E / KC;
   const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
-  const int beta = __builtin_amdgcn_readfirstlane(a.epi.ks_beta);
   const bool acc_out = a.epi.accumulate;
   const uint64_t* tm = a.epi.tmu + e;
-  const uint64_t* kp[kMaxKsBeta];
+  const uint64_t* kp[BETA];
 #pragma unroll
-  for (int d = 0; d < kMaxKsBeta; ++d) kp[d] = d < beta ? a.epi.evk[d] + tr.poly * a.epi.evk_poly_stride + e : tm;
+  for (int d = 0; d < BETA; ++d) kp[d] = a.epi.evk[d] + tr.poly * a.epi.evk_poly_stride + e;
   uint64_t* o = a.epi.out + tr.poly * a.epi.out_stride + e;
   const uint64_t w = a.epi.w[tr.buf_limb], ws = a.epi.ws[tr.buf_limb];
   const uint64_t* ad = a.epi.add_c ? a.epi.add_c + tr.poly * a.epi.add_stride + e : nullptr;
   const uint64_t pm = ad ? a.epi.pmod[tr.buf_limb] : 0, pms = ad ? a.epi.pmod_shoup[tr.buf_limb] : 0;
-  uint64_t tb[2][kMaxKsBeta][KC], kb[2][kMaxKsBeta][KC], ob[2][KC];
+  const uint64_t* third = acc_out ? o : (ad ? ad : tm);  // (accumulate and addend never come together)
+  uint64_t tb[2][BETA][KC], kb[2][BETA][KC], ob[2][KC];
   auto load = [&](int c, int s) {
 #pragma unroll
-    for (int d = 0; d < kMaxKsBeta; ++d) {
-      if (d < beta) {
+    for (int d = 0; d < BETA; ++d)
 #pragma unroll
-        for (int i = 0; i < KC; ++i) {
-          tb[s][d][i] = __builtin_nontemporal_load(tm + d * a.epi.tmu_stride + (c * KC + i) * T);
-          kb[s][d][i] = __builtin_nontemporal_load(kp[d] + (c * KC + i) * T);
-        }
+      for (int i = 0; i < KC; ++i) {
+        tb[s][d][i] = __builtin_nontemporal_load(tm + d * a.epi.tmu_stride + (c * KC + i) * T);
+        kb[s][d][i] = __builtin_nontemporal_load(kp[d] + (c * KC + i) * T);
       }
-    }
-    if (acc_out) {
 #pragma unroll
-      for (int i = 0; i < KC; ++i) ob[s][i] = __builtin_nontemporal_load(o + (c * KC + i) * T);
-    } else if (ad) {  // (the two are never both set: accumulate is the relinearize form)
-#pragma unroll
-      for (int i = 0; i < KC; ++i) ob[s][i] = __builtin_nontemporal_load(ad + (c * KC + i) * T);
-    }
+    for (int i = 0; i < KC; ++i) ob[s][i] = __builtin_nontemporal_load(third + (c * KC + i) * T);
   };
   load(0, 0);
   static_for<NC>([&](auto cc) {
@@ -529,8 +524,7 @@ __device__ __forceinline__ void ks_epilogue(const KArgs& a, const TileRef& tr, c
     for (int i = 0; i < KC; ++i) {
       u128 acc{0, 0};
 #pragma unroll
-      for (int d = 0; d < kMaxKsBeta; ++d)
-        if (d < beta) add128(acc, mul_wide(tb[s][d][i], kb[s][d][i]));
+      for (int d = 0; d < BETA; ++d) add128(acc, mul_wide(tb[s][d][i], kb[s][d][i]));
       uint64_t cx = barrett_reduce_128(acc, q, r0, r1);
       if (ad) cx = add_mod(cx, mul_shoup(ob[s][i], pm, pms, q), q);
       uint64_t v = mul_shoup(sub_mod(cx, y[c * KC + i], q), w, ws, q);
@@ -538,6 +532,16 @@ __device__ __forceinline__ void ks_epilogue(const KArgs& a, const TileRef& tr, c
       store_wt(o + (c * KC + i) * T, v);
     }
   });
+}
+
+template <int T>
+__device__ __forceinline__ void ks_epilogue(const KArgs& a, const TileRef& tr, const uint64_t (&y)[E], uint64_t q,
+                                            uint64_t r0, uint64_t r1) {
+  switch (__builtin_amdgcn_readfirstlane(a.epi.ks_beta)) {
+    case 1: ks_epilogue_b<T, 1>(a, tr, y, q, r0, r1); break;
+    case 2: ks_epilogue_b<T, 2>(a, tr, y, q, r0, r1); break;
+    default: ks_epilogue_b<T, 3>(a, tr, y, q, r0, r1); break;
+  }
 }
 
 // Row-pass block order of the key-switch epilogue: the polynomials' blocks of one row group are
