@@ -16,7 +16,7 @@ mods = PA.coeff_modulus_create(N, [60] + [50] * 44 + [60] * 15)[:L]
 t = PA.NttTables(N, mods)
 rng = np.random.default_rng(0x5EED)
 base = np.concatenate([rng.integers(0, q, size=N, dtype=np.uint64) for q in mods])
-ring = [torch.from_numpy(base.view(np.int64).copy()).cuda() for _ in range(12)]  # 12: each buffer stays on one stream for 1, 2 or 3 streams
+ring = [torch.from_numpy(base.view(np.int64).copy()).cuda() for _ in range(12)]  # 12: each buffer stays on one stream for 1, 2, 3 or 4 streams
 BYTES = 2 * 16 * N * L  # fwd + inv, 16 B per coefficient per transform
 
 
@@ -43,7 +43,7 @@ def run(nstreams, steps=400, warm=40):
     return steps * BYTES / dt / 1e9, dt / steps * 1e6
 
 
-for k in (1, 2, 3, 1, 2, 3):
+for k in (1, 2, 3, 4, 1, 2, 3, 4):
     gbs, us = run(k)
     print(f"streams {k}: {gbs:8.1f} GB/s  {us:6.2f} us/step", flush=True)
 h = ring[0].cpu().numpy().view(np.uint64)
