@@ -418,7 +418,10 @@ constexpr int kMfmaWaves = PHX_BCONV_MFMA_WAVES;  // waves per workgroup; two wo
 constexpr int kMfmaMaxJB = kBconvMfmaMaxObase / 16;
 constexpr uint32_t kDropRow = 0x80000000u;  // byte offset of output rows past obase
 constexpr int kBufferWord3 = 0x00020000;    // raw buffer resource word 3 (gfx9: 32-bit data format)
-constexpr int kStoreSc1 = 16;               // write-through output stores (sc1): 27.3 -> 25.8 us mean, nt 27.6
+#ifndef PHX_BCONV_STORE_AUX
+#define PHX_BCONV_STORE_AUX 16
+#endif
+constexpr int kStoreSc1 = PHX_BCONV_STORE_AUX;  // write-through output stores (sc1): 27.3 -> 25.8 us mean, nt 27.6
 
 __device__ __forceinline__ uint64_t signed_digits(uint64_t t) {
   constexpr uint64_t k80 = 0x8080808080808080ull;
