@@ -140,11 +140,23 @@ __device__ __forceinline__ uint64_t opaque(uint64_t v) {
   asm("" : "+v"(v));
   return v;
 }
-// x - m if that is >= 0 else x, for x, m < 2^63, given nm = -m mod 2^64
+#ifndef PHX_CSUB_BFI
+#define PHX_CSUB_BFI 1
+#endif
+// x - m if that is >= 0 else x, for x, m < 2^63, given nm = -m mod 2^64.  t = x - m, s = its sign
+// as a 32-bit mask, then the select (s & x) | (~s & t) as one v_bfi_b32 per half: 4 instructions
+// (the masked add-back form, t + (m & s), takes 5).
 __device__ __forceinline__ uint64_t csub_n(uint64_t x, uint64_t m, uint64_t nm) {
   const uint64_t t = add64(x, nm);
   const uint32_t s = static_cast<uint32_t>(static_cast<int32_t>(hi32(t)) >> 31);
+#if PHX_CSUB_BFI
+  uint32_t lo, hi;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(lo) : "v"(s), "v"(lo32(x)), "v"(lo32(t)));
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(hi) : "v"(s), "v"(hi32(x)), "v"(hi32(t)));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+#else
   return add64(t, (static_cast<uint64_t>(hi32(m) & s) << 32) | (lo32(m) & s));
+#endif
 }
 // a w mod q in [0, 4q) (as mul_shoup_lazy4 below), given nq = -q mod 2^64: a w + Q' (-q)
 __device__ __forceinline__ uint64_t mul_shoup_lazy4(uint64_t a, uint64_t w, uint64_t ws, uint64_t q) {
