@@ -72,6 +72,31 @@ def test_c2_forward_inverse_n65536_l44(rng, c3):
     assert np.array_equal(to_host(d), a)
 
 
+def test_c2_batches_on_three_streams(rng, c3):
+    """bench.py's C2 stepping: independent [44][65536] batches dealt round-robin to 3 HIP streams
+    (the tables shared). Every batch's forward equals the oracle's and its inverse restores it."""
+    import torch
+    n, mods, t = c3
+    L = 44
+    lib = PA.load()
+    batches = [O.random_limbs(rng, n, mods[:L]) for _ in range(6)]
+    devs = [to_dev(a) for a in batches]
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    cur = torch.cuda.current_stream()
+    for s in streams:
+        s.wait_stream(cur)
+    for i, d in enumerate(devs):
+        PA.check(lib.phantom_nwt_forward_inplace(ptr(d), t.handle, L, 0, streams[i % 3].cuda_stream))
+    torch.cuda.synchronize()
+    for a, d in zip(batches[:2], devs[:2]):  # the oracle's forward is slow: two of them
+        assert np.array_equal(to_host(d), O.ntt_fwd(a, n, mods[:L]))
+    for i, d in enumerate(devs):
+        PA.check(lib.phantom_nwt_backward_inplace(ptr(d), t.handle, L, 0, streams[i % 3].cuda_stream))
+    torch.cuda.synchronize()
+    for a, d in zip(batches, devs):
+        assert np.array_equal(to_host(d), a)
+
+
 def test_start_modulus_idx_offsets_data_and_tables(rng, c3):
     n, mods, t = c3
     L, start = 5, 40
