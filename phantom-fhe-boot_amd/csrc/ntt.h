@@ -114,6 +114,10 @@ struct NttEpilogue {
   size_t add_stride = 0;
   const uint64_t* pmod = nullptr;
   const uint64_t* pmod_shoup = nullptr;
+  // inverse prologue only (ntt_inverse_ks): tmu limb of buffer limb 0, and how many leading buffer
+  // limbs take the addend
+  size_t tmu_limb0 = 0;
+  int add_limbs = 0;
 };
 hipError_t ntt_forward_fused(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                              const uint64_t* bcast, size_t bcast_stride, const NttEpilogue& epi, hipStream_t stream);
@@ -142,6 +146,17 @@ hipError_t ntt_forward_bconv(const NttTables& t, uint64_t* out, const LimbMap& m
 // nwt_2d_radix8_backward_scale used by modup, src/ntt/ntt_modup.cu:356-393).
 hipError_t ntt_inverse(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                        const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream);
+
+// Inverse NTT whose input is the key-switch inner product of the moddown's dropped limbs (the P
+// limbs, plus q_last for a relinearize + rescale): buffer limb i of polynomial p (table row r) is
+//   x[k] = sum_{d < ks_beta} tmu[d][tmu_limb0 + i][k] * evk[d][p][r][k]
+//          (+ P_r * add_c[p][tmu_limb0 + i][k] for i < add_limbs)  mod q_r
+// (src/eval_key_switch.cu:26-85 for those limbs) formed in the first pass's registers, so the
+// inner product's dropped half makes no HBM round trip either.  There is no `in`; `ks` carries
+// ks_beta, tmu, tmu_stride, evk, evk_poly_stride, tmu_limb0 and the optional addend (add_c,
+// add_stride, pmod / pmod_shoup indexed by tmu_limb0 + i).  2-D sizes (n >= 2^10) only.
+hipError_t ntt_inverse_ks(const NttTables& t, uint64_t* out, const LimbMap& map, const uint64_t* scale,
+                          const uint64_t* scale_shoup, const NttEpilogue& ks, hipStream_t stream);
 
 // Inverse NTT that also copies its (NTT-form) input: the first pass stores every loaded input
 // limb l (buffer limb index) unchanged at copy + (l / alpha) * digit_stride + l * n as well.  This

@@ -544,6 +544,59 @@ __device__ __forceinline__ void ks_epilogue(const KArgs& a, const TileRef& tr, c
   }
 }
 
+// Key-switch prologue of the inverse row pass (ntt_inverse_ks): x = sum_d tmu[d] evk[d][p] (+ P add)
+// mod q for the row's E elements, in KC-element groups whose next loads are issued before the
+// current products (as ks_epilogue_b).  The third stream is the addend, else a re-read of tmu.
+template <int T, int BETA>
+__device__ __forceinline__ void ks_prologue_b(const KArgs& a, const TileRef& tr, uint64_t (&x)[E]) {
+  constexpr int KC = 4, NC = E / KC;
+  const size_t n = static_cast<size_t>(a.n);
+  const size_t tl = a.epi.tmu_limb0 + tr.buf_limb;
+  const uint64_t* tm = a.epi.tmu + tl * n + tr.k;
+  const uint64_t* kp[BETA];
+#pragma unroll
+  for (int d = 0; d < BETA; ++d) kp[d] = a.epi.evk[d] + tr.poly * a.epi.evk_poly_stride + (size_t)tr.row * n + tr.k;
+  const bool add = tr.buf_limb < a.epi.add_limbs;  // wave-uniform
+  const uint64_t* ad = add ? a.epi.add_c + tr.poly * a.epi.add_stride + tl * n + tr.k : tm;
+  const uint64_t pm = add ? a.epi.pmod[tl] : 0, pms = add ? a.epi.pmod_shoup[tl] : 0;
+  const uint64_t q = a.modulus[tr.row], r0 = a.barrett[2 * tr.row], r1 = a.barrett[2 * tr.row + 1];
+  uint64_t tb[2][BETA][KC], kb[2][BETA][KC], ob[2][KC];
+  auto load = [&](int c, int s) {
+#pragma unroll
+    for (int d = 0; d < BETA; ++d)
+#pragma unroll
+      for (int i = 0; i < KC; ++i) {
+        tb[s][d][i] = __builtin_nontemporal_load(tm + d * a.epi.tmu_stride + (c * KC + i) * T);
+        kb[s][d][i] = __builtin_nontemporal_load(kp[d] + (c * KC + i) * T);
+      }
+#pragma unroll
+    for (int i = 0; i < KC; ++i) ob[s][i] = __builtin_nontemporal_load(ad + (c * KC + i) * T);
+  };
+  load(0, 0);
+  static_for<NC>([&](auto cc) {
+    constexpr int c = decltype(cc)::value, s = c & 1;
+    if constexpr (c + 1 < NC) load(c + 1, s ^ 1);
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      u128 acc{0, 0};
+#pragma unroll
+      for (int d = 0; d < BETA; ++d) add128(acc, mul_wide(tb[s][d][i], kb[s][d][i]));
+      uint64_t v = barrett_reduce_128(acc, q, r0, r1);
+      if (add) v = add_mod(v, mul_shoup(ob[s][i], pm, pms, q), q);
+      x[c * KC + i] = v;
+    }
+  });
+}
+
+template <int T>
+__device__ __forceinline__ void ks_prologue(const KArgs& a, const TileRef& tr, uint64_t (&x)[E]) {
+  switch (__builtin_amdgcn_readfirstlane(a.epi.ks_beta)) {
+    case 1: ks_prologue_b<T, 1>(a, tr, x); break;
+    case 2: ks_prologue_b<T, 2>(a, tr, x); break;
+    default: ks_prologue_b<T, 3>(a, tr, x); break;
+  }
+}
+
 // Row-pass block order of the key-switch epilogue: the polynomials' blocks of one row group are
 // dealt to one XCD back to back (blocks b and b + 8 share an XCD under round-robin placement;
 // speed only, any placement is correct), so the second polynomial reads tmu from that XCD's L2.
@@ -847,7 +900,8 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
   {
     const TileRef tr = row_ref<S1_LOG, S2_LOG>(a, item, lr, t, r);
     uint64_t x[E];
-    row_load<S2_LOG>(x, a.in + tr.in_off);
+    if constexpr (!FWD && KS) ks_prologue<T>(a, tr, x);  // ntt_inverse_ks: no input buffer
+    else row_load<S2_LOG>(x, a.in + tr.in_off);
     if (!FWD && a.copy.out) row_copy<S2_LOG>(a, tr, x);  // workgroup-uniform branch
     const LimbCtx lc = limb_ctx(a, tr.row);
     uint64_t* dst = a.out + tr.off;
@@ -1030,9 +1084,10 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
 
 // The epilogue form holds its operands (EpiOperands) through the butterflies: two waves per SIMD
 // give it the registers to do so without spilling (168 VGPRs at three waves spilled 47).
-// KS: the epilogue is the key-switch form (ks_epilogue; EPI must be set too).
+// KS: forward, the epilogue is the key-switch form (ks_epilogue; EPI must be set too); inverse, the
+// input is the key-switch prologue (ks_prologue).
 template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false, bool LZ = false, bool KS = false>
-__global__ __launch_bounds__(BLOCK, EPI ? 2 : PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) {
+__global__ __launch_bounds__(BLOCK, (EPI || KS) ? 2 : PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) {
   using RS = RowShape<S1_LOG, S2_LOG>;
   __shared__ uint64_t lds[RS::LDS_WORDS];
   __shared__ double tw0[RS::TW0];
@@ -1221,10 +1276,14 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
     else
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, false, false>), grid_r, block_r, 0, stream, a);
   } else {
-    hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false>), grid_r, block_r, 0, stream, a);
+    if (a.epi.ks_beta > 0)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false, false, false, true>), grid_r, block_r, 0, stream, a);
+    else
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false>), grid_r, block_r, 0, stream, a);
     a.in = out;
     a.map.in_stride = a.map.out_stride;
     a.copy = NttCopy{};  // the row pass made the copy
+    a.epi = NttEpilogue{};  // ... and consumed the key-switch prologue
     hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false>), grid_c, block_c, 0, stream, a);
   }
   return hipGetLastError();
@@ -1276,6 +1335,14 @@ hipError_t ntt_forward_bconv(const NttTables& t, uint64_t* out, const LimbMap& m
 hipError_t ntt_inverse(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                        const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream) {
   return dispatch(t, in, out, map, true, scale, scale_shoup, stream);
+}
+
+hipError_t ntt_inverse_ks(const NttTables& t, uint64_t* out, const LimbMap& map, const uint64_t* scale,
+                          const uint64_t* scale_shoup, const NttEpilogue& ks, hipStream_t stream) {
+  if (ks.ks_beta < 1 || ks.ks_beta > kMaxKsBeta || !ks.tmu || !ks.evk) return hipErrorInvalidValue;
+  if (ks.add_limbs > 0 && (!ks.add_c || !ks.pmod || !ks.pmod_shoup)) return hipErrorInvalidValue;
+  if (t.log_n < 10) return hipErrorNotSupported;
+  return dispatch(t, nullptr, out, map, true, scale, scale_shoup, stream, nullptr, 0, ks);
 }
 
 hipError_t ntt_inverse_copy(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,

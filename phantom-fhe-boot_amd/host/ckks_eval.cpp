@@ -307,16 +307,20 @@ void relinearize_rescale_raw(const PhantomContext& ctx, size_t chain_index, cons
   uint64_t* t_mod_up = rt.workspace().get(s, Workspace::kKsModup, beta * QlP * n);
   rt.modup(t_mod_up, d3 + 2 * Ql * n, ctx.gpu_rns_tables(), s);
   uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * QlP * n);
-  phx::KsAddend add;
-  add.c = d3;
-  add.pmod = rt.bigP_mod_q();
-  add.pmod_shoup = rt.bigP_mod_q_shoup();
-  // the inner product's dropped limbs (q_last, P) here; its first Ql - 1 limbs inside the finish
-  // (NTT epilogue, ntt.h NttEpilogue::ks_beta), so they make no HBM round trip (PHX_KS_EPI=0: off)
+  // the inner product is formed inside the moddown-rescale: its dropped limbs (q_last with the
+  // addend, P) in the INTT's prologue, its first Ql - 1 limbs in the finish's epilogue (ntt.h
+  // ntt_inverse_ks, NttEpilogue::ks_beta), so no limb of it makes an HBM round trip
+  // (PHX_KS_EPI=0: the whole inner product in one kernel)
   const bool fuse = ks_epilogue_enabled() && beta <= (size_t)phx::kMaxKsBeta && n >= 1024 && Ql >= 2;
-  hip_ok(phx::keyswitch_inner_prod(t_mod_up, evk, cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, Ql, ctx.size_Q(),
-                                   ctx.size_P(), beta, s, add, fuse ? Ql - 1 : 0),
-         "relinearize inner product");
+  if (!fuse) {
+    phx::KsAddend add;
+    add.c = d3;
+    add.pmod = rt.bigP_mod_q();
+    add.pmod_shoup = rt.bigP_mod_q_shoup();
+    hip_ok(phx::keyswitch_inner_prod(t_mod_up, evk, cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, Ql, ctx.size_Q(),
+                                     ctx.size_P(), beta, s, add),
+           "relinearize inner product");
+  }
   phx::NttEpilogue ks;
   if (fuse) {
     ks.ks_beta = (int)beta;

@@ -32,12 +32,14 @@ void keyswitch_raw(const PhantomContext& ctx, size_t chain_index, uint64_t* ct, 
   uint64_t* t_mod_up = rt.workspace().get(s, Workspace::kKsModup, beta * size_QlP * n);
   rt.modup(t_mod_up, c2, ctx.gpu_rns_tables(), s);
   uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * size_QlP * n);
-  // the inner product's P limbs here; its Ql limbs inside the moddown finish (NTT epilogue), so
-  // they make no HBM round trip (PHX_KS_EPI=0: the whole inner product in one kernel, as before)
+  // the inner product is formed inside the moddown: its P limbs in the INTT(P) prologue, its Ql
+  // limbs in the finish's epilogue (ntt.h ntt_inverse_ks, NttEpilogue::ks_beta), so no limb of it
+  // makes an HBM round trip (PHX_KS_EPI=0: the whole inner product in one kernel, as before)
   const bool fuse = ks_epilogue_enabled() && beta <= (size_t)phx::kMaxKsBeta && n >= 1024;
-  hip_ok(phx::keyswitch_inner_prod(t_mod_up, evk, cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, size_Ql,
-                                   ctx.size_Q(), ctx.size_P(), beta, s, phx::KsAddend{}, fuse ? size_Ql : 0),
-         "keyswitch inner product");
+  if (!fuse)
+    hip_ok(phx::keyswitch_inner_prod(t_mod_up, evk, cx, ctx.mod_QP().q, ctx.mod_QP().barrett, n, size_Ql,
+                                     ctx.size_Q(), ctx.size_P(), beta, s),
+           "keyswitch inner product");
   traffic::keys(traffic::limb_bytes(beta * 2 * size_QlP, n));
   traffic::ciphertexts(traffic::limb_bytes(5 * size_Ql, n));  // c2 + (c0, c1) read, (c0, c1) written
   rt.moddown_add(ct, cx, true, ctx.gpu_rns_tables(), s, 2, fuse ? t_mod_up : nullptr, fuse ? evk : nullptr);

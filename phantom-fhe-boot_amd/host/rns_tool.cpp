@@ -290,14 +290,30 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
   pm.first_a = 0;
   pm.first_b = (int)size_Q_;
   const bool fused = fused_bconv_ok(size_P_) && polys <= (size_t)phx::kMaxBconvPolys;
+  phx::NttEpilogue ksf;  // the key-switch form: prologue of INTT(P), epilogue of the finish
+  if (tmu) {
+    if (beta() > (size_t)phx::kMaxKsBeta) throw std::invalid_argument("moddown_add: too many key-switch digits");
+    ksf.ks_beta = (int)beta();
+    ksf.tmu = tmu;
+    ksf.tmu_stride = size_QlP * n_;
+    ksf.evk = evk;
+    ksf.evk_poly_stride = size_QP() * n_;
+  }
   // the INTT also applies the converter's qHat^-1 (the conversion's prescale, otherwise redone
-  // by every output group of the conversion)
-  hip_ok(phx::ntt_inverse(ntt, cp, cp, pm.batched(np, size_QlP * n_, size_QlP * n_), p_to_ql_.d_qhat_inv.get(),
-                          p_to_ql_.d_qhat_inv_shoup.get(), s),
-         "moddown INTT(P)");
+  // by every output group of the conversion); with tmu its input is the inner product's P limbs
+  const phx::LimbMap pmb = pm.batched(np, size_QlP * n_, size_QlP * n_);
+  if (tmu) {
+    phx::NttEpilogue pro = ksf;
+    pro.tmu_limb0 = size_Ql;
+    hip_ok(phx::ntt_inverse_ks(ntt, cp, pmb, p_to_ql_.d_qhat_inv.get(), p_to_ql_.d_qhat_inv_shoup.get(), pro, s),
+           "moddown inner product + INTT(P)");
+  } else {
+    hip_ok(phx::ntt_inverse(ntt, cp, cp, pmb, p_to_ql_.d_qhat_inv.get(), p_to_ql_.d_qhat_inv_shoup.get(), s),
+           "moddown INTT(P)");
+  }
   uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, polys * size_Ql * n_);
   // NTT(delta) with the finish (cx - delta) P^-1 (+ ct) as its epilogue
-  phx::NttEpilogue epi;
+  phx::NttEpilogue epi = ksf;
   epi.c = cx;
   epi.c_stride = size_QlP * n_;
   epi.out = ct;
@@ -305,14 +321,6 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
   epi.w = d_bigPInv_mod_q_.get();
   epi.ws = d_bigPInv_mod_q_shoup_.get();
   epi.accumulate = accumulate;
-  if (tmu) {
-    if (beta() > (size_t)phx::kMaxKsBeta) throw std::invalid_argument("moddown_add: too many key-switch digits");
-    epi.ks_beta = (int)beta();
-    epi.tmu = tmu;
-    epi.tmu_stride = size_QlP * n_;
-    epi.evk = evk;
-    epi.evk_poly_stride = size_QP() * n_;
-  }
   const phx::LimbMap dm = phx::LimbMap::contiguous((int)size_Ql, 0).batched(np);
   if (fused) {
     phx::BconvPrologue bcv;
@@ -378,9 +386,20 @@ void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables&
   dm.first_a = (int)Ln;
   dm.first_b = (int)size_Q_;
   const bool fused = fused_bconv_ok(1 + size_P_) && polys <= (size_t)phx::kMaxBconvPolys;
-  hip_ok(phx::ntt_inverse(ntt, dropped, dropped, dm.batched(np, size_QlP * n_, size_QlP * n_),
-                          pq_to_ql1_.d_qhat_inv.get(), pq_to_ql1_.d_qhat_inv_shoup.get(), s),
-         "moddown-rescale INTT");
+  const phx::LimbMap dmb = dm.batched(np, size_QlP * n_, size_QlP * n_);
+  if (ks) {  // the inner product's dropped limbs (q_last with its addend, P) as the INTT's prologue
+    if (ks->ks_beta > phx::kMaxKsBeta) throw std::invalid_argument("moddown_rescale: too many key-switch digits");
+    phx::NttEpilogue pro = *ks;
+    pro.tmu_limb0 = Ln;
+    pro.add_limbs = ks->add_c ? 1 : 0;
+    hip_ok(phx::ntt_inverse_ks(ntt, dropped, dmb, pq_to_ql1_.d_qhat_inv.get(), pq_to_ql1_.d_qhat_inv_shoup.get(), pro,
+                               s),
+           "moddown-rescale inner product + INTT");
+  } else {
+    hip_ok(phx::ntt_inverse(ntt, dropped, dropped, dmb, pq_to_ql1_.d_qhat_inv.get(), pq_to_ql1_.d_qhat_inv_shoup.get(),
+                            s),
+           "moddown-rescale INTT");
+  }
   uint64_t* delta = ws_->get(s, Workspace::kModdownDelta, polys * Ln * n_);
   phx::NttEpilogue epi;
   epi.c = cx;
@@ -390,7 +409,6 @@ void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables&
   epi.w = d_PQinv_.get();
   epi.ws = d_PQinv_shoup_.get();
   if (ks) {
-    if (ks->ks_beta > phx::kMaxKsBeta) throw std::invalid_argument("moddown_rescale: too many key-switch digits");
     epi.ks_beta = ks->ks_beta;
     epi.tmu = ks->tmu;
     epi.tmu_stride = ks->tmu_stride;

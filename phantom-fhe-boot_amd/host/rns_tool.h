@@ -47,8 +47,9 @@ class RnsTool {
   // moddown_from_NTT (src/rns_bconv.cu:791-843) fused with add_to_ct_kernel, for `polys`
   // polynomials at once: cx is [polys][size_QlP][n] NTT form (its P limbs are clobbered);
   // ct [polys][size_Ql][n] (+)= moddown(cx).  With tmu/evk (a key switch's t_mod_up and key
-  // digits, polys = 2): only the P limbs of cx are read; its Ql limbs, the inner product
-  // sum_d tmu[d] evk[d][p], are formed in the finish's epilogue (ntt.h NttEpilogue::ks_beta).
+  // digits, polys = 2): cx is not read, only its P limbs used as scratch; the inner product
+  // sum_d tmu[d] evk[d][p] is formed in the INTT(P)'s prologue (its P limbs, ntt.h ntt_inverse_ks)
+  // and in the finish's epilogue (its Ql limbs, NttEpilogue::ks_beta).
   void moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx::NttTables& ntt, hipStream_t s,
                    size_t polys = 1, const uint64_t* tmu = nullptr, const uint64_t* const* evk = nullptr) const;
   // moddown of an extended-basis polynomial fused with the modup of its result (giant-step
@@ -65,8 +66,9 @@ class RnsTool {
   // the ciphertext rescaled to the next level (scale S / q_last).  One INTT over the 1 + size_P
   // dropped limbs, one base conversion, one NTT and one finish instead of a moddown (INTT P,
   // NTT Ql) followed by a rescale (INTT 1, NTT Ql - 1).  cx's dropped limbs are clobbered.
-  // With `ks` (polys = 2, a key switch's t_mod_up / key digits / P-scaled addend): only the dropped
-  // limbs of cx are read; its first size_Ql - 1 limbs are formed in the finish's epilogue.
+  // With `ks` (polys = 2, a key switch's t_mod_up / key digits / P-scaled addend): cx is not read,
+  // only its dropped limbs used as scratch; the inner product's dropped limbs are formed in the
+  // INTT's prologue (ntt_inverse_ks) and its first size_Ql - 1 limbs in the finish's epilogue.
   void moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables& ntt, hipStream_t s,
                        size_t polys = 1, const phx::NttEpilogue* ks = nullptr) const;
   // divide_and_round_q_last_ntt (src/rns.cu:1160-1184): in [polys][size_Ql][n] -> out
