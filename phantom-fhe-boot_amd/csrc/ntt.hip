@@ -484,15 +484,28 @@ __device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr
 
 // Key-switch epilogue (NttEpilogue::ks_beta > 0): out = (sum_d tmu[d] evk[d][p] (+ P add) mod q
 // - y) w (+ out), the inner product of eval_key_switch.cu:26-85 (128-bit sums, one Barrett-128
-// per element) formed where the moddown finish consumes it.  KC elements at a time; the next
-// group's loads are issued before the current group's products.  BETA is a template parameter
+// per element) formed where the moddown finish consumes it.  KC (PHX_KS_KC) elements at a time;
+// the next group's loads are issued before the current group's products.  BETA is a template parameter
 // and every load is unconditional (the third operand stream is `out` when accumulating, else the
 // addend, else a harmless re-read of tmu), so the compiler can count the loads in flight
 // (s_waitcnt vmcnt(N)) instead of draining them all (vmcnt(0)) before every group.
+// Elements per load group of the key-switch epilogue / prologue, and waves per SIMD of the
+// epilogue's row pass.  One element per group (loads of the next element in flight) at 3 waves
+// (158 VGPRs, no spill) beat 4 per group at 2 waves (234 VGPRs): C3 relinearize 0.274-0.288 ->
+// 0.268-0.274 ms, bootstrap 23.41-23.57 -> 23.17-23.37 ms (profiles/r03/ks_waves/).
+#ifndef PHX_KS_KC
+#define PHX_KS_KC 1
+#endif
+#ifndef PHX_KS_WAVES
+#define PHX_KS_WAVES 3
+#endif
+#ifndef PHX_KSP_WAVES
+#define PHX_KSP_WAVES 2  // ... and of the inverse row pass with the key-switch prologue
+#endif
 template <int T, int BETA>
 __device__ __forceinline__ void ks_epilogue_b(const KArgs& a, const TileRef& tr, const uint64_t (&y)[E], uint64_t q,
                                               uint64_t r0, uint64_t r1) {
-  constexpr int KC = 4, NC = E / KC;
+  constexpr int KC = PHX_KS_KC, NC = E / KC;
   const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
   const bool acc_out = a.epi.accumulate;
   const uint64_t* tm = a.epi.tmu + e;
@@ -549,7 +562,7 @@ __device__ __forceinline__ void ks_epilogue(const KArgs& a, const TileRef& tr, c
 // current products (as ks_epilogue_b).  The third stream is the addend, else a re-read of tmu.
 template <int T, int BETA>
 __device__ __forceinline__ void ks_prologue_b(const KArgs& a, const TileRef& tr, uint64_t (&x)[E]) {
-  constexpr int KC = 4, NC = E / KC;
+  constexpr int KC = PHX_KS_KC, NC = E / KC;
   const size_t n = static_cast<size_t>(a.n);
   const size_t tl = a.epi.tmu_limb0 + tr.buf_limb;
   const uint64_t* tm = a.epi.tmu + tl * n + tr.k;
@@ -1087,7 +1100,8 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
 // KS: forward, the epilogue is the key-switch form (ks_epilogue; EPI must be set too); inverse, the
 // input is the key-switch prologue (ks_prologue).
 template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false, bool LZ = false, bool KS = false>
-__global__ __launch_bounds__(BLOCK, (EPI || KS) ? 2 : PHX_NTT_WAVES_PER_EU) void ntt_row(KArgs a) {
+__global__ __launch_bounds__(BLOCK, KS ? (FWD ? PHX_KS_WAVES : PHX_KSP_WAVES) : EPI ? 2 : PHX_NTT_WAVES_PER_EU)
+void ntt_row(KArgs a) {
   using RS = RowShape<S1_LOG, S2_LOG>;
   __shared__ uint64_t lds[RS::LDS_WORDS];
   __shared__ double tw0[RS::TW0];
