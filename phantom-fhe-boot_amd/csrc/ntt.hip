@@ -482,6 +482,45 @@ __device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr
   store_wt(o, v);
 }
 
+// PHX_EPI_LATE = K > 0: the epilogue's operands are loaded after the butterflies instead, K
+// elements per group with the next group in flight (as the key-switch epilogue), so the
+// butterflies do not hold them and the row pass can run at PHX_EPI_WAVES waves per SIMD.
+#ifndef PHX_EPI_LATE
+#define PHX_EPI_LATE 0
+#endif
+#ifndef PHX_EPI_WAVES
+#define PHX_EPI_WAVES 2
+#endif
+template <int T>
+__device__ __forceinline__ void epilogue_late(const KArgs& a, const TileRef& tr, const uint64_t (&y)[E], uint64_t q) {
+  constexpr int KC = PHX_EPI_LATE > 0 ? PHX_EPI_LATE : 1, NC = E / KC;
+  const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
+  const uint64_t* c = a.epi.c + tr.poly * a.epi.c_stride + e;
+  uint64_t* o = a.epi.out + tr.poly * a.epi.out_stride + e;
+  const bool acc = a.epi.accumulate;
+  const uint64_t* second = acc ? o : c;  // (a harmless re-read of c when not accumulating)
+  const uint64_t w = a.epi.w[tr.buf_limb], ws = a.epi.ws[tr.buf_limb];
+  uint64_t cb[2][KC], ob[2][KC];
+  auto load = [&](int g, int s) {
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      cb[s][i] = __builtin_nontemporal_load(c + (g * KC + i) * T);
+      ob[s][i] = __builtin_nontemporal_load(second + (g * KC + i) * T);
+    }
+  };
+  load(0, 0);
+  static_for<NC>([&](auto gg) {
+    constexpr int g = decltype(gg)::value, s = g & 1;
+    if constexpr (g + 1 < NC) load(g + 1, s ^ 1);
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      uint64_t v = mul_shoup(sub_mod(cb[s][i], y[g * KC + i], q), w, ws, q);
+      if (acc) v = add_mod(v, ob[s][i], q);
+      store_wt(o + (g * KC + i) * T, v);
+    }
+  });
+}
+
 // Key-switch epilogue (NttEpilogue::ks_beta > 0): out = (sum_d tmu[d] evk[d][p] (+ P add) mod q
 // - y) w (+ out), the inner product of eval_key_switch.cu:26-85 (128-bit sums, one Barrett-128
 // per element) formed where the moddown finish consumes it.  KC (PHX_KS_KC) elements at a time;
@@ -949,7 +988,7 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
           }
         }
       });
-      if constexpr (FWD && EPI && !KS) epilogue_load(a, tr, T, eo);
+      if constexpr (FWD && EPI && !KS && PHX_EPI_LATE == 0) epilogue_load(a, tr, T, eo);
 #pragma unroll
       for (int k = 0; k < K0; ++k) {
         const uint32_t e = t + 1 + T * k;
@@ -991,6 +1030,11 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
 #pragma unroll
           for (int j = 0; j < E; ++j) y[j] = f64_to_canonical(v[j], lc.qd, lc.qinv);
           ks_epilogue<T>(a, tr, y, lc.q, a.barrett[2 * tr.row], a.barrett[2 * tr.row + 1]);
+        } else if constexpr (EPI && PHX_EPI_LATE > 0) {
+          uint64_t y[E];
+#pragma unroll
+          for (int j = 0; j < E; ++j) y[j] = f64_to_canonical(v[j], lc.qd, lc.qinv);
+          epilogue_late<T>(a, tr, y, lc.q);
         } else if constexpr (EPI) {
 #pragma unroll
           for (int j = 0; j < E; ++j) epilogue_store(a, tr, j, T, eo, f64_to_canonical(v[j], lc.qd, lc.qinv), lc.q);
@@ -1052,7 +1096,7 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
             if constexpr (R > 0) relayout<S2_LOG, R - 1, R>(v, lrow, idx, sync, t);
             uint64_t w[E], ws[E];
             get_tw(rc, w, ws);
-            if constexpr (EPI && !KS && R == RN - 1) epilogue_load(a, tr, T, eo);  // behind the last twiddles
+            if constexpr (EPI && !KS && PHX_EPI_LATE == 0 && R == RN - 1) epilogue_load(a, tr, T, eo);  // behind the last twiddles
             if constexpr (LZ)
               ct_round_int16<S2_LOG, R, P::row_lz.mask>(v, w, ws, lc.q);
             else
@@ -1068,6 +1112,11 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
 #pragma unroll
             for (int j = 0; j < E; ++j) y[j] = canon(v[j]);
             ks_epilogue<T>(a, tr, y, lc.q, a.barrett[2 * tr.row], a.barrett[2 * tr.row + 1]);
+          } else if constexpr (EPI && PHX_EPI_LATE > 0) {
+            uint64_t y[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j) y[j] = canon(v[j]);
+            epilogue_late<T>(a, tr, y, lc.q);
           } else if constexpr (EPI) {
 #pragma unroll
             for (int j = 0; j < E; ++j) epilogue_store(a, tr, j, T, eo, canon(v[j]), lc.q);
@@ -1100,7 +1149,8 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
 // KS: forward, the epilogue is the key-switch form (ks_epilogue; EPI must be set too); inverse, the
 // input is the key-switch prologue (ks_prologue).
 template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false, bool LZ = false, bool KS = false>
-__global__ __launch_bounds__(BLOCK, KS ? (FWD ? PHX_KS_WAVES : PHX_KSP_WAVES) : EPI ? 2 : PHX_NTT_WAVES_PER_EU)
+__global__ __launch_bounds__(BLOCK, KS ? (FWD ? PHX_KS_WAVES : PHX_KSP_WAVES)
+                                      : EPI ? (PHX_EPI_LATE > 0 ? PHX_EPI_WAVES : 2) : PHX_NTT_WAVES_PER_EU)
 void ntt_row(KArgs a) {
   using RS = RowShape<S1_LOG, S2_LOG>;
   __shared__ uint64_t lds[RS::LDS_WORDS];
