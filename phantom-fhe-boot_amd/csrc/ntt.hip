@@ -30,14 +30,11 @@
 #include "ntt.h"
 
 #include <algorithm>
-#include <cstdio>
-#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
 #include "arith.h"
 #include "farith.h"
-#include "stream_fork.h"
 
 namespace phx {
 namespace {
@@ -1374,80 +1371,10 @@ hipError_t dispatch(const NttTables& tb, const uint64_t* in, uint64_t* out, cons
 #undef PHX_NTT_CASE
 }
 
-// ---------------------------------------------------------------------------------------
-// Limb-chunk pipelining of one transform across HIP streams (stream_fork.h).  A pass pays a ~2 us
-// HBM-latency ramp and a ~3 us store tail (DESIGN.md §3 wave timeline); splitting the limbs into
-// chunks dealt round-robin to `lanes` streams lets the column pass of one chunk run under the row
-// pass (ramp and tail) of another.  Whole limbs per chunk, so every limb's two passes stay in one
-// chunk and the result is the same function of the input.  PHX_NTT_PIPE="chunks,lanes[,min]"
-// (min = fewest limbs per chunk; "0" disables).
-// ---------------------------------------------------------------------------------------
-struct PipeCfg {
-  int chunks = 0, lanes = 0, min_limbs = 8;
-};
-#ifndef PHX_NTT_PIPE_DEFAULT
-#define PHX_NTT_PIPE_DEFAULT "0"
-#endif
-const PipeCfg& pipe_cfg() {
-  static const PipeCfg c = [] {
-    PipeCfg p;
-    const char* e = std::getenv("PHX_NTT_PIPE");
-    if (!e) e = PHX_NTT_PIPE_DEFAULT;
-    int ch = 0, la = 0, mi = 8;
-    const int got = std::sscanf(e, "%d,%d,%d", &ch, &la, &mi);
-    if (got >= 2 && ch > 1 && la > 1) {
-      p.chunks = ch;
-      p.lanes = std::min(la, kMaxForkLanes);
-      p.min_limbs = std::max(1, mi);
-    }
-    return p;
-  }();
-  return c;
-}
-
-// buffer limbs [b, e) of `m` as a map of their own (pointers offset by b limbs by the caller)
-LimbMap sub_map(const LimbMap& m, int b, int e) {
-  LimbMap s = m;
-  s.num_limbs = e - b;
-  s.split = std::clamp(m.split - b, 0, e - b);
-  s.first_a = m.first_a + b;
-  s.first_b = m.first_b + std::max(0, b - m.split);
-  s.skip_begin = s.skip_end = 0;
-  s.in_stride = s.out_stride = 0;
-  return s;
-}
-
-// Runs f(sub_map, first_limb, stream) per chunk when pipelining applies; returns
-// hipErrorNotSupported (nothing enqueued) when it does not: batched or ranged maps, 1-D sizes,
-// too few limbs.
-template <typename F>
-hipError_t pipelined(const NttTables& tb, const LimbMap& map, hipStream_t stream, F&& f) {
-  const PipeCfg& c = pipe_cfg();
-  if (c.chunks < 2 || tb.log_n < 10 || map.polys != 1 || map.skip_begin != map.skip_end) return hipErrorNotSupported;
-  const int L = map.num_limbs;
-  const int chunks = std::min(c.chunks, L / c.min_limbs);
-  if (chunks < 2) return hipErrorNotSupported;
-  StreamFork& fk = StreamFork::get(stream, std::min(c.lanes, chunks));
-  const int lanes = std::min({c.lanes, chunks, fk.lanes_available()});
-  if (lanes < 2) return hipErrorNotSupported;
-  hipError_t e = fk.fork(lanes);
-  for (int i = 0; i < chunks && e == hipSuccess; ++i) {
-    const int b = i * L / chunks, en = (i + 1) * L / chunks;
-    e = f(sub_map(map, b, en), b, fk.lane(i % lanes));
-  }
-  const hipError_t j = fk.join(lanes);  // always re-join the caller, even after a failed launch
-  return e != hipSuccess ? e : j;
-}
-
 }  // namespace
 
 hipError_t ntt_forward(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                        hipStream_t stream) {
-  const size_t n = t.n;
-  const hipError_t p = pipelined(t, map, stream, [&](const LimbMap& m, int b, hipStream_t s) {
-    return dispatch(t, in + b * n, out + b * n, m, false, nullptr, nullptr, s);
-  });
-  if (p != hipErrorNotSupported) return p;
   return dispatch(t, in, out, map, false, nullptr, nullptr, stream);
 }
 
@@ -1471,12 +1398,6 @@ hipError_t ntt_forward_bconv(const NttTables& t, uint64_t* out, const LimbMap& m
 
 hipError_t ntt_inverse(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                        const uint64_t* scale, const uint64_t* scale_shoup, hipStream_t stream) {
-  const size_t n = t.n;
-  const hipError_t p = pipelined(t, map, stream, [&](const LimbMap& m, int b, hipStream_t s) {
-    return dispatch(t, in + b * n, out + b * n, m, true, scale ? scale + b : nullptr,
-                    scale_shoup ? scale_shoup + b : nullptr, s);
-  });
-  if (p != hipErrorNotSupported) return p;
   return dispatch(t, in, out, map, true, scale, scale_shoup, stream);
 }
 
