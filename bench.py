@@ -38,7 +38,8 @@ L = 44
 C3_BITS = [60] + [50] * 44 + [60] * 15
 BYTES_PER_TRANSFORM = 16 * N * L  # 46,137,344
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-RING_BYTES = 320 << 20  # > 256 MiB Infinity Cache
+RING_BYTES = 512 << 20  # > 2 x the 256 MiB Infinity Cache: a buffer is cold again when the ring comes back to it
+FWD_LAUNCHES = 200  # forward launches behind the roofline's fwd_ms (independent of --steps)
 
 
 def _oracle_ntt_rate(O, mods, threads, seconds):
@@ -318,6 +319,24 @@ def pmc_traffic():
         return None
 
 
+# rocprofv3 kernel-trace average durations of the forward's two kernels at HEAD (bench.py's own C2
+# command profiled on MI355X): fwd_ms minus their sum is the column -> row launch gap
+KERNEL_SUM_SOURCE = "profiles/r04/c2_fwd_kernels.json"
+
+
+def _kernel_sum_ms():
+    path = os.path.join(ROOT, KERNEL_SUM_SOURCE)
+    try:
+        with open(path) as f:
+            k = json.load(f)
+        return round((k["ntt_col_fwd_us"] + k["ntt_row_fwd_us"]) * 1e-3, 5)
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+KERNEL_SUM_MS = _kernel_sum_ms()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -370,8 +389,8 @@ def main():
     for ls in lanes:
         ls.wait_stream(stream)
 
-    def step(i, ev=None, k=None):
-        d = ring[i % nbuf].data_ptr()
+    def step(i, ev=None, k=None, buf=None):
+        d = ring[(i if buf is None else buf) % nbuf].data_ptr()
         st = stream if k is None else lanes[i % k]
         h = st.cuda_stream
         if ev is not None:
@@ -381,6 +400,9 @@ def main():
             ev[1].record(st)
         PA.check(lib.phantom_nwt_backward_inplace(d, tables.handle, L, 0, h))
 
+    # warm-up steps use ring buffers 0 .. W-1 and the timed steps continue from buffer W, so no timed
+    # step reads a buffer an earlier step left in the Infinity Cache: the ring (> 2 x 256 MiB) comes
+    # back to a buffer only after every other buffer has been read and written since
     def timed(k):
         for i in range(args.warmup):
             step(i, k=k)
@@ -390,7 +412,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(args.steps):
-            step(i, k=k)
+            step(i, k=k, buf=args.warmup + i)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -403,19 +425,22 @@ def main():
         stream.wait_stream(ls)
 
     # forward-NTT launch duration for the roofline: HIP events on the launch stream around
-    # `steps` back-to-back forward transforms over the buffer ring (average per launch), and,
-    # for reference, the mean of per-launch bracketed events (adds the event overhead)
+    # FWD_LAUNCHES back-to-back forward transforms over the cold buffer ring (average per launch;
+    # rocprofv3's kernel sum col + row of the same launches misses only the col -> row launch gap),
+    # and the median of single forwards bracketed by events (adds the event overhead)
+    for i in range(5):
+        PA.check(lib.phantom_nwt_forward_inplace(ring[i % nbuf].data_ptr(), tables.handle, L, 0, sh))
     fa, fb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fa.record(stream)
-    for i in range(args.steps):
-        PA.check(lib.phantom_nwt_forward_inplace(ring[i % nbuf].data_ptr(), tables.handle, L, 0, sh))
+    for i in range(FWD_LAUNCHES):
+        PA.check(lib.phantom_nwt_forward_inplace(ring[(5 + i) % nbuf].data_ptr(), tables.handle, L, 0, sh))
     fb.record(stream)
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(40)]
     for i, ev in enumerate(events):
-        step(i, ev)
+        step(i, ev, buf=5 + FWD_LAUNCHES + i)
     torch.cuda.synchronize()
-    fwd_ms = fa.elapsed_time(fb) / args.steps
-    fwd_ms_isolated = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    fwd_ms = fa.elapsed_time(fb) / FWD_LAUNCHES
+    fwd_ms_isolated = float(np.median([a.elapsed_time(b) for a, b in events]))
     elapsed, elapsed_1, fwd_ms, fwd_ms_isolated = max_over_ranks(
         dist if world > 1 else None, [elapsed, elapsed_1, fwd_ms, fwd_ms_isolated], "cuda")
 
@@ -452,7 +477,9 @@ def main():
                 "streams_per_rank": K,
                 "parallelism": f"replicas x{world} (independent batches per rank, dealt to {K} HIP streams)",
             },
-            "single_stream": {"value": round(value_1, 2), "ms_per_step": round(elapsed_1 / args.steps * 1e3, 5)},
+            # the same steps on one stream (no overlap of independent batches): the per-transform rate
+            "single_stream": {"value": round(value_1, 2), "ms_per_step": round(elapsed_1 / args.steps * 1e3, 5),
+                              "per_transform_ms": round(elapsed_1 / args.steps * 1e3 / 2, 5)},
             "roofline": {
                 "bound": "hbm",
                 "kernel": "forward NTT (ntt_col_pass + ntt_row_pass)",
@@ -462,7 +489,11 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "job_frac": round(value / world / HBM_PEAK_GBS, 4),
                 "fwd_ms": round(fwd_ms, 5),
-                "fwd_ms_isolated": round(fwd_ms_isolated, 5),
+                "fwd_launches": FWD_LAUNCHES,
+                "fwd_ms_isolated_median": round(fwd_ms_isolated, 5),
+                "kernel_sum_ms": KERNEL_SUM_MS,
+                "kernel_sum_source": KERNEL_SUM_SOURCE,
+                "launch_gap_ms": round(fwd_ms - KERNEL_SUM_MS, 5) if KERNEL_SUM_MS else None,
                 "traffic": pmc_traffic(),
                 "traffic_source": PMC_TRAFFIC_FILE,
             },

@@ -135,6 +135,16 @@ int phantom_relinearize(const phantom_context *ctx, size_t chain_index, uint64_t
  * to the P-scaled extended (c0, c1) + KeySwitch(c2). */
 int phantom_relinearize_rescale(const phantom_context *ctx, size_t chain_index, const uint64_t *ct3, uint64_t *out,
                                 const uint64_t *const *key_digits, size_t dnum, hipStream_t stream);
+/* `count` relinearize + rescale products (1 <= count <= 16) in shared launches: every stage of the key
+ * switch (modup INTT, digit conversions, digit NTTs, moddown-rescale INTT, conversion, NTT + finish)
+ * runs once over all of them.  Product k: ct3 + k ct3_stride ([3][L][n]) -> out + k out_stride
+ * ([2][L-1][n]); bit-identical to phantom_relinearize_rescale on each.  The reference issues one
+ * relinearize_inplace + rescale_to_next_inplace per product (src/evaluate.cu:1552-1647); EvalMod's
+ * Chebyshev ladder and double angle (src/bootstrap.cu:1657-1668, src/evaluate.cu:3264-3535) run
+ * their independent products this way. */
+int phantom_relinearize_rescale_batch(const phantom_context *ctx, size_t chain_index, const uint64_t *ct3,
+                                      size_t ct3_stride, size_t count, uint64_t *out, size_t out_stride,
+                                      const uint64_t *const *key_digits, size_t dnum, hipStream_t stream);
 /* keyswitch_inplace core: ct [2][L][n] += KeySwitch(c2 [L][n]) */
 int phantom_keyswitch(const phantom_context *ctx, size_t chain_index, uint64_t *ct, const uint64_t *c2,
                       const uint64_t *const *key_digits, size_t dnum, hipStream_t stream);

@@ -144,6 +144,25 @@ int phantom_relinearize_rescale(const phantom_context* ctx, size_t chain_index, 
   });
 }
 
+int phantom_relinearize_rescale_batch(const phantom_context* ctx, size_t chain_index, const uint64_t* ct3,
+                                      size_t ct3_stride, size_t count, uint64_t* out, size_t out_stride,
+                                      const uint64_t* const* key_digits, size_t dnum, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& rt = tool(ctx, chain_index);
+    const size_t n = ctx->ctx->poly_degree(), L = rt.size_Ql();
+    if (!ct3 || !out || count < 1 || count > static_cast<size_t>(phx::kMaxKsProds))
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "bad batch (1 <= count <= 16)");
+    if (count > 1 && (ct3_stride < 3 * L * n || out_stride < 2 * (L - 1) * n))
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "batch strides overlap");
+    auto* c = const_cast<phantom_context*>(ctx);
+    const uint64_t* const* evk = c->device_key_array(key_digits, dnum, rt.beta());
+    std::vector<uint64_t*> outs(count);
+    for (size_t k = 0; k < count; ++k) outs[k] = out + k * out_stride;
+    phantom::relinearize_rescale_batch_raw(*ctx->ctx, chain_index, ct3, ct3_stride, count, outs.data(), evk, stream);
+    return from_hip(hipGetLastError());
+  });
+}
+
 int phantom_modup(const phantom_context* ctx, size_t chain_index, const uint64_t* c2, uint64_t* t_mod_up,
                   hipStream_t stream) {
   PHX_CAPI_GUARD({

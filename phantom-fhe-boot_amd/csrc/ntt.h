@@ -51,6 +51,8 @@ inline int ntt_split_log_s1(int log_n) { return log_n == 16 ? PHX_NTT16_S1 : log
 // Batching: `polys` polynomials of the same shape go through one launch.  Polynomial p starts
 // at in + p * in_stride / out + p * out_stride (elements; 0 = num_limbs * n, i.e. contiguous)
 // and skips [skip_begin + p * skip_step, skip_end + p * skip_step) — the modup digits.
+// Grouped batches (period > 0): polynomial p = g * period + j starts at g * in_outer + j * in_stride
+// (out likewise) and skips by j only — the digits of several key switches' modups in one launch.
 struct LimbMap {
   int num_limbs = 0;
   int split = 0;
@@ -62,6 +64,16 @@ struct LimbMap {
   int skip_step = 0;
   size_t in_stride = 0;
   size_t out_stride = 0;
+  int period = 0;
+  size_t in_outer = 0;
+  size_t out_outer = 0;
+  __host__ __device__ int skip_index(int p) const { return period > 0 ? p % period : p; }
+  __host__ __device__ size_t in_off(int p) const {
+    return period > 0 ? (size_t)(p / period) * in_outer + (size_t)(p % period) * in_stride : (size_t)p * in_stride;
+  }
+  __host__ __device__ size_t out_off(int p) const {
+    return period > 0 ? (size_t)(p / period) * out_outer + (size_t)(p % period) * out_stride : (size_t)p * out_stride;
+  }
   static LimbMap contiguous(int num_limbs, int first) {
     LimbMap m;
     m.num_limbs = num_limbs; m.split = num_limbs; m.first_a = first; m.first_b = 0;
@@ -71,6 +83,14 @@ struct LimbMap {
   LimbMap batched(int count, size_t in_s = 0, size_t out_s = 0) const {
     LimbMap m = *this;
     m.polys = count; m.in_stride = in_s; m.out_stride = out_s;
+    return m;
+  }
+  // `count` polynomials in groups of `per` (see above)
+  LimbMap grouped(int count, int per, size_t stride, size_t outer) const {
+    LimbMap m = *this;
+    m.polys = count; m.period = per;
+    m.in_stride = m.out_stride = stride;
+    m.in_outer = m.out_outer = outer;
     return m;
   }
 };
@@ -94,7 +114,12 @@ hipError_t ntt_forward(const NttTables& t, const uint64_t* in, uint64_t* out, co
 //    (src/eval_key_switch.cu:26-85 for limbs i < size_Ql), so the inner product's Ql half never
 //    makes an HBM round trip (tmu: digit stride tmu_stride; evk: device array of ks_beta digit
 //    pointers, polynomial stride evk_poly_stride; the buffer limbs must be the first Ql limbs).
+//  - several ciphertexts in one launch (ks_prods > 1, polys = 2 ks_prods): polynomial p is c(p % 2)
+//    of ciphertext k = p / 2, written to out_p[k] + (p % 2) out_stride (any epilogue); in the
+//    key-switch form its tmu starts at tmu + k tmu_prod_stride and its addend at add_p[k] (+ (p % 2)
+//    add_stride), the key shared.  ks_prods <= 1 uses out / add_c.
 constexpr int kMaxKsBeta = 3;  // digits of the key-switch form (C3: 3, the C4 chain: <= 3)
+constexpr int kMaxKsProds = 16;
 struct NttEpilogue {
   const uint64_t* c = nullptr;
   size_t c_stride = 0;
@@ -118,6 +143,18 @@ struct NttEpilogue {
   // limbs take the addend
   size_t tmu_limb0 = 0;
   int add_limbs = 0;
+  // batched key switches (see above)
+  int ks_prods = 1;
+  size_t tmu_prod_stride = 0;
+  uint64_t* out_p[kMaxKsProds] = {};
+  const uint64_t* add_p[kMaxKsProds] = {};
+  __host__ __device__ uint64_t* ks_out(int p) const {
+    return (ks_prods > 1 ? out_p[p >> 1] : out) + (size_t)(ks_prods > 1 ? (p & 1) : p) * out_stride;
+  }
+  __host__ __device__ const uint64_t* ks_add(int p) const {
+    return (ks_prods > 1 ? add_p[p >> 1] : add_c) + (size_t)(ks_prods > 1 ? (p & 1) : p) * add_stride;
+  }
+  __host__ __device__ const uint64_t* ks_tmu(int p) const { return tmu + (size_t)(p >> 1) * tmu_prod_stride; }
 };
 hipError_t ntt_forward_fused(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                              const uint64_t* bcast, size_t bcast_stride, const NttEpilogue& epi, hipStream_t stream);
@@ -166,6 +203,7 @@ struct NttCopy {
   uint64_t* out = nullptr;
   size_t digit_stride = 0;  // elements between digits
   int alpha = 1;            // limbs per digit
+  size_t poly_stride = 0;   // batched inverses: polynomial p's digits start at out + p * poly_stride
 };
 hipError_t ntt_inverse_copy(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                             const uint64_t* scale, const uint64_t* scale_shoup, const NttCopy& copy,

@@ -375,7 +375,7 @@ __device__ __forceinline__ void resolve_limb(const KArgs& a, int y, int& poly, i
   const LimbMap& m = a.map;
   poly = m.polys > 1 ? y / a.limbs_per_poly : 0;
   int i = y - poly * a.limbs_per_poly;
-  if (i >= m.skip_begin + poly * m.skip_step) i += (m.skip_end - m.skip_begin);
+  if (i >= m.skip_begin + m.skip_index(poly) * m.skip_step) i += (m.skip_end - m.skip_begin);
   buf_limb = i;
   row = i < m.split ? m.first_a + i : m.first_b + (i - m.split);
 }
@@ -465,7 +465,7 @@ struct EpiOperands {
 __device__ __forceinline__ void epilogue_load(const KArgs& a, const TileRef& tr, uint32_t T, EpiOperands& eo) {
   const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
   const uint64_t* c = a.epi.c + tr.poly * a.epi.c_stride + e;
-  const uint64_t* o = a.epi.out + tr.poly * a.epi.out_stride + e;
+  const uint64_t* o = a.epi.ks_out(tr.poly) + e;
 #pragma unroll
   for (int j = 0; j < E; ++j) eo.c[j] = __builtin_nontemporal_load(c + j * T);
   if (a.epi.accumulate) {
@@ -476,7 +476,7 @@ __device__ __forceinline__ void epilogue_load(const KArgs& a, const TileRef& tr,
 __device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr, uint32_t j, uint32_t T,
                                                const EpiOperands& eo, uint64_t y, uint64_t q) {
   const size_t e = (size_t)tr.buf_limb * a.n + tr.k + j * T;
-  uint64_t* o = a.epi.out + tr.poly * a.epi.out_stride + e;
+  uint64_t* o = a.epi.ks_out(tr.poly) + e;
   uint64_t v = mul_shoup(sub_mod(eo.c[j], y, q), a.epi.w[tr.buf_limb], a.epi.ws[tr.buf_limb], q);
   if (a.epi.accumulate) v = add_mod(v, eo.o[j], q);
   store_wt(o, v);
@@ -496,7 +496,7 @@ __device__ __forceinline__ void epilogue_late(const KArgs& a, const TileRef& tr,
   constexpr int KC = PHX_EPI_LATE > 0 ? PHX_EPI_LATE : 1, NC = E / KC;
   const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
   const uint64_t* c = a.epi.c + tr.poly * a.epi.c_stride + e;
-  uint64_t* o = a.epi.out + tr.poly * a.epi.out_stride + e;
+  uint64_t* o = a.epi.ks_out(tr.poly) + e;
   const bool acc = a.epi.accumulate;
   const uint64_t* second = acc ? o : c;  // (a harmless re-read of c when not accumulating)
   const uint64_t w = a.epi.w[tr.buf_limb], ws = a.epi.ws[tr.buf_limb];
@@ -547,13 +547,13 @@ __device__ __forceinline__ void ks_epilogue_b(const KArgs& a, const TileRef& tr,
   constexpr int KC = PHX_KS_KC, NC = E / KC;
   const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
   const bool acc_out = a.epi.accumulate;
-  const uint64_t* tm = a.epi.tmu + e;
+  const uint64_t* tm = a.epi.ks_tmu(tr.poly) + e;
   const uint64_t* kp[BETA];
 #pragma unroll
-  for (int d = 0; d < BETA; ++d) kp[d] = a.epi.evk[d] + tr.poly * a.epi.evk_poly_stride + e;
-  uint64_t* o = a.epi.out + tr.poly * a.epi.out_stride + e;
+  for (int d = 0; d < BETA; ++d) kp[d] = a.epi.evk[d] + (tr.poly & 1) * a.epi.evk_poly_stride + e;
+  uint64_t* o = a.epi.ks_out(tr.poly) + e;
   const uint64_t w = a.epi.w[tr.buf_limb], ws = a.epi.ws[tr.buf_limb];
-  const uint64_t* ad = a.epi.add_c ? a.epi.add_c + tr.poly * a.epi.add_stride + e : nullptr;
+  const uint64_t* ad = a.epi.add_c ? a.epi.ks_add(tr.poly) + e : nullptr;
   const uint64_t pm = ad ? a.epi.pmod[tr.buf_limb] : 0, pms = ad ? a.epi.pmod_shoup[tr.buf_limb] : 0;
   const uint64_t* third = acc_out ? o : (ad ? ad : tm);  // (accumulate and addend never come together)
   uint64_t tb[2][BETA][KC], kb[2][BETA][KC], ob[2][KC];
@@ -592,7 +592,8 @@ __device__ __forceinline__ void ks_epilogue(const KArgs& a, const TileRef& tr, c
   switch (__builtin_amdgcn_readfirstlane(a.epi.ks_beta)) {
     case 1: ks_epilogue_b<T, 1>(a, tr, y, q, r0, r1); break;
     case 2: ks_epilogue_b<T, 2>(a, tr, y, q, r0, r1); break;
-    default: ks_epilogue_b<T, 3>(a, tr, y, q, r0, r1); break;
+    case 3: ks_epilogue_b<T, 3>(a, tr, y, q, r0, r1); break;
+    default: break;  // rejected on the host (check_ks)
   }
 }
 
@@ -604,12 +605,13 @@ __device__ __forceinline__ void ks_prologue_b(const KArgs& a, const TileRef& tr,
   constexpr int KC = PHX_KS_KC, NC = E / KC;
   const size_t n = static_cast<size_t>(a.n);
   const size_t tl = a.epi.tmu_limb0 + tr.buf_limb;
-  const uint64_t* tm = a.epi.tmu + tl * n + tr.k;
+  const uint64_t* tm = a.epi.ks_tmu(tr.poly) + tl * n + tr.k;
   const uint64_t* kp[BETA];
 #pragma unroll
-  for (int d = 0; d < BETA; ++d) kp[d] = a.epi.evk[d] + tr.poly * a.epi.evk_poly_stride + (size_t)tr.row * n + tr.k;
+  for (int d = 0; d < BETA; ++d)
+    kp[d] = a.epi.evk[d] + (tr.poly & 1) * a.epi.evk_poly_stride + (size_t)tr.row * n + tr.k;
   const bool add = tr.buf_limb < a.epi.add_limbs;  // wave-uniform
-  const uint64_t* ad = add ? a.epi.add_c + tr.poly * a.epi.add_stride + tl * n + tr.k : tm;
+  const uint64_t* ad = add ? a.epi.ks_add(tr.poly) + tl * n + tr.k : tm;
   const uint64_t pm = add ? a.epi.pmod[tl] : 0, pms = add ? a.epi.pmod_shoup[tl] : 0;
   const uint64_t q = a.modulus[tr.row], r0 = a.barrett[2 * tr.row], r1 = a.barrett[2 * tr.row + 1];
   uint64_t tb[2][BETA][KC], kb[2][BETA][KC], ob[2][KC];
@@ -645,7 +647,8 @@ __device__ __forceinline__ void ks_prologue(const KArgs& a, const TileRef& tr, u
   switch (__builtin_amdgcn_readfirstlane(a.epi.ks_beta)) {
     case 1: ks_prologue_b<T, 1>(a, tr, x); break;
     case 2: ks_prologue_b<T, 2>(a, tr, x); break;
-    default: ks_prologue_b<T, 3>(a, tr, x); break;
+    case 3: ks_prologue_b<T, 3>(a, tr, x); break;
+    default: break;  // rejected on the host (check_ks)
   }
 }
 
@@ -744,8 +747,8 @@ __device__ __forceinline__ TileRef col_ref(const KArgs& a, int tile, uint32_t c)
   r.poly = poly;
   r.k = (tile % CT) * COLS + c;
   const size_t e = (size_t)r.buf_limb * a.n + r.k;
-  r.off = poly * a.map.out_stride + e;
-  r.in_off = a.bcast ? poly * a.bcast_stride + r.k : poly * a.map.in_stride + e;
+  r.off = a.map.out_off(poly) + e;
+  r.in_off = a.bcast ? poly * a.bcast_stride + r.k : a.map.in_off(poly) + e;
   return r;
 }
 
@@ -903,8 +906,8 @@ __device__ __forceinline__ TileRef row_ref(const KArgs& a, int item, uint32_t lr
   tr.poly = poly;
   tr.k = (size_t)r * S2 + t;
   const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
-  tr.off = poly * a.map.out_stride + e;
-  tr.in_off = poly * a.map.in_stride + e;
+  tr.off = a.map.out_off(poly) + e;
+  tr.in_off = a.map.in_off(poly) + e;
   return tr;
 }
 
@@ -917,7 +920,7 @@ __device__ __forceinline__ void row_load(uint64_t (&x)[E], const uint64_t* src) 
 // inverse row pass with NttCopy: the loaded input limb stored unchanged into its digit's slot
 template <int S2_LOG>
 __device__ __forceinline__ void row_copy(const KArgs& a, const TileRef& tr, const uint64_t (&x)[E]) {
-  uint64_t* dst = a.copy.out + (size_t)(tr.buf_limb / a.copy.alpha) * a.copy.digit_stride +
+  uint64_t* dst = a.copy.out + tr.poly * a.copy.poly_stride + (size_t)(tr.buf_limb / a.copy.alpha) * a.copy.digit_stride +
                   (size_t)tr.buf_limb * a.n + tr.k;
 #pragma unroll
   for (int j = 0; j < E; ++j) store_wt(dst + j * Sub<S2_LOG>::T, x[j]);
@@ -1193,7 +1196,7 @@ __global__ __launch_bounds__(1024) void ntt_1d(KArgs a) {
   for (int k = i; k < n; k += half) {
     uint64_t x;
     if (FWD && a.bcast) x = barrett_reduce_64(a.bcast[poly * a.bcast_stride + k], q, a.barrett[2 * row + 1]);
-    else x = a.in[poly * a.map.in_stride + e0 + k];
+    else x = a.in[a.map.in_off(poly) + e0 + k];
     v[k] = x;
   }
   __syncthreads();
@@ -1216,13 +1219,13 @@ __global__ __launch_bounds__(1024) void ntt_1d(KArgs a) {
       __syncthreads();
     }
   }
-  uint64_t* out = a.out + poly * a.map.out_stride + e0;
+  uint64_t* out = a.out + a.map.out_off(poly) + e0;
   for (int k = i; k < n; k += half) {
     uint64_t y = v[k];
     if constexpr (FWD) {
       y = csub(csub(y, q2), q);
       if (a.epi.out) {
-        uint64_t* o = a.epi.out + poly * a.epi.out_stride + e0 + k;
+        uint64_t* o = a.epi.ks_out(poly) + e0 + k;
         uint64_t r = mul_shoup(sub_mod(a.epi.c[poly * a.epi.c_stride + e0 + k], y, q), a.epi.w[buf_limb],
                                a.epi.ws[buf_limb], q);
         if (a.epi.accumulate) r = add_mod(r, *o, q);
@@ -1325,6 +1328,7 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
       hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true, false, false>), grid_c, block_c, 0, stream, a);
     a.in = out;
     a.map.in_stride = a.map.out_stride;
+    a.map.in_outer = a.map.out_outer;
     a.bcast = nullptr;  // the row pass reads the intermediate
     a.epi = epi_row;
     if (a.epi.out && a.epi.ks_beta > 0 && lz)
@@ -1346,6 +1350,7 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false>), grid_r, block_r, 0, stream, a);
     a.in = out;
     a.map.in_stride = a.map.out_stride;
+    a.map.in_outer = a.map.out_outer;
     a.copy = NttCopy{};  // the row pass made the copy
     a.epi = NttEpilogue{};  // ... and consumed the key-switch prologue
     hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false>), grid_c, block_c, 0, stream, a);
@@ -1371,6 +1376,21 @@ hipError_t dispatch(const NttTables& tb, const uint64_t* in, uint64_t* out, cons
 #undef PHX_NTT_CASE
 }
 
+// the key-switch form's operands (ntt.h NttEpilogue): every launcher that can receive one checks them
+hipError_t check_ks(const NttTables& t, const LimbMap& map, const NttEpilogue& ks) {
+  if (ks.ks_prods < 1 || ks.ks_prods > kMaxKsProds) return hipErrorInvalidValue;
+  if (ks.ks_prods > 1) {  // per-pair outputs (and addends): the map must hold exactly those pairs
+    if (map.polys != 2 * ks.ks_prods) return hipErrorInvalidValue;
+    for (int k = 0; k < ks.ks_prods; ++k)
+      if (!ks.out_p[k] || (ks.ks_beta > 0 && ks.add_c && !ks.add_p[k])) return hipErrorInvalidValue;
+  }
+  if (ks.ks_beta == 0) return hipSuccess;
+  if (ks.ks_beta < 1 || ks.ks_beta > kMaxKsBeta || !ks.tmu || !ks.evk) return hipErrorInvalidValue;
+  if (map.polys != 2 * ks.ks_prods) return hipErrorInvalidValue;
+  if (t.log_n < 10) return hipErrorNotSupported;  // the 1-D path has no key-switch form
+  return hipSuccess;
+}
+
 }  // namespace
 
 hipError_t ntt_forward(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
@@ -1381,12 +1401,14 @@ hipError_t ntt_forward(const NttTables& t, const uint64_t* in, uint64_t* out, co
 hipError_t ntt_forward_fused(const NttTables& t, const uint64_t* in, uint64_t* out, const LimbMap& map,
                              const uint64_t* bcast, size_t bcast_stride, const NttEpilogue& epi, hipStream_t stream) {
   if (epi.out && (!epi.c || !epi.w || !epi.ws)) return hipErrorInvalidValue;
+  if (hipError_t e = check_ks(t, map, epi)) return e;
   return dispatch(t, in, out, map, false, nullptr, nullptr, stream, bcast, bcast_stride, epi);
 }
 
 hipError_t ntt_forward_bconv(const NttTables& t, uint64_t* out, const LimbMap& map, const BconvPrologue& bcv,
                              const NttEpilogue& epi, hipStream_t stream) {
   if (epi.out && (!epi.c || !epi.w || !epi.ws)) return hipErrorInvalidValue;
+  if (hipError_t e = check_ks(t, map, epi)) return e;
   if (!bcv.in || bcv.ob <= 0 || map.polys < 1 || map.polys > kMaxBconvPolys) return hipErrorInvalidValue;
   const int per_poly = map.num_limbs - (map.skip_end - map.skip_begin);
   for (int p = 0; p < map.polys; ++p) {
@@ -1403,9 +1425,9 @@ hipError_t ntt_inverse(const NttTables& t, const uint64_t* in, uint64_t* out, co
 
 hipError_t ntt_inverse_ks(const NttTables& t, uint64_t* out, const LimbMap& map, const uint64_t* scale,
                           const uint64_t* scale_shoup, const NttEpilogue& ks, hipStream_t stream) {
-  if (ks.ks_beta < 1 || ks.ks_beta > kMaxKsBeta || !ks.tmu || !ks.evk) return hipErrorInvalidValue;
+  if (ks.ks_beta < 1) return hipErrorInvalidValue;
+  if (hipError_t e = check_ks(t, map, ks)) return e;
   if (ks.add_limbs > 0 && (!ks.add_c || !ks.pmod || !ks.pmod_shoup)) return hipErrorInvalidValue;
-  if (t.log_n < 10) return hipErrorNotSupported;
   return dispatch(t, nullptr, out, map, true, scale, scale_shoup, stream, nullptr, 0, ks);
 }
 

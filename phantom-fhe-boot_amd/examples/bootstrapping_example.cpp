@@ -264,7 +264,7 @@ int main(int argc, char** argv) {
       report("flex_mult_plain_auto", max_abs_err(decrypt_decode(ctx, sk, enc, mp), want_of([](double v) { return 0.5 * v; })),
              1e-5, mp.chain_index());
     }
-    // Chebyshev series on [1, 5]: degree 4 (the linear method) and 30 (the fused recursion),
+    // Chebyshev series on [1, 5]: degree 4 (the linear method) and 30 (Paterson-Stockmeyer),
     // against the host value of the same interpolant; levels consumed reported
     for (uint32_t deg : {4u, 30u}) {
       auto f = [](double t) { return std::sin(t) / t; };
@@ -290,6 +290,51 @@ int main(int argc, char** argv) {
     return g_ok ? 0 : 1;
   }
 
+  if (mode == "chebdepth") {
+    // EvalChebyshevSeries through the reference's Paterson-Stockmeyer (host/chebyshev_ps.cpp) for
+    // every degree 5..119 on three intervals: levels consumed (a pending rescale counts) against
+    // the reference's GetDepthByDegree (src/util.cu:44-71), and the decrypted value against the
+    // host evaluation of the same interpolant
+    PhantomRelinKey rlk = sk.gen_relinkey(ctx);
+    ct.PreComputeScale(ctx, scale);
+    const std::vector<double> sfR = ct.getScalingFactorsReal(), sfB = ct.getScalingFactorsRealBig();
+    const int dmin = argc > 4 ? std::atoi(argv[4]) : 5, dmax = argc > 5 ? std::atoi(argv[5]) : 119;
+    struct Iv {
+      double a, b, shift;  // inputs x + shift (x in [1, 5]) lie inside [a, b]
+    };
+    for (const Iv iv : {Iv{-1.0, 1.0, -3.0}, Iv{0.0, 5.0, 0.0}, Iv{-8.0, 3.0, -4.0}}) {
+      std::vector<double> xs(slots);
+      for (size_t j = 0; j < slots; ++j) xs[j] = iv.shift == -3.0 ? (x[j] - 3.0) / 2.0 : x[j] + iv.shift;
+      PhantomPlaintext px;
+      enc.encode(ctx, xs, sf[0], px, 1);
+      PhantomCiphertext cx;
+      sk.encrypt_symmetric(ctx, px, cx);
+      auto f = [](double t) { return 1.0 / (1.0 + t * t); };
+      for (int deg = dmin; deg <= dmax; ++deg) {
+        const std::vector<double> co = EvalChebyshevCoefficients(f, iv.a, iv.b, static_cast<uint32_t>(deg));
+        PhantomCiphertext cs = EvalChebyshevSeries(ctx, rlk, cx, co, iv.a, iv.b, sfR, sfB);
+        std::vector<std::complex<double>> host(slots);
+        for (size_t j = 0; j < slots; ++j) {
+          const double y = (2.0 * xs[j] - iv.a - iv.b) / (iv.b - iv.a);
+          double t0 = 1.0, t1 = y, acc = co[0] / 2 + co[1] * y;
+          for (size_t k = 2; k < co.size(); ++k) {
+            const double t2 = 2.0 * y * t1 - t0;
+            acc += co[k] * t2;
+            t0 = t1;
+            t1 = t2;
+          }
+          host[j] = acc;
+        }
+        const size_t used = cs.chain_index() - cx.chain_index() + (cs.GetNoiseScaleDeg() > 1 ? 1 : 0);
+        const double err = max_abs_err(decrypt_decode(ctx, sk, enc, cs), host);
+        std::printf("{\"cheb\": %d, \"a\": %g, \"b\": %g, \"levels_used\": %zu, \"depth_by_degree\": %u, "
+                    "\"degree_out\": %zu, \"max_abs_err\": %.3e}\n",
+                    deg, iv.a, iv.b, used, ps::GetDepthByDegree(static_cast<size_t>(deg)), cs.GetNoiseScaleDeg(), err);
+      }
+    }
+    std::printf("{\"done\": \"chebdepth\", \"ok\": true}\n");
+    return 0;
+  }
   if (mode == "ops") {
     PhantomGaloisKey gk = sk.create_galois_keys_fused(
         ctx, {FindAutomorphismIndex2nComplex(1, N), FindAutomorphismIndex2nComplex(-3, N), static_cast<uint32_t>(2 * N - 1)});

@@ -5,7 +5,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
+#include <deque>
 #include <exception>
+#include <set>
 #include <stdexcept>
 #include <thread>
 
@@ -160,72 +162,136 @@ int cheb_depth(int d) {
   return std::max(std::max(cheb_depth(d - m), ceil_log2(m)) + 1, cheb_depth(m - 1));
 }
 
+// The evaluator runs B independent series inputs ("lanes", all at one level and scale) in lockstep:
+// EvalMod evaluates the same series on the real and the imaginary half of the CoeffToSlot output,
+// so every product of the two halves shares one key switch launch sequence (MulAddRescaleBatch),
+// and the members of a power-ladder generation do too.
+using Lanes = std::vector<PhantomCiphertext>;
+
 struct ChebEvaluator {
   const PhantomContext& cc;
   const PhantomRelinKey& rlk;
   const std::vector<double>& sf;
   LeafTableCache& tables;
-  std::map<int, PhantomCiphertext> T;
-  std::map<std::pair<int, size_t>, PhantomCiphertext> aligned_;  // T_i brought to a deeper level
-  std::mutex mu;  // the maps, when the power ladder runs a generation on two streams
+  size_t B = 1;
+  std::map<int, Lanes> T;
+  std::map<std::pair<int, size_t>, Lanes> aligned_;  // T_i brought to a deeper level
 
-  // T_i at level `lvl` (>= its own), cached: the power ladder re-uses T_1, T_2, .. at the level
-  // of every larger factor
-  const PhantomCiphertext& aligned(int i, size_t lvl) {
-    const PhantomCiphertext& t = get(i);
-    if (level_of(t) == lvl) return t;
-    auto key = std::make_pair(i, lvl);
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      auto it = aligned_.find(key);
-      if (it != aligned_.end()) return it->second;
+  static size_t lvl(const Lanes& v) { return level_of(v.at(0)); }
+
+  // T_i at level `l` (>= its own), cached: the power ladder re-uses T_1, T_2, .. at the level of
+  // every larger factor
+  const Lanes& aligned(int i, size_t l) {
+    const Lanes& t = get(i);
+    if (lvl(t) == l) return t;
+    auto key = std::make_pair(i, l);
+    auto it = aligned_.find(key);
+    if (it != aligned_.end()) return it->second;
+    Lanes v(B);
+    for (size_t b = 0; b < B; ++b) {
+      PhantomCiphertext tmp;
+      const PhantomCiphertext& r = AtLevel(cc, t[b], l, sf, tmp);
+      v[b] = &r == &t[b] ? PhantomCiphertext(t[b]) : std::move(tmp);
     }
-    PhantomCiphertext tmp;
-    const PhantomCiphertext& r = AtLevel(cc, t, lvl, sf, tmp);
-    PhantomCiphertext v = &r == &t ? PhantomCiphertext(t) : std::move(tmp);
-    std::lock_guard<std::mutex> lk(mu);
     return aligned_.emplace(key, std::move(v)).first->second;
   }
 
-  // the operands T_a, T_(i-a) of T_i at their common level (computed ahead of a parallel
-  // generation, so that no stream uses an aligned copy another stream is still writing)
-  void prepare(int i) {
-    int a = 1;
-    while (2 * a < i) a *= 2;
-    if (2 * a == i) return;
-    const size_t lvl = std::max(level_of(get(a)), level_of(get(i - a)));
-    aligned(a, lvl);
-    aligned(i - a, lvl);
+  // T_i at level l for every (i, l) of `want` (not yet cached), all lanes, in shared launches
+  // (AtLevelBatch: the scaled copies side by side, one batched rescale per target level)
+  void align_many(const std::vector<std::pair<int, size_t>>& want) {
+    std::set<std::pair<int, size_t>> keys;
+    for (const auto& w : want)
+      if (lvl(get(w.first)) != w.second && !aligned_.count(w)) keys.insert(w);
+    if (keys.empty()) return;
+    std::vector<const PhantomCiphertext*> src;
+    std::vector<size_t> tgt;
+    for (const auto& [i, l] : keys)
+      for (size_t b = 0; b < B; ++b) {
+        src.push_back(&get(i)[b]);
+        tgt.push_back(l);
+      }
+    std::vector<PhantomCiphertext> r = AtLevelBatch(cc, src, tgt, sf);
+    size_t k = 0;
+    for (const auto& key : keys) {
+      Lanes v(B);
+      for (size_t b = 0; b < B; ++b, ++k) v[b] = r[k].size() ? std::move(r[k]) : PhantomCiphertext(get(key.first)[b]);
+      aligned_.emplace(key, std::move(v));
+    }
   }
 
-  const PhantomCiphertext& get(int i) {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      auto it = T.find(i);
-      if (it != T.end()) return it->second;
-    }
-    PhantomCiphertext r;
+  static int half_of(int i) {
     int a = 1;
     while (2 * a < i) a *= 2;  // a >= i / 2, a < i
-    if (2 * a == i) {
-      // T_2a = 2 T_a^2 - 1, the doubling and the constant folded in before the one key switch
-      const PhantomCiphertext& ta = get(a);
-      r = MulAddRescale(cc, ta, ta, rlk, 2, {}, -1.0);
-    } else {
-      // T_i = 2 T_a T_(i-a) - T_(2a-i); T_(2a-i) joins the product before its rescale
-      const size_t lvl = std::max(level_of(get(a)), level_of(get(i - a)));
-      const PhantomCiphertext& x = aligned(a, lvl);
-      const PhantomCiphertext& y = aligned(i - a, lvl);
-      const PhantomCiphertext& z = get(2 * a - i);
-      if (level_of(z) <= lvl) {
-        r = MulAddRescale(cc, x, y, rlk, 2, {{&z, -1.0}}, 0.0);
-      } else {
-        r = MulAddRescale(cc, x, y, rlk, 2, {}, 0.0);
-        EvalSubAutoInplace(cc, r, z, sf);
+    return a;
+  }
+
+  // T_i for every i of `idx` (absent so far, operands present or computable), all lanes, the
+  // products in one batch: T_2a = 2 T_a^2 - 1 (doubling and constant folded in before the one
+  // key switch); T_i = 2 T_a T_(i-a) - T_(2a-i), T_(2a-i) joining the product before its rescale
+  // when it is not deeper than the product
+  void compute(const std::vector<int>& idx) {
+    for (int i : idx) {  // operands first (they may need a batch of their own)
+      const int a = half_of(i);
+      get(a);
+      if (2 * a != i) {
+        get(i - a);
+        get(2 * a - i);
       }
     }
-    std::lock_guard<std::mutex> lk(mu);
-    return T.emplace(i, std::move(r)).first->second;
+    std::vector<std::pair<int, size_t>> want;  // the operands' alignments, made together
+    for (int i : idx) {
+      const int a = half_of(i);
+      if (2 * a == i) continue;
+      const size_t l = std::max(lvl(get(a)), lvl(get(i - a)));
+      want.push_back({a, l});
+      want.push_back({i - a, l});
+    }
+    align_many(want);
+    std::vector<MulAddJob> jobs;
+    std::vector<std::pair<int, const Lanes*>> late;  // T_(2a-i) deeper than the product: subtracted after
+    for (int i : idx) {
+      const int a = half_of(i);
+      if (2 * a == i) {
+        const Lanes& ta = get(a);
+        for (size_t b = 0; b < B; ++b) jobs.push_back(MulAddJob{&ta[b], &ta[b], 2, {}, -1.0});
+        continue;
+      }
+      const size_t l = std::max(lvl(get(a)), lvl(get(i - a)));
+      const Lanes& x = aligned(a, l);
+      const Lanes& y = aligned(i - a, l);
+      const Lanes& z = get(2 * a - i);
+      const bool fold = lvl(z) <= l;
+      for (size_t b = 0; b < B; ++b) {
+        MulAddJob j{&x[b], &y[b], 2, {}, 0.0};
+        if (fold) j.terms.push_back({&z[b], -1.0});
+        jobs.push_back(std::move(j));
+      }
+      if (!fold) late.push_back({i, &z});
+    }
+    // products of one level share a batch (a generation's members always do)
+    std::map<size_t, std::vector<size_t>> by_level;
+    for (size_t k = 0; k < jobs.size(); ++k) by_level[level_of(*jobs[k].a)].push_back(k);
+    std::vector<PhantomCiphertext> out(jobs.size());
+    for (auto& [l, ks] : by_level) {
+      std::vector<MulAddJob> part;
+      for (size_t k : ks) part.push_back(jobs[k]);
+      std::vector<PhantomCiphertext> r = MulAddRescaleBatch(cc, part, rlk);
+      for (size_t m = 0; m < ks.size(); ++m) out[ks[m]] = std::move(r[m]);
+    }
+    for (size_t m = 0; m < idx.size(); ++m) {
+      Lanes v(B);
+      for (size_t b = 0; b < B; ++b) v[b] = std::move(out[m * B + b]);
+      T.emplace(idx[m], std::move(v));
+    }
+    for (auto& [i, z] : late)
+      for (size_t b = 0; b < B; ++b) EvalSubAutoInplace(cc, T.at(i)[b], (*z)[b], sf);
+  }
+
+  const Lanes& get(int i) {
+    auto it = T.find(i);
+    if (it != T.end()) return it->second;
+    compute({i});
+    return T.at(i);
   }
 
   // ---- the series as a tree: p = q T_m + r down to degree <= kLeafDegree leaves ----------
@@ -233,7 +299,7 @@ struct ChebEvaluator {
     std::vector<double> c;  // leaf coefficients
     int m = 0;              // inner node: q T_m + r
     std::unique_ptr<Node> q, r;
-    PhantomCiphertext v;    // a leaf's value
+    Lanes v;                // a leaf's value
   };
 
   static std::unique_ptr<Node> plan(const std::vector<double>& c) {
@@ -269,25 +335,27 @@ struct ChebEvaluator {
   }
 
   // every leaf sum_i c_i T_i lands on the deepest level of its T_1..T_d with scale sf[l]^2;
-  // the leaves of one level are evaluated together by one kernel that reads each T_i once
-  // (FHECKKSRNS::leaf_tables caches the constant tables), then each is rescaled
+  // the leaves of one level are evaluated together by one kernel per lane that reads each T_i
+  // once (FHECKKSRNS::leaf_tables caches the constant tables) into one buffer, and rescaled
+  // together by one batched rescale into their own ciphertexts
   void eval_leaves(std::vector<Node*>& leaves) {
     std::map<size_t, std::vector<Node*>> by_level;
     for (Node* lf : leaves) {
       const int d = static_cast<int>(lf->c.size()) - 1;
-      if (d < 1) continue;  // a constant remainder: combine() folds it into its parent's product
-      size_t lvl = 0;
-      for (int i = 1; i <= d; ++i) lvl = std::max(lvl, level_of(get(i)));
-      by_level[lvl].push_back(lf);
+      if (d < 1) continue;  // a constant remainder: its parent's product takes it as a constant
+      size_t l = 0;
+      for (int i = 1; i <= d; ++i) l = std::max(l, lvl(get(i)));
+      by_level[l].push_back(lf);
     }
     const size_t n = cc.poly_degree();
-    for (auto& [lvl, group] : by_level) {
+    hipStream_t s = cc.stream();
+    for (auto& [l, group] : by_level) {
       for (size_t g0 = 0; g0 < group.size(); g0 += phx::kLeafMaxM) {
         const int M = static_cast<int>(std::min<size_t>(phx::kLeafMaxM, group.size() - g0));
         int K = 0;
         for (int m = 0; m < M; ++m) K = std::max(K, static_cast<int>(group[g0 + m]->c.size()) - 1);
-        const size_t chain = lvl + 1, L = cc.get_context_data(chain).coeff_modulus_size();
-        const double target = sf.at(lvl) * sf.at(lvl);
+        const size_t chain = l + 1, L = cc.get_context_data(chain).coeff_modulus_size();
+        const double target = sf.at(l) * sf.at(l);
         std::vector<uint64_t> tab(2 * static_cast<size_t>(M) * K * L + static_cast<size_t>(M) * L, 0);
         uint64_t* cv = tab.data();
         uint64_t* cs = cv + static_cast<size_t>(M) * K * L;
@@ -297,175 +365,169 @@ struct ChebEvaluator {
           for (int k = 0; k < K; ++k) {
             const double coeff = k + 1 < static_cast<int>(c.size()) ? c[k + 1] : 0.0;
             const size_t off = (static_cast<size_t>(m) * K + k) * L;
-            ScalarResidues(cc, chain, coeff * target / get(k + 1).scale(), cv + off, cs + off);
+            ScalarResidues(cc, chain, coeff * target / get(k + 1)[0].scale(), cv + off, cs + off);
           }
           ScalarResidues(cc, chain, c[0] * target, ca + static_cast<size_t>(m) * L, nullptr);
         }
-        phx::LeafArgs la;
-        la.K = K;
-        la.M = M;
-        la.L = static_cast<int>(L);
-        la.q = cc.mod_QP().q;
-        la.barrett = cc.mod_QP().barrett;
-        la.coef = tables.get(tab, cc.stream());
-        la.cadd = la.coef + 2 * static_cast<size_t>(M) * K * L;
-        for (int k = 0; k < K; ++k) {
-          la.in[k] = get(k + 1).data();
-          la.in_stride[k] = get(k + 1).coeff_modulus_size() * n;
+        const uint64_t* coef = tables.get(tab, s);
+        const size_t cts = static_cast<size_t>(M) * B, ct_words = 2 * L * n;
+        DeviceBuffer<uint64_t> w(cts * ct_words, s);  // leaf (m, lane b) at ((m B + b) 2 L) n
+        for (size_t b = 0; b < B; ++b) {
+          phx::LeafArgs la;
+          la.K = K;
+          la.M = M;
+          la.L = static_cast<int>(L);
+          la.q = cc.mod_QP().q;
+          la.barrett = cc.mod_QP().barrett;
+          la.coef = coef;
+          la.cadd = la.coef + 2 * static_cast<size_t>(M) * K * L;
+          for (int k = 0; k < K; ++k) {
+            la.in[k] = get(k + 1)[b].data();
+            la.in_stride[k] = get(k + 1)[b].coeff_modulus_size() * n;
+          }
+          for (int m = 0; m < M; ++m) la.out[m] = w.get() + (static_cast<size_t>(m) * B + b) * ct_words;
+          hip_ok(phx::leaf_combine(la, n, s), "Chebyshev leaves");
         }
+        // scale target / q_last, degree 1 (EvalModReduceInPlace of a degree-2 leaf)
+        const RnsTool& rt = cc.get_context_data(chain).gpu_rns_tool();
+        const double qlast = static_cast<double>(rt.base_Ql().back());
+        std::vector<uint64_t*> outs(cts);
         for (int m = 0; m < M; ++m) {
-          PhantomCiphertext& v = group[g0 + m]->v;
-          v.resize(cc, chain, 2, cc.stream(), false);
-          v.set_ntt_form(true);
-          v.set_scale(target);
-          v.SetNoiseScaleDeg(2);
-          la.out[m] = v.data();
+          Lanes& v = group[g0 + m]->v;
+          v.assign(B, PhantomCiphertext());
+          for (size_t b = 0; b < B; ++b) {
+            v[b].resize(cc, chain + 1, 2, s, false);
+            v[b].set_ntt_form(true);
+            v[b].set_scale(target / qlast);
+            v[b].SetNoiseScaleDeg(1);
+            outs[static_cast<size_t>(m) * B + b] = v[b].data();
+          }
         }
-        hip_ok(phx::leaf_combine(la, n, cc.stream()), "Chebyshev leaves");
-        for (int m = 0; m < M; ++m) EvalModReduceInPlace(cc, group[g0 + m]->v, 1);
+        for (size_t c0 = 0; c0 < cts; c0 += phx::kMaxKsProds)
+          rt.rescale_ntt_to(w.get() + c0 * ct_words, outs.data() + c0,
+                            std::min<size_t>(phx::kMaxKsProds, cts - c0), cc.gpu_rns_tables(), s);
       }
     }
   }
 
-  PhantomCiphertext combine(Node* node) {
-    if (!node->m) return std::move(node->v);
-    PhantomCiphertext qv = combine(node->q.get());
-    PhantomCiphertext rv = (node->r->m || node->r->c.size() > 1) ? combine(node->r.get()) : PhantomCiphertext();
-    // q T_m + r: r joins the product before its rescale when it is not deeper than it
-    const size_t lvl = std::max(level_of(qv), level_of(get(node->m)));
-    PhantomCiphertext tmp;
-    const PhantomCiphertext& x = AtLevel(cc, qv, lvl, sf, tmp);
-    const PhantomCiphertext& y = aligned(node->m, lvl);
-    if (!node->r->m && node->r->c.size() <= 1)  // constant remainder
-      return MulAddRescale(cc, x, y, rlk, 1, {}, node->r->c.empty() ? 0.0 : node->r->c[0]);
-    if (level_of(rv) <= lvl) return MulAddRescale(cc, x, y, rlk, 1, {{&rv, 1.0}}, 0.0);
-    PhantomCiphertext res = MulAddRescale(cc, x, y, rlk, 1, {}, 0.0);
-    EvalAddAutoInplace(cc, res, rv, sf);
-    return res;
+  static bool has_value(const Node* nd) { return nd->m || nd->c.size() > 1; }
+
+  // the products q T_m + r of every node in `nodes` (their children evaluated), one batched key
+  // switch per product level: r joins a product before its rescale when it is not deeper than it,
+  // a constant r as the product's constant
+  void combine_round(const std::vector<Node*>& nodes) {
+    std::deque<PhantomCiphertext> tmp;  // AtLevel copies, alive through the batch
+    std::vector<MulAddJob> jobs;
+    std::vector<std::pair<Node*, size_t>> dst;
+    std::vector<Node*> late;  // r deeper than the product: added after the rescale
+    // every operand's alignment first, in shared launches: T_m (cached) and the q values
+    std::vector<std::pair<int, size_t>> want;
+    std::vector<const PhantomCiphertext*> qsrc;
+    std::vector<size_t> qtgt;
+    for (Node* nd : nodes) {
+      const size_t l = std::max(lvl(nd->q->v), lvl(get(nd->m)));
+      want.push_back({nd->m, l});
+      for (size_t b = 0; b < B; ++b) {
+        qsrc.push_back(&nd->q->v[b]);
+        qtgt.push_back(l);
+      }
+    }
+    align_many(want);
+    std::vector<PhantomCiphertext> qal = AtLevelBatch(cc, qsrc, qtgt, sf);
+    size_t qk = 0;
+    for (Node* nd : nodes) {
+      const Lanes& qv = nd->q->v;
+      const Node* rn = nd->r.get();
+      const size_t l = std::max(lvl(qv), lvl(get(nd->m)));
+      const Lanes& y = aligned(nd->m, l);
+      const bool rv = has_value(rn), fold = rv && lvl(rn->v) <= l;
+      for (size_t b = 0; b < B; ++b, ++qk) {
+        tmp.emplace_back(std::move(qal[qk]));
+        const PhantomCiphertext& x = tmp.back().size() ? tmp.back() : qv[b];
+        MulAddJob j{&x, &y[b], 1, {}, 0.0};
+        if (!rv) j.constant = rn->c.empty() ? 0.0 : rn->c[0];
+        if (fold) j.terms.push_back({&rn->v[b], 1.0});
+        jobs.push_back(std::move(j));
+        dst.push_back({nd, b});
+      }
+      if (rv && !fold) late.push_back(nd);
+      nd->v.assign(B, PhantomCiphertext());
+    }
+    std::map<size_t, std::vector<size_t>> by_level;
+    for (size_t k = 0; k < jobs.size(); ++k) by_level[level_of(*jobs[k].a)].push_back(k);
+    for (auto& [l, ks] : by_level) {
+      std::vector<MulAddJob> part;
+      for (size_t k : ks) part.push_back(jobs[k]);
+      std::vector<PhantomCiphertext> r = MulAddRescaleBatch(cc, part, rlk);
+      for (size_t m = 0; m < ks.size(); ++m) dst[ks[m]].first->v[dst[ks[m]].second] = std::move(r[m]);
+    }
+    for (Node* nd : late)
+      for (size_t b = 0; b < B; ++b) EvalAddAutoInplace(cc, nd->v[b], nd->r->v[b], sf);
+    for (Node* nd : nodes) {  // the children's values are consumed
+      nd->q->v.clear();
+      nd->r->v.clear();
+    }
   }
 
-  PhantomCiphertext eval(const std::vector<double>& c) {
+  static int height(Node* nd, std::map<int, std::vector<Node*>>& by_h) {
+    if (!nd->m) return 0;
+    const int h = 1 + std::max(height(nd->q.get(), by_h), height(nd->r.get(), by_h));
+    by_h[h].push_back(nd);
+    return h;
+  }
+
+  // every T_i the tree reads: the leaves' T_1 .. T_d and the split points T_m
+  static void needed(const Node* nd, std::set<int>& need) {
+    if (!nd->m) {
+      for (int i = 1; i < static_cast<int>(nd->c.size()); ++i) need.insert(i);
+      return;
+    }
+    need.insert(nd->m);
+    needed(nd->q.get(), need);
+    needed(nd->r.get(), need);
+  }
+
+  Lanes eval(const std::vector<double>& c) {
     std::unique_ptr<Node> root = plan(c);
+    std::set<int> need;
+    needed(root.get(), need);
+    ladder(need);
     std::vector<Node*> leaves;
     collect(root.get(), leaves);
     eval_leaves(leaves);
-    return combine(root.get());
+    std::map<int, std::vector<Node*>> by_h;
+    height(root.get(), by_h);
+    for (auto& [h, nodes] : by_h) combine_round(nodes);  // bottom-up, one round per height
+    return std::move(root->v);
+  }
+
+  // the needed T_i (and what they are built from) generation by generation: T_(2^(g-1)+1) ..
+  // T_(2^g) depend only on earlier generations and share a level, so each generation is one
+  // batched key switch (T_16 joins T_9 .. T_15)
+  void ladder(const std::set<int>& need) {
+    std::set<int> all;
+    std::vector<int> stack(need.begin(), need.end());
+    while (!stack.empty()) {
+      const int i = stack.back();
+      stack.pop_back();
+      if (i < 2 || !all.insert(i).second) continue;
+      const int a = half_of(i);
+      stack.push_back(a);
+      if (2 * a != i) {
+        stack.push_back(i - a);
+        stack.push_back(2 * a - i);
+      }
+    }
+    for (int lo = 2, hi = 2; !all.empty() && lo <= *all.rbegin(); lo = hi + 1, hi *= 2) {
+      std::vector<int> members;
+      for (int i : all)
+        if (i >= lo && i <= hi && !T.count(i)) members.push_back(i);
+      if (!members.empty()) compute(members);
+    }
   }
 };
 
 }  // namespace
-
-PhantomCiphertext EvalChebyshevSeriesPS(const PhantomContext& ctx, const PhantomRelinKey& rlk, const PhantomCiphertext& x,
-                                        const std::vector<double>& coeffs, double a, double b,
-                                        const std::vector<double>& sf, const std::vector<double>& sfBig) {
-  size_t d = coeffs.size() ? coeffs.size() - 1 : 0;
-  while (d > 0 && coeffs[d] == 0.0) --d;
-  if (d < 2) return EvalChebyshevSeriesLinear(ctx, rlk, x, {coeffs.at(0), d ? coeffs[1] : 0.0}, a, b, sf, sfBig);
-  // y = (2 x - a - b) / (b - a) at degree 1 (as EvalChebyshevSeriesLinear's T_1, src/evaluate.cu:3195-3207)
-  PhantomCiphertext y = x;
-  const bool unit = std::fabs(a + 1.0) < 1e-10 && std::fabs(b - 1.0) < 1e-10;
-  if (!unit) {
-    EvalMultConstInplace(ctx, y, 2.0 / (b - a), sf);
-    EvalAddConstInPlaceWrap(ctx, y, -1.0 - 2.0 * a / (b - a), sf, sfBig);
-  }
-  if (y.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(ctx, y, 1);
-  // the reference's series adds c_0 / 2; the evaluator's p = sum c_k T_k takes c_0 as is
-  std::vector<double> c(coeffs.begin(), coeffs.begin() + static_cast<long>(d) + 1);
-  c[0] *= 0.5;
-  LeafTableCache tables;
-  ChebEvaluator ev{ctx, rlk, sf, tables, {}, {}, {}};
-  ev.T.emplace(1, std::move(y));
-  PhantomCiphertext r = ev.eval(c);
-  PHX_CHECK(hipStreamSynchronize(ctx.stream()));  // the leaf tables die with this frame
-  return r;
-}
-
-// ======================================================================================
-// concurrent chains: task(0) on this thread's stream, task(i) from worker thread i on stream i
-// of a pool (StreamScope): at top level the pool is the context's aux streams; inside a task
-// it is the task's spare stream, so two levels of nesting can each run two chains.  Every
-// pool stream starts after everything already enqueued on this thread's stream, which
-// continues after all of them.  Buffers allocated on one stream and used on another must stay
-// alive until this returns.
-// ======================================================================================
-// true on every thread while it runs a task of run_parallel (the main thread included)
-static bool& in_parallel_section() {
-  static thread_local bool b = false;
-  return b;
-}
-
-template <typename Task>
-static void run_parallel(const PhantomContext& cc, int k, Task&& task) {
-  std::vector<hipStream_t> pool;
-  if (!in_parallel_section()) {
-    for (int i = 0; i < PhantomContext::kAuxStreams; ++i) pool.push_back(cc.aux_stream(i));
-  } else if (StreamScope::spare()) {
-    pool.push_back(StreamScope::spare());
-  }
-  k = std::min<int>(k, 1 + static_cast<int>(pool.size()));
-  if (k <= 1) {
-    for (int i = 0; i < std::max(k, 1); ++i) task(i);
-    return;
-  }
-  // pool[0 .. k-2] run the workers; the rest become the tasks' spare streams
-  auto spare_of = [&](int t) -> hipStream_t {
-    const size_t i = static_cast<size_t>(k - 1 + t);
-    return i < pool.size() ? pool[i] : nullptr;
-  };
-  const hipStream_t s0 = cc.stream();
-  hipEvent_t fork;
-  std::vector<hipEvent_t> join(k - 1);
-  PHX_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-  for (auto& e : join) PHX_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  PHX_CHECK(hipEventRecord(fork, s0));
-  for (int i = 1; i < k; ++i) PHX_CHECK(hipStreamWaitEvent(pool[i - 1], fork, 0));
-  std::vector<std::exception_ptr> err(k);
-  std::vector<std::thread> workers;
-  const int lane = LaneScope::current();
-  for (int i = 1; i < k; ++i)
-    workers.emplace_back([&, i] {
-      LaneScope::current() = lane;
-      in_parallel_section() = true;
-      try {
-        StreamScope scope(pool[i - 1]);
-        StreamScope::spare() = spare_of(i);
-        task(i);
-        StreamScope::spare() = nullptr;
-      } catch (...) {
-        StreamScope::spare() = nullptr;
-        err[i] = std::current_exception();
-      }
-      in_parallel_section() = false;
-    });
-  const hipStream_t own_spare = StreamScope::spare();
-  const bool own_flag = in_parallel_section();
-  in_parallel_section() = true;
-  try {
-    StreamScope::spare() = spare_of(0);
-    task(0);
-  } catch (...) {
-    err[0] = std::current_exception();
-  }
-  StreamScope::spare() = own_spare;
-  in_parallel_section() = own_flag;
-  for (auto& w : workers) w.join();
-  hipError_t e = hipSuccess;
-  for (int i = 1; i < k; ++i) {
-    if (e == hipSuccess) e = hipEventRecord(join[i - 1], pool[i - 1]);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s0, join[i - 1], 0);
-  }
-  bool failed = e != hipSuccess;
-  for (auto& x : err) failed |= static_cast<bool>(x);
-  if (failed) {
-    for (int i = 1; i < k; ++i) (void)hipStreamSynchronize(pool[i - 1]);
-    (void)hipStreamSynchronize(s0);
-  }
-  (void)hipEventDestroy(fork);
-  for (auto& j : join) (void)hipEventDestroy(j);
-  for (auto& x : err)
-    if (x) std::rethrow_exception(x);
-  PHX_CHECK(e);
-}
 
 // ======================================================================================
 // FHECKKSRNS
@@ -486,14 +548,7 @@ FHECKKSRNS::FHECKKSRNS(PhantomCKKSEncoder& encoder) : encoder_(encoder) {}
 
 // GetDepthByDegree (src/util.cu:44-71): the reference's Paterson-Stockmeyer depth of a degree-d
 // Chebyshev series, its affine map included
-static uint32_t reference_series_depth(int d) {
-  static const int bounds[] = {5, 6, 14, 28, 60, 120, 248, 496, 1008, 2032};
-  if (d < 5 || d > 2031) throw std::invalid_argument("Polynomial degree is supported from 5 to 2031 inclusive");
-  uint32_t depth = 3;
-  for (int b : bounds)
-    if (d >= b) ++depth;
-  return depth;
-}
+static uint32_t reference_series_depth(int d) { return ps::GetDepthByDegree(static_cast<size_t>(d)); }
 
 uint32_t FHECKKSRNS::GetBootstrapDepth(const std::vector<uint32_t>& levelBudget) {
   return levelBudget.at(0) + levelBudget.at(1) + reference_series_depth(kChebDegree) + R_UNIFORM;
@@ -934,39 +989,55 @@ PhantomCiphertext FHECKKSRNS::EvalSlotsToCoeffs(const PhantomCiphertext& ct, con
 
 PhantomCiphertext FHECKKSRNS::EvalChebyshevSeries(const PhantomCiphertext& ct, const PhantomContext& cc,
                                                   const std::vector<double>& coeffs) const {
-  ChebEvaluator ev{cc, mul_key_, sf_, leaf_tables_, {}, {}, {}};
-  PhantomCiphertext x = ct;
-  if (x.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, x, 1);
-  ev.T.emplace(1, std::move(x));
-  // the power ladder T_2 .. T_15 generation by generation (T_(2^(g-1)+1) .. T_(2^g) depend only
-  // on earlier generations), each generation's members alternating between two streams
-  const int top = std::min<int>(kLeafDegree, static_cast<int>(coeffs.size()) - 1);
-  for (int lo = 2, hi = 2; lo <= top; lo = hi + 1, hi = std::min(2 * hi, top)) {
-    std::vector<int> members;
-    for (int i = lo; i <= hi; ++i) members.push_back(i);
-    for (int i : members) ev.prepare(i);
-    const int k = std::min<int>(2, static_cast<int>(members.size()));
-    run_parallel(cc, k, [&](int t) {
-      for (size_t m = t; m < members.size(); m += k) ev.get(members[m]);
-    });
-    for (int i : members) const_cast<PhantomCiphertext&>(ev.get(i)).retag(cc.stream());
-  }
+  std::vector<PhantomCiphertext> in(1);
+  in[0] = ct;
+  return std::move(chebyshev_lanes(std::move(in), cc, coeffs).at(0));
+}
+
+std::vector<PhantomCiphertext> FHECKKSRNS::chebyshev_lanes(std::vector<PhantomCiphertext> in, const PhantomContext& cc,
+                                                           const std::vector<double>& coeffs) const {
+  ChebEvaluator ev{cc, mul_key_, sf_, leaf_tables_};
+  ev.B = in.size();
+  for (auto& x : in)
+    if (x.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, x, 1);
+  ev.T.emplace(1, std::move(in));
   return ev.eval(coeffs);
 }
 
 void FHECKKSRNS::ApplyDoubleAngleIterations(PhantomCiphertext& ct, const PhantomContext& cc, uint32_t numIter) const {
+  std::vector<PhantomCiphertext> v(1);
+  v[0] = std::move(ct);
+  double_angle_lanes(v, cc, numIter);
+  ct = std::move(v[0]);
+}
+
+void FHECKKSRNS::double_angle_lanes(std::vector<PhantomCiphertext>& v, const PhantomContext& cc,
+                                    uint32_t numIter) const {
   const int r = static_cast<int>(numIter);
   for (int j = 1; j <= r; ++j) {
-    // 2 ct^2 - (2 pi)^(-2^(j - r)): doubling and constant folded in before the key switch
-    if (ct.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, ct, 1);
-    ct = MulAddRescale(cc, ct, ct, mul_key_, 2, {}, -1.0 / std::pow(2.0 * M_PI, std::pow(2.0, j - r)));
+    // 2 ct^2 - (2 pi)^(-2^(j - r)): doubling and constant folded in before the key switch; the
+    // lanes' squarings share one batched key switch
+    const double c = -1.0 / std::pow(2.0 * M_PI, std::pow(2.0, j - r));
+    std::vector<MulAddJob> jobs;
+    for (auto& ct : v) {
+      if (ct.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(cc, ct, 1);
+      jobs.push_back(MulAddJob{&ct, &ct, 2, {}, c});
+    }
+    v = MulAddRescaleBatch(cc, jobs, mul_key_);
   }
 }
 
-PhantomCiphertext FHECKKSRNS::eval_mod(const PhantomCiphertext& ct, const PhantomContext& cc) const {
-  PhantomCiphertext r = EvalChebyshevSeries(ct, cc, cheb_);
-  ApplyDoubleAngleIterations(r, cc, R_UNIFORM);
+std::vector<PhantomCiphertext> FHECKKSRNS::eval_mod_lanes(std::vector<PhantomCiphertext> in,
+                                                          const PhantomContext& cc) const {
+  std::vector<PhantomCiphertext> r = chebyshev_lanes(std::move(in), cc, cheb_);
+  double_angle_lanes(r, cc, R_UNIFORM);
   return r;
+}
+
+PhantomCiphertext FHECKKSRNS::eval_mod(const PhantomCiphertext& ct, const PhantomContext& cc) const {
+  std::vector<PhantomCiphertext> in(1);
+  in[0] = ct;
+  return std::move(eval_mod_lanes(std::move(in), cc).at(0));
 }
 
 PhantomCiphertext FHECKKSRNS::RaiseWithCorrection(const PhantomCiphertext& in, const PhantomContext& cc) const {
@@ -1003,7 +1074,7 @@ std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<
                                                               uint32_t numSlots) const {
   const int k = std::max(1, std::min({lanes, PhantomContext::kLanes, static_cast<int>(in.size())}));
   std::vector<PhantomCiphertext> out(in.size());
-  if (k == 1 || in_parallel_section()) {
+  if (k == 1) {
     for (size_t i = 0; i < in.size(); ++i) out[i] = EvalBootstrap(in[i], cc, numSlots);
     return out;
   }
@@ -1098,29 +1169,15 @@ PhantomCiphertext FHECKKSRNS::bootstrap_once(const PhantomCiphertext& in, const 
     add_inplace(cc, enc, conj);
     MultByMonomialInPlace(cc, enc_i, 3 * M / 4);  // times -i
     trace(cc, "conj-split", enc_i);
-    // approximate modular reduction of both halves, concurrently: the imaginary half runs on the
-    // context's second stream from a second host thread (both are chains of small, dependent
-    // launches that leave most of the GPU idle on their own)
-    // enc_i (allocated on the main stream) stays alive until the main stream has joined
-    PhantomCiphertext im;
-    auto half = [&](int t) {
-      if (t == 0) {
-        enc = eval_mod(enc, cc);
-      } else {
-        im = eval_mod(enc_i, cc);
-        MultByMonomialInPlace(cc, im, M / 4);  // times i
-      }
-    };
-    // PHX_EVALMOD_SERIAL=1: the halves one after the other on the main stream (measurement aid)
-    static const bool serial = std::getenv("PHX_EVALMOD_SERIAL") != nullptr;
-    if (serial) {
-      half(0);
-      trace(cc, "evalmod-re", enc);
-      half(1);
-    } else {
-      run_parallel(cc, 2, half);
-    }
-    im.retag(cc.stream());
+    // approximate modular reduction of both halves in lockstep: every product of the real and
+    // the imaginary half shares one batched key switch (ChebEvaluator lanes, MulAddRescaleBatch)
+    std::vector<PhantomCiphertext> halves(2);
+    halves[0] = std::move(enc);
+    halves[1] = std::move(enc_i);
+    halves = eval_mod_lanes(std::move(halves), cc);
+    enc = std::move(halves[0]);
+    PhantomCiphertext im = std::move(halves[1]);
+    MultByMonomialInPlace(cc, im, M / 4);  // times i
     trace(cc, "evalmod", enc);
     EvalAddAutoInplace(cc, enc, im, sf_);
     // SlotToCoeff

@@ -170,6 +170,12 @@ class FHECKKSRNS {
   const Precom& precom(uint32_t numSlots, const PhantomContext& cc) const;
   PhantomCiphertext apply_level(const PhantomContext& cc, const PhantomCiphertext& ct, const LTLevel& lv) const;
   PhantomCiphertext eval_mod(const PhantomCiphertext& ct, const PhantomContext& cc) const;
+  // the series / double angle / EvalMod on several ciphertexts in lockstep (one level and scale):
+  // their products share batched key switches (the real and imaginary halves of EvalMod)
+  std::vector<PhantomCiphertext> eval_mod_lanes(std::vector<PhantomCiphertext> in, const PhantomContext& cc) const;
+  std::vector<PhantomCiphertext> chebyshev_lanes(std::vector<PhantomCiphertext> in, const PhantomContext& cc,
+                                                 const std::vector<double>& coeffs) const;
+  void double_angle_lanes(std::vector<PhantomCiphertext>& v, const PhantomContext& cc, uint32_t numIter) const;
   PhantomCiphertext bootstrap_once(const PhantomCiphertext& ct, const PhantomContext& cc, const Precom& pc) const;
 
   PhantomCKKSEncoder& encoder_;

@@ -274,6 +274,55 @@ const PhantomCiphertext& AtLevel(const PhantomContext& ctx, const PhantomCiphert
   return tmp;
 }
 
+std::vector<PhantomCiphertext> AtLevelBatch(const PhantomContext& ctx, const std::vector<const PhantomCiphertext*>& cts,
+                                            const std::vector<size_t>& targets, const std::vector<double>& sf) {
+  if (cts.size() != targets.size()) throw std::invalid_argument("AtLevelBatch: size mismatch");
+  std::vector<PhantomCiphertext> out(cts.size());
+  const size_t n = ctx.poly_degree();
+  hipStream_t s = ctx.stream();
+  // the ones adjusted() would handle (degree 1, two polynomials, below their target), grouped by
+  // target level; the rest one by one (AtLevel)
+  std::map<size_t, std::vector<size_t>> groups;
+  for (size_t k = 0; k < cts.size(); ++k) {
+    const PhantomCiphertext& c = *cts[k];
+    if (c.GetNoiseScaleDeg() <= 1 && level_of(c) == targets[k]) continue;  // as it is (empty result)
+    if (c.GetNoiseScaleDeg() <= 1 && c.size() == 2 && level_of(c) < targets[k]) {
+      groups[targets[k]].push_back(k);
+    } else {
+      PhantomCiphertext tmp;
+      const PhantomCiphertext& r = AtLevel(ctx, c, targets[k], sf, tmp);
+      out[k] = &r == &c ? PhantomCiphertext(c) : std::move(tmp);
+    }
+  }
+  for (auto& [target, ks] : groups) {
+    // adjusted(): round(k) times the leading limbs at chain `target` (one level above the target
+    // level), then one rescale; every ciphertext's scaled copy side by side, the rescale batched
+    const size_t mid = target, L = ctx.get_context_data(mid).coeff_modulus_size(), words = 2 * L * n;
+    const RnsTool& rt = ctx.get_context_data(mid).gpu_rns_tool();
+    const double qdrop = static_cast<double>(rt.base_Ql().back());
+    for (size_t c0 = 0; c0 < ks.size(); c0 += phx::kMaxKsProds) {
+      const size_t cnt = std::min<size_t>(phx::kMaxKsProds, ks.size() - c0);
+      DeviceBuffer<uint64_t> w(cnt * words, s);
+      std::vector<uint64_t*> outs(cnt);
+      for (size_t j = 0; j < cnt; ++j) {
+        const PhantomCiphertext& c = *cts[ks[c0 + j]];
+        const double k = sf.at(target) * qdrop / c.scale();
+        hip_ok(phx::mul_scalar_v(c.data(), limb_scalars(ctx, mid, k), w.get() + j * words, ctx.mod_QP().q, n, L, s, 2,
+                                 c.coeff_modulus_size() * n),
+               "scaled mod switch");
+        PhantomCiphertext& o = out[ks[c0 + j]];
+        o.resize(ctx, mid + 1, 2, s, false);
+        o.set_ntt_form(true);
+        o.set_scale(sf.at(target));
+        o.SetNoiseScaleDeg(1);
+        outs[j] = o.data();
+      }
+      rt.rescale_ntt_to(w.get(), outs.data(), cnt, ctx.gpu_rns_tables(), s);
+    }
+  }
+  return out;
+}
+
 void AdjustToLevel(const PhantomContext& ctx, PhantomCiphertext& ct, size_t target, const std::vector<double>& sf) {
   if (ct.GetNoiseScaleDeg() > 1) EvalModReduceInPlace(ctx, ct, 1);
   const size_t lvl = level_of(ct);
@@ -336,6 +385,124 @@ void relinearize_rescale_raw(const PhantomContext& ctx, size_t chain_index, cons
   traffic::keys(traffic::limb_bytes(beta * 2 * QlP, n));
   traffic::ciphertexts(traffic::limb_bytes(3 * Ql + 2 * (Ql - 1), n));  // d read, the rescaled result written
   rt.moddown_rescale(out, cx, ctx.gpu_rns_tables(), s, 2, fuse ? &ks : nullptr);
+}
+
+void relinearize_rescale_batch_raw(const PhantomContext& ctx, size_t chain_index, const uint64_t* d3, size_t d3_stride,
+                                   size_t count, uint64_t* const* out, const uint64_t* const* evk, hipStream_t s) {
+  if (chain_index < 1 || chain_index + 1 >= ctx.total_parm_size())
+    throw std::invalid_argument("end of modulus switching chain reached");
+  const RnsTool& rt = ctx.get_context_data(chain_index).gpu_rns_tool();
+  const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P(), beta = rt.beta();
+  if (count < 1 || count > static_cast<size_t>(phx::kMaxKsProds) || (count > 1 && d3_stride < 3 * Ql * n))
+    throw std::invalid_argument("relinearize_rescale_batch: bad batch");
+  const bool fuse = ks_epilogue_enabled() && beta <= (size_t)phx::kMaxKsBeta && n >= 1024 && Ql >= 2;
+  if (!fuse || count == 1) {
+    for (size_t k = 0; k < count; ++k) relinearize_rescale_raw(ctx, chain_index, d3 + k * d3_stride, out[k], evk, s);
+    return;
+  }
+  // every stage once over all `count` key switches: one batched modup (INTT, digit conversions,
+  // digit NTTs), one moddown-rescale over 2 count polynomials with the inner products formed in
+  // its INTT prologue and NTT epilogue (ntt.h NttEpilogue::ks_prods)
+  uint64_t* t_mod_up = rt.workspace().get(s, Workspace::kKsModup, count * beta * QlP * n);
+  rt.modup(t_mod_up, d3 + 2 * Ql * n, ctx.gpu_rns_tables(), s, count, d3_stride);
+  uint64_t* cx = rt.workspace().get(s, Workspace::kKsCx, 2 * count * QlP * n);
+  phx::NttEpilogue ks;
+  ks.ks_beta = (int)beta;
+  ks.tmu = t_mod_up;
+  ks.tmu_stride = QlP * n;
+  ks.evk = evk;
+  ks.evk_poly_stride = ctx.size_QP() * n;
+  ks.add_c = d3;
+  ks.add_stride = Ql * n;
+  ks.pmod = rt.bigP_mod_q();
+  ks.pmod_shoup = rt.bigP_mod_q_shoup();
+  ks.ks_prods = static_cast<int>(count);
+  ks.tmu_prod_stride = beta * QlP * n;
+  for (size_t k = 0; k < count; ++k) {
+    ks.out_p[k] = out[k];
+    ks.add_p[k] = d3 + k * d3_stride;
+  }
+  traffic::keys(traffic::limb_bytes(count * beta * 2 * QlP, n));
+  traffic::ciphertexts(traffic::limb_bytes(count * (3 * Ql + 2 * (Ql - 1)), n));
+  rt.moddown_rescale(out[0], cx, ctx.gpu_rns_tables(), s, 2 * count, &ks);
+}
+
+std::vector<PhantomCiphertext> MulAddRescaleBatch(const PhantomContext& ctx, const std::vector<MulAddJob>& jobs,
+                                                  const PhantomRelinKey& rlk) {
+  std::vector<PhantomCiphertext> res;
+  if (jobs.empty()) return res;
+  const size_t chain = jobs[0].a->chain_index();
+  for (const MulAddJob& j : jobs)
+    if (j.a->chain_index() != chain) throw std::invalid_argument("MulAddRescaleBatch: products at different levels");
+  const size_t n = ctx.poly_degree(), L = jobs[0].a->coeff_modulus_size();
+  if (L > static_cast<size_t>(phx::kMaxScalarLimbs)) {  // (the per-limb constants travel by value)
+    for (const MulAddJob& j : jobs) res.push_back(MulAddRescale(ctx, *j.a, *j.b, rlk, j.factor, j.terms, j.constant));
+    return res;
+  }
+  hipStream_t s = ctx.stream();
+  const uint64_t* q = ctx.mod_QP().q;
+  for (size_t b0 = 0; b0 < jobs.size(); b0 += phx::kMaxKsProds) {
+    const size_t cnt = std::min<size_t>(phx::kMaxKsProds, jobs.size() - b0);
+    // the products' tensors side by side in one buffer (the batched modup reads their c2 with one
+    // stride); the buffer is freed on this stream after the key switch has read it
+    DeviceBuffer<uint64_t> d(cnt * 3 * L * n, s);
+    std::vector<double> scales(cnt);
+    for (size_t k = 0; k < cnt; ++k) {
+      const MulAddJob& j = jobs[b0 + k];
+      if (j.a->chain_index() != j.b->chain_index() || j.a->GetNoiseScaleDeg() > 1 || j.b->GetNoiseScaleDeg() > 1)
+        throw std::invalid_argument("MulAddRescale: operands must be level-aligned and of degree 1");
+      for (const ScaledTerm& t : j.terms)
+        if (t.ct->chain_index() > chain || t.ct->GetNoiseScaleDeg() > 1 || t.ct->size() != 2)
+          throw std::invalid_argument("MulAddRescale: a term is below the product's level");
+      uint64_t* dk = d.get() + k * 3 * L * n;
+      const double S = j.a->scale() * j.b->scale();
+      scales[k] = S;
+      phx::TensorLinArgs ta;
+      ta.ct1 = j.a->data();
+      ta.ct2 = j.b->data();
+      ta.out = dk;
+      ta.q = q;
+      ta.barrett = ctx.mod_QP().barrett;
+      ta.scale = j.factor != 1;
+      if (ta.scale) ta.f = limb_scalars(ctx, chain, static_cast<double>(j.factor));
+      if (!j.terms.empty()) {
+        ta.t = j.terms[0].ct->data();
+        ta.t_stride = j.terms[0].ct->coeff_modulus_size() * n;
+        ta.c = limb_scalars(ctx, chain, j.terms[0].coeff * S / j.terms[0].ct->scale());
+      }
+      hip_ok(phx::tensor_lin(ta, n, L, s), "tensor + linear epilogue");
+      traffic::ciphertexts(traffic::limb_bytes(4 * L + 2 * L * j.terms.size(), n));
+      for (size_t i = 1; i < j.terms.size(); ++i) {
+        const ScaledTerm& t = j.terms[i];
+        const phx::LimbScalars cb = limb_scalars(ctx, chain, t.coeff * S / t.ct->scale());
+        hip_ok(phx::lin_comb_v(dk, 2, nullptr, t.ct->data(), 2, t.ct->coeff_modulus_size() * n, cb, q, n, L, s),
+               "mul-add term");
+      }
+      if (j.constant != 0.0) {
+        const auto& mods = ctx.get_context_data(chain).moduli();
+        phx::LimbScalars v;
+        for (size_t l = 0; l < L; ++l) v.v[l] = residue_of_double(j.constant * S, mods[l]);
+        hip_ok(phx::add_scalar_v(dk, v, dk, q, n, L, s), "add const");
+      }
+    }
+    std::vector<uint64_t*> outs(cnt);
+    for (size_t k = 0; k < cnt; ++k) {
+      PhantomCiphertext o;
+      o.resize(ctx, chain + 1, 2, s, false);
+      outs[k] = o.data();
+      res.push_back(std::move(o));
+    }
+    relinearize_rescale_batch_raw(ctx, chain, d.get(), 3 * L * n, cnt, outs.data(), rlk.public_keys_ptr(), s);
+    const double qlast = static_cast<double>(ctx.get_context_data(chain).gpu_rns_tool().base_Ql().back());
+    for (size_t k = 0; k < cnt; ++k) {
+      PhantomCiphertext& o = res[b0 + k];
+      o.set_ntt_form(true);
+      o.set_scale(scales[k] / qlast);
+      o.set_correction_factor(jobs[b0 + k].a->correction_factor());
+      o.SetNoiseScaleDeg(1);
+    }
+  }
+  return res;
 }
 
 PhantomCiphertext RelinearizeRescale(const PhantomContext& ctx, const PhantomCiphertext& d, const PhantomRelinKey& rlk) {

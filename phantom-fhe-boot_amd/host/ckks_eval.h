@@ -71,6 +71,11 @@ void AccumulateScaled(const PhantomContext& ctx, PhantomCiphertext& acc, const P
 // already is, else a new ciphertext stored in `tmp` (no copy when nothing is to be done)
 const PhantomCiphertext& AtLevel(const PhantomContext& ctx, const PhantomCiphertext& ct, size_t target,
                                  const std::vector<double>& sf, PhantomCiphertext& tmp);
+// AtLevel for many ciphertexts at once (their targets may differ): result k is empty when cts[k]
+// already is at targets[k] (use it as it is), else a new ciphertext; those of one target level
+// share one batched rescale.  Bit-identical to AtLevel.
+std::vector<PhantomCiphertext> AtLevelBatch(const PhantomContext& ctx, const std::vector<const PhantomCiphertext*>& cts,
+                                            const std::vector<size_t>& targets, const std::vector<double>& sf);
 // EvalAddAutoInplace / EvalSubAuto: level- and scale-aligned add / subtract
 void EvalAddAutoInplace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b,
                         const std::vector<double>& sf);
@@ -96,6 +101,23 @@ struct ScaledTerm {
 PhantomCiphertext MulAddRescale(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
                                 const PhantomRelinKey& rlk, int factor, const std::vector<ScaledTerm>& terms,
                                 double constant);
+// `count` MulAddRescale products at one level in shared launches: every stage of the key switch
+// (modup INTT, digit conversions and NTTs, the moddown-rescale with its fused inner products) runs
+// once over all of them.  Bit-identical to calling MulAddRescale on each job.
+struct MulAddJob {
+  const PhantomCiphertext* a;
+  const PhantomCiphertext* b;
+  int factor = 1;
+  std::vector<ScaledTerm> terms;
+  double constant = 0.0;
+};
+std::vector<PhantomCiphertext> MulAddRescaleBatch(const PhantomContext& ctx, const std::vector<MulAddJob>& jobs,
+                                                  const PhantomRelinKey& rlk);
+// relinearize + rescale of `count` products d3 + k d3_stride ([3][Ql][n] each) into out[k]
+// ([2][Ql - 1][n]); count <= phx::kMaxKsProds
+void relinearize_rescale_batch_raw(const PhantomContext& ctx, size_t chain_index, const uint64_t* d3,
+                                   size_t d3_stride, size_t count, uint64_t* const* out, const uint64_t* const* evk,
+                                   hipStream_t s);
 // level-aligned multiply + relinearize + rescale (EvalMultAuto + ModReduce)
 PhantomCiphertext EvalMultRescale(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b,
                                   const PhantomRelinKey& rlk, const std::vector<double>& sf);
@@ -227,9 +249,10 @@ std::vector<double> EvalChebyshevCoefficients(const std::function<double(double)
                                               uint32_t degree);
 // EvalChebyshevSeries (src/evaluate.cu:3176-3186): sum c_k T_k((2x - a - b) / (b - a)) with c_0
 // halved.  Degree < 5: the reference's linear method (EvalChebyshevSeriesLinear, :3188-3262);
-// otherwise this engine's fused p = q T_m + r recursion (the bootstrap's EvalMod evaluator,
-// host/bootstrap.cpp) after the affine map.  Depth: 1 (affine map, skipped on [-1, 1]) + the
-// recursion's depth; e.g. degree 88 consumes 8 levels, as the reference's Paterson-Stockmeyer.
+// otherwise the reference's Paterson-Stockmeyer split (EvalChebyshevSeriesPS, :3264-3535, and
+// InnerEvalChebyshevPS, :2998-3174; host/chebyshev_ps.cpp), the same operation sequence through
+// the FLEXIBLEAUTO helpers above, so the result's level, degree and scale are the reference's.
+// (The bootstrap's EvalMod uses its own fused evaluator, host/bootstrap.cpp.)
 PhantomCiphertext EvalChebyshevSeries(const PhantomContext& ctx, const PhantomRelinKey& rlk, const PhantomCiphertext& x,
                                       const std::vector<double>& coeffs, double a, double b,
                                       const std::vector<double>& sf, const std::vector<double>& sfBig);
@@ -239,6 +262,24 @@ PhantomCiphertext EvalChebyshevSeriesLinear(const PhantomContext& ctx, const Pha
 PhantomCiphertext EvalChebyshevSeriesPS(const PhantomContext& ctx, const PhantomRelinKey& rlk, const PhantomCiphertext& x,
                                         const std::vector<double>& coeffs, double a, double b,
                                         const std::vector<double>& sf, const std::vector<double>& sfBig);
+// the reference's [-1, 1] test of the series interval (src/evaluate.cu:3208): signed differences
+bool ChebyshevUnitInterval(double a, double b);
+// EvalLinearWSumMutable (include/evaluate.cuh:371, src/evaluate.cu:3537-3583): sum w_i ct_i after
+// bringing every ct_i to the deepest one's level and degree (the operands are adjusted in place)
+PhantomCiphertext EvalLinearWSumMutable(const PhantomContext& ctx, std::vector<PhantomCiphertext*>& cts,
+                                        const std::vector<double>& w, const std::vector<double>& sf,
+                                        const std::vector<double>& sfBig);
+// the Paterson-Stockmeyer host helpers of src/util.cu:15-312
+namespace ps {
+struct Division {
+  std::vector<double> q, r;
+};
+uint32_t Degree(const std::vector<double>& c);  // last non-zero index (0 when all are zero)
+uint32_t GetDepthByDegree(size_t degree);        // degrees 5 .. 2031
+uint32_t GetMultiplicativeDepthByCoeffVector(const std::vector<double>& vec, bool isNormalized);
+std::vector<uint32_t> ComputeDegreesPS(uint32_t n);  // {k, m}
+Division LongDivisionChebyshev(const std::vector<double>& f, const std::vector<double>& g);
+}  // namespace ps
 // EvalChebyshevFunction (include/evaluate.cuh:381-388)
 inline PhantomCiphertext EvalChebyshevFunction(const std::function<double(double)>& func, const PhantomContext& ctx,
                                                const PhantomRelinKey& rlk, const PhantomCiphertext& ct, double a,

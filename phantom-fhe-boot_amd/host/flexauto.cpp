@@ -235,24 +235,17 @@ std::vector<double> EvalChebyshevCoefficients(const std::function<double(double)
   return c;
 }
 
-// degree of a coefficient vector: its last non-zero index
-static size_t series_degree(const std::vector<double>& c) {
-  size_t d = c.size() ? c.size() - 1 : 0;
-  while (d > 0 && c[d] == 0.0) --d;
-  return d;
-}
-
 // EvalChebyshevSeriesLinear (src/evaluate.cu:3188-3262): T_1..T_k by the doubling / product
 // recurrences, then sum c_i T_i + c_0 / 2, all through the FLEXIBLEAUTO helpers above
 PhantomCiphertext EvalChebyshevSeriesLinear(const PhantomContext& ctx, const PhantomRelinKey& rlk,
                                             const PhantomCiphertext& x, const std::vector<double>& coeffs, double a,
                                             double b, const std::vector<double>& sf, const std::vector<double>& sfBig) {
+  // k = coefficients.size() - 1 as the reference takes it: trailing zero coefficients still
+  // build their T_i (and cost their levels)
   const size_t k = coeffs.size() - 1;
   if (k < 1) throw std::invalid_argument("a Chebyshev series needs degree 1 or more");
   std::vector<PhantomCiphertext> T(k);
-  const bool unit = std::fabs(a - std::round(a)) < 1e-10 && std::fabs(b - std::round(b)) < 1e-10 &&
-                    std::round(a) == -1 && std::round(b) == 1;
-  if (unit) {
+  if (ChebyshevUnitInterval(a, b)) {
     T[0] = x;
   } else {  // y = (2 x - a - b) / (b - a)
     T[0] = EvalMultConst(ctx, x, 2.0 / (b - a), sf);
@@ -288,11 +281,8 @@ PhantomCiphertext EvalChebyshevSeriesLinear(const PhantomContext& ctx, const Pha
 PhantomCiphertext EvalChebyshevSeries(const PhantomContext& ctx, const PhantomRelinKey& rlk, const PhantomCiphertext& x,
                                       const std::vector<double>& coeffs, double a, double b,
                                       const std::vector<double>& sf, const std::vector<double>& sfBig) {
-  if (series_degree(coeffs) < 5) {
-    std::vector<double> c(coeffs.begin(), coeffs.begin() + static_cast<long>(series_degree(coeffs)) + 1);
-    if (c.size() < 2) c.push_back(0.0);
-    return EvalChebyshevSeriesLinear(ctx, rlk, x, c, a, b, sf, sfBig);
-  }
+  // src/evaluate.cu:3176-3186: the degree picks the method, the vector goes in as given
+  if (ps::Degree(coeffs) < 5) return EvalChebyshevSeriesLinear(ctx, rlk, x, coeffs, a, b, sf, sfBig);
   return EvalChebyshevSeriesPS(ctx, rlk, x, coeffs, a, b, sf, sfBig);
 }
 

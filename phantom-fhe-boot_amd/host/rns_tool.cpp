@@ -219,63 +219,77 @@ void RnsTool::digit_bconv(const uint64_t* t_cks, uint64_t* t_mod_up, hipStream_t
   }
 }
 
-void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables& ntt, hipStream_t s) const {
+void RnsTool::modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables& ntt, hipStream_t s, size_t count,
+                    size_t c2_stride) const {
   const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_, alpha = size_P_;
-  uint64_t* t_cks = ws_->get(s, Workspace::kModupInv, size_Ql * n_);
+  const size_t beta = converters_.size(), dig = beta * size_QlP * n_;  // one key switch's digits
+  if (count < 1 || (count > 1 && c2_stride < size_Ql * n_)) throw std::invalid_argument("modup: bad batch");
+  const int nc = static_cast<int>(count);
+  uint64_t* t_cks = ws_->get(s, Workspace::kModupInv, count * size_Ql * n_);
   // INTT(c2) * partQlHatInv (nwt_2d_radix8_backward_scale)
   // and the digits' own limbs (modup_copy_partQl_kernel) stored by the INTT's first pass, which
-  // reads c2 anyway
+  // reads c2 anyway; `count` key switches' c2 in one launch
+  const phx::LimbMap im = phx::LimbMap::contiguous((int)size_Ql, 0).batched(nc, c2_stride, size_Ql * n_);
   if (n_ >= 1024) {
     phx::NttCopy cp;
     cp.out = t_mod_up;
     cp.digit_stride = size_QlP * n_;
     cp.alpha = (int)alpha;
-    hip_ok(phx::ntt_inverse_copy(ntt, c2, t_cks, phx::LimbMap::contiguous((int)size_Ql, 0), d_partQlHatInv_.get(),
-                                 d_partQlHatInv_shoup_.get(), cp, s),
+    cp.poly_stride = dig;
+    hip_ok(phx::ntt_inverse_copy(ntt, c2, t_cks, im, d_partQlHatInv_.get(), d_partQlHatInv_shoup_.get(), cp, s),
            "modup INTT + copy");
   } else {
-    hip_ok(phx::ntt_inverse(ntt, c2, t_cks, phx::LimbMap::contiguous((int)size_Ql, 0), d_partQlHatInv_.get(),
-                            d_partQlHatInv_shoup_.get(), s),
-           "modup INTT");
-    hip_ok(phx::modup_copy_digits(c2, t_mod_up, n_, size_Ql, size_QlP, alpha, s), "modup copy");
+    hip_ok(phx::ntt_inverse(ntt, c2, t_cks, im, d_partQlHatInv_.get(), d_partQlHatInv_shoup_.get(), s), "modup INTT");
+    for (size_t k = 0; k < count; ++k)
+      hip_ok(phx::modup_copy_digits(c2 + k * c2_stride, t_mod_up + k * dig, n_, size_Ql, size_QlP, alpha, s),
+             "modup copy");
   }
   // per digit: the complement limbs = NTT(bconv(digit)), every limb but the digit's own
-  // (include_special_mod_exclude_range); the full digits in one launch (digit b skips
-  // [b alpha, (b + 1) alpha)), a short last digit apart.  At n >= 2^10 the conversion is the
-  // column pass's prologue (ntt.h BconvPrologue): its output never goes to HBM.
-  const size_t beta = converters_.size();
+  // (include_special_mod_exclude_range); the full digits of every key switch in one launch
+  // (digit b skips [b alpha, (b + 1) alpha)), a short last digit apart.  PHX_FUSED_BCONV=1: the
+  // conversion is the column pass's prologue (ntt.h BconvPrologue), one key switch per launch.
   const size_t full = digit_size_.back() == alpha ? beta : beta - 1;
   const bool fused = fused_bconv_ok(alpha);
-  if (!fused) digit_bconv(t_cks, t_mod_up, s);
-  auto run = [&](size_t b0, size_t cnt) {
-    const size_t part = digit_size_[b0];
+  if (!fused) digit_bconv(t_cks, t_mod_up, s, count);
+  auto digit_map = [&](size_t b0) {
     phx::LimbMap m;
     m.num_limbs = (int)size_QlP;
     m.split = (int)size_Ql;
     m.first_a = 0;
     m.first_b = (int)size_Q_;
     m.skip_begin = (int)digit_start_[b0];
-    m.skip_end = (int)(digit_start_[b0] + part);
+    m.skip_end = (int)(digit_start_[b0] + digit_size_[b0]);
     m.skip_step = (int)alpha;
-    uint64_t* dst = t_mod_up + b0 * size_QlP * n_;
-    if (fused) {
-      phx::BconvPrologue bcv;
-      bcv.in = t_cks + digit_start_[b0] * n_;
-      bcv.in_stride = alpha * n_;
-      bcv.ob = (int)(size_QlP - part);
-      for (size_t i = 0; i < cnt; ++i) {
-        bcv.mat[i] = converters_[b0 + i].d_qhat_mod_p.get();
-        bcv.ib[i] = (int)digit_size_[b0 + i];
-      }
-      hip_ok(phx::ntt_forward_bconv(ntt, dst, m.batched((int)cnt), bcv, phx::NttEpilogue{}, s), "modup bconv + NTT");
-    } else {
-      hip_ok(phx::ntt_forward(ntt, dst, dst, m.batched((int)cnt), s), "modup NTT");
-    }
+    return m;
   };
-  // one launch per group of full digits (at most kMaxBconvPolys prologue tables per launch)
-  const size_t group = fused ? (size_t)phx::kMaxBconvPolys : full;
-  for (size_t b0 = 0; b0 < full; b0 += group) run(b0, std::min(group, full - b0));
-  if (full < beta) run(full, 1);
+  if (fused) {
+    for (size_t k = 0; k < count; ++k) {
+      auto run = [&](size_t b0, size_t cnt) {
+        phx::BconvPrologue bcv;
+        bcv.in = t_cks + k * size_Ql * n_ + digit_start_[b0] * n_;
+        bcv.in_stride = alpha * n_;
+        bcv.ob = (int)(size_QlP - digit_size_[b0]);
+        for (size_t i = 0; i < cnt; ++i) {
+          bcv.mat[i] = converters_[b0 + i].d_qhat_mod_p.get();
+          bcv.ib[i] = (int)digit_size_[b0 + i];
+        }
+        uint64_t* dst = t_mod_up + k * dig + b0 * size_QlP * n_;
+        hip_ok(phx::ntt_forward_bconv(ntt, dst, digit_map(b0).batched((int)cnt), bcv, phx::NttEpilogue{}, s),
+               "modup bconv + NTT");
+      };
+      for (size_t b0 = 0; b0 < full; b0 += phx::kMaxBconvPolys) run(b0, std::min<size_t>(phx::kMaxBconvPolys, full - b0));
+      if (full < beta) run(full, 1);
+    }
+    return;
+  }
+  if (full > 0)
+    hip_ok(phx::ntt_forward(ntt, t_mod_up, t_mod_up,
+                            digit_map(0).grouped(nc * (int)full, (int)full, size_QlP * n_, dig), s),
+           "modup NTT");
+  if (full < beta) {
+    uint64_t* dst = t_mod_up + full * size_QlP * n_;
+    hip_ok(phx::ntt_forward(ntt, dst, dst, digit_map(full).grouped(nc, 1, 0, dig), s), "modup NTT (short digit)");
+  }
 }
 
 void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx::NttTables& ntt, hipStream_t s,
@@ -418,6 +432,12 @@ void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables&
     epi.add_stride = ks->add_stride;
     epi.pmod = ks->pmod;
     epi.pmod_shoup = ks->pmod_shoup;
+    epi.ks_prods = ks->ks_prods;
+    epi.tmu_prod_stride = ks->tmu_prod_stride;
+    for (int k = 0; k < phx::kMaxKsProds; ++k) {
+      epi.out_p[k] = ks->out_p[k];
+      epi.add_p[k] = ks->add_p[k];
+    }
   }
   const phx::LimbMap om = phx::LimbMap::contiguous((int)Ln, 0).batched(np);
   if (fused) {
@@ -438,6 +458,32 @@ void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables&
   ba.out_stride = Ln * n_;
   hip_ok(phx::bconv(ba, n_, s), "moddown-rescale bconv");
   hip_ok(phx::ntt_forward_fused(ntt, delta, delta, om, nullptr, 0, epi, s), "moddown-rescale NTT + finish");
+}
+
+void RnsTool::rescale_ntt_to(const uint64_t* in, uint64_t* const* outs, size_t cts, const phx::NttTables& ntt,
+                             hipStream_t s) const {
+  const size_t L = base_Ql_.size();
+  if (L < 2) throw std::invalid_argument("end of modulus switching chain reached");
+  if (cts < 1 || cts > static_cast<size_t>(phx::kMaxKsProds)) throw std::invalid_argument("rescale: bad batch");
+  const size_t Ln = L - 1, polys = 2 * cts;
+  const int np = static_cast<int>(polys);
+  uint64_t* last = ws_->get(s, Workspace::kRescaleLast, polys * n_);
+  hip_ok(phx::ntt_inverse(ntt, in + Ln * n_, last, phx::LimbMap::contiguous(1, (int)Ln).batched(np, L * n_, n_),
+                          nullptr, nullptr, s),
+         "rescale INTT(last)");
+  // the two passes' intermediate in scratch; the finish writes each ciphertext's own buffer
+  uint64_t* mid = ws_->get(s, Workspace::kModdownDelta, polys * Ln * n_);
+  phx::NttEpilogue epi;
+  epi.c = in;
+  epi.c_stride = L * n_;
+  epi.out = outs[0];
+  epi.out_stride = Ln * n_;
+  epi.w = d_inv_qlast_.get();
+  epi.ws = d_inv_qlast_shoup_.get();
+  epi.ks_prods = static_cast<int>(cts);
+  for (size_t k = 0; k < cts; ++k) epi.out_p[k] = outs[k];
+  hip_ok(phx::ntt_forward_fused(ntt, nullptr, mid, phx::LimbMap::contiguous((int)Ln, 0).batched(np), last, n_, epi, s),
+         "rescale NTT + finish");
 }
 
 void RnsTool::rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const phx::NttTables& ntt,

@@ -42,8 +42,11 @@ class RnsTool {
   size_t beta() const { return converters_.size(); }
   const std::vector<uint64_t>& base_Ql() const { return base_Ql_; }
 
-  // modup (src/rns_bconv.cu:530-628): c2 [size_Ql][n] NTT form -> t_mod_up [beta][size_QlP][n]
-  void modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables& ntt, hipStream_t s) const;
+  // modup (src/rns_bconv.cu:530-628): c2 [size_Ql][n] NTT form -> t_mod_up [beta][size_QlP][n];
+  // `count` independent ones per launch: c2 of job k at c2 + k c2_stride, its digits at
+  // t_mod_up + k beta size_QlP n
+  void modup(uint64_t* t_mod_up, const uint64_t* c2, const phx::NttTables& ntt, hipStream_t s, size_t count = 1,
+             size_t c2_stride = 0) const;
   // moddown_from_NTT (src/rns_bconv.cu:791-843) fused with add_to_ct_kernel, for `polys`
   // polynomials at once: cx is [polys][size_QlP][n] NTT form (its P limbs are clobbered);
   // ct [polys][size_Ql][n] (+)= moddown(cx).  With tmu/evk (a key switch's t_mod_up and key
@@ -75,6 +78,10 @@ class RnsTool {
   // [polys][size_Ql-1][n], NTT form.  `in` is not modified.
   void rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const phx::NttTables& ntt,
                    hipStream_t s) const;
+  // the same for `cts` two-polynomial ciphertexts (in contiguous [cts][2][size_Ql][n]) whose
+  // results go to their own buffers outs[k] ([2][size_Ql-1][n]); cts <= phx::kMaxKsProds
+  void rescale_ntt_to(const uint64_t* in, uint64_t* const* outs, size_t cts, const phx::NttTables& ntt,
+                      hipStream_t s) const;
 
   // scratch space shared by the drivers (owned by the PhantomContext)
   void set_workspace(Workspace* ws) { ws_ = ws; }

@@ -41,6 +41,7 @@ _SIGS = {
     "phantom_square": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_relinearize": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, vp]),
     "phantom_relinearize_rescale": (ctypes.c_int, [vp, sz, vp, vp, ctypes.POINTER(vp), sz, vp]),
+    "phantom_relinearize_rescale_batch": (ctypes.c_int, [vp, sz, vp, sz, sz, vp, sz, ctypes.POINTER(vp), sz, vp]),
     "phantom_keyswitch": (ctypes.c_int, [vp, sz, vp, vp, ctypes.POINTER(vp), sz, vp]),
     "phantom_modup": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_keyswitch_inner_prod": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, vp, vp]),

@@ -283,3 +283,22 @@ def test_ntt_tables_match_oracle(c4, idx):
     assert O.lib().or_mulmod(int(got[2][1]), want_ninv, q) == int(want[2][1])
     assert int(ninv[0]) == want_ninv
     t.close()
+
+
+@pytest.mark.parametrize("chain,count", [(4, 2), (12, 4), (20, 2)])
+def test_relinearize_rescale_batch_c4(c4, rng, chain, count):
+    """EvalMod's batched products at C4 chains (the real and imaginary halves, a ladder
+    generation): phantom_relinearize_rescale_batch bit-exact vs the oracle composition per product
+    (tests/ks_oracle.py; src/evaluate.cu:1552-1647, src/rns_bconv.cu:530-843)."""
+    import ks_oracle as KO
+    L = len(c4.ql(chain))
+    cts = [_rand(rng, c4.ql(chain), 3) for _ in range(count)]
+    keys, dkeys = _keys(rng, c4)
+    d = to_dev(np.concatenate(cts))
+    s_out = 2 * (L - 1) * N
+    dout = to_dev(np.zeros(count * s_out, dtype=np.uint64))
+    PA.check(_lib().phantom_relinearize_rescale_batch(c4.handle, chain, ptr(d), 3 * L * N, count, ptr(dout), s_out,
+                                                      _vp(dkeys), len(dkeys), stream()))
+    got = to_host(dout)
+    for k in range(count):
+        assert np.array_equal(got[k * s_out:(k + 1) * s_out], KO.relinearize_rescale(c4, chain, cts[k], keys)), k

@@ -62,7 +62,8 @@ def test_deferred_setup_reference_arguments():
 def test_flexibleauto_surface():
     """EvalMultAuto / EvalSquare / EvalAddAuto / EvalSubAuto / EvalAddConst / EvalMultConst (lazy) /
     EvalMultAutoInplace with a plaintext / EvalChebyshevFunction (degree 4: the reference's linear
-    method; degree 30: the fused recursion), each decrypted against the plaintext computation."""
+    method; degree 30: the reference's Paterson-Stockmeyer), each decrypted against the plaintext
+    computation."""
     rc, lines, err = _run("flex", "16")
     checks = {l["check"]: l for l in lines if "check" in l}
     assert rc == 0, (lines, err)
@@ -71,7 +72,7 @@ def test_flexibleauto_surface():
                  "flex_mult_plain_auto", "flex_chebyshev_linear", "flex_chebyshev_ps"]:
         assert checks[name]["ok"], checks[name]
     used = {l["chebyshev_degree"]: l["levels_used"] for l in lines if "chebyshev_degree" in l}
-    assert used[30] <= 7, used  # GetDepthByDegree(30) = 7 (src/util.cu:44-58)
+    assert used[30] == 7, used  # GetDepthByDegree(30) = 7 on [1, 5] (src/util.cu:44-58)
 
 
 def test_bootstrapping_example_verbatim():

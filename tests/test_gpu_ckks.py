@@ -11,6 +11,7 @@ import ctypes
 import numpy as np
 import pytest
 
+import ks_oracle as KO
 import oracle_lib as O
 import phantom_amd as PA
 from gpu_util import ptr, stream, to_dev, to_host
@@ -231,29 +232,32 @@ def test_relinearize_rescale(request, rng, fixture, chain):
     dout = to_dev(np.zeros(2 * (L - 1) * n, dtype=np.uint64))
     kp = PA.ptr_array([ptr(k) for k in dkeys])
     PA.check(_lib().phantom_relinearize_rescale(ctx.handle, chain, ptr(d), ptr(dout), kp, len(dkeys), stream()))
-    beta = -(-L // ctx.size_P)
-    qlp = list(ql) + list(p)
-    tmu = np.zeros(beta * len(qlp) * n, dtype=np.uint64)
-    O.lib().or_modup(O.P(ct[2 * L * n:].copy()), O.P(tmu), n, O.P(O.arr(ql)), L, O.P(O.arr(p)), len(p))
-    cx = np.zeros(2 * len(qlp) * n, dtype=np.uint64)
-    O.lib().or_keyswitch_inner_prod(O.P(tmu), _oracle_keys(keys), O.P(cx), n, L, ctx.size_Q, ctx.size_P, beta,
-                                    O.P(O.arr(ctx.moduli)))
-    P = 1
-    for v in p:
-        P *= int(v)
-    pmod = O.arr([P % int(q) for q in ql])
-    want = []
-    for t in range(2):
-        c = cx[t * len(qlp) * n:(t + 1) * len(qlp) * n].copy()
-        scaled = np.zeros(L * n, dtype=np.uint64)
-        O.lib().or_poly_mul_scalar(O.P(ct[t * L * n:(t + 1) * L * n].copy()), O.P(pmod), O.P(scaled), n, L,
-                                   O.P(O.arr(ql)))
-        O.lib().or_poly_add(O.P(c[:L * n].copy()), O.P(scaled), O.P(c[:L * n]), n, L, O.P(O.arr(ql)))
-        w = np.zeros((L - 1) * n, dtype=np.uint64)
-        O.lib().or_moddown_from_ntt(O.P(c), O.P(w), n, O.P(O.arr(ql[:-1])), L - 1, O.P(O.arr([ql[-1]] + list(p))),
-                                    len(p) + 1)
-        want.append(w)
-    assert np.array_equal(to_host(dout), np.concatenate(want))
+    assert np.array_equal(to_host(dout), KO.relinearize_rescale(ctx, chain, ct, keys))
+
+
+@pytest.mark.parametrize("fixture,chain,count", [("c3", 1, 2), ("c3", 30, 3), ("small", 1, 5), ("small", 5, 1)])
+def test_relinearize_rescale_batch(request, rng, fixture, chain, count):
+    """`count` relinearize + rescale products in shared launches (include/phantom_amd.h
+    phantom_relinearize_rescale_batch: batched modup with grouped digit NTTs, one moddown-rescale
+    over 2 count polynomials with per-product outputs and addends): every product bit-exact vs the
+    oracle composition, with padded strides between the products."""
+    ctx = request.getfixturevalue(fixture)
+    L, n = len(ctx.ql(chain)), ctx.n
+    cts = [_rand_ct(rng, ctx, chain, 3) for _ in range(count)]
+    keys, dkeys = _keys(rng, ctx)
+    s_in, s_out = 3 * L * n + 5 * n, 2 * (L - 1) * n + 3 * n
+    buf = np.zeros(count * s_in, dtype=np.uint64)
+    for k, ct in enumerate(cts):
+        buf[k * s_in:k * s_in + 3 * L * n] = ct
+    d = to_dev(buf)
+    dout = to_dev(np.full(count * s_out, 9, dtype=np.uint64))
+    kp = PA.ptr_array([ptr(k) for k in dkeys])
+    PA.check(_lib().phantom_relinearize_rescale_batch(ctx.handle, chain, ptr(d), s_in, count, ptr(dout), s_out, kp,
+                                                      len(dkeys), stream()))
+    got = to_host(dout)
+    for k, ct in enumerate(cts):
+        assert np.array_equal(got[k * s_out:k * s_out + 2 * (L - 1) * n], KO.relinearize_rescale(ctx, chain, ct, keys)), k
+        assert np.all(got[k * s_out + 2 * (L - 1) * n:(k + 1) * s_out] == 9), k  # padding untouched
 
 
 @pytest.mark.parametrize("fixture,chain", [("c3", 1), ("c3", 44), ("small", 1), ("small", 6)])
