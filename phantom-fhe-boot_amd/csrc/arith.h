@@ -120,11 +120,6 @@ __device__ __forceinline__ uint64_t mulhi_approx(uint64_t a, uint64_t s) {
   return static_cast<uint64_t>(a1) * s1 + h;
 }
 
-#ifndef PHX_INT_NOCARRY
-#define PHX_INT_NOCARRY 1
-#endif
-
-#if PHX_INT_NOCARRY
 // Carry-free forms.  A 64-bit subtraction compiles to v_sub_co / v_subb_co with the borrow in
 // VCC, and gfx950 needs wait states (s_nop) between the VCC write and the VCC read; a csub adds
 // a 64-bit compare and two v_cndmask behind another VCC hazard.  Here every constant subtraction
@@ -140,23 +135,17 @@ __device__ __forceinline__ uint64_t opaque(uint64_t v) {
   asm("" : "+v"(v));
   return v;
 }
-#ifndef PHX_CSUB_BFI
-#define PHX_CSUB_BFI 1
-#endif
 // x - m if that is >= 0 else x, for x, m < 2^63, given nm = -m mod 2^64.  t = x - m, s = its sign
 // as a 32-bit mask, then the select (s & x) | (~s & t) as one v_bfi_b32 per half: 4 instructions
 // (the masked add-back form, t + (m & s), takes 5).
 __device__ __forceinline__ uint64_t csub_n(uint64_t x, uint64_t m, uint64_t nm) {
   const uint64_t t = add64(x, nm);
   const uint32_t s = static_cast<uint32_t>(static_cast<int32_t>(hi32(t)) >> 31);
-#if PHX_CSUB_BFI
+  (void)m;
   uint32_t lo, hi;
   asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(lo) : "v"(s), "v"(lo32(x)), "v"(lo32(t)));
   asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(hi) : "v"(s), "v"(hi32(x)), "v"(hi32(t)));
   return (static_cast<uint64_t>(hi) << 32) | lo;
-#else
-  return add64(t, (static_cast<uint64_t>(hi32(m) & s) << 32) | (lo32(m) & s));
-#endif
 }
 // a w mod q in [0, 4q) (as mul_shoup_lazy4 below), given nq = -q mod 2^64: a w + Q' (-q)
 __device__ __forceinline__ uint64_t mul_shoup_lazy4(uint64_t a, uint64_t w, uint64_t ws, uint64_t q) {
@@ -210,46 +199,5 @@ __device__ __forceinline__ uint64_t reduce16(uint64_t v, uint64_t q) {
   v = csub_n(v, q << 3, opaque(0 - (q << 3)));
   return reduce8(v, q);
 }
-#else
-// a w mod q in [0, 4q) for any a < 2^64, w < q, ws = floor(w 2^64 / q)
-__device__ __forceinline__ uint64_t mul_shoup_lazy4(uint64_t a, uint64_t w, uint64_t ws, uint64_t q) {
-  return a * w - mulhi_approx(a, ws) * q;
-}
-
-// forward CT butterfly: x, y in [0, 8q) -> [0, 8q)
-__device__ __forceinline__ void ct_bfly8(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
-  const uint64_t q4 = q << 2;
-  const uint64_t t = mul_shoup_lazy4(y, w, ws, q);
-  const uint64_t u = csub(x, q4);
-  x = u + t;
-  y = u + q4 - t;
-}
-
-// inverse GS butterfly: x, y in [0, 4q) -> [0, 4q)
-__device__ __forceinline__ void gs_bfly4(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
-  const uint64_t q4 = q << 2;
-  const uint64_t d = x + q4 - y;
-  x = csub(x + y, q4);
-  y = mul_shoup_lazy4(d, w, ws, q);
-}
-
-// [0, 8q) -> [0, q)
-__device__ __forceinline__ uint64_t reduce8(uint64_t v, uint64_t q) { return csub(csub(csub(v, q << 2), q << 1), q); }
-
-// lazy range up to 16q for q < 2^60 (see the carry-free forms above)
-__device__ __forceinline__ void ct_bfly_nored(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
-  const uint64_t t = mul_shoup_lazy4(y, w, ws, q);
-  y = x + (q << 2) - t;
-  x = x + t;
-}
-__device__ __forceinline__ void ct_bfly_c8(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
-  const uint64_t t = mul_shoup_lazy4(y, w, ws, q);
-  const uint64_t u = csub(x, q << 3);
-  x = u + t;
-  y = u + (q << 2) - t;
-}
-__device__ __forceinline__ uint64_t reduce16(uint64_t v, uint64_t q) { return reduce8(csub(v, q << 3), q); }
-
-#endif  // PHX_INT_NOCARRY
 
 }  // namespace phx

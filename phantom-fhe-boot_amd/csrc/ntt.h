@@ -39,10 +39,7 @@ struct NttTables {
 };
 
 // log2 of the column-pass size S1 for a given log2(n) (the row pass handles the rest)
-#ifndef PHX_NTT16_S1
-#define PHX_NTT16_S1 8
-#endif
-inline int ntt_split_log_s1(int log_n) { return log_n == 16 ? PHX_NTT16_S1 : log_n / 2; }
+inline int ntt_split_log_s1(int log_n) { return log_n / 2; }
 
 // Which table row each buffer limb uses.  Buffer limb i (0 <= i < num_limbs) maps to
 // table row (i < split ? first_a + i : first_b + (i - split)); limbs in

@@ -41,15 +41,12 @@ namespace {
 
 constexpr int E_LOG = 4;  // elements per thread per round = 16 (radix-16 rounds)
 constexpr int E = 1 << E_LOG;
-#ifndef PHX_NTT_COLS
-#define PHX_NTT_COLS 16
-#endif
-constexpr int COLS = PHX_NTT_COLS;  // columns per column-pass tile
+// columns per column-pass tile: 16 x 8 B = one 128 B line per row (8 / 16 / 32 measured 36.7 /
+// 26.6 / 28.4 us for the 50-bit forward, profiles/r03/ntt_experiments/cols_*.txt)
+constexpr int COLS = 16;
 constexpr int BLOCK = 256;
 constexpr int CBLOCK = COLS * 16 > BLOCK ? COLS * 16 : BLOCK;  // column-pass workgroup bound
-#ifndef PHX_NTT_WAVES_PER_EU
-#define PHX_NTT_WAVES_PER_EU 3  // __launch_bounds__ occupancy target (waves per SIMD) of one-tile grids
-#endif
+constexpr int kNttWavesPerEU = 3;  // __launch_bounds__ occupancy target (waves per SIMD) of one-tile grids
 
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 
@@ -445,9 +442,6 @@ __device__ __forceinline__ void stamp_now(int slot, int i, bool wait) {
 #else
 #define PHX_STAMP(slot, i, wait) ((void)0)
 #endif
-#ifndef PHX_ROW_TWD
-#define PHX_ROW_TWD 1  // integer row pass: 1 = later rounds derive w from ws, 2 = and load them up front
-#endif
 
 struct TileRef {
   int buf_limb, row, poly;
@@ -482,48 +476,9 @@ __device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr
   store_wt(o, v);
 }
 
-// PHX_EPI_LATE = K > 0: the epilogue's operands are loaded after the butterflies instead, K
-// elements per group with the next group in flight (as the key-switch epilogue), so the
-// butterflies do not hold them and the row pass can run at PHX_EPI_WAVES waves per SIMD.
-#ifndef PHX_EPI_LATE
-#define PHX_EPI_LATE 0
-#endif
-#ifndef PHX_EPI_WAVES
-#define PHX_EPI_WAVES 2
-#endif
-template <int T>
-__device__ __forceinline__ void epilogue_late(const KArgs& a, const TileRef& tr, const uint64_t (&y)[E], uint64_t q) {
-  constexpr int KC = PHX_EPI_LATE > 0 ? PHX_EPI_LATE : 1, NC = E / KC;
-  const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
-  const uint64_t* c = a.epi.c + tr.poly * a.epi.c_stride + e;
-  uint64_t* o = a.epi.ks_out(tr.poly) + e;
-  const bool acc = a.epi.accumulate;
-  const uint64_t* second = acc ? o : c;  // (a harmless re-read of c when not accumulating)
-  const uint64_t w = a.epi.w[tr.buf_limb], ws = a.epi.ws[tr.buf_limb];
-  uint64_t cb[2][KC], ob[2][KC];
-  auto load = [&](int g, int s) {
-#pragma unroll
-    for (int i = 0; i < KC; ++i) {
-      cb[s][i] = __builtin_nontemporal_load(c + (g * KC + i) * T);
-      ob[s][i] = __builtin_nontemporal_load(second + (g * KC + i) * T);
-    }
-  };
-  load(0, 0);
-  static_for<NC>([&](auto gg) {
-    constexpr int g = decltype(gg)::value, s = g & 1;
-    if constexpr (g + 1 < NC) load(g + 1, s ^ 1);
-#pragma unroll
-    for (int i = 0; i < KC; ++i) {
-      uint64_t v = mul_shoup(sub_mod(cb[s][i], y[g * KC + i], q), w, ws, q);
-      if (acc) v = add_mod(v, ob[s][i], q);
-      store_wt(o + (g * KC + i) * T, v);
-    }
-  });
-}
-
 // Key-switch epilogue (NttEpilogue::ks_beta > 0): out = (sum_d tmu[d] evk[d][p] (+ P add) mod q
 // - y) w (+ out), the inner product of eval_key_switch.cu:26-85 (128-bit sums, one Barrett-128
-// per element) formed where the moddown finish consumes it.  KC (PHX_KS_KC) elements at a time;
+// per element) formed where the moddown finish consumes it.  KC (kKsKC) elements at a time;
 // the next group's loads are issued before the current group's products.  BETA is a template parameter
 // and every load is unconditional (the third operand stream is `out` when accumulating, else the
 // addend, else a harmless re-read of tmu), so the compiler can count the loads in flight
@@ -532,19 +487,12 @@ __device__ __forceinline__ void epilogue_late(const KArgs& a, const TileRef& tr,
 // epilogue's row pass.  One element per group (loads of the next element in flight) at 3 waves
 // (158 VGPRs, no spill) beat 4 per group at 2 waves (234 VGPRs): C3 relinearize 0.274-0.288 ->
 // 0.268-0.274 ms, bootstrap 23.41-23.57 -> 23.17-23.37 ms (profiles/r03/ks_waves/).
-#ifndef PHX_KS_KC
-#define PHX_KS_KC 1
-#endif
-#ifndef PHX_KS_WAVES
-#define PHX_KS_WAVES 3
-#endif
-#ifndef PHX_KSP_WAVES
-#define PHX_KSP_WAVES 2  // ... and of the inverse row pass with the key-switch prologue
-#endif
+constexpr int kKsKC = 1, kKsWaves = 3;
+constexpr int kKspWaves = 2;  // ... and of the inverse row pass with the key-switch prologue
 template <int T, int BETA>
 __device__ __forceinline__ void ks_epilogue_b(const KArgs& a, const TileRef& tr, const uint64_t (&y)[E], uint64_t q,
                                               uint64_t r0, uint64_t r1) {
-  constexpr int KC = PHX_KS_KC, NC = E / KC;
+  constexpr int KC = kKsKC, NC = E / KC;
   const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
   const bool acc_out = a.epi.accumulate;
   const uint64_t* tm = a.epi.ks_tmu(tr.poly) + e;
@@ -602,7 +550,7 @@ __device__ __forceinline__ void ks_epilogue(const KArgs& a, const TileRef& tr, c
 // current products (as ks_epilogue_b).  The third stream is the addend, else a re-read of tmu.
 template <int T, int BETA>
 __device__ __forceinline__ void ks_prologue_b(const KArgs& a, const TileRef& tr, uint64_t (&x)[E]) {
-  constexpr int KC = PHX_KS_KC, NC = E / KC;
+  constexpr int KC = kKsKC, NC = E / KC;
   const size_t n = static_cast<size_t>(a.n);
   const size_t tl = a.epi.tmu_limb0 + tr.buf_limb;
   const uint64_t* tm = a.epi.ks_tmu(tr.poly) + tl * n + tr.k;
@@ -874,7 +822,7 @@ __device__ __forceinline__ void col_tile(const KArgs& a, int tile, uint64_t* lds
 }
 
 template <int S1_LOG, int S2_LOG, bool FWD, bool BCV = false, bool LZ = false>
-__global__ __launch_bounds__(CBLOCK, BCV ? 2 : PHX_NTT_WAVES_PER_EU) void ntt_col(KArgs a) {
+__global__ __launch_bounds__(CBLOCK, BCV ? 2 : kNttWavesPerEU) void ntt_col(KArgs a) {
   constexpr int NT = COLS * Sub<S1_LOG>::T, CT = (1 << S2_LOG) / COLS;
   __shared__ uint64_t lds[col_lds_words<S1_LOG>()];
   if (threadIdx.x >= NT) return;  // no barrier involves the idle threads' absence (NT is a multiple of 64)
@@ -991,7 +939,7 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
           }
         }
       });
-      if constexpr (FWD && EPI && !KS && PHX_EPI_LATE == 0) epilogue_load(a, tr, T, eo);
+      if constexpr (FWD && EPI && !KS) epilogue_load(a, tr, T, eo);
 #pragma unroll
       for (int k = 0; k < K0; ++k) {
         const uint32_t e = t + 1 + T * k;
@@ -1033,11 +981,6 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
 #pragma unroll
           for (int j = 0; j < E; ++j) y[j] = f64_to_canonical(v[j], lc.qd, lc.qinv);
           ks_epilogue<T>(a, tr, y, lc.q, a.barrett[2 * tr.row], a.barrett[2 * tr.row + 1]);
-        } else if constexpr (EPI && PHX_EPI_LATE > 0) {
-          uint64_t y[E];
-#pragma unroll
-          for (int j = 0; j < E; ++j) y[j] = f64_to_canonical(v[j], lc.qd, lc.qinv);
-          epilogue_late<T>(a, tr, y, lc.q);
         } else if constexpr (EPI) {
 #pragma unroll
           for (int j = 0; j < E; ++j) epilogue_store(a, tr, j, T, eo, f64_to_canonical(v[j], lc.qd, lc.qinv), lc.q);
@@ -1064,29 +1007,16 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
       const uint64_t* tw = a.tw + (size_t)tr.row * a.n;
       const uint64_t* tws = a.tws + (size_t)tr.row * a.n;
       uint64_t(&v)[E] = x;
-      // PHX_ROW_TWD: rounds after the first (whose twiddles are row-uniform: one broadcast line)
-      // read only the Shoup quotients and derive w (w_from_shoup): half the row pass's twiddle
-      // bytes (the (S1 + row)-indexed tables are ~2x the data).  2: those loads are issued up
-      // front with the tile, so no twiddle round trip sits between two rounds.
-      [[maybe_unused]] uint64_t wsr[RN][E];
-      if constexpr (PHX_ROW_TWD == 2) {
-        static_for<RN>([&](auto rc) {
-          constexpr int R = decltype(rc)::value;
-          if constexpr (R > 0) load_tw<S2_LOG, R>(wsr[R], tws, Round<S2_LOG, R>::p_thread(t), B);
-        });
-      }
+      // rounds after the first (whose twiddles are row-uniform: one broadcast line) read only
+      // the Shoup quotients and derive w (w_from_shoup): half the row pass's twiddle bytes (the
+      // (S1 + row)-indexed tables are ~2x the data; inverse -1.5 us, profiles/r03/ntt_experiments/twd_*.txt)
       auto get_tw = [&](auto rc, uint64_t (&w)[E], uint64_t (&ws)[E]) {
         constexpr int R = decltype(rc)::value;
-        if constexpr (PHX_ROW_TWD == 0 || R == 0) {
+        if constexpr (R == 0) {
           load_tw<S2_LOG, R>(w, tw, Round<S2_LOG, R>::p_thread(t), B);
           load_tw<S2_LOG, R>(ws, tws, Round<S2_LOG, R>::p_thread(t), B);
         } else {
-          if constexpr (PHX_ROW_TWD == 2) {
-#pragma unroll
-            for (int s = 0; s < E; ++s) ws[s] = wsr[R][s];
-          } else {
-            load_tw<S2_LOG, R>(ws, tws, Round<S2_LOG, R>::p_thread(t), B);
-          }
+          load_tw<S2_LOG, R>(ws, tws, Round<S2_LOG, R>::p_thread(t), B);
           w_from_shoup_round<S2_LOG, R>(w, ws, lc.q);
         }
       };
@@ -1099,7 +1029,7 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
             if constexpr (R > 0) relayout<S2_LOG, R - 1, R>(v, lrow, idx, sync, t);
             uint64_t w[E], ws[E];
             get_tw(rc, w, ws);
-            if constexpr (EPI && !KS && PHX_EPI_LATE == 0 && R == RN - 1) epilogue_load(a, tr, T, eo);  // behind the last twiddles
+            if constexpr (EPI && !KS && R == RN - 1) epilogue_load(a, tr, T, eo);  // behind the last twiddles
             if constexpr (LZ)
               ct_round_int16<S2_LOG, R, P::row_lz.mask>(v, w, ws, lc.q);
             else
@@ -1115,11 +1045,6 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
 #pragma unroll
             for (int j = 0; j < E; ++j) y[j] = canon(v[j]);
             ks_epilogue<T>(a, tr, y, lc.q, a.barrett[2 * tr.row], a.barrett[2 * tr.row + 1]);
-          } else if constexpr (EPI && PHX_EPI_LATE > 0) {
-            uint64_t y[E];
-#pragma unroll
-            for (int j = 0; j < E; ++j) y[j] = canon(v[j]);
-            epilogue_late<T>(a, tr, y, lc.q);
           } else if constexpr (EPI) {
 #pragma unroll
             for (int j = 0; j < E; ++j) epilogue_store(a, tr, j, T, eo, canon(v[j]), lc.q);
@@ -1152,8 +1077,7 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
 // KS: forward, the epilogue is the key-switch form (ks_epilogue; EPI must be set too); inverse, the
 // input is the key-switch prologue (ks_prologue).
 template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false, bool LZ = false, bool KS = false>
-__global__ __launch_bounds__(BLOCK, KS ? (FWD ? PHX_KS_WAVES : PHX_KSP_WAVES)
-                                      : EPI ? (PHX_EPI_LATE > 0 ? PHX_EPI_WAVES : 2) : PHX_NTT_WAVES_PER_EU)
+__global__ __launch_bounds__(BLOCK, KS ? (FWD ? kKsWaves : kKspWaves) : EPI ? 2 : kNttWavesPerEU)
 void ntt_row(KArgs a) {
   using RS = RowShape<S1_LOG, S2_LOG>;
   __shared__ uint64_t lds[RS::LDS_WORDS];
@@ -1370,7 +1294,7 @@ hipError_t dispatch(const NttTables& tb, const uint64_t* in, uint64_t* out, cons
   }
   switch (tb.log_n) {
     PHX_NTT_CASE(10, 5, 5) PHX_NTT_CASE(11, 5, 6) PHX_NTT_CASE(12, 6, 6) PHX_NTT_CASE(13, 6, 7)
-    PHX_NTT_CASE(14, 7, 7) PHX_NTT_CASE(15, 7, 8) PHX_NTT_CASE(16, PHX_NTT16_S1, 16 - PHX_NTT16_S1) PHX_NTT_CASE(17, 8, 9)
+    PHX_NTT_CASE(14, 7, 7) PHX_NTT_CASE(15, 7, 8) PHX_NTT_CASE(16, 8, 8) PHX_NTT_CASE(17, 8, 9)
     default: return hipErrorInvalidValue;
   }
 #undef PHX_NTT_CASE

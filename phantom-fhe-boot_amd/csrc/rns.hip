@@ -219,10 +219,7 @@ __device__ __forceinline__ BconvBlock bconv_block(uint32_t chunks, int groups) {
   }
   return {b % chunks, static_cast<int>(b / chunks)};
 }
-#ifndef PHX_BCONV_J
-#define PHX_BCONV_J 5
-#endif
-constexpr int kBconvJ = PHX_BCONV_J;
+constexpr int kBconvJ = 5;
 
 // the job of a multi-converter launch (BconvArgs::jobs): its matrix, output base and skip
 __device__ __forceinline__ void bconv_select_job(BconvArgs& a) {
@@ -408,20 +405,11 @@ __global__ __launch_bounds__(kBlock) void bconv_fixed_kernel(BconvArgs a, uint32
 // ---------------------------------------------------------------------------------------
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-#ifndef PHX_BCONV_CONTIG
-#define PHX_BCONV_CONTIG 0
-#endif
-#ifndef PHX_BCONV_MFMA_WAVES
-#define PHX_BCONV_MFMA_WAVES 8
-#endif
-constexpr int kMfmaWaves = PHX_BCONV_MFMA_WAVES;  // waves per workgroup; two workgroups per CU
-constexpr int kMfmaMaxJB = kBconvMfmaMaxObase / 16;
+// waves per workgroup, two workgroups per CU (4 / 16 measured slower, profiles/r03/ntt_experiments/bconv_c3.txt)
+constexpr int kMfmaWaves = 8;
 constexpr uint32_t kDropRow = 0x80000000u;  // byte offset of output rows past obase
 constexpr int kBufferWord3 = 0x00020000;    // raw buffer resource word 3 (gfx9: 32-bit data format)
-#ifndef PHX_BCONV_STORE_AUX
-#define PHX_BCONV_STORE_AUX 16
-#endif
-constexpr int kStoreSc1 = PHX_BCONV_STORE_AUX;  // write-through output stores (sc1): 27.3 -> 25.8 us mean, nt 27.6
+constexpr int kStoreSc1 = 16;  // write-through output stores (sc1): 27.3 -> 25.8 us mean, nt 27.6
 
 __device__ __forceinline__ uint64_t signed_digits(uint64_t t) {
   constexpr uint64_t k80 = 0x8080808080808080ull;
@@ -444,15 +432,9 @@ void bconv_mfma_kernel(BconvArgs a, uint32_t n) {
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t c = lane & 15, g = lane >> 4;
   const uint32_t tiles = n / 16;
-#if PHX_BCONV_CONTIG  // experiment: each wave owns a contiguous run of tiles
-  const uint32_t nwaves = gridDim.x * kMfmaWaves, per = (tiles + nwaves - 1) / nwaves, step = 1;
-  uint32_t tile = (blockIdx.x * kMfmaWaves + wave) * per;
-  const uint32_t tile_end = min(tile + per, tiles);
-#else
   const uint32_t step = gridDim.x * kMfmaWaves;
   uint32_t tile = blockIdx.x * kMfmaWaves + wave;
   const uint32_t tile_end = tiles;
-#endif
   // this lane's input limbs: s = 8 t + 2 g + u.  Loads are unconditional: limbs past ib read limb
   // ib - 1 (zeroed when converted) and tiles past the end read the last tile
   auto load = [&](uint64_t (&x)[KT][2], uint32_t tl) {

@@ -10,6 +10,7 @@
 // Prints one JSON object per check; exit status 0 iff every check meets its bound.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <complex>
@@ -290,6 +291,98 @@ int main(int argc, char** argv) {
     return g_ok ? 0 : 1;
   }
 
+  if (mode == "refapi") {
+    // the reference-signature FHECKKSRNS surface (include/bootstrap.cuh:116-175) at a small ring:
+    // rotation-index finders, CoeffsToSlots / SlotsToCoeffs through the precompute + evaluate pair,
+    // the dense linear transform, GetMultKey / GetGaloisKey, and the evaluator's
+    // KeySwitchDownFirstElement / EvalMultExt / EvalAddExt value forms
+    ct.PreComputeScale(ctx, scale);
+    const std::vector<double> sfR = ct.getScalingFactorsReal(), sfB = ct.getScalingFactorsRealBig();
+    FHECKKSRNS boot(enc);
+    std::vector<uint32_t> budget = levelBudget;
+    boot.EvalBootstrapSetup(ctx, budget, scale, sfR, sfB);
+    boot.EvalMultKeyGen(sk, ctx);
+    boot.EvalBootstrapKeyGen(sk, ctx, static_cast<uint32_t>(slots));
+    const uint32_t M = static_cast<uint32_t>(2 * N);
+    std::vector<int32_t> all = boot.FindBootstrapRotationIndices(static_cast<uint32_t>(slots), M);
+    std::vector<int> own = boot.rotation_indices();
+    std::sort(own.begin(), own.end());
+    const bool idx_ok = std::vector<int>(all.begin(), all.end()) == own &&
+                        std::is_sorted(all.begin(), all.end()) && !all.empty();
+    report("refapi_rotation_indices", idx_ok ? 0.0 : 1.0, 0.5, 0);
+    report("refapi_get_keys", (&boot.GetMultKey() != nullptr && boot.GetGaloisKey().has(
+                                  FindAutomorphismIndex2nComplex(all.front(), N))) ? 0.0 : 1.0, 0.5, 0);
+    // ksiPows and rotGroup as EvalBootstrapSetup computes them (bootstrap.cu:92-107)
+    std::vector<std::complex<double>> ksi(M + 1);
+    for (uint32_t j = 0; j < M; ++j) ksi[j] = std::polar(1.0, 2.0 * M_PI * j / M);
+    ksi[M] = ksi[0];
+    std::vector<uint32_t> rot(slots);
+    for (size_t j = 0, g5 = 1; j < slots; ++j, g5 = g5 * 5 % M) rot[j] = static_cast<uint32_t>(g5);
+    // lEnc = L0 - levelBudget - 1: the encoding starts at chain 2; the decoding right after it
+    const uint32_t L0 = static_cast<uint32_t>(ctx.size_Q());
+    auto ctsPre = boot.EvalCoeffsToSlotsPrecompute(ctx, ksi, rot, sfR, false, 1.0, L0 - budget[0] - 1);
+    auto stcPre = boot.EvalSlotsToCoeffsPrecompute(ctx, ksi, rot, sfR, false, 1.0, L0 - budget[0] - 1 - budget[1]);
+    PhantomCiphertext in2 = ct;
+    EvalMultConstInplace(ctx, in2, 1.0, sfR);  // at chain 2
+    EvalModReduceInPlace(ctx, in2, 1);
+    PhantomCiphertext slotsCt = boot.EvalCoeffsToSlots(ctsPre, in2, ctx);
+    PhantomCiphertext back = boot.EvalSlotsToCoeffs(stcPre, slotsCt, ctx);
+    report("refapi_cts_stc_roundtrip", max_abs_err(decrypt_decode(ctx, sk, enc, back), xz), 1e-6, back.chain_index());
+    // the coefficient-domain view: CtS puts the message polynomial's coefficients (scaled by 1 /
+    // its encoding scale) into the slots, bit-reversed; their norm equals the message's
+    {
+      const auto cv = decrypt_decode(ctx, sk, enc, slotsCt);
+      double e_slots = 0, e_msg = 0;
+      for (size_t j = 0; j < slots; ++j) {
+        e_slots += std::norm(cv[j]);
+        e_msg += x[j] * x[j];
+      }
+      // Parseval for the canonical embedding: sum |z_j|^2 = (N / 2) sum |c_k|^2 over the N coefficients,
+      // and the slots hold c_lo + i c_hi: sum |slot|^2 = sum |c_k|^2
+      report("refapi_cts_parseval", std::fabs(e_slots * static_cast<double>(slots) - e_msg) / e_msg, 1e-6,
+             slotsCt.chain_index());
+    }
+    // KeySwitchDownFirstElement / EvalMultExt / EvalAddExt on a P-scaled extended ciphertext
+    {
+      PhantomCiphertext ext = KeySwitchExt(ctx, ct);
+      PhantomCiphertext two = EvalAddExt(ctx, ext, ext);
+      PhantomCiphertext down = KeySwitchDown(ctx, static_cast<const PhantomCiphertext&>(two));
+      std::vector<std::complex<double>> want2(slots);
+      for (size_t j = 0; j < slots; ++j) want2[j] = 2.0 * x[j];
+      report("refapi_add_ext_keyswitch_down", max_abs_err(decrypt_decode(ctx, sk, enc, down), want2), 1e-6,
+             down.chain_index());
+      PhantomCiphertext first = KeySwitchDownFirstElement(ctx, two);
+      PhantomCiphertext full = KeySwitchDown(ctx, static_cast<const PhantomCiphertext&>(two));
+      const auto a = first.to_host(ctx.stream()), b = full.to_host(ctx.stream());
+      const bool same = a.size() * 2 == b.size() && std::equal(a.begin(), a.end(), b.begin());
+      report("refapi_keyswitch_down_first_element", same && first.size() == 1 ? 0.0 : 1.0, 0.5, first.chain_index());
+      PhantomPlaintext half;
+      std::vector<double> hv(slots, 0.5);
+      enc.encode_ext(ctx, std::vector<std::complex<double>>(hv.begin(), hv.end()), scale, half, ct.chain_index());
+      PhantomCiphertext prod = EvalMultExt(ctx, ext, half);
+      PhantomCiphertext pd = KeySwitchDown(ctx, static_cast<const PhantomCiphertext&>(prod));
+      EvalModReduceInPlace(ctx, pd, 1);
+      std::vector<std::complex<double>> wanth(slots);
+      for (size_t j = 0; j < slots; ++j) wanth[j] = 0.5 * x[j];
+      report("refapi_mult_ext", max_abs_err(decrypt_decode(ctx, sk, enc, pd), wanth), 1e-6, pd.chain_index());
+    }
+    // a dense slots x slots transform: A[p][q] = cos(p + 2q) / slots + i sin(3p - q) / slots
+    if (slots <= 2048) {  // one level of g <= 32 baby and b <= 64 giant steps (csrc/ckks.h kLtMaxG, kLtMaxB)
+      std::vector<std::vector<std::complex<double>>> A(slots, std::vector<std::complex<double>>(slots));
+      for (size_t p = 0; p < slots; ++p)
+        for (size_t q = 0; q < slots; ++q)
+          A[p][q] = std::complex<double>(std::cos(double(p + 2 * q)), std::sin(3.0 * p - double(q))) / double(slots);
+      boot.EvalRotationKeyGen(sk, ctx, boot.FindLinearTransformRotationIndices(static_cast<uint32_t>(slots), M));
+      auto ltPre = boot.EvalLinearTransformPrecompute(ctx, A, 1.0, 0);
+      PhantomCiphertext lt = boot.EvalLinearTransform(ltPre, ct, ctx);
+      std::vector<std::complex<double>> want(slots);
+      for (size_t p = 0; p < slots; ++p)
+        for (size_t q = 0; q < slots; ++q) want[p] += A[p][q] * x[q];
+      report("refapi_linear_transform", max_abs_err(decrypt_decode(ctx, sk, enc, lt), want), 1e-6, lt.chain_index());
+    }
+    std::printf("{\"done\": \"refapi\", \"ok\": %s}\n", g_ok ? "true" : "false");
+    return g_ok ? 0 : 1;
+  }
   if (mode == "chebdepth") {
     // EvalChebyshevSeries through the reference's Paterson-Stockmeyer (host/chebyshev_ps.cpp) for
     // every degree 5..119 on three intervals: levels consumed (a pending rescale counts) against

@@ -490,6 +490,46 @@ static void example_ckks_galois_key_layout() {
     threw = true;
   }
   require(threw, "save of a partial key set must throw");
+  // ... and so can a set with a key outside the list (save_with_elements names it)
+  PhantomGaloisKey extra = secret_key.create_galois_keys(context);
+  extra.merge(secret_key.create_galois_keys(context, {125 * 125 % (2 * N)}));
+  threw = false;
+  try {
+    std::stringstream t;
+    extra.save(context, t);
+  } catch (const std::invalid_argument&) {
+    threw = true;
+  }
+  require(threw, "save of a key outside the context's list must throw");
+  // a file of the round-3 build (keys in ascending element order, then the element list: the
+  // save_with_elements layout) loads through load() with every key on its own element, and the
+  // stream is left after the element list
+  {
+    std::stringstream legacy;
+    gk.save_with_elements(context, legacy);
+    const uint64_t marker = 0x5EEDC0DEull;
+    legacy.write(reinterpret_cast<const char*>(&marker), sizeof(marker));
+    PhantomGaloisKey l2;
+    l2.load(context, legacy);
+    uint64_t after = 0;
+    legacy.read(reinterpret_cast<char*>(&after), sizeof(after));
+    require(legacy && after == marker, "legacy Galois key stream consumed exactly");
+    for (uint32_t e : elts) {
+      std::vector<uint64_t> a(2 * QP * N), b(2 * QP * N);
+      PHX_CHECK(hipMemcpy(a.data(), gk.get(e).digit(0), a.size() * 8, hipMemcpyDeviceToHost));
+      PHX_CHECK(hipMemcpy(b.data(), l2.get(e).digit(0), b.size() * 8, hipMemcpyDeviceToHost));
+      require(a == b, "legacy Galois key bound to its own element");
+    }
+    // the reference layout followed by other data is not mistaken for the legacy one
+    std::stringstream ref;
+    gk.save(context, ref);
+    ref.write(reinterpret_cast<const char*>(&marker), sizeof(marker));
+    PhantomGaloisKey l3;
+    l3.load(context, ref);
+    after = 0;
+    ref.read(reinterpret_cast<char*>(&after), sizeof(after));
+    require(ref && after == marker, "reference Galois key stream leaves the following data");
+  }
 }
 
 // 3_ckks.cu:761-818

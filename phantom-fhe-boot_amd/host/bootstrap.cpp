@@ -595,98 +595,115 @@ void FHECKKSRNS::build_levels(const PhantomContext& cc, bool encode_dir, const L
       T = boot::compose(boot::stage(ns, s, encode_dir), T, ns);
     }
     const bool scale_here = encode_dir ? gi == 0 : gi + 1 == sizes.size();
-    if (scale_here)
+    if (scale_here) {
+      const std::complex<double> cf = args.times_i ? std::complex<double>(0.0, constant) : std::complex<double>(constant, 0.0);
       for (auto& kv : T)
-        for (auto& x : kv.second) x *= constant;
+        for (auto& x : kv.second) x *= cf;
+    }
     if (ns < n) {
       const bool last_enc = encode_dir && gi + 1 == sizes.size();
       const bool first_dec = !encode_dir && gi == 0;
       T = boot::lift_blocks(T, ns, n, last_enc ? &out_mask : nullptr, first_dec ? &in_mask : nullptr);
     }
     LTLevel lv;
-    lv.stride = 1 << (s_min - 1);
-    int kmin = 0, kmax = 0;
-    for (const auto& kv : T) {
-      int a = kv.first;
-      if (a > static_cast<int>(n / 2)) a -= static_cast<int>(n);
-      if (a % lv.stride) throw std::logic_error("diagonal offset not a multiple of the stride");
-      kmin = std::min(kmin, a / lv.stride);
-      kmax = std::max(kmax, a / lv.stride);
-    }
-    lv.center = -kmin;
-    lv.D = kmax - kmin + 1;
-    lv.g = 1;
-    if (dim1) {
-      if (dim1 & (dim1 - 1)) throw std::invalid_argument("dim1 must be a power of two");
-      lv.g = static_cast<int>(std::min<uint32_t>(dim1, static_cast<uint32_t>(phx::kLtMaxG)));
-    } else {
-      // g^2 >= 2 D: twice the baby steps of the square split.  A hoisted baby step is one fused
-      // key switch + automorphism; a giant step is a moddown + modup (one INTT over Ql u P and an
-      // NTT over every digit) before its key switch, so fewer giant steps pay: 256 diagonals as
-      // g 32 x b 8 instead of 16 x 16 take the bootstrap from 29.7 to 27.9 ms
-      // (profiles/r02/lt_baby_giant_split.txt); PHX_LT_SQUARE=1 restores the square split.
-      static const bool square = std::getenv("PHX_LT_SQUARE") != nullptr;
-      while (lv.g * lv.g < (square ? 1 : 2) * lv.D && lv.g < phx::kLtMaxG) lv.g *= 2;
-    }
-    lv.b = (lv.D + lv.g - 1) / lv.g;
+    lt_shape(lv, T, n, dim1, 1 << (s_min - 1));
     lv.chain = first_chain + gi;
-    if (lv.g > phx::kLtMaxG || lv.b > phx::kLtMaxB) throw std::invalid_argument("linear transform level too large");
-    if (!encode) {
-      out.push_back(std::move(lv));
-      continue;
-    }
-    const double scale = sf_.at(lv.chain - 1);
-    lv.pts.resize(lv.D);
-    // the level's diagonals: their host encodings (FFT + exact RNS rounding) run on host threads,
-    // a chunk at a time, each chunk's uploads + NTTs queued behind it on the stream
-    std::vector<std::pair<int, const boot::cvec*>> jobs;
-    for (int u = 0; u < lv.D; ++u) {
-      const long off = static_cast<long>(u - lv.center) * lv.stride;
-      const int key = static_cast<int>(((off % static_cast<long>(n)) + static_cast<long>(n)) % static_cast<long>(n));
-      auto it = T.find(key);
-      if (it != T.end()) jobs.emplace_back(u, &it->second);
-    }
-    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<std::vector<uint64_t>> host(nt);
-    for (size_t c0 = 0; c0 < jobs.size(); c0 += nt) {
-      const size_t cnt = std::min<size_t>(nt, jobs.size() - c0);
-      auto work = [&](size_t w) {
-        const int u = jobs[c0 + w].first;
-        const boot::cvec& diag = *jobs[c0 + w].second;
-        // pre-rotate by -(g i stride) so the giant rotation can follow the inner sum
-        const size_t sh = static_cast<size_t>((u / lv.g) * lv.g) * lv.stride % n;
-        boot::cvec rot(n);
-        for (size_t p = 0; p < n; ++p) rot[p] = diag[(p + n - sh) % n];
-        encoder_.encode_ext_host(cc, rot, scale, lv.chain, host[w], 1);
-      };
-      std::vector<std::thread> th;
-      for (size_t w = 1; w < cnt; ++w) th.emplace_back(work, w);
-      work(0);
-      for (auto& t : th) t.join();
-      for (size_t w = 0; w < cnt; ++w) {
-        auto pt = std::make_unique<PhantomPlaintext>();
-        encoder_.upload_ext_async(cc, host[w], scale, *pt, lv.chain);
-        lv.pts[jobs[c0 + w].first] = std::move(pt);
-      }
-      PHX_CHECK(hipStreamSynchronize(cc.stream()));  // host[] is rewritten by the next chunk
-    }
-    // pointer table [b][g] for the kernel; absent diagonals read a zero plaintext
-    std::vector<const uint64_t*> ptrs(static_cast<size_t>(lv.b) * lv.g, nullptr);
-    for (size_t u = 0; u < ptrs.size(); ++u) {
-      if (u < static_cast<size_t>(lv.D) && lv.pts[u]) {
-        ptrs[u] = lv.pts[u]->data();
-        continue;
-      }
-      if (!lv.zero) {
-        const size_t limbs = cc.get_context_data(lv.chain).coeff_modulus_size() + cc.size_P();
-        lv.zero.allocate(limbs * cc.poly_degree(), cc.stream());
-        PHX_CHECK(hipMemsetAsync(lv.zero.get(), 0, limbs * cc.poly_degree() * sizeof(uint64_t), cc.stream()));
-      }
-      ptrs[u] = lv.zero.get();
-    }
-    lv.d_pts.upload(ptrs, cc.stream());
+    if (encode) encode_level(cc, lv, T);
     out.push_back(std::move(lv));
   }
+}
+
+void FHECKKSRNS::lt_shape(LTLevel& lv, const boot::DiagMap& T, size_t n, uint32_t dim1, int stride) {
+  lv.stride = stride;
+  int kmin = 0, kmax = 0;
+  for (const auto& kv : T) {
+    int a = kv.first;
+    if (a > static_cast<int>(n / 2)) a -= static_cast<int>(n);
+    if (a % lv.stride) throw std::logic_error("diagonal offset not a multiple of the stride");
+    kmin = std::min(kmin, a / lv.stride);
+    kmax = std::max(kmax, a / lv.stride);
+  }
+  lv.center = -kmin;
+  lv.D = kmax - kmin + 1;
+  lv.g = 1;
+  if (dim1) {
+    if (dim1 & (dim1 - 1)) throw std::invalid_argument("dim1 must be a power of two");
+    lv.g = static_cast<int>(std::min<uint32_t>(dim1, static_cast<uint32_t>(phx::kLtMaxG)));
+  } else {
+    // g^2 >= 2 D: twice the baby steps of the square split.  A hoisted baby step is one fused
+    // key switch + automorphism; a giant step is a moddown + modup (one INTT over Ql u P and an
+    // NTT over every digit) before its key switch, so fewer giant steps pay: 256 diagonals as
+    // g 32 x b 8 instead of 16 x 16 take the bootstrap from 29.7 to 27.9 ms
+    // (profiles/r02/lt_baby_giant_split.txt); PHX_LT_SQUARE=1 restores the square split.
+    static const bool square = std::getenv("PHX_LT_SQUARE") != nullptr;
+    while (lv.g * lv.g < (square ? 1 : 2) * lv.D && lv.g < phx::kLtMaxG) lv.g *= 2;
+  }
+  lv.b = (lv.D + lv.g - 1) / lv.g;
+  if (lv.g > phx::kLtMaxG || lv.b > phx::kLtMaxB) throw std::invalid_argument("linear transform level too large");
+}
+
+void FHECKKSRNS::encode_level(const PhantomContext& cc, LTLevel& lv, const boot::DiagMap& T) const {
+  const size_t n = cc.poly_degree() / 2;
+  const double scale = sf_.at(lv.chain - 1);
+  lv.pts.clear();
+  lv.pts.resize(lv.D);
+  // the level's diagonals: their host encodings (FFT + exact RNS rounding) run on host threads,
+  // a chunk at a time, each chunk's uploads + NTTs queued on the stream behind it
+  std::vector<std::pair<int, const boot::cvec*>> jobs;
+  for (int u = 0; u < lv.D; ++u) {
+    const long off = static_cast<long>(u - lv.center) * lv.stride;
+    const int key = static_cast<int>(((off % static_cast<long>(n)) + static_cast<long>(n)) % static_cast<long>(n));
+    auto it = T.find(key);
+    if (it != T.end()) jobs.emplace_back(u, &it->second);
+  }
+  const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::vector<uint64_t>> host(nt);
+  for (size_t c0 = 0; c0 < jobs.size(); c0 += nt) {
+    const size_t cnt = std::min<size_t>(nt, jobs.size() - c0);
+    auto work = [&](size_t w) {
+      const int u = jobs[c0 + w].first;
+      const boot::cvec& diag = *jobs[c0 + w].second;
+      // pre-rotate by -(g i stride) so the giant rotation can follow the inner sum
+      const size_t sh = static_cast<size_t>((u / lv.g) * lv.g) * lv.stride % n;
+      boot::cvec rot(n);
+      for (size_t p = 0; p < n; ++p) rot[p] = diag[(p + n - sh) % n];
+      encoder_.encode_ext_host(cc, rot, scale, lv.chain, host[w], 1);
+    };
+    std::vector<std::thread> th;
+    for (size_t w = 1; w < cnt; ++w) th.emplace_back(work, w);
+    work(0);
+    for (auto& t : th) t.join();
+    for (size_t w = 0; w < cnt; ++w) {
+      auto pt = std::make_unique<PhantomPlaintext>();
+      encoder_.upload_ext_async(cc, host[w], scale, *pt, lv.chain);
+      lv.pts[jobs[c0 + w].first] = std::move(pt);
+    }
+    PHX_CHECK(hipStreamSynchronize(cc.stream()));  // host[] is rewritten by the next chunk
+  }
+  std::vector<std::shared_ptr<PhantomPlaintext>> view;  // (attach reads the pointers only)
+  attach(cc, lv, view);
+}
+
+// the device pointer table [b][g] of a level's plaintexts (lv.pts when `ext` is empty, else the
+// caller's set); absent diagonals read a zero plaintext
+void FHECKKSRNS::attach(const PhantomContext& cc, LTLevel& lv,
+                        const std::vector<std::shared_ptr<PhantomPlaintext>>& ext) const {
+  std::vector<const uint64_t*> ptrs(static_cast<size_t>(lv.b) * lv.g, nullptr);
+  for (size_t u = 0; u < ptrs.size(); ++u) {
+    const PhantomPlaintext* p = nullptr;
+    if (u < static_cast<size_t>(lv.D)) p = ext.empty() ? lv.pts[u].get() : ext[u].get();
+    if (p) {
+      ptrs[u] = p->data();
+      continue;
+    }
+    if (!lv.zero) {
+      const size_t limbs = cc.get_context_data(lv.chain).coeff_modulus_size() + cc.size_P();
+      lv.zero.allocate(limbs * cc.poly_degree(), cc.stream());
+      PHX_CHECK(hipMemsetAsync(lv.zero.get(), 0, limbs * cc.poly_degree() * sizeof(uint64_t), cc.stream()));
+    }
+    ptrs[u] = lv.zero.get();
+  }
+  lv.d_pts.upload(ptrs, cc.stream());
 }
 
 void FHECKKSRNS::EvalBootstrapSetup(const PhantomContext& cc, const std::vector<uint32_t>& levelBudget, double scale,
@@ -811,6 +828,7 @@ size_t FHECKKSRNS::OutputChainIndex(const std::vector<uint32_t>& levelBudget, ui
 
 size_t FHECKKSRNS::output_chain_index(uint32_t numSlots, uint32_t numIterations) const {
   const uint32_t slots = numSlots ? numSlots : static_cast<uint32_t>(encoder_.slot_count());
+  std::lock_guard<std::mutex> lk(precom_mu_);  // a deferred encoding may be reassigning pc.dec
   auto it = precom_.find(slots);
   if (it == precom_.end() || it->second.dec.empty()) throw std::invalid_argument("bootstrap setup missing");
   return it->second.dec.back().chain + 1 + (numIterations > 1 ? 1 : 0);
@@ -824,6 +842,7 @@ std::vector<int> FHECKKSRNS::rotation_indices(uint32_t numSlots) const {
     if (v != 0 && std::find(r.begin(), r.end(), v) == r.end()) r.push_back(v);
   };
   const uint32_t slots = numSlots ? numSlots : static_cast<uint32_t>(n);
+  std::lock_guard<std::mutex> lk(precom_mu_);
   auto it = precom_.find(slots);
   if (it == precom_.end()) throw std::invalid_argument("bootstrap setup missing for this slot count");
   for (const auto* lvs : {&it->second.enc, &it->second.dec})
@@ -845,6 +864,15 @@ void FHECKKSRNS::EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext&
   for (uint32_t e : elts)
     if (!galois_keys_.has(e)) need.push_back(e);
   galois_keys_.merge(sk.create_galois_keys_fused(cc, need));
+}
+
+void FHECKKSRNS::EvalRotationKeyGen(PhantomSecretKey& sk, const PhantomContext& cc, const std::vector<int32_t>& indices) {
+  std::vector<uint32_t> need;
+  for (int32_t r : indices) {
+    const uint32_t e = FindAutomorphismIndex2nComplex(r, cc.poly_degree());
+    if (e != 1 && !galois_keys_.has(e) && std::find(need.begin(), need.end(), e) == need.end()) need.push_back(e);
+  }
+  if (!need.empty()) galois_keys_.merge(sk.create_galois_keys_fused(cc, need));
 }
 
 void FHECKKSRNS::EvalMultKeyGen(PhantomSecretKey& sk, const PhantomContext& cc) { mul_key_ = sk.gen_relinkey(cc); }
@@ -985,6 +1013,228 @@ PhantomCiphertext FHECKKSRNS::EvalSlotsToCoeffs(const PhantomCiphertext& ct, con
   PhantomCiphertext r = apply_level(cc, ct, pc.dec.at(0));
   for (size_t i = 1; i < pc.dec.size(); ++i) r = apply_level(cc, r, pc.dec[i]);
   return r;
+}
+
+// ---- the reference's precompute / evaluate / rotation-index surface ------------------------------
+
+std::vector<int32_t> FHECKKSRNS::dir_rotations(uint32_t slots, uint32_t M, bool encode_dir) const {
+  std::lock_guard<std::mutex> lk(precom_mu_);
+  auto it = precom_.find(slots);
+  if (it == precom_.end())
+    throw std::invalid_argument("Precomputations for " + std::to_string(slots) +
+                                " slots were not generated Need to call EvalBootstrapSetup to proceed");
+  const long quarter = static_cast<long>(M / 4);
+  std::vector<int32_t> r;
+  auto reduce = [](long x, long m) { return static_cast<int32_t>(((x % m) + m) % m); };  // ReduceRotation
+  for (const LTLevel& lv : encode_dir ? it->second.enc : it->second.dec) {
+    for (int j = 0; j < lv.g; ++j) r.push_back(reduce(static_cast<long>(j - lv.center) * lv.stride, quarter));
+    for (int i = 0; i < lv.b; ++i) r.push_back(reduce(static_cast<long>(lv.g) * i * lv.stride, quarter));
+  }
+  // sparse packing: the partial sums before CoeffToSlot, the fold after SlotToCoeff
+  if (4 * static_cast<long>(slots) != static_cast<long>(M)) {
+    if (encode_dir) {
+      for (long j = 1; j * 4 * static_cast<long>(slots) < static_cast<long>(M); j <<= 1) r.push_back(static_cast<int32_t>(j * slots));
+    } else {
+      r.push_back(static_cast<int32_t>(slots));
+    }
+  }
+  std::sort(r.begin(), r.end());
+  r.erase(std::unique(r.begin(), r.end()), r.end());
+  r.erase(std::remove(r.begin(), r.end(), 0), r.end());
+  r.erase(std::remove(r.begin(), r.end(), static_cast<int32_t>(quarter)), r.end());
+  return r;
+}
+
+std::vector<int32_t> FHECKKSRNS::FindCoeffsToSlotsRotationIndices(uint32_t slots, uint32_t M) const {
+  return dir_rotations(slots, M, true);
+}
+
+std::vector<int32_t> FHECKKSRNS::FindSlotsToCoeffsRotationIndices(uint32_t slots, uint32_t M) const {
+  return dir_rotations(slots, M, false);
+}
+
+std::vector<int32_t> FHECKKSRNS::FindBootstrapRotationIndices(uint32_t slots, uint32_t M) const {
+  std::vector<int32_t> r = FindCoeffsToSlotsRotationIndices(slots, M);
+  const std::vector<int32_t> d = FindSlotsToCoeffsRotationIndices(slots, M);
+  r.insert(r.end(), d.begin(), d.end());
+  std::sort(r.begin(), r.end());
+  r.erase(std::unique(r.begin(), r.end()), r.end());
+  return r;
+}
+
+// the dense transform's level: every diagonal offset 0 .. slots-1 (stride 1)
+static uint32_t dense_g(uint32_t slots, uint32_t dim) {
+  if (dim) return dim;
+  uint32_t g = 1;
+  while (g * g < slots && g < static_cast<uint32_t>(phx::kLtMaxG)) g *= 2;
+  return g;
+}
+
+std::vector<int32_t> FHECKKSRNS::FindLinearTransformRotationIndices(uint32_t slots, uint32_t M, uint32_t dim) const {
+  if (slots == 0 || slots > M / 4) throw std::invalid_argument("FindLinearTransformRotationIndices: bad slot count");
+  const uint32_t g = dense_g(slots, dim), b = (slots + g - 1) / g;
+  std::vector<int32_t> r;
+  for (uint32_t j = 1; j < g; ++j) r.push_back(static_cast<int32_t>(j % slots));
+  for (uint32_t i = 1; i < b; ++i) r.push_back(static_cast<int32_t>((g * i) % slots));
+  std::sort(r.begin(), r.end());
+  r.erase(std::unique(r.begin(), r.end()), r.end());
+  r.erase(std::remove(r.begin(), r.end(), 0), r.end());
+  return r;
+}
+
+std::vector<std::shared_ptr<PhantomPlaintext>> FHECKKSRNS::EvalLinearTransformPrecompute(
+    const PhantomContext& cc, const std::vector<std::vector<std::complex<double>>>& A, double scale, uint32_t L) const {
+  const size_t n = cc.poly_degree() / 2, slots = A.size();
+  if (slots != n) throw std::invalid_argument("EvalLinearTransformPrecompute: A must be (N/2) x (N/2) (full packing)");
+  for (const auto& row : A)
+    if (row.size() != slots) throw std::invalid_argument("EvalLinearTransformPrecompute: A is not square");
+  // diagonal k: d_k[p] = A[p][(p + k) mod slots] (ExtractShiftedDiagonal, util.cu:298-312)
+  boot::DiagMap T;
+  for (size_t k = 0; k < slots; ++k) {
+    boot::cvec d(slots);
+    bool nz = false;
+    for (size_t p = 0; p < slots; ++p) {
+      d[p] = A[p][(p + k) % slots] * scale;
+      nz |= d[p] != std::complex<double>(0.0, 0.0);
+    }
+    if (nz) T.emplace(static_cast<int>(k), std::move(d));
+  }
+  LTLevel lv;
+  lv.stride = 1;
+  lv.center = 0;
+  lv.D = static_cast<int>(slots);
+  lv.g = static_cast<int>(dense_g(static_cast<uint32_t>(slots), 0));
+  lv.b = (lv.D + lv.g - 1) / lv.g;
+  if (lv.g > phx::kLtMaxG || lv.b > phx::kLtMaxB)
+    throw std::invalid_argument("EvalLinearTransformPrecompute: more diagonals than one level evaluates (N <= 2^12)");
+  lv.chain = 1 + L;
+  if (lv.chain >= cc.total_parm_size()) throw std::invalid_argument("EvalLinearTransformPrecompute: L beyond the chain");
+  encode_level(cc, lv, T);
+  std::vector<std::shared_ptr<PhantomPlaintext>> out(lv.D);
+  for (int u = 0; u < lv.D; ++u) out[u] = std::shared_ptr<PhantomPlaintext>(std::move(lv.pts[u]));
+  return out;
+}
+
+std::vector<std::shared_ptr<PhantomPlaintext>> FHECKKSRNS::EvalLinearTransformPrecompute(
+    const PhantomContext&, const std::vector<std::vector<std::complex<double>>>&,
+    const std::vector<std::vector<std::complex<double>>>&, uint32_t, double, uint32_t) const {
+  throw std::logic_error(
+      "EvalLinearTransformPrecompute(A, B, orientation): the reference declares it (include/bootstrap.cuh:133-136) "
+      "but defines no body; sparse packing runs through EvalCoeffsToSlots / EvalSlotsToCoeffs instead");
+}
+
+PhantomCiphertext FHECKKSRNS::EvalLinearTransform(const std::vector<std::shared_ptr<PhantomPlaintext>>& A,
+                                                  const PhantomCiphertext& ct, const PhantomContext& cc) const {
+  const size_t n = cc.poly_degree() / 2;
+  if (A.size() != n) throw std::invalid_argument("EvalLinearTransform: expects EvalLinearTransformPrecompute's N/2 plaintexts");
+  LTLevel lv;
+  lv.stride = 1;
+  lv.center = 0;
+  lv.D = static_cast<int>(n);
+  lv.g = static_cast<int>(dense_g(static_cast<uint32_t>(n), 0));
+  lv.b = (lv.D + lv.g - 1) / lv.g;
+  lv.chain = 0;
+  for (const auto& p : A)
+    if (p) lv.chain = p->chain_index();
+  if (!lv.chain) throw std::invalid_argument("EvalLinearTransform: every diagonal is zero");
+  attach(cc, lv, A);
+  return apply_level(cc, ct, lv);
+}
+
+std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>> FHECKKSRNS::precompute_dir(
+    const PhantomContext& cc, bool encode_dir, const std::vector<std::complex<double>>& A,
+    const std::vector<uint32_t>& rotGroup, bool flag_i, double scale, uint32_t L) const {
+  const uint32_t slots = static_cast<uint32_t>(rotGroup.size());
+  const uint64_t M = 2 * cc.poly_degree();
+  // the roots this engine's factorisation uses (ksiPows and the powers of 5, bootstrap.cu:92-107)
+  if (A.size() < M) throw std::invalid_argument("A must hold the 2N-th roots of unity (ksiPows)");
+  for (uint64_t j = 0; j < M; ++j) {
+    const double ang = 2.0 * M_PI * static_cast<double>(j) / static_cast<double>(M);
+    if (std::abs(A[j] - std::complex<double>(std::cos(ang), std::sin(ang))) > 1e-9)
+      throw std::invalid_argument("A[" + std::to_string(j) + "] is not exp(2 pi i j / 2N)");
+  }
+  uint64_t g5 = 1;
+  for (uint32_t j = 0; j < slots; ++j, g5 = g5 * 5 % M)
+    if (rotGroup[j] != g5) throw std::invalid_argument("rotGroup must be 5^j mod 2N");
+  LevelArgs args;
+  {
+    std::lock_guard<std::mutex> lk(precom_mu_);
+    auto it = precom_.find(slots);
+    if (it == precom_.end())
+      throw std::invalid_argument("Precomputations for " + std::to_string(slots) +
+                                  " slots were not generated Need to call EvalBootstrapSetup to proceed");
+    args = encode_dir ? it->second.enc_args : it->second.dec_args;
+  }
+  args.constant = scale;
+  args.times_i = flag_i;
+  // lEnc / lDec: the first level's chain, 1 + (size_Q - L - levelBudget) dropped towers (L = 0: chain 1)
+  const size_t budget = args.sizes.size();
+  if (L != 0 && static_cast<size_t>(L) + budget > cc.size_Q()) throw std::invalid_argument("L leaves too few levels");
+  args.first_chain = L == 0 ? 1 : 1 + cc.size_Q() - L - budget;
+  std::vector<LTLevel> levels;
+  build_levels(cc, encode_dir, args, slots, levels, true);
+  std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>> out(levels.size());
+  for (size_t gi = 0; gi < levels.size(); ++gi) {
+    out[gi].resize(levels[gi].D);
+    for (int u = 0; u < levels[gi].D; ++u) out[gi][u] = std::shared_ptr<PhantomPlaintext>(std::move(levels[gi].pts[u]));
+  }
+  return out;
+}
+
+PhantomCiphertext FHECKKSRNS::apply_dir(const std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>>& A,
+                                        const PhantomCiphertext& ct, const PhantomContext& cc, uint32_t numSlots,
+                                        bool encode_dir) const {
+  const uint32_t slots = numSlots ? numSlots : static_cast<uint32_t>(cc.poly_degree() / 2);
+  LevelArgs args;
+  {
+    std::lock_guard<std::mutex> lk(precom_mu_);
+    auto it = precom_.find(slots);
+    if (it == precom_.end())
+      throw std::invalid_argument("Precomputations for " + std::to_string(slots) +
+                                  " slots were not generated Need to call EvalBootstrapSetup to proceed");
+    args = encode_dir ? it->second.enc_args : it->second.dec_args;
+  }
+  std::vector<LTLevel> levels;
+  build_levels(cc, encode_dir, args, slots, levels, false);  // the shape only
+  if (A.size() != levels.size()) throw std::invalid_argument("plaintext set does not match the setup's level budget");
+  PhantomCiphertext r;
+  for (size_t gi = 0; gi < levels.size(); ++gi) {
+    LTLevel& lv = levels[gi];
+    if (A[gi].size() != static_cast<size_t>(lv.D)) throw std::invalid_argument("plaintext set does not match the setup");
+    lv.chain = 0;
+    for (const auto& p : A[gi])
+      if (p) lv.chain = p->chain_index();
+    if (!lv.chain) throw std::invalid_argument("a level of the plaintext set is empty");
+    attach(cc, lv, A[gi]);
+    r = apply_level(cc, gi ? r : ct, lv);
+  }
+  return r;
+}
+
+std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>> FHECKKSRNS::EvalCoeffsToSlotsPrecompute(
+    const PhantomContext& cc, const std::vector<std::complex<double>>& A, const std::vector<uint32_t>& rotGroup,
+    const std::vector<double>& sf, bool flag_i, double scale, uint32_t L) const {
+  if (!sf.empty() && sf.size() != sf_.size()) throw std::invalid_argument("scaling factors differ from the setup's");
+  return precompute_dir(cc, true, A, rotGroup, flag_i, scale, L);
+}
+
+std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>> FHECKKSRNS::EvalSlotsToCoeffsPrecompute(
+    const PhantomContext& cc, const std::vector<std::complex<double>>& A, const std::vector<uint32_t>& rotGroup,
+    const std::vector<double>& sf, bool flag_i, double scale, uint32_t L) const {
+  if (!sf.empty() && sf.size() != sf_.size()) throw std::invalid_argument("scaling factors differ from the setup's");
+  return precompute_dir(cc, false, A, rotGroup, flag_i, scale, L);
+}
+
+PhantomCiphertext FHECKKSRNS::EvalCoeffsToSlots(const std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>>& A,
+                                                const PhantomCiphertext& ctxt, const PhantomContext& cc,
+                                                uint32_t numSlots) const {
+  return apply_dir(A, ctxt, cc, numSlots, true);
+}
+
+PhantomCiphertext FHECKKSRNS::EvalSlotsToCoeffs(const std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>>& A,
+                                                const PhantomCiphertext& ctxt, const PhantomContext& cc,
+                                                uint32_t numSlots) const {
+  return apply_dir(A, ctxt, cc, numSlots, false);
 }
 
 PhantomCiphertext FHECKKSRNS::EvalChebyshevSeries(const PhantomCiphertext& ct, const PhantomContext& cc,

@@ -87,6 +87,9 @@ class FHECKKSRNS {
   // baby/giant steps, the sparse partial sums and conjugation, and the relinearization key.
   void EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext& cc, uint32_t numSlots = 0);
   void EvalMultKeyGen(PhantomSecretKey& sk, const PhantomContext& cc);
+  // fused rotation keys for further slot rotations (e.g. FindLinearTransformRotationIndices for
+  // EvalLinearTransform); keys already held are kept
+  void EvalRotationKeyGen(PhantomSecretKey& sk, const PhantomContext& cc, const std::vector<int32_t>& indices);
   // EvalBootstrap (bootstrap.cu:843-1129); the input needs at least two limbs.  numSlots: the
   // setup to use (0: N/2).  numIterations > 1: iterative bootstrapping (bootstrap.cu:856-900):
   // bootstrap, scale the residual error up by 2^precision, bootstrap it and subtract.
@@ -107,6 +110,57 @@ class FHECKKSRNS {
   void ApplyDoubleAngleIterations(PhantomCiphertext& ct, const PhantomContext& cc, uint32_t numIter) const;
   // ModRaise input preparation (AdjustCiphertext, bootstrap.cu:1131-1155) + RaiseMod
   PhantomCiphertext RaiseWithCorrection(const PhantomCiphertext& ct, const PhantomContext& cc) const;
+
+  // ---- the reference's rotation-index / precompute / evaluate surface (include/bootstrap.cuh:116-175)
+  // Find*RotationIndices (bootstrap.cu:610-820): the slot rotations whose keys the transforms of
+  // a setup read (M = 2N), sorted, without 0 and M/4.  They describe this engine's level structure
+  // (baby steps j stride, giant steps g i stride per level, plus the sparse partial sums / fold).
+  std::vector<int32_t> FindBootstrapRotationIndices(uint32_t slots, uint32_t M) const;
+  std::vector<int32_t> FindCoeffsToSlotsRotationIndices(uint32_t slots, uint32_t M) const;
+  std::vector<int32_t> FindSlotsToCoeffsRotationIndices(uint32_t slots, uint32_t M) const;
+  // a dense slots x slots linear transform evaluated by baby steps g = dim (0: the smallest power of
+  // two with g^2 >= slots) and giant steps g i: rotations 1 .. g-1 and g, 2g, ..
+  std::vector<int32_t> FindLinearTransformRotationIndices(uint32_t slots, uint32_t M, uint32_t dim = 0) const;
+  // EvalLinearTransformPrecompute (include/bootstrap.cuh:128-131; declared but never defined in the
+  // reference): the diagonals of A (times scale), pre-rotated for the baby-step giant-step
+  // evaluation, encoded in the extended basis Ql u P at chain 1 + L (L = limbs dropped)
+  std::vector<std::shared_ptr<PhantomPlaintext>> EvalLinearTransformPrecompute(
+      const PhantomContext& cc, const std::vector<std::vector<std::complex<double>>>& A, double scale = 1,
+      uint32_t L = 0) const;
+  // the two-matrix (sparse) form: declared by the reference without a definition either; throws
+  std::vector<std::shared_ptr<PhantomPlaintext>> EvalLinearTransformPrecompute(
+      const PhantomContext& cc, const std::vector<std::vector<std::complex<double>>>& A,
+      const std::vector<std::vector<std::complex<double>>>& B, uint32_t orientation = 0, double scale = 1,
+      uint32_t L = 0) const;
+  // A(ct) for the plaintexts of EvalLinearTransformPrecompute (the reference's EvalLinearTransform,
+  // commented out in include/bootstrap.cuh:152): one hoisted modup, g rotations, b giant steps
+  PhantomCiphertext EvalLinearTransform(const std::vector<std::shared_ptr<PhantomPlaintext>>& A,
+                                        const PhantomCiphertext& ct, const PhantomContext& cc) const;
+  // EvalCoeffsToSlotsPrecompute / EvalSlotsToCoeffsPrecompute (bootstrap.cu:183-560): the level
+  // plaintexts of the homomorphic encoding / decoding of the setup for rotGroup.size() slots, with
+  // `scale` (times i when flag_i) folded in, at the levels L selects (the reference's lEnc / lDec:
+  // chain 1 + size_Q - L - levelBudget; 0 = chain 1).  A must be the 2N-th roots of unity
+  // (ksiPows, A[j] = exp(2 pi i j / 2N)) and rotGroup the powers 5^j mod 2N: this engine factors the
+  // same canonical embedding into its own slot-domain butterfly stages, so the
+  // plaintext sets are that factorisation's [level][diagonal], not the reference's collapsed-FFT
+  // coefficients.  Requires EvalBootstrapSetup for that slot count.
+  std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>> EvalCoeffsToSlotsPrecompute(
+      const PhantomContext& cc, const std::vector<std::complex<double>>& A, const std::vector<uint32_t>& rotGroup,
+      const std::vector<double>& sf, bool flag_i, double scale = 1, uint32_t L = 0) const;
+  std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>> EvalSlotsToCoeffsPrecompute(
+      const PhantomContext& cc, const std::vector<std::complex<double>>& A, const std::vector<uint32_t>& rotGroup,
+      const std::vector<double>& sf, bool flag_i, double scale = 1, uint32_t L = 0) const;
+  // EvalCoeffsToSlots / EvalSlotsToCoeffs with those plaintext sets (bootstrap.cu:1157-1655)
+  PhantomCiphertext EvalCoeffsToSlots(const std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>>& A,
+                                      const PhantomCiphertext& ctxt, const PhantomContext& cc,
+                                      uint32_t numSlots = 0) const;
+  PhantomCiphertext EvalSlotsToCoeffs(const std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>>& A,
+                                      const PhantomCiphertext& ctxt, const PhantomContext& cc,
+                                      uint32_t numSlots = 0) const;
+  // GetMultKey / GetGaloisKey (include/bootstrap.cuh:169-175): the relinearization key and the
+  // fused rotation keys the bootstrap uses
+  const PhantomRelinKey& GetMultKey() const { return mul_key_; }
+  const PhantomGaloisKey& GetGaloisKey() const { return galois_keys_; }
 
   // GetBootstrapDepth (bootstrap.cu:595-604): the reference's level budget, levelBudget[0] +
   // levelBudget[1] + GetMultiplicativeDepthByCoeffVector(88) (8, util.cu:44-58) + R (6) = 18 for
@@ -155,6 +209,7 @@ class FHECKKSRNS {
     double constant = 1.0;
     size_t first_chain = 1;
     uint32_t dim1 = 0;
+    bool times_i = false;  // the constant is i * constant (EvalCoeffsToSlotsPrecompute's flag_i)
   };
   struct Precom {
     uint32_t slots = 0;
@@ -169,6 +224,21 @@ class FHECKKSRNS {
                     std::vector<LTLevel>& out, bool encode) const;
   const Precom& precom(uint32_t numSlots, const PhantomContext& cc) const;
   PhantomCiphertext apply_level(const PhantomContext& cc, const PhantomCiphertext& ct, const LTLevel& lv) const;
+  // the reference-signature precompute / evaluate pair (above): one direction's levels built from
+  // a caller's roots, and the level structure re-attached to a caller's plaintext set
+  std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>> precompute_dir(
+      const PhantomContext& cc, bool encode_dir, const std::vector<std::complex<double>>& A,
+      const std::vector<uint32_t>& rotGroup, bool flag_i, double scale, uint32_t L) const;
+  PhantomCiphertext apply_dir(const std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>>& A,
+                              const PhantomCiphertext& ct, const PhantomContext& cc, uint32_t numSlots,
+                              bool encode_dir) const;
+  void attach(const PhantomContext& cc, LTLevel& lv, const std::vector<std::shared_ptr<PhantomPlaintext>>& pts) const;
+  // the baby-step giant-step shape of a level from its diagonal map (n ring slots, offsets multiples
+  // of `stride`; dim1 = 0: g^2 >= 2 D)
+  static void lt_shape(LTLevel& lv, const boot::DiagMap& T, size_t n, uint32_t dim1, int stride);
+  // encode a level's diagonals (pre-rotated by -g i stride) in the extended basis at lv.chain
+  void encode_level(const PhantomContext& cc, LTLevel& lv, const boot::DiagMap& T) const;
+  std::vector<int32_t> dir_rotations(uint32_t slots, uint32_t M, bool encode_dir) const;
   PhantomCiphertext eval_mod(const PhantomCiphertext& ct, const PhantomContext& cc) const;
   // the series / double angle / EvalMod on several ciphertexts in lockstep (one level and scale):
   // their products share batched key switches (the real and imaginary halves of EvalMod)

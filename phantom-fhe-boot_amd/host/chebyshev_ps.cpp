@@ -138,6 +138,26 @@ Division LongDivisionChebyshev(const std::vector<double>& f, const std::vector<d
   return {q, r};
 }
 
+// power-basis long division f = q g + r (src/util.cu:93-138)
+Division LongDivisionPoly(const std::vector<double>& f, const std::vector<double>& g) {
+  uint32_t n = Degree(f);
+  const uint32_t k = Degree(g);
+  if (n != f.size() - 1) throw std::invalid_argument("LongDivisionPoly: The dominant coefficient of the divident is zero.");
+  if (k != g.size() - 1) throw std::invalid_argument("LongDivisionPoly: The dominant coefficient of the divisor is zero.");
+  if (n < k) return {std::vector<double>(1, 0.0), f};
+  std::vector<double> q(n - k + 1, 0.0), r(f);
+  while (n >= k) {
+    const uint32_t s = n - k;
+    q[s] = r.back();
+    if (not_one(g[k])) q[s] /= g.back();
+    for (uint32_t i = 0; i <= k; ++i) r[s + i] -= g[i] * q[s];  // r -= q_s x^s g
+    if (r.size() == 1) break;  // (a constant remainder: the reference would loop on it forever)
+    n = Degree(r);
+    r.resize(n + 1);
+  }
+  return {q, r};
+}
+
 }  // namespace ps
 
 // ---- EvalLinearWSumMutable (src/evaluate.cu:3537-3583) --------------------------------------
@@ -161,6 +181,14 @@ PhantomCiphertext EvalLinearWSumMutable(const PhantomContext& ctx, std::vector<P
     EvalAddAutoInplace(ctx, sum, t, sf, sfBig);
   }
   return sum;
+}
+
+PhantomCiphertext EvalLinearWSumMutable(const PhantomContext& ctx, std::vector<std::shared_ptr<PhantomCiphertext>>& cts,
+                                        const std::vector<double>& w, const std::vector<double>& sf,
+                                        const std::vector<double>& sfBig) {
+  std::vector<PhantomCiphertext*> p(cts.size());
+  for (size_t i = 0; i < cts.size(); ++i) p[i] = cts[i].get();
+  return EvalLinearWSumMutable(ctx, p, w, sf, sfBig);
 }
 
 namespace {

@@ -768,6 +768,29 @@ PhantomCiphertext KeySwitchDown(const PhantomContext& ctx, PhantomCiphertext& ex
   return out;
 }
 
+PhantomCiphertext KeySwitchDown(const PhantomContext& ctx, const PhantomCiphertext& ext) {
+  PhantomCiphertext t = ext;  // the moddown uses its input's P limbs as scratch
+  return KeySwitchDown(ctx, t);
+}
+
+PhantomCiphertext KeySwitchDownFirstElement(const PhantomContext& ctx, const PhantomCiphertext& ext) {
+  const RnsTool& rt = ctx.get_context_data(ext.chain_index()).gpu_rns_tool();
+  const size_t n = ctx.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + ctx.size_P();
+  if (ext.coeff_modulus_size() != QlP) throw std::invalid_argument("not an extended-basis ciphertext");
+  hipStream_t s = ctx.stream();
+  // moddown_from_NTT of the first polynomial alone (src/evaluate.cu:2875-2892), from a copy of it
+  // (the moddown uses its input's P limbs as scratch; the argument stays intact)
+  DeviceBuffer<uint64_t> c0(QlP * n, s);
+  PHX_CHECK(hipMemcpyAsync(c0.get(), ext.data(), QlP * n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+  PhantomCiphertext out;
+  out.resize(ctx, ext.chain_index(), 1, s, false);
+  rt.moddown_add(out.data(), c0.get(), false, ctx.gpu_rns_tables(), s, 1);
+  out.set_scale(ext.scale());
+  out.SetNoiseScaleDeg(ext.GetNoiseScaleDeg());
+  out.set_ntt_form(true);
+  return out;
+}
+
 // one launch over both polynomials of an extended-basis ciphertext (moduli Ql u P)
 static void ext_binary(const PhantomContext& ctx, size_t chain, uint64_t* a, const uint64_t* b, size_t b_stride,
                        size_t polys, bool mul) {

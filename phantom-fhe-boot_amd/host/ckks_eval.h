@@ -13,6 +13,7 @@
 #include <complex>
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <vector>
 
 #include "ciphertext.h"
@@ -156,9 +157,25 @@ PhantomCiphertext KeySwitchExt(const PhantomContext& ctx, const PhantomCiphertex
 // KeySwitchDown: extended -> Ql (moddown of both polynomials); `ext` is consumed (its P limbs
 // are clobbered)
 PhantomCiphertext KeySwitchDown(const PhantomContext& ctx, PhantomCiphertext& ext);
+// the reference's const form (include/evaluate.cuh:347): the argument is copied first
+PhantomCiphertext KeySwitchDown(const PhantomContext& ctx, const PhantomCiphertext& ext);
+// KeySwitchDownFirstElement (include/evaluate.cuh:349, src/evaluate.cu:2875-2892): the moddown of
+// the extended-basis ciphertext's first polynomial alone, a one-polynomial ciphertext over Ql
+PhantomCiphertext KeySwitchDownFirstElement(const PhantomContext& ctx, const PhantomCiphertext& ext);
 // EvalMultExtInPlace / EvalAddExtInPlace over Ql u P
 void EvalMultExtInPlace(const PhantomContext& ctx, PhantomCiphertext& ext, const PhantomPlaintext& pt_ext);
 void EvalAddExtInPlace(const PhantomContext& ctx, PhantomCiphertext& a, const PhantomCiphertext& b);
+// the value forms (include/evaluate.cuh:458-475)
+inline PhantomCiphertext EvalMultExt(const PhantomContext& ctx, const PhantomCiphertext& ext, const PhantomPlaintext& pt) {
+  PhantomCiphertext d = ext;
+  EvalMultExtInPlace(ctx, d, pt);
+  return d;
+}
+inline PhantomCiphertext EvalAddExt(const PhantomContext& ctx, const PhantomCiphertext& a, const PhantomCiphertext& b) {
+  PhantomCiphertext d = a;
+  EvalAddExtInPlace(ctx, d, b);
+  return d;
+}
 // rotation / conjugation through the hoisted path (one key switch)
 PhantomCiphertext EvalRotateFused(const PhantomContext& ctx, const PhantomCiphertext& ct,
                                   const PhantomGaloisKey& fused_keys, int index);
@@ -269,6 +286,10 @@ bool ChebyshevUnitInterval(double a, double b);
 PhantomCiphertext EvalLinearWSumMutable(const PhantomContext& ctx, std::vector<PhantomCiphertext*>& cts,
                                         const std::vector<double>& w, const std::vector<double>& sf,
                                         const std::vector<double>& sfBig);
+// the reference's argument type (shared pointers, adjusted in place the same way)
+PhantomCiphertext EvalLinearWSumMutable(const PhantomContext& ctx, std::vector<std::shared_ptr<PhantomCiphertext>>& cts,
+                                        const std::vector<double>& w, const std::vector<double>& sf,
+                                        const std::vector<double>& sfBig);
 // the Paterson-Stockmeyer host helpers of src/util.cu:15-312
 namespace ps {
 struct Division {
@@ -279,6 +300,7 @@ uint32_t GetDepthByDegree(size_t degree);        // degrees 5 .. 2031
 uint32_t GetMultiplicativeDepthByCoeffVector(const std::vector<double>& vec, bool isNormalized);
 std::vector<uint32_t> ComputeDegreesPS(uint32_t n);  // {k, m}
 Division LongDivisionChebyshev(const std::vector<double>& f, const std::vector<double>& g);
+Division LongDivisionPoly(const std::vector<double>& f, const std::vector<double>& g);  // power basis
 }  // namespace ps
 // EvalChebyshevFunction (include/evaluate.cuh:381-388)
 inline PhantomCiphertext EvalChebyshevFunction(const std::function<double(double)>& func, const PhantomContext& ctx,

@@ -48,12 +48,17 @@ void PhantomKSwitchKey::load(const PhantomContext& ctx, std::istream& is) {
 }
 
 void PhantomGaloisKey::save(const PhantomContext& ctx, std::ostream& os) const {
-  // the reference's layout: keys in the order of the context's Galois element list, no elements
+  // the reference's layout: keys in the order of the context's Galois element list, no elements.
+  // Exactly that key set: a missing key or an extra one (which this layout cannot name) throws.
   const std::vector<uint32_t> elts = ctx.key_galois_elts();
   for (uint32_t e : elts)
     if (!has(e))
       throw std::invalid_argument("PhantomGaloisKey lacks the key of Galois element " + std::to_string(e) +
                                   " of the context's list (save_with_elements writes any key set)");
+  for (const auto& kv : keys_)
+    if (std::find(elts.begin(), elts.end(), kv.first) == elts.end())
+      throw std::invalid_argument("PhantomGaloisKey holds the key of Galois element " + std::to_string(kv.first) +
+                                  ", outside the context's list, which save() cannot name (use save_with_elements)");
   ser::write_u64(os, elts.size());
   for (uint32_t e : elts) keys_.at(e).save(ctx, os);
 }
@@ -63,8 +68,28 @@ void PhantomGaloisKey::load(const PhantomContext& ctx, std::istream& is) {
   const uint64_t count = ser::read_u64(is);
   if (count != elts.size())
     throw std::invalid_argument("Galois key count does not match the context's Galois element list");
+  std::vector<PhantomKSwitchKey> read(count);
+  for (auto& k : read) k.load(ctx, is);
+  // Files of this engine's earlier builds (round 3 and before) wrote the keys in ascending element
+  // order followed by that element list (the save_with_elements layout).  Their trailing list is
+  // the context's element set, sorted: bind by it and consume it, instead of binding the keys to
+  // the context order (which would attach them to the wrong elements).
+  std::vector<uint32_t> bind = elts;
+  const std::istream::pos_type pos = is.tellg();
+  if (pos != std::istream::pos_type(-1)) {
+    std::vector<uint32_t> trail(count);
+    is.read(reinterpret_cast<char*>(trail.data()), static_cast<std::streamsize>(count * sizeof(uint32_t)));
+    std::vector<uint32_t> sorted = elts;
+    std::sort(sorted.begin(), sorted.end());
+    if (is && trail == sorted && sorted != elts) {
+      bind = trail;  // the legacy layout
+    } else {
+      is.clear();
+      is.seekg(pos);  // the reference layout: what follows belongs to the next reader
+    }
+  }
   std::map<uint32_t, PhantomKSwitchKey> keys;
-  for (uint32_t e : elts) keys[e].load(ctx, is);
+  for (size_t i = 0; i < read.size(); ++i) keys[bind[i]] = std::move(read[i]);
   keys_ = std::move(keys);
 }
 

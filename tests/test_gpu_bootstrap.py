@@ -75,6 +75,23 @@ def test_flexibleauto_surface():
     assert used[30] == 7, used  # GetDepthByDegree(30) = 7 on [1, 5] (src/util.cu:44-58)
 
 
+def test_reference_precompute_evaluate_api():
+    """The reference-signature FHECKKSRNS surface (include/bootstrap.cuh:116-175) at N = 2^12:
+    FindBootstrapRotationIndices equals the keys the setup generates; EvalCoeffsToSlotsPrecompute /
+    EvalSlotsToCoeffsPrecompute from ksiPows + rotGroup (bootstrap.cu:92-107) with lEnc / lDec, then
+    EvalCoeffsToSlots(A, ...) / EvalSlotsToCoeffs(A, ...) round-trip the message (and CoeffToSlot's
+    slots carry its energy, Parseval); GetMultKey / GetGaloisKey; a dense 2048 x 2048
+    EvalLinearTransformPrecompute + EvalLinearTransform against the host product; the evaluator's
+    KeySwitchDownFirstElement (== c0 of KeySwitchDown, bit for bit), EvalAddExt and EvalMultExt."""
+    rc, lines, err = _run("refapi", "12")
+    checks = {l["check"]: l for l in lines if "check" in l}
+    assert rc == 0, (lines, err)
+    for name in ["refapi_rotation_indices", "refapi_get_keys", "refapi_cts_stc_roundtrip", "refapi_cts_parseval",
+                 "refapi_add_ext_keyswitch_down", "refapi_keyswitch_down_first_element", "refapi_mult_ext",
+                 "refapi_linear_transform"]:
+        assert checks[name]["ok"], checks[name]
+
+
 def test_bootstrapping_example_verbatim():
     """bootstrapping_example.cu:69-198 compiled unchanged (cudaSetDevice -> hipSetDevice):
     OS-entropy keys, public-key encryption, the bare 25 x EvalMultConstInplace(x, 1) drain and
