@@ -471,7 +471,11 @@ static void example_ckks_galois_key_layout() {
     }
   }
   PhantomGaloisKey loaded;
-  loaded.load(context, ss);
+  try {
+    loaded.load(context, ss);
+  } catch (const std::exception& e) {
+    throw std::logic_error(std::string("reference-layout reload: ") + e.what());
+  }
   std::vector<cplx> x = random_msg(encoder.slot_count()), out;
   PhantomPlaintext p;
   encoder.encode(context, x, std::pow(2.0, 40), p);
@@ -510,7 +514,11 @@ static void example_ckks_galois_key_layout() {
     const uint64_t marker = 0x5EEDC0DEull;
     legacy.write(reinterpret_cast<const char*>(&marker), sizeof(marker));
     PhantomGaloisKey l2;
-    l2.load(context, legacy);
+    try {
+      l2.load(context, legacy);
+    } catch (const std::exception& e) {
+      throw std::logic_error(std::string("legacy reload: ") + e.what());
+    }
     uint64_t after = 0;
     legacy.read(reinterpret_cast<char*>(&after), sizeof(after));
     require(legacy && after == marker, "legacy Galois key stream consumed exactly");
@@ -525,7 +533,11 @@ static void example_ckks_galois_key_layout() {
     gk.save(context, ref);
     ref.write(reinterpret_cast<const char*>(&marker), sizeof(marker));
     PhantomGaloisKey l3;
-    l3.load(context, ref);
+    try {
+      l3.load(context, ref);
+    } catch (const std::exception& e) {
+      throw std::logic_error(std::string("reference reload with trailing data: ") + e.what());
+    }
     after = 0;
     ref.read(reinterpret_cast<char*>(&after), sizeof(after));
     require(ref && after == marker, "reference Galois key stream leaves the following data");

@@ -65,29 +65,37 @@ void PhantomGaloisKey::save(const PhantomContext& ctx, std::ostream& os) const {
 
 void PhantomGaloisKey::load(const PhantomContext& ctx, std::istream& is) {
   const std::vector<uint32_t> elts = ctx.key_galois_elts();
+  // Files of this engine's earlier builds (round 3 and before) wrote the keys in ascending element
+  // order followed by that element list (the save_with_elements layout): one key per distinct
+  // element (the default list repeats 5^(N/2) = 5^(-N/2)).  Their trailing list is the context's
+  // distinct elements, sorted: bind by it and consume it, instead of binding the keys to the
+  // context order (which would attach them to the wrong elements).
+  std::vector<uint32_t> distinct = elts;
+  std::sort(distinct.begin(), distinct.end());
+  distinct.erase(std::unique(distinct.begin(), distinct.end()), distinct.end());
   const uint64_t count = ser::read_u64(is);
-  if (count != elts.size())
-    throw std::invalid_argument("Galois key count does not match the context's Galois element list");
+  if (count != elts.size() && count != distinct.size())
+    throw std::invalid_argument("Galois key count " + std::to_string(count) +
+                                " does not match the context's Galois element list (" + std::to_string(elts.size()) + ")");
   std::vector<PhantomKSwitchKey> read(count);
   for (auto& k : read) k.load(ctx, is);
-  // Files of this engine's earlier builds (round 3 and before) wrote the keys in ascending element
-  // order followed by that element list (the save_with_elements layout).  Their trailing list is
-  // the context's element set, sorted: bind by it and consume it, instead of binding the keys to
-  // the context order (which would attach them to the wrong elements).
   std::vector<uint32_t> bind = elts;
+  bool legacy = false;
   const std::istream::pos_type pos = is.tellg();
-  if (pos != std::istream::pos_type(-1)) {
+  if (pos != std::istream::pos_type(-1) && count == distinct.size()) {
     std::vector<uint32_t> trail(count);
     is.read(reinterpret_cast<char*>(trail.data()), static_cast<std::streamsize>(count * sizeof(uint32_t)));
-    std::vector<uint32_t> sorted = elts;
-    std::sort(sorted.begin(), sorted.end());
-    if (is && trail == sorted && sorted != elts) {
-      bind = trail;  // the legacy layout
+    legacy = is && trail == distinct && (count != elts.size() || distinct != elts);
+    if (legacy) {
+      bind = trail;
     } else {
       is.clear();
       is.seekg(pos);  // the reference layout: what follows belongs to the next reader
     }
   }
+  if (!legacy && count != elts.size())
+    throw std::invalid_argument("Galois key count " + std::to_string(count) +
+                                " does not match the context's Galois element list (" + std::to_string(elts.size()) + ")");
   std::map<uint32_t, PhantomKSwitchKey> keys;
   for (size_t i = 0; i < read.size(); ++i) keys[bind[i]] = std::move(read[i]);
   keys_ = std::move(keys);
