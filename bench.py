@@ -132,39 +132,115 @@ def c3_leg(PA, lib, torch, steps=20, warmup=3):
     }
 
 
-def c4_reference_bytes():
-    """Algorithmic bytes of one C4 bootstrap under the REFERENCE's schedule (engine-independent:
-    the denominator does not move when this engine issues more or fewer key switches).  Chain c of
-    Q = {60, 29 x 59} holds Ql = 31 - c limbs; P = 10; a key switch reads dnum = ceil(Ql / 10)
-    digits x 2 x (Ql + 10) limbs of key; a diagonal plaintext is Ql + 10 limbs (encode_ext).
-      * linear transforms (bootstrap.cu:1157-1655; SelectLayers(15, 2) = {8, 1, 7},
-        GetCollapsedFFTParams, util.cu:733-816): the 8-layer level has 511 diagonals, g 64 / b 8,
-        i.e. 63 baby + 7 giant rotations; the remainder level 255 diagonals, g 32 / b 8, 31 + 7.
-        CoeffToSlot runs at chains 2 (8 layers) and 3 (remainder), SlotToCoeff at 17 and 18
-        (raise + const-mult at chain 1 -> 2, output chain 19 = 1 + GetBootstrapDepth {2, 2});
-      * EvalMod: the conjugation (1 key switch, chain 4); two Chebyshev series of degree 88 by
-        Paterson-Stockmeyer, ComputeDegreesPS(88) = (k 6, m 4), k + 2m + 2^(m-1) - 4 = 18
-        multiplications each (util.cu:260-296), priced at the series' middle level (chain 7);
-        6 double-angle squarings per half at chains 11..16;
-      * ciphertext I/O: the input at chain 26 read, the output at chain 19 written.
-    Returns (total, {"keys", "plaintexts", "ciphertexts"})."""
+# ---- the reference's bootstrap schedule, from its own parameter functions (util.cu) ------------
+def select_layers(log_slots, budget):
+    """SelectLayers (src/util.cu:733-763): {layers, rows, rem}."""
+    import math
+    layers = math.ceil(log_slots / budget)
+    rows, rem = log_slots // layers, log_slots % layers
+    dim = rows + (1 if rem else 0)
+    if dim < budget:
+        layers -= 1
+        rows = log_slots // layers
+        rem = log_slots - rows * layers
+        dim = rows + (1 if rem else 0)
+        while dim != budget:
+            rows -= 1
+            rem = log_slots - rows * layers
+            dim = rows + (1 if rem else 0)
+    return layers, rows, rem
+
+
+def collapsed_fft_params(slots, budget):
+    """GetCollapsedFFTParams (src/util.cu:765-816) with dim1 = 0: (layers, rem, rotations, b, g,
+    rotations_rem, b_rem, g_rem); g baby steps, b giant steps per level."""
+    log_slots = max(1, slots.bit_length() - 1)
+    layers, _, rem = select_layers(log_slots, budget)
+    rot = (1 << (layers + 1)) - 1
+    rot_rem = (1 << (rem + 1)) - 1
+    g = 1 << (layers // 2 + (2 if rot > 7 else 1))
+    b = (rot + 1) // g
+    g_rem = b_rem = 0
+    if rem:
+        g_rem = 1 << (rem // 2 + (2 if rot_rem > 7 else 1))
+        b_rem = (rot_rem + 1) // g_rem
+    return layers, rem, rot, b, g, rot_rem, b_rem, g_rem
+
+
+def depth_by_degree(d):
+    """GetDepthByDegree (src/util.cu:44-71)."""
+    for hi, depth in ((4, 3), (5, 4), (13, 5), (27, 6), (59, 7), (119, 8), (247, 9), (495, 10), (1007, 11), (2031, 12)):
+        if d <= hi:
+            return depth
+    raise ValueError(d)
+
+
+def compute_degrees_ps(n):
+    """ComputeDegreesPS (src/util.cu:260-296) for n <= 2204: (k, m)."""
+    for hi, m in ((2, 1), (11, 2), (13, 3), (17, 2), (55, 3), (59, 4), (76, 3), (239, 4), (247, 5), (284, 4),
+                  (991, 5), (1007, 6), (1083, 5), (2015, 6), (2031, 7), (2204, 6)):
+        if n <= hi:
+            return n // ((1 << m) - 1) + 1, m
+    raise ValueError(n)
+
+
+def c4_reference_bytes(N=N, size_Q=30, size_P=10, level_budget=(2, 2), degree=88, r_double=6, input_chain=26):
+    """Algorithmic bytes of one bootstrap under the REFERENCE's schedule (engine-independent: the
+    denominator does not move when this engine issues more or fewer key switches), derived from the
+    reference's own parameter functions (ported above) for the given parameters; the defaults are
+    config C4 (bootstrapping_example.cu:69-116: N 2^16, Q = {60, 29 x 59}, P = 10 x 60, budget {2, 2},
+    EvalMod degree 88, R = 6; input at chain 26 after the example's 25 EvalMultConst drains).
+    Chain c holds Ql = size_Q + 1 - c limbs; a key switch reads dnum = ceil(Ql / size_P) digits x 2 x
+    (Ql + size_P) limbs of key; a diagonal plaintext is Ql + size_P limbs (encode_ext).
+      * linear transforms (bootstrap.cu:1157-1655): per direction, the full levels (2^(layers+1) - 1
+        diagonals, g - 1 baby + b - 1 giant rotations) then the remainder level (bootstrap.cu:240-330,
+        470-540); CoeffToSlot from chain 2 (lEnc = L0 - budget - 1), SlotToCoeff from chain
+        1 + depthBT - budget (lDec = L0 - depthBT);
+      * EvalMod: the conjugation at CoeffToSlot's output chain; two Chebyshev series by
+        Paterson-Stockmeyer, k + 2m + 2^(m-1) - 4 products each (ComputeDegreesPS), priced at the
+        series' middle level; R double-angle squarings per half after it;
+      * ciphertext I/O: the input read at `input_chain`, the output written at 1 + depthBT.
+    Returns (total, {"keys", "plaintexts", "ciphertexts"}, derivation)."""
     import math
     word = 8 * N
+    slots = N // 2
 
     def ql(c):
-        return 31 - c
+        return size_Q + 1 - c
 
     def key(c):
-        return math.ceil(ql(c) / 10) * 2 * (ql(c) + 10) * word
+        return math.ceil(ql(c) / size_P) * 2 * (ql(c) + size_P) * word
 
     def pt(c):
-        return (ql(c) + 10) * word
+        return (ql(c) + size_P) * word
 
-    keys = (70 * key(2) + 38 * key(3) + 70 * key(17) + 38 * key(18) + key(4) + 2 * 18 * key(7)
-            + 2 * sum(key(c) for c in range(11, 17)))
-    pts = 511 * pt(2) + 255 * pt(3) + 511 * pt(17) + 255 * pt(18)
-    cts = 2 * ql(26) * word + 2 * ql(19) * word
-    return keys + pts + cts, {"keys": keys, "plaintexts": pts, "ciphertexts": cts}
+    depth_mod = depth_by_degree(degree) + r_double
+    depth_bt = depth_mod + level_budget[0] + level_budget[1]
+    keys = pts = 0
+    levels = []
+    for direction, budget, first in (("cts", level_budget[0], 2), ("stc", level_budget[1], 1 + depth_bt - level_budget[1])):
+        layers, rem, rot, b, g, rot_rem, b_rem, g_rem = collapsed_fft_params(slots, budget)
+        full = budget - (1 if rem else 0)
+        shapes = [(rot, g, b)] * full + ([(rot_rem, g_rem, b_rem)] if rem else [])  # remainder level last
+        for i, (diags, gg, bb) in enumerate(shapes):
+            c = first + i
+            keys += (gg - 1 + bb - 1) * key(c)
+            pts += diags * pt(c)
+            levels.append({"dir": direction, "chain": c, "diagonals": diags, "g": gg, "b": bb})
+    k, m = compute_degrees_ps(degree)
+    mults = k + 2 * m + (1 << (m - 1)) - 4
+    conj_chain = 2 + level_budget[0]
+    # the series consumes chains conj .. conj + depth - 1: priced at their middle, rounded down
+    ps_mid = conj_chain + (depth_by_degree(degree) + 1) // 2 - 1
+    keys += key(conj_chain) + 2 * mults * key(ps_mid)
+    da_first = conj_chain + depth_by_degree(degree) - 1
+    keys += 2 * sum(key(c) for c in range(da_first, da_first + r_double))
+    out_chain = 1 + depth_bt
+    cts = 2 * ql(input_chain) * word + 2 * ql(out_chain) * word
+    deriv = {"levels": levels, "ps_k_m": [k, m], "ps_products_per_half": mults, "depth_bt": depth_bt,
+             "output_chain": out_chain, "conj_chain": conj_chain, "ps_mid_chain": ps_mid,
+             "double_angle_chains": [da_first, da_first + r_double - 1]}
+    return keys + pts + cts, {"keys": keys, "plaintexts": pts, "ciphertexts": cts}, deriv
 
 
 def c4_leg(iters=3, timeout=240):
@@ -190,15 +266,24 @@ def c4_leg(iters=3, timeout=240):
     }
     # roofline: the reference schedule's bytes (c4_reference_bytes) over the latency; the bytes
     # this engine's own kernels stream (host/traffic.h counters) are reported beside it
-    total, parts = c4_reference_bytes()
+    total, parts, deriv = c4_reference_bytes()
+    # the derivation must describe the run it prices: the example's output chain and level count
+    if deriv["output_chain"] != b.get("chain_out") or b.get("levels_after") != 30 - deriv["output_chain"]:
+        return {**res, "error": f"reference schedule (output chain {deriv['output_chain']}) does not match the run {b}"}
     achieved = total / (b["ms_median"] * 1e-3) / 1e9
     res["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes": total, "bytes": parts,
                        "source": "bench.c4_reference_bytes: key + diagonal bytes of the reference's own schedule "
-                                 "(216 linear-transform rotations, 49 EvalMod key switches) + ciphertext I/O"}
+                                 "(SelectLayers / GetCollapsedFFTParams / ComputeDegreesPS ported) + ciphertext I/O",
+                       "derivation": deriv}
     ab = b.get("alg_bytes")
     if ab:
-        res["engine_streamed_bytes"] = {**ab, "total": ab["keys"] + ab["plaintexts"] + ab["ciphertexts"]}
+        eng = ab["keys"] + ab["plaintexts"] + ab["ciphertexts"]
+        res["engine_streamed_bytes"] = {**ab, "total": eng}
+        # the same latency over the bytes this engine's kernels stream (host/traffic.h counters)
+        e_ach = eng / (b["ms_median"] * 1e-3) / 1e9
+        res["roofline_engine_bytes"] = {"bound": "hbm", "achieved": round(e_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                        "frac": round(e_ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": eng}
     return res
 
 
