@@ -162,6 +162,18 @@ int phantom_keyswitch_inner_prod(const phantom_context *ctx, size_t chain_index,
  * before returning (a test / one-off entry; the drivers keep converters per level). */
 int phantom_fast_bconv(const uint64_t *ibase, size_t ibase_size, const uint64_t *obase, size_t obase_size,
                        const uint64_t *src, uint64_t *dst, size_t n, int prescale, hipStream_t stream);
+/* A converter kept across calls, as the reference's DBaseConverter object (include/rns_bconv.cuh
+ * DBaseConverter; init at src/rns_bconv.cu:10-38): phantom_bconv_create builds the tables once
+ * (the matrix-core fragments included) from host moduli and synchronizes `stream`;
+ * phantom_bconv_run is bConv_BEHZ (src/rns_bconv.cu:212-229) with the same meaning as
+ * phantom_fast_bconv, asynchronous on `stream`, no allocation; phantom_bconv_destroy frees the
+ * tables (the caller makes sure no run on them is still in flight). */
+typedef struct phantom_bconv phantom_bconv;
+int phantom_bconv_create(const uint64_t *ibase, size_t ibase_size, const uint64_t *obase, size_t obase_size,
+                         hipStream_t stream, phantom_bconv **out);
+int phantom_bconv_run(const phantom_bconv *conv, const uint64_t *src, uint64_t *dst, size_t n, int prescale,
+                      hipStream_t stream);
+int phantom_bconv_destroy(phantom_bconv *conv);
 /* DRNSTool::moddown_from_NTT (src/rns_bconv.cu:791-843): cx_i [L+P][n] NTT form (P limbs clobbered)
  * -> out [L][n] = (cx_i - NTT(bconv(INTT(cx_i|P)))) * P^-1 */
 int phantom_moddown_from_ntt(const phantom_context *ctx, size_t chain_index, uint64_t *cx_i, uint64_t *out,

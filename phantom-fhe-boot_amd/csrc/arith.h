@@ -169,6 +169,17 @@ __device__ __forceinline__ void gs_bfly4(uint64_t& x, uint64_t& y, uint64_t w, u
   y = mul_shoup_lazy4(d, w, ws, q);
 }
 
+// inverse GS butterfly for q < 2^60 with inputs below 8q: d = x + 8q - y < 16q < 2^64 and
+// x' = x + y < 16q, brought below 8q only when RED (ntt.hip lazy_gs decides per element)
+template <bool RED>
+__device__ __forceinline__ void gs_bfly8(uint64_t& x, uint64_t& y, uint64_t w, uint64_t ws, uint64_t q) {
+  const uint64_t q8 = q << 3;
+  const uint64_t d = x + q8 - y;
+  const uint64_t s = add64(x, y);
+  x = RED ? csub_n(s, q8, opaque(0 - q8)) : s;
+  y = mul_shoup_lazy4(d, w, ws, q);
+}
+
 // [0, 8q) -> [0, q)
 __device__ __forceinline__ uint64_t reduce8(uint64_t v, uint64_t q) {
   v = csub_n(v, q << 2, opaque(0 - (q << 2)));

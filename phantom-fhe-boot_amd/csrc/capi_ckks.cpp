@@ -197,6 +197,39 @@ int phantom_fast_bconv(const uint64_t* ibase, size_t ibase_size, const uint64_t*
   });
 }
 
+struct phantom_bconv {
+  phantom::DeviceBaseConverter conv;
+};
+
+int phantom_bconv_create(const uint64_t* ibase, size_t ibase_size, const uint64_t* obase, size_t obase_size,
+                         hipStream_t stream, phantom_bconv** out) {
+  PHX_CAPI_GUARD({
+    if (!ibase || !obase || !out || ibase_size == 0 || obase_size == 0)
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "bconv_create: empty base");
+    auto h = std::make_unique<phantom_bconv>();
+    h->conv.init(std::vector<uint64_t>(ibase, ibase + ibase_size), std::vector<uint64_t>(obase, obase + obase_size),
+                 stream);
+    PHX_CHECK(hipStreamSynchronize(stream));
+    *out = h.release();
+    return PHANTOM_OK;
+  });
+}
+
+int phantom_bconv_run(const phantom_bconv* conv, const uint64_t* src, uint64_t* dst, size_t n, int prescale,
+                      hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (!conv || !src || !dst || n == 0 || n % 2 != 0)
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "bconv_run: null handle or odd-sized input");
+    const hipError_t e = phx::bconv(conv->conv.args(src, dst, prescale != 0), n, stream);
+    return from_hip(e != hipSuccess ? e : hipGetLastError());
+  });
+}
+
+int phantom_bconv_destroy(phantom_bconv* conv) {
+  delete conv;
+  return PHANTOM_OK;
+}
+
 int phantom_moddown_from_ntt(const phantom_context* ctx, size_t chain_index, uint64_t* cx_i, uint64_t* out,
                              hipStream_t stream) {
   PHX_CAPI_GUARD({

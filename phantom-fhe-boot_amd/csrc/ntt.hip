@@ -141,6 +141,34 @@ constexpr LazySched lazy_ct(int s, int start) {
   return r;
 }
 
+// Integer inverse path for q < 2^60 (arith.h gs_bfly8): every value stays below 8q between
+// stages and rounds.  The bound of each of a thread's E elements is tracked through a round's
+// stages (x' = x + y sums the two bounds, y' = the product < 4q); bit j of m[gl] = reduce x' of
+// element j below 8q at stage gl, needed only when the sum's bound passes 8q.  A full round
+// from inputs < 8q reduces 20 of its 32 sums; the eager form (gs_bfly4) reduced all 32.
+struct LazyGs {
+  uint32_t m[E_LOG];
+};
+constexpr LazyGs lazy_gs(int er, int b_in) {
+  LazyGs r{};
+  int b[E] = {};
+  for (int j = 0; j < E; ++j) b[j] = b_in;
+  for (int gl = er - 1; gl >= 0; --gl) {
+    const int h = 1 << (E_LOG - 1 - gl);
+    for (int j = 0; j < E; ++j) {
+      if (j & h) continue;
+      int sum = b[j] + b[j | h];
+      if (sum > 8) {
+        r.m[gl] |= 1u << j;
+        sum = 8;
+      }
+      b[j] = sum;
+      b[j | h] = 4;
+    }
+  }
+  return r;
+}
+
 template <int S1_LOG, int S2_LOG>
 struct Plan {
   static constexpr LazySched col_lz = lazy_ct(S1_LOG, 1);
@@ -324,6 +352,28 @@ __device__ __forceinline__ void gs_round_int(uint64_t (&v)[E], const uint64_t (&
       if (j & h) continue;
       const int sl = tw_slot<Rd::ex>(gl, tw_key<Rd::ex>(gl, j));
       gs_bfly4(v[j], v[j | h], w[sl], ws[sl], q);
+    }
+  }
+}
+
+// inverse GS round, integer path for q < 2^60: values below 8q (gs_bfly8, lazy_gs); B_IN = the
+// bound of the round's input in units of q
+template <int S_LOG, int R, int B_IN>
+__device__ __forceinline__ void gs_round_int8(uint64_t (&v)[E], const uint64_t (&w)[E], const uint64_t (&ws)[E],
+                                              uint64_t q) {
+  using Rd = Round<S_LOG, R>;
+  constexpr LazyGs lz = lazy_gs(Rd::er, B_IN);
+#pragma unroll
+  for (int gl = Rd::er - 1; gl >= 0; --gl) {
+    const int h = 1 << (E_LOG - 1 - gl);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      if (j & h) continue;
+      const int sl = tw_slot<Rd::ex>(gl, tw_key<Rd::ex>(gl, j));
+      if ((lz.m[gl] >> j) & 1u)
+        gs_bfly8<true>(v[j], v[j | h], w[sl], ws[sl], q);
+      else
+        gs_bfly8<false>(v[j], v[j | h], w[sl], ws[sl], q);
     }
   }
 }
@@ -796,6 +846,8 @@ __device__ __forceinline__ void col_tile(const KArgs& a, int tile, uint64_t* lds
             ct_round_int16<S1_LOG, R, P::col_lz.mask>(v, w, ws, lc.q);
           else if constexpr (FWD)
             ct_round_int<S1_LOG, R>(v, w, ws, lc.q);
+          else if constexpr (LZ)
+            gs_round_int8<S1_LOG, R, 8>(v, w, ws, lc.q);  // the row pass hands over values < 8q
           else
             gs_round_int<S1_LOG, R>(v, w, ws, lc.q);
         });
@@ -1063,10 +1115,13 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
           if constexpr (R < RN - 1) relayout<S2_LOG, R + 1, R>(v, lrow, idx, sync, t);
           uint64_t w[E], ws[E];
           get_tw(std::integral_constant<int, R>{}, w, ws);
-          gs_round_int<S2_LOG, R>(v, w, ws, lc.q);
+          if constexpr (LZ)
+            gs_round_int8<S2_LOG, R, R == RN - 1 ? 4 : 8>(v, w, ws, lc.q);  // input < 4q, as gs_bfly4
+          else
+            gs_round_int<S2_LOG, R>(v, w, ws, lc.q);
         });
 #pragma unroll
-        for (int j = 0; j < E; ++j) store_wt(dst + j * T, v[j]);  // [0, 4q), column pass follows
+        for (int j = 0; j < E; ++j) store_wt(dst + j * T, v[j]);  // [0, 4q) ([0, 8q) LZ), column pass follows
       }
     }
   }
@@ -1268,8 +1323,14 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
     else
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, false, false>), grid_r, block_r, 0, stream, a);
   } else {
-    if (a.epi.ks_beta > 0)
+    // one lazy range for the whole launch, as forward
+    const bool lz = tb.lazy16;
+    if (a.epi.ks_beta > 0 && lz)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false, false, true, true>), grid_r, block_r, 0, stream, a);
+    else if (a.epi.ks_beta > 0)
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false, false, false, true>), grid_r, block_r, 0, stream, a);
+    else if (lz)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false, false, true>), grid_r, block_r, 0, stream, a);
     else
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false>), grid_r, block_r, 0, stream, a);
     a.in = out;
@@ -1277,7 +1338,10 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
     a.map.in_outer = a.map.out_outer;
     a.copy = NttCopy{};  // the row pass made the copy
     a.epi = NttEpilogue{};  // ... and consumed the key-switch prologue
-    hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false>), grid_c, block_c, 0, stream, a);
+    if (lz)
+      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false, false, true>), grid_c, block_c, 0, stream, a);
+    else
+      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false>), grid_c, block_c, 0, stream, a);
   }
   return hipGetLastError();
 }

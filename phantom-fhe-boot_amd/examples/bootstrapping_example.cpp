@@ -7,6 +7,11 @@
 //   boot : full bootstrap of 2^(log_n - 1) uniform reals in [1, 5] (the example's input),
 //          levelBudget {2, 2}, scale 2^59, Q = {60, 29 x 59}, P = 10 x 60
 //   batch: `iterations` independent bootstraps, `lanes` at a time side by side (C5 on one GPU)
+//   tail : `iterations` fresh ciphertexts under one key (4th argument: key seed, 0 = OS entropy),
+//          each bootstrapped; per ciphertext the precision, the raised plaintext's overflow I
+//          (t = m + q0 I, from decrypting RaiseWithCorrection's output mod q0 and q1) and the
+//          output error in the coefficient domain, so a low-precision outlier can be traced to
+//          the coefficients that carry its error
 // Prints one JSON object per check; exit status 0 iff every check meets its bound.
 #include <hip/hip_runtime.h>
 
@@ -106,7 +111,9 @@ int main(int argc, char** argv) {
 
   double t0 = now_ms();
   PhantomContext ctx(parms);
-  PhantomSecretKey sk = PhantomSecretKey::for_testing(ctx, 0x5EED);
+  // "tail" takes the key seed as its 4th argument (0 = fresh OS-entropy key)
+  const uint64_t key_seed = (mode == "tail" && argc > 4) ? std::strtoull(argv[4], nullptr, 0) : 0x5EED;
+  PhantomSecretKey sk = key_seed ? PhantomSecretKey::for_testing(ctx, key_seed) : PhantomSecretKey(ctx);
   PhantomCKKSEncoder enc(ctx);
   const std::vector<double> sf = precompute_scaling_factors(ctx, scale);
   std::printf("{\"stage\": \"context+keys\", \"ms\": %.1f, \"N\": %zu, \"limbs_Q\": %zu, \"limbs_P\": %zu}\n",
@@ -560,6 +567,90 @@ int main(int argc, char** argv) {
               setup_ms, keygen_ms, boot.rotation_indices().size() + 1, FHECKKSRNS::GetBootstrapDepth(levelBudget),
               boot.correction_factor());
   std::fflush(stdout);
+
+  if (mode == "tail") {
+    // decrypt `c` and return its first two limbs in coefficient form (q0, q1 residues)
+    DeviceBuffer<uint64_t> tmp(2 * N, nullptr);
+    auto coeffs2 = [&](const PhantomPlaintext& p) {
+      PHX_CHECK(hipMemcpy(tmp.get(), p.data(), 2 * N * sizeof(uint64_t), hipMemcpyDeviceToDevice));
+      PHX_CHECK(phx::ntt_inverse(ctx.gpu_rns_tables(), tmp.get(), tmp.get(), phx::LimbMap::contiguous(2, 0), nullptr,
+                                 nullptr, nullptr));
+      return tmp.download(nullptr);
+    };
+    const uint64_t q0 = ctx.key_moduli()[0], q1 = ctx.key_moduli()[1];
+    auto centered = [](uint64_t v, uint64_t q) { return v > q / 2 ? (__int128)v - (__int128)q : (__int128)v; };
+    const int K = FHECKKSRNS::K_UNIFORM;
+    __int128 q0inv = 1;  // q0^-1 mod q1 (Fermat)
+    for (__int128 b = q0 % q1, e = q1 - 2; e > 0; e >>= 1, b = b * b % q1)
+      if (e & 1) q0inv = q0inv * b % q1;
+    double worst_bits = 1e9, sum_bits = 0;
+    for (int it = 0; it < std::max(1, iters); ++it) {
+      std::vector<double> xt(slots);
+      for (auto& v : xt) v = dis(rng);
+      PhantomPlaintext pin;
+      enc.encode(ctx, xt, ct.scale(), pin, ct.chain_index());
+      PhantomCiphertext cin;
+      sk.encrypt_symmetric(ctx, pin, cin);
+      // the overflow of the raised plaintext t = c0 + c1 s = t0 + q0 I (|t| << q0 q1 / 2): t0 the
+      // centered residue mod q0, I = (t1 - t0) q0^-1 mod q1, centered (CRT of the first two limbs)
+      PhantomPlaintext praw;
+      sk.decrypt(ctx, boot.RaiseWithCorrection(cin, ctx), praw);
+      const std::vector<uint64_t> r = coeffs2(praw);
+      std::vector<int> I(N);
+      int max_i = 0;
+      size_t arg_i = 0;
+      for (size_t k = 0; k < N; ++k) {
+        const __int128 t0 = centered(r[k], q0);
+        const __int128 d = ((__int128)r[N + k] - t0 % (__int128)q1 + 2 * (__int128)q1) % (__int128)q1;
+        I[k] = static_cast<int>(centered(static_cast<uint64_t>(d * q0inv % (__int128)q1), q1));
+        if (std::abs(I[k]) > max_i) { max_i = std::abs(I[k]); arg_i = k; }
+      }
+      PhantomCiphertext o = boot.EvalBootstrap(cin, ctx);
+      std::vector<std::complex<double>> z = decrypt_decode(ctx, sk, enc, o);
+      std::vector<double> res(slots);
+      for (size_t j = 0; j < slots; ++j) res[j] = z[j].real();
+      const double bits = compute_bit_precision(xt, res);
+      worst_bits = std::min(worst_bits, bits);
+      sum_bits += bits;
+      // output error per coefficient, in units of the output scale
+      PhantomPlaintext pout, pref;
+      sk.decrypt(ctx, o, pout);
+      enc.encode(ctx, xt, o.scale(), pref, o.chain_index());
+      const std::vector<uint64_t> a = coeffs2(pout), b = coeffs2(pref);
+      std::vector<double> e(N);
+      double ss = 0;
+      for (size_t k = 0; k < N; ++k) {
+        const uint64_t d = a[k] >= b[k] ? a[k] - b[k] : a[k] + q0 - b[k];
+        e[k] = static_cast<double>(centered(d, q0)) / o.scale();
+        ss += e[k] * e[k];
+      }
+      std::vector<size_t> idx(N);
+      for (size_t k = 0; k < N; ++k) idx[k] = k;
+      std::partial_sort(idx.begin(), idx.begin() + 4, idx.end(),
+                        [&](size_t u, size_t v) { return std::abs(e[u]) > std::abs(e[v]); });
+      // mean |e| by |I| band (width K / 8)
+      double band_sum[9] = {0}, band_n[9] = {0};
+      for (size_t k = 0; k < N; ++k) {
+        const int bnd = std::min(8, std::abs(I[k]) * 8 / K);
+        band_sum[bnd] += std::abs(e[k]);
+        band_n[bnd] += 1;
+      }
+      std::ostringstream top, bands;
+      for (int t = 0; t < 4; ++t)
+        top << (t ? ", " : "") << "[" << idx[t] << ", " << e[idx[t]] << ", " << I[idx[t]] << "]";
+      for (int bnd = 0; bnd < 9; ++bnd)
+        bands << (bnd ? ", " : "") << (band_n[bnd] ? band_sum[bnd] / band_n[bnd] : 0.0);
+      const double rms = std::sqrt(ss / N);
+      std::printf("{\"tail\": %d, \"avg_bits\": %.3f, \"I0\": %d, \"e0\": %.4e, \"max_abs_I\": %d, \"argmax_I\": %zu, \"err_rms\": %.3e, "
+                  "\"top_err_share\": %.4f, \"top_err\": [%s], \"mean_err_by_I_band\": [%s]}\n",
+                  it, bits, I[0], e[0], max_i, arg_i, rms, e[idx[0]] * e[idx[0]] / ss, top.str().c_str(), bands.str().c_str());
+      std::fflush(stdout);
+    }
+    std::printf("{\"stage\": \"tail\", \"ciphertexts\": %d, \"key_seed\": %llu, \"K\": %d, \"min_avg_bits\": %.3f, "
+                "\"mean_avg_bits\": %.3f}\n",
+                std::max(1, iters), (unsigned long long)key_seed, K, worst_bits, sum_bits / std::max(1, iters));
+    return 0;
+  }
 
   if (mode == "batch") {
     // C5 on one GPU: `iters` independent bootstraps, `lanes` of them side by side

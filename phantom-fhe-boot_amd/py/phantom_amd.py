@@ -47,6 +47,9 @@ _SIGS = {
     "phantom_keyswitch_inner_prod": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, vp, vp]),
     "phantom_moddown_from_ntt": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_fast_bconv": (ctypes.c_int, [u64p, sz, u64p, sz, vp, vp, sz, ctypes.c_int, vp]),
+    "phantom_bconv_create": (ctypes.c_int, [u64p, sz, u64p, sz, vp, ctypes.POINTER(vp)]),
+    "phantom_bconv_run": (ctypes.c_int, [vp, vp, vp, sz, ctypes.c_int, vp]),
+    "phantom_bconv_destroy": (ctypes.c_int, [vp]),
     "phantom_moddown_modup": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_moddown_modup_batch": (ctypes.c_int, [vp, sz, vp, sz, sz, vp, vp]),
     "phantom_ciphertext_serialize": (ctypes.c_int, [vp, vp, vp, sz, vp]),

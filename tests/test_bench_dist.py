@@ -93,6 +93,11 @@ def test_c4_reference_bytes_by_hand():
             + 2 * sum(key[c] for c in range(11, 17))) * w
     pts = (511 * 39 + 255 * 38 + 511 * 24 + 255 * 23) * w
     cts = (2 * 5 + 2 * 12) * w
-    total, parts = bench.c4_reference_bytes()
+    total, parts, der = bench.c4_reference_bytes()
     assert parts == {"keys": keys, "plaintexts": pts, "ciphertexts": cts}
+    # the schedule the terms above hard-code, as bench derives it from the reference's level
+    # selection (SelectLayers / GetCollapsedFFTParams / ComputeDegreesPS)
+    assert [(l["dir"], l["chain"], l["diagonals"]) for l in der["levels"]] == [
+        ("cts", 2, 511), ("cts", 3, 255), ("stc", 17, 511), ("stc", 18, 255)]
+    assert der["ps_k_m"] == [6, 4] and der["output_chain"] == 19 and der["double_angle_chains"] == [11, 16]
     assert total == keys + pts + cts == 48196747264

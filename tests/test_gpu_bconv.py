@@ -71,6 +71,21 @@ def test_fast_bconv_matches_oracle(rng, n, ib_bits, ob_bits, prescale):
     assert np.all(got[len(obase) * n:] == SENTINEL), "write past obase"
     assert np.array_equal(got[: len(obase) * n], want)
 
+    # the same conversion through a kept converter (phantom_bconv_create / _run), run twice on
+    # one handle: the tables are built once and reused
+    h = PA.vp()
+    PA.check(lib.phantom_bconv_create(ib_arr.ctypes.data_as(PA.u64p), len(ibase), ob_arr.ctypes.data_as(PA.u64p),
+                                      len(obase), stream(), ctypes.byref(h)))
+    try:
+        for _ in range(2):
+            d_out2 = to_dev(np.full((len(obase) + 1) * n, SENTINEL, dtype=np.uint64))
+            PA.check(lib.phantom_bconv_run(h, ptr(d_in), ptr(d_out2), n, prescale, stream()))
+            got2 = to_host(d_out2)
+            assert np.all(got2[len(obase) * n:] == SENTINEL), "write past obase"
+            assert np.array_equal(got2[: len(obase) * n], want)
+    finally:
+        PA.check(lib.phantom_bconv_destroy(h))
+
 
 def test_fast_bconv_rejects_empty():
     lib = PA.load()
@@ -78,3 +93,7 @@ def test_fast_bconv_rejects_empty():
     rc = lib.phantom_fast_bconv(one.ctypes.data_as(PA.u64p), 0, one.ctypes.data_as(PA.u64p), 1, None, None, 16, 1,
                                 stream())
     assert rc != 0
+    assert lib.phantom_bconv_run(None, None, None, 16, 1, stream()) != 0
+    h = PA.vp()
+    assert lib.phantom_bconv_create(one.ctypes.data_as(PA.u64p), 0, one.ctypes.data_as(PA.u64p), 1, stream(),
+                                    ctypes.byref(h)) != 0
