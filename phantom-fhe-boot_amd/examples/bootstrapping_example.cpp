@@ -7,7 +7,7 @@
 //   boot : full bootstrap of 2^(log_n - 1) uniform reals in [1, 5] (the example's input),
 //          levelBudget {2, 2}, scale 2^59, Q = {60, 29 x 59}, P = 10 x 60
 //   batch: `iterations` independent bootstraps, `lanes` at a time side by side (C5 on one GPU)
-//   tail : `iterations` fresh ciphertexts under one key (4th argument: key seed, 0 = OS entropy),
+//   tail : `iterations` fresh ciphertexts under each of `keys` fresh keys (4th argument, default 1),
 //          each bootstrapped; per ciphertext the precision, the raised plaintext's overflow I
 //          (t = m + q0 I, from decrypting RaiseWithCorrection's output mod q0 and q1) and the
 //          output error in the coefficient domain, so a low-precision outlier can be traced to
@@ -111,8 +111,8 @@ int main(int argc, char** argv) {
 
   double t0 = now_ms();
   PhantomContext ctx(parms);
-  // "tail" takes the key seed as its 4th argument (0 = fresh OS-entropy key)
-  const uint64_t key_seed = (mode == "tail" && argc > 4) ? std::strtoull(argv[4], nullptr, 0) : 0x5EED;
+  // "tail" draws fresh OS-entropy keys
+  const uint64_t key_seed = mode == "tail" ? 0 : 0x5EED;
   PhantomSecretKey sk = key_seed ? PhantomSecretKey::for_testing(ctx, key_seed) : PhantomSecretKey(ctx);
   PhantomCKKSEncoder enc(ctx);
   const std::vector<double> sf = precompute_scaling_factors(ctx, scale);
@@ -387,6 +387,21 @@ int main(int argc, char** argv) {
         for (size_t q = 0; q < slots; ++q) want[p] += A[p][q] * x[q];
       report("refapi_linear_transform", max_abs_err(decrypt_decode(ctx, sk, enc, lt), want), 1e-6, lt.chain_index());
     }
+    // a second secret: EvalMultKeyGen / EvalBootstrapKeyGen replace the first secret's keys
+    // (bootstrap.cu:824-841), so a ciphertext under the new secret bootstraps correctly
+    {
+      const size_t nkeys = boot.GetGaloisKey().size();
+      PhantomSecretKey sk2(ctx);
+      boot.EvalMultKeyGen(sk2, ctx);
+      boot.EvalBootstrapKeyGen(sk2, ctx, static_cast<uint32_t>(slots));
+      PhantomPlaintext p2;
+      enc.encode(ctx, x, ct.scale(), p2, ct.chain_index());
+      PhantomCiphertext c2;
+      sk2.encrypt_symmetric(ctx, p2, c2);
+      PhantomCiphertext r2 = boot.EvalBootstrap(c2, ctx);
+      const double err = max_abs_err(decrypt_decode(ctx, sk2, enc, r2), xz);
+      report("refapi_rekey_bootstrap", boot.GetGaloisKey().size() <= nkeys ? err : 1.0, 0.05, r2.chain_index());
+    }
     std::printf("{\"done\": \"refapi\", \"ok\": %s}\n", g_ok ? "true" : "false");
     return g_ok ? 0 : 1;
   }
@@ -584,6 +599,22 @@ int main(int argc, char** argv) {
     for (__int128 b = q0 % q1, e = q1 - 2; e > 0; e >>= 1, b = b * b % q1)
       if (e & 1) q0inv = q0inv * b % q1;
     double worst_bits = 1e9, sum_bits = 0;
+    const int nkeys = argc > 4 ? std::max(1, std::atoi(argv[4])) : 1;
+    for (int key = 0; key < nkeys; ++key) {
+    if (key > 0) {
+      sk = PhantomSecretKey(ctx);
+      boot.EvalMultKeyGen(sk, ctx);
+      boot.EvalBootstrapKeyGen(sk, ctx);
+    }
+    {  // the secret's value at the first slot's root, s(zeta) with zeta = e^(i pi / N): the rounding
+       // bias of a rescale / moddown, -1/2 per coefficient of c0 and c1, sums to (1 + s(zeta)) / (zeta - 1)
+       // in that slot and to far less in any other
+      std::complex<double> sz = 0;
+      const auto& sc = sk.coefficients();
+      for (size_t k = 0; k < N; ++k) sz += static_cast<double>(sc[k]) * std::polar(1.0, M_PI * static_cast<double>(k) / N);
+      std::printf("{\"key\": %d, \"s_zeta\": [%.2f, %.2f], \"hamming\": %zu}\n", key, sz.real(), sz.imag(),
+                  static_cast<size_t>(std::count_if(sc.begin(), sc.end(), [](int8_t v) { return v != 0; })));
+    }
     for (int it = 0; it < std::max(1, iters); ++it) {
       std::vector<double> xt(slots);
       for (auto& v : xt) v = dis(rng);
@@ -606,6 +637,16 @@ int main(int argc, char** argv) {
         if (std::abs(I[k]) > max_i) { max_i = std::abs(I[k]); arg_i = k; }
       }
       PhantomCiphertext o = boot.EvalBootstrap(cin, ctx);
+      // the same input bootstrapped again must give the same ciphertext bit for bit (the
+      // computation is deterministic; a difference would be a race)
+      PhantomCiphertext o2 = boot.EvalBootstrap(cin, ctx);
+      PHX_CHECK(hipDeviceSynchronize());  // the context's streams do not synchronise with hipMemcpy
+      const size_t words = o.size() * o.coeff_modulus_size() * N;
+      std::vector<uint64_t> h1(words), h2(words);
+      PHX_CHECK(hipMemcpy(h1.data(), o.data(), words * 8, hipMemcpyDeviceToHost));
+      PHX_CHECK(hipMemcpy(h2.data(), o2.data(), words * 8, hipMemcpyDeviceToHost));
+      const bool repeat_equal = h1 == h2;
+      g_ok &= repeat_equal;
       std::vector<std::complex<double>> z = decrypt_decode(ctx, sk, enc, o);
       std::vector<double> res(slots);
       for (size_t j = 0; j < slots; ++j) res[j] = z[j].real();
@@ -628,28 +669,51 @@ int main(int argc, char** argv) {
       for (size_t k = 0; k < N; ++k) idx[k] = k;
       std::partial_sort(idx.begin(), idx.begin() + 4, idx.end(),
                         [&](size_t u, size_t v) { return std::abs(e[u]) > std::abs(e[v]); });
-      // mean |e| by |I| band (width K / 8)
+      // mean |e| by the distance d of I to the nearest multiple of 32, where the double-angle
+      // steps amplify an error of the series most (64 / |sin(pi (I + f - 1/4) / 32)|); bands
+      // d = 0, 1, 2-3, 4-7, 8-16; coefficients 0 and N/2 (slot 0 of CoeffToSlot) left out
       double band_sum[9] = {0}, band_n[9] = {0};
-      for (size_t k = 0; k < N; ++k) {
-        const int bnd = std::min(8, std::abs(I[k]) * 8 / K);
+      for (size_t k = 1; k < N; ++k) {
+        if (k == N / 2) continue;
+        const int r = ((I[k] % 32) + 32) % 32, d = std::min(r, 32 - r);
+        const int bnd = d == 0 ? 0 : d == 1 ? 1 : d <= 3 ? 2 : d <= 7 ? 3 : 4;
         band_sum[bnd] += std::abs(e[k]);
         band_n[bnd] += 1;
       }
+      // coefficients with I = 0 other than 0 and N/2: the double-angle steps amplify their error most
+      double z_sum = 0, z_max = 0, z_n = 0;
+      for (size_t k = 1; k < N; ++k) {
+        if (k == N / 2 || I[k] != 0) continue;
+        z_sum += std::abs(e[k]);
+        z_max = std::max(z_max, std::abs(e[k]));
+        z_n += 1;
+      }
+      // the same message under a second, independent encryption
+      PhantomCiphertext cin2;
+      sk.encrypt_symmetric(ctx, pin, cin2);
+      PhantomCiphertext o3 = boot.EvalBootstrap(cin2, ctx);
+      PhantomPlaintext pout3;
+      sk.decrypt(ctx, o3, pout3);
+      const std::vector<uint64_t> a3 = coeffs2(pout3);
+      const uint64_t d3 = a3[0] >= b[0] ? a3[0] - b[0] : a3[0] + q0 - b[0];
+      const double e0_reenc = static_cast<double>(centered(d3, q0)) / o3.scale();
       std::ostringstream top, bands;
       for (int t = 0; t < 4; ++t)
         top << (t ? ", " : "") << "[" << idx[t] << ", " << e[idx[t]] << ", " << I[idx[t]] << "]";
-      for (int bnd = 0; bnd < 9; ++bnd)
+      for (int bnd = 0; bnd < 5; ++bnd)
         bands << (bnd ? ", " : "") << (band_n[bnd] ? band_sum[bnd] / band_n[bnd] : 0.0);
       const double rms = std::sqrt(ss / N);
-      std::printf("{\"tail\": %d, \"avg_bits\": %.3f, \"I0\": %d, \"e0\": %.4e, \"max_abs_I\": %d, \"argmax_I\": %zu, \"err_rms\": %.3e, "
-                  "\"top_err_share\": %.4f, \"top_err\": [%s], \"mean_err_by_I_band\": [%s]}\n",
-                  it, bits, I[0], e[0], max_i, arg_i, rms, e[idx[0]] * e[idx[0]] / ss, top.str().c_str(), bands.str().c_str());
+      std::printf("{\"key\": %d, \"tail\": %d, \"repeat_equal\": %s, \"avg_bits\": %.3f, \"I0\": %d, \"e0\": %.4e, "
+                  "\"e0_reencrypted\": %.4e, \"I_half\": %d, \"e_half\": %.4e, \"I_zero_others\": [%.0f, %.3e, %.3e], \"max_abs_I\": %d, \"argmax_I\": %zu, \"err_rms\": %.3e, "
+                  "\"top_err_share\": %.4f, \"top_err\": [%s], \"mean_err_by_I_mod32_band\": [%s]}\n",
+                  key, it, repeat_equal ? "true" : "false", bits, I[0], e[0], e0_reenc, I[N / 2], e[N / 2], z_n, z_n ? z_sum / z_n : 0.0, z_max, max_i, arg_i, rms, e[idx[0]] * e[idx[0]] / ss, top.str().c_str(), bands.str().c_str());
       std::fflush(stdout);
     }
-    std::printf("{\"stage\": \"tail\", \"ciphertexts\": %d, \"key_seed\": %llu, \"K\": %d, \"min_avg_bits\": %.3f, "
+    }
+    std::printf("{\"stage\": \"tail\", \"keys\": %d, \"ciphertexts_per_key\": %d, \"K\": %d, \"min_avg_bits\": %.3f, "
                 "\"mean_avg_bits\": %.3f}\n",
-                std::max(1, iters), (unsigned long long)key_seed, K, worst_bits, sum_bits / std::max(1, iters));
-    return 0;
+                nkeys, std::max(1, iters), K, worst_bits, sum_bits / (nkeys * std::max(1, iters)));
+    return g_ok ? 0 : 1;
   }
 
   if (mode == "batch") {

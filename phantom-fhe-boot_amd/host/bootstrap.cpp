@@ -855,11 +855,20 @@ std::vector<int> FHECKKSRNS::rotation_indices(uint32_t numSlots) const {
   return r;
 }
 
+void FHECKKSRNS::claim_galois_keys(const PhantomSecretKey& sk) {
+  uint64_t h = 0xcbf29ce484222325ull;  // FNV-1a over the secret's coefficients
+  for (int8_t c : sk.coefficients()) h = (h ^ static_cast<uint8_t>(c)) * 0x100000001b3ull;
+  if (h != galois_owner_) galois_keys_ = PhantomGaloisKey{};
+  galois_owner_ = h;
+}
+
 void FHECKKSRNS::EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext& cc, uint32_t numSlots) {
+  claim_galois_keys(sk);
   std::vector<uint32_t> elts;
   for (int r : rotation_indices(numSlots)) elts.push_back(FindAutomorphismIndex2nComplex(r, cc.poly_degree()));
   elts.push_back(static_cast<uint32_t>(2 * cc.poly_degree() - 1));  // conjugation
-  // keys of earlier setups (other slot counts) stay; only the missing elements are generated
+  // keys of earlier setups (other slot counts) under the same secret stay; only the missing
+  // elements are generated
   std::vector<uint32_t> need;
   for (uint32_t e : elts)
     if (!galois_keys_.has(e)) need.push_back(e);
@@ -867,6 +876,7 @@ void FHECKKSRNS::EvalBootstrapKeyGen(PhantomSecretKey& sk, const PhantomContext&
 }
 
 void FHECKKSRNS::EvalRotationKeyGen(PhantomSecretKey& sk, const PhantomContext& cc, const std::vector<int32_t>& indices) {
+  claim_galois_keys(sk);
   std::vector<uint32_t> need;
   for (int32_t r : indices) {
     const uint32_t e = FindAutomorphismIndex2nComplex(r, cc.poly_degree());

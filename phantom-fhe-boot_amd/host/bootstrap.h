@@ -265,6 +265,11 @@ class FHECKKSRNS {
   const void* baby_table(const PhantomContext& cc, const LTLevel& lv, size_t QlP) const;
   PhantomRelinKey mul_key_;
   PhantomGaloisKey galois_keys_;  // fused keys
+  // fingerprint of the secret the Galois keys were made from: keys of earlier setups (other slot
+  // counts) are kept only while the secret stays the same; a new secret replaces them all, as the
+  // reference's EvalBootstrapKeyGen replaces its key set (bootstrap.cu:824-836)
+  uint64_t galois_owner_ = 0;
+  void claim_galois_keys(const PhantomSecretKey& sk);
 };
 
 }  // namespace phantom
