@@ -1,4 +1,5 @@
-"""Profiling driver (tools only): MODE=ntt50 | ntt60 | c3.  ntt50/ntt60: forward NTT of [L][2^16]
+"""Profiling driver (tools only): MODE=ntt50 | ntt60 | ntt60fi | c3.  ntt50/ntt60: forward NTT of [L][2^16]
+(ntt60fi: forward then inverse)
 (44 50-bit primes / the C4 chain's 40 primes) over a ring of 15 buffers; c3: relinearize of a
 45-limb ciphertext (P = 15, dnum 3) with random keys.  Used under rocprofv3 (kernel trace, PMC)."""
 import os
@@ -25,8 +26,8 @@ def limbs(ms, polys=1):
     return torch.from_numpy(a.view(np.int64)).cuda()
 
 
-if mode in ("ntt50", "ntt60"):
-    if mode == "ntt60":
+if mode in ("ntt50", "ntt60", "ntt60fi"):
+    if mode != "ntt50":
         mods = PA.coeff_modulus_create(N, [60] + [59] * 29 + [60] * 10)
     else:
         mods = PA.coeff_modulus_create(N, [60] + [50] * 44 + [60] * 15)[:44]
@@ -37,6 +38,8 @@ if mode in ("ntt50", "ntt60"):
     t0 = time.perf_counter()
     for i in range(iters):
         PA.check(lib.phantom_nwt_forward_inplace(ring[i % 15].data_ptr(), t.handle, L, 0, s))
+        if mode == "ntt60fi":
+            PA.check(lib.phantom_nwt_backward_inplace(ring[i % 15].data_ptr(), t.handle, L, 0, s))
     torch.cuda.synchronize()
 else:
     mods = PA.coeff_modulus_create(N, [60] + [50] * 44 + [60] * 15)
