@@ -103,6 +103,30 @@ struct TensorLinArgs {
 };
 hipError_t tensor_lin(const TensorLinArgs& a, size_t n, size_t L, hipStream_t s);
 
+// tensor_lin of up to kTensorBatchMax independent products at one level in one launch (one grid
+// row per product), with the product's constant folded in as well: for product k,
+// out[k] = factor ct1 x ct2 (+ t c in polys 0, 1) (+ cadd in poly 0), every per-limb constant a
+// residue (c, cadd) in `limb` [count][2][L] by value.  The values are those of tensor_lin followed
+// by add_scalar_v, bit for bit.
+constexpr int kTensorBatchMax = 8, kTensorBatchLimbWords = 384;
+struct TensorLinJob {
+  const uint64_t* ct1;
+  const uint64_t* ct2;
+  uint64_t* out;
+  const uint64_t* t;  // null: no term
+  uint64_t t_stride;
+  uint64_t factor;    // 1: unscaled
+  uint32_t has_const;
+};
+struct TensorLinBatchArgs {
+  const uint64_t* q;
+  const uint64_t* barrett;
+  uint32_t L = 0, count = 0;
+  TensorLinJob job[kTensorBatchMax];
+  uint64_t limb[kTensorBatchLimbWords];
+};
+hipError_t tensor_lin_batch(const TensorLinBatchArgs& a, size_t n, hipStream_t s);
+
 // d[p] = d[p] * ca (ca may be null: unscaled) + (p < t_polys ? t[p] * cb : 0) for p < d_polys;
 // d contiguous [d_polys][L][n], t[p] at t + p * t_stride (its first L limbs)
 hipError_t lin_comb_v(uint64_t* d, size_t d_polys, const LimbScalars* ca, const uint64_t* t, size_t t_polys,

@@ -353,6 +353,36 @@ __global__ __launch_bounds__(kBlock) void tensor_lin_kernel(TensorLinArgs a, uin
   }
 }
 
+// tensor_lin over the products of one batch: grid row blockIdx.y = product (see ckks.h)
+__global__ __launch_bounds__(kBlock) void tensor_lin_batch_kernel(TensorLinBatchArgs a, uint32_t log_n, size_t total) {
+  const uint32_t k = blockIdx.y;
+  const TensorLinJob& J = a.job[k];
+  const uint64_t* cl = a.limb + static_cast<size_t>(k) * 2 * a.L;
+  const size_t stride = total;
+  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+    const uint64_t q = a.q[l], r0 = a.barrett[2 * l], r1 = a.barrett[2 * l + 1];
+    const uint64_t a0 = J.ct1[e], a1 = J.ct1[stride + e], b0 = J.ct2[e], b1 = J.ct2[stride + e];
+    u128 c1 = mul_wide(a0, b1);
+    add128(c1, mul_wide(a1, b0));
+    uint64_t d0 = mul_mod(a0, b0, q, r0, r1), d1 = barrett_reduce_128(c1, q, r0, r1), d2 = mul_mod(a1, b1, q, r0, r1);
+    if (J.factor != 1) {  // product-uniform branches
+      d0 = mul_mod(d0, J.factor, q, r0, r1);
+      d1 = mul_mod(d1, J.factor, q, r0, r1);
+      d2 = mul_mod(d2, J.factor, q, r0, r1);
+    }
+    if (J.t) {
+      const uint64_t c = cl[l];
+      d0 = add_mod(d0, mul_mod(J.t[e], c, q, r0, r1), q);
+      d1 = add_mod(d1, mul_mod(J.t[J.t_stride + e], c, q, r0, r1), q);
+    }
+    if (J.has_const) d0 = add_mod(d0, cl[a.L + l], q);
+    J.out[e] = d0;
+    J.out[stride + e] = d1;
+    J.out[2 * stride + e] = d2;
+  }
+}
+
 int grid_for(size_t items) {
   const size_t b = (items + kBlock - 1) / kBlock;
   return static_cast<int>(std::max<size_t>(1, std::min<size_t>(b, 2048)));
@@ -432,6 +462,18 @@ hipError_t tensor_lin(const TensorLinArgs& a, size_t n, size_t L, hipStream_t s)
   else if (a.scale) tensor_lin_kernel<true, false><<<grid, kBlock, 0, s>>>(a, log_n, total);
   else if (a.t) tensor_lin_kernel<false, true><<<grid, kBlock, 0, s>>>(a, log_n, total);
   else tensor_lin_kernel<false, false><<<grid, kBlock, 0, s>>>(a, log_n, total);
+  return hipGetLastError();
+}
+
+hipError_t tensor_lin_batch(const TensorLinBatchArgs& a, size_t n, hipStream_t s) {
+  if (a.count < 1 || a.count > static_cast<uint32_t>(kTensorBatchMax) || a.L < 1 ||
+      static_cast<size_t>(a.count) * 2 * a.L > static_cast<size_t>(kTensorBatchLimbWords) || !a.q || !a.barrett)
+    return hipErrorInvalidValue;
+  for (uint32_t k = 0; k < a.count; ++k)
+    if (!a.job[k].ct1 || !a.job[k].ct2 || !a.job[k].out || a.job[k].factor == 0) return hipErrorInvalidValue;
+  const size_t total = n * a.L;
+  const dim3 grid(static_cast<unsigned>(std::max(1, grid_for(total) / static_cast<int>(a.count))), a.count);
+  tensor_lin_batch_kernel<<<grid, kBlock, 0, s>>>(a, __builtin_ctzll(n), total);
   return hipGetLastError();
 }
 

@@ -387,6 +387,38 @@ int main(int argc, char** argv) {
         for (size_t q = 0; q < slots; ++q) want[p] += A[p][q] * x[q];
       report("refapi_linear_transform", max_abs_err(decrypt_decode(ctx, sk, enc, lt), want), 1e-6, lt.chain_index());
     }
+    // MulAddRescaleBatch (the EvalMod products' shared launches) equals MulAddRescale per job, bit
+    // for bit: factors 1 / 2 / 3, zero / one / two terms, with and without a constant, 11 jobs
+    // (more than one launch of the batched tensor kernel)
+    {
+      PhantomCiphertext c2 = ct;
+      EvalMultConstInplace(ctx, c2, 0.5, sfR);
+      EvalModReduceInPlace(ctx, c2, 1);
+      PhantomCiphertext c1 = c2;
+      EvalMultConstInplace(ctx, c1, 1.5, sfR);
+      EvalModReduceInPlace(ctx, c1, 1);  // one level below c2
+      PhantomCiphertext c3 = c2;
+      EvalMultConstInplace(ctx, c3, 1.0, sfR);
+      EvalModReduceInPlace(ctx, c3, 1);
+      const PhantomRelinKey& rk = boot.GetMultKey();
+      std::vector<MulAddJob> jobs;
+      for (int k = 0; k < 11; ++k) {
+        MulAddJob j{&c1, k % 2 ? &c3 : &c1, 1 + k % 3, {}, 0.0};
+        if (k % 4 >= 1) j.terms.push_back({&c2, k % 2 ? -1.0 : 0.75});
+        if (k % 4 == 3) j.terms.push_back({&c1, 2.0});
+        if (k % 5 >= 2) j.constant = k % 2 ? -1.0 : 0.25;
+        jobs.push_back(std::move(j));
+      }
+      const std::vector<PhantomCiphertext> got = MulAddRescaleBatch(ctx, jobs, rk);
+      bool same = got.size() == jobs.size();
+      for (size_t k = 0; same && k < jobs.size(); ++k) {
+        const PhantomCiphertext want = MulAddRescale(ctx, *jobs[k].a, *jobs[k].b, rk, jobs[k].factor, jobs[k].terms,
+                                                     jobs[k].constant);
+        same = want.to_host(ctx.stream()) == got[k].to_host(ctx.stream()) && want.scale() == got[k].scale() &&
+               want.chain_index() == got[k].chain_index();
+      }
+      report("refapi_muladd_batch_bitexact", same ? 0.0 : 1.0, 0.5, got.empty() ? 0 : got[0].chain_index());
+    }
     // a second secret: EvalMultKeyGen / EvalBootstrapKeyGen replace the first secret's keys
     // (bootstrap.cu:824-841), so a ciphertext under the new secret bootstraps correctly
     {

@@ -447,6 +447,18 @@ std::vector<PhantomCiphertext> MulAddRescaleBatch(const PhantomContext& ctx, con
     // stride); the buffer is freed on this stream after the key switch has read it
     DeviceBuffer<uint64_t> d(cnt * 3 * L * n, s);
     std::vector<double> scales(cnt);
+    // the tensors (factor, first term and constant folded in) in shared launches of up to
+    // kTensorBatchMax products; further terms (rare) after them
+    const auto& mods = ctx.get_context_data(chain).moduli();
+    phx::TensorLinBatchArgs tb;
+    tb.q = q;
+    tb.barrett = ctx.mod_QP().barrett;
+    tb.L = static_cast<uint32_t>(L);
+    auto flush = [&] {
+      if (!tb.count) return;
+      hip_ok(phx::tensor_lin_batch(tb, n, s), "tensor + linear epilogue (batch)");
+      tb.count = 0;
+    };
     for (size_t k = 0; k < cnt; ++k) {
       const MulAddJob& j = jobs[b0 + k];
       if (j.a->chain_index() != j.b->chain_index() || j.a->GetNoiseScaleDeg() > 1 || j.b->GetNoiseScaleDeg() > 1)
@@ -454,35 +466,41 @@ std::vector<PhantomCiphertext> MulAddRescaleBatch(const PhantomContext& ctx, con
       for (const ScaledTerm& t : j.terms)
         if (t.ct->chain_index() > chain || t.ct->GetNoiseScaleDeg() > 1 || t.ct->size() != 2)
           throw std::invalid_argument("MulAddRescale: a term is below the product's level");
-      uint64_t* dk = d.get() + k * 3 * L * n;
+      if (j.factor < 1) throw std::invalid_argument("MulAddRescale: factor must be positive");
       const double S = j.a->scale() * j.b->scale();
       scales[k] = S;
-      phx::TensorLinArgs ta;
-      ta.ct1 = j.a->data();
-      ta.ct2 = j.b->data();
-      ta.out = dk;
-      ta.q = q;
-      ta.barrett = ctx.mod_QP().barrett;
-      ta.scale = j.factor != 1;
-      if (ta.scale) ta.f = limb_scalars(ctx, chain, static_cast<double>(j.factor));
+      if (tb.count == static_cast<uint32_t>(phx::kTensorBatchMax) ||
+          (tb.count + 1) * 2 * L > static_cast<size_t>(phx::kTensorBatchLimbWords))
+        flush();
+      phx::TensorLinJob& tj = tb.job[tb.count];
+      uint64_t* cl = tb.limb + static_cast<size_t>(tb.count) * 2 * L;
+      tj.ct1 = j.a->data();
+      tj.ct2 = j.b->data();
+      tj.out = d.get() + k * 3 * L * n;
+      tj.factor = static_cast<uint64_t>(j.factor);
+      tj.t = nullptr;
+      tj.t_stride = 0;
       if (!j.terms.empty()) {
-        ta.t = j.terms[0].ct->data();
-        ta.t_stride = j.terms[0].ct->coeff_modulus_size() * n;
-        ta.c = limb_scalars(ctx, chain, j.terms[0].coeff * S / j.terms[0].ct->scale());
+        // round(c S / scale_t) t carries c m_t at the product's scale S
+        tj.t = j.terms[0].ct->data();
+        tj.t_stride = j.terms[0].ct->coeff_modulus_size() * n;
+        for (size_t l = 0; l < L; ++l) cl[l] = residue_of_double(j.terms[0].coeff * S / j.terms[0].ct->scale(), mods[l]);
       }
-      hip_ok(phx::tensor_lin(ta, n, L, s), "tensor + linear epilogue");
+      tj.has_const = j.constant != 0.0;
+      if (tj.has_const)
+        for (size_t l = 0; l < L; ++l) cl[L + l] = residue_of_double(j.constant * S, mods[l]);
+      ++tb.count;
       traffic::ciphertexts(traffic::limb_bytes(4 * L + 2 * L * j.terms.size(), n));
+    }
+    flush();
+    for (size_t k = 0; k < cnt; ++k) {
+      const MulAddJob& j = jobs[b0 + k];
       for (size_t i = 1; i < j.terms.size(); ++i) {
         const ScaledTerm& t = j.terms[i];
-        const phx::LimbScalars cb = limb_scalars(ctx, chain, t.coeff * S / t.ct->scale());
-        hip_ok(phx::lin_comb_v(dk, 2, nullptr, t.ct->data(), 2, t.ct->coeff_modulus_size() * n, cb, q, n, L, s),
+        const phx::LimbScalars cb = limb_scalars(ctx, chain, t.coeff * scales[k] / t.ct->scale());
+        hip_ok(phx::lin_comb_v(d.get() + k * 3 * L * n, 2, nullptr, t.ct->data(), 2, t.ct->coeff_modulus_size() * n, cb,
+                               q, n, L, s),
                "mul-add term");
-      }
-      if (j.constant != 0.0) {
-        const auto& mods = ctx.get_context_data(chain).moduli();
-        phx::LimbScalars v;
-        for (size_t l = 0; l < L; ++l) v.v[l] = residue_of_double(j.constant * S, mods[l]);
-        hip_ok(phx::add_scalar_v(dk, v, dk, q, n, L, s), "add const");
       }
     }
     std::vector<uint64_t*> outs(cnt);

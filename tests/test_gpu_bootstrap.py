@@ -88,7 +88,7 @@ def test_reference_precompute_evaluate_api():
     assert rc == 0, (lines, err)
     for name in ["refapi_rotation_indices", "refapi_get_keys", "refapi_cts_stc_roundtrip", "refapi_cts_parseval",
                  "refapi_add_ext_keyswitch_down", "refapi_keyswitch_down_first_element", "refapi_mult_ext",
-                 "refapi_linear_transform", "refapi_rekey_bootstrap"]:
+                 "refapi_linear_transform", "refapi_rekey_bootstrap", "refapi_muladd_batch_bitexact"]:
         assert checks[name]["ok"], checks[name]
 
 
