@@ -1088,8 +1088,9 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
               ct_round_int<S2_LOG, R>(v, w, ws, lc.q);
           });
           if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, lrow, idx, sync, t);
+          [[maybe_unused]] const float rq = static_cast<float>(4294967296.0 / static_cast<double>(lc.q));
           auto canon = [&](uint64_t y) {
-            if constexpr (LZ && P::row_lz.out > 8) return reduce16(y, lc.q);
+            if constexpr (LZ && P::row_lz.out > 8) return reduce16_est(y, lc.q, rq);
             else return reduce8(y, lc.q);
           };
           if constexpr (KS) {
