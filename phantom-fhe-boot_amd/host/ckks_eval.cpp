@@ -435,7 +435,9 @@ std::vector<PhantomCiphertext> MulAddRescaleBatch(const PhantomContext& ctx, con
   for (const MulAddJob& j : jobs)
     if (j.a->chain_index() != chain) throw std::invalid_argument("MulAddRescaleBatch: products at different levels");
   const size_t n = ctx.poly_degree(), L = jobs[0].a->coeff_modulus_size();
-  if (L > static_cast<size_t>(phx::kMaxScalarLimbs)) {  // (the per-limb constants travel by value)
+  bool positive = true;  // the batched tensor kernel takes a factor >= 1 (the EvalMod products' 1 and 2)
+  for (const MulAddJob& j : jobs) positive &= j.factor >= 1;
+  if (L > static_cast<size_t>(phx::kMaxScalarLimbs) || !positive) {  // (the per-limb constants travel by value)
     for (const MulAddJob& j : jobs) res.push_back(MulAddRescale(ctx, *j.a, *j.b, rlk, j.factor, j.terms, j.constant));
     return res;
   }
@@ -466,7 +468,6 @@ std::vector<PhantomCiphertext> MulAddRescaleBatch(const PhantomContext& ctx, con
       for (const ScaledTerm& t : j.terms)
         if (t.ct->chain_index() > chain || t.ct->GetNoiseScaleDeg() > 1 || t.ct->size() != 2)
           throw std::invalid_argument("MulAddRescale: a term is below the product's level");
-      if (j.factor < 1) throw std::invalid_argument("MulAddRescale: factor must be positive");
       const double S = j.a->scale() * j.b->scale();
       scales[k] = S;
       if (tb.count == static_cast<uint32_t>(phx::kTensorBatchMax) ||
