@@ -175,15 +175,13 @@ __global__ __launch_bounds__(kBlock, 2) void lt_bsgs_kernel(LtArgs a, uint32_t l
 // every giant step's 128-bit sums stay in registers across the two halves, so each baby and each
 // plaintext is still read once (the register-resident form of lt_bsgs_kernel<32> spills).
 template <int G, int B>
-__global__ __launch_bounds__(kBlock, 2) void lt_bsgs_wide_kernel(LtArgs a, uint32_t log_n, size_t total) {
+__device__ __forceinline__ void lt_bsgs_wide(const LtArgs& a, uint32_t log_n, size_t total, uint32_t block,
+                                             uint32_t nblocks, const uint64_t* const* ptab) {
   constexpr uint64_t kM30 = (1ull << 30) - 1;
   constexpr int C = 8;
   static_assert(G % C == 0, "whole chunks of babies");
-  extern __shared__ const uint64_t* ptab[];
-  for (int k = threadIdx.x; k < a.b * G; k += kBlock) ptab[k] = a.pts[k];
-  __syncthreads();
   const size_t pstride = total;
-  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
+  for (size_t e = block * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)nblocks * kBlock) {
     const int l = static_cast<int>(e >> log_n);
     const int row = l < a.Ql ? l : a.size_Q + (l - a.Ql);
     const uint64_t q = a.q[row], r0 = a.barrett[2 * row], r1 = a.barrett[2 * row + 1];
@@ -238,6 +236,28 @@ __global__ __launch_bounds__(kBlock, 2) void lt_bsgs_wide_kernel(LtArgs a, uint3
       o[pstride + e] = barrett_reduce_128(acc[i][1], q, r0, r1);
     }
   }
+}
+
+template <int G, int B>
+__global__ __launch_bounds__(kBlock, 2) void lt_bsgs_wide_kernel(LtArgs a, uint32_t log_n, size_t total) {
+  extern __shared__ const uint64_t* ptab[];
+  for (int k = threadIdx.x; k < a.b * G; k += kBlock) ptab[k] = a.pts[k];
+  __syncthreads();
+  lt_bsgs_wide<G, B>(a, log_n, total, blockIdx.x, gridDim.x, ptab);
+}
+
+// two ciphertexts through the same plaintexts (lt_bsgs_pair): the blocks of the two that cover
+// the same elements are dealt to one XCD 8 dispatches apart (blocks b and b + 8 share an XCD under
+// round-robin placement), so the second one's plaintext reads are served by that XCD's L2
+template <int G, int B>
+__global__ __launch_bounds__(kBlock, 2) void lt_bsgs_pair_kernel(LtPairArgs pa, uint32_t log_n, size_t total) {
+  extern __shared__ const uint64_t* ptab[];
+  const LtArgs& a0 = pa.a[0];
+  for (int k = threadIdx.x; k < a0.b * G; k += kBlock) ptab[k] = a0.pts[k];
+  __syncthreads();
+  const uint32_t b = blockIdx.x, x = b % 8, k = b / 8;
+  const uint32_t c = k % 2, blk = (k / 2) * 8 + x, nblk = gridDim.x / 2;
+  lt_bsgs_wide<G, B>(pa.a[c], log_n, total, blk, nblk, ptab);
 }
 
 template <bool MUL, bool ACC>
@@ -450,6 +470,22 @@ hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s) {
       break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t lt_bsgs_pair(const LtPairArgs& pa, size_t n, hipStream_t s) {
+  const LtArgs& a = pa.a[0];
+  const LtArgs& b = pa.a[1];
+  if (a.g != 32 || a.b < 1 || a.b > 8 || !a.pts || b.g != a.g || b.b != a.b || b.pts != a.pts || b.Ql != a.Ql ||
+      b.P != a.P || b.size_Q != a.size_Q)
+    return hipErrorInvalidValue;
+  for (const LtArgs* x : {&a, &b})
+    for (int i = 0; i < x->b; ++i)
+      if (!x->out[i]) return hipErrorInvalidValue;
+  const size_t total = n * static_cast<size_t>(a.Ql + a.P);
+  const size_t lds = static_cast<size_t>(a.b) * a.g * sizeof(const uint64_t*);
+  const int per = (grid_for(total) + 7) / 8 * 8;  // blocks per ciphertext, whole XCD rounds
+  lt_bsgs_pair_kernel<32, 8><<<2 * per, kBlock, lds, s>>>(pa, __builtin_ctzll(n), total);
   return hipGetLastError();
 }
 

@@ -756,13 +756,27 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_kernel(KsRotateArgs a, uint3
 // Full blocks (BETA > 0): the block's digits and P c0 are loaded once into registers and shared by
 // every entry, so an entry reads only its key halves from HBM; those loads are issued for entry
 // k + 1 before entry k's barrier and gather, so they are in flight while the gather runs.
-template <int BETA>
-__global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchArgs a, uint32_t log_n) {
+//
+// PAIR: two ciphertexts' baby steps through the same keys (two bootstraps in lockstep) in one
+// launch; the two ciphertexts' workgroups of the same (limb, source block) are dealt to one XCD 8
+// dispatches apart (blocks b and b + 8 share an XCD under round-robin placement), so the second
+// reads the key halves from that XCD's L2.
+template <int BETA, bool PAIR>
+__global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchPairArgs pa, uint32_t log_n) {
   constexpr uint32_t bsz = kGalB;
   constexpr int PP = kGalB / 2 / kBlock;  // pairs per thread
   __shared__ uint64_t s0[2][kGalB], s1[2][kGalB];
   const uint32_t nb = (1u << log_n) / bsz;
-  const uint32_t l = blockIdx.x / nb, sblk = blockIdx.x % nb;
+  uint32_t bid = blockIdx.x;
+  int c = 0;
+  if constexpr (PAIR) {
+    const uint32_t x = bid % 8, k = bid / 8;
+    c = static_cast<int>(k % 2);
+    bid = (k / 2) * 8 + x;
+  }
+  const KsRotateBatchArgs& a = pa.a[c];
+  if (PAIR && bid >= a.qlp * nb) return;  // the rounding of the pair grid (workgroup-uniform, no barrier passed)
+  const uint32_t l = bid / nb, sblk = bid % nb;
   const uint32_t twr = l >= a.ql ? a.size_q + (l - a.ql) : l;
   const uint64_t q = a.qp[twr], r0 = a.qp_barrett[2 * twr], r1 = a.qp_barrett[2 * twr + 1];
   const size_t lbase = (size_t)l << log_n, kbase = (size_t)twr << log_n;
@@ -1217,11 +1231,37 @@ hipError_t keyswitch_rotate_batch(const KsRotateBatchArgs& a, size_t n, hipStrea
   const uint32_t log_n = __builtin_ctzll(n), bsz = static_cast<uint32_t>(std::min<size_t>(n, kGalB));
   const dim3 grid(static_cast<uint32_t>(a.qlp * (n / bsz)));
   switch (bsz == kGalB ? a.beta : 0) {
-    case 1: ks_rotate_batch_full<1><<<grid, kBlock, 0, s>>>(a, log_n); break;
-    case 2: ks_rotate_batch_full<2><<<grid, kBlock, 0, s>>>(a, log_n); break;
-    case 3: ks_rotate_batch_full<3><<<grid, kBlock, 0, s>>>(a, log_n); break;
-    case 4: ks_rotate_batch_full<4><<<grid, kBlock, 0, s>>>(a, log_n); break;
+    case 1: ks_rotate_batch_full<1, false><<<grid, kBlock, 0, s>>>(KsRotateBatchPairArgs{{a, a}}, log_n); break;
+    case 2: ks_rotate_batch_full<2, false><<<grid, kBlock, 0, s>>>(KsRotateBatchPairArgs{{a, a}}, log_n); break;
+    case 3: ks_rotate_batch_full<3, false><<<grid, kBlock, 0, s>>>(KsRotateBatchPairArgs{{a, a}}, log_n); break;
+    case 4: ks_rotate_batch_full<4, false><<<grid, kBlock, 0, s>>>(KsRotateBatchPairArgs{{a, a}}, log_n); break;
     default: ks_rotate_batch_kernel<<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t keyswitch_rotate_batch_pair(const KsRotateBatchPairArgs& pa, size_t n, hipStream_t s) {
+  const KsRotateBatchArgs& a = pa.a[0];
+  const KsRotateBatchArgs& b = pa.a[1];
+  for (const KsRotateBatchArgs* x : {&a, &b})
+    if (!x->digits || !x->entries || !x->ct || !x->out || !x->pmod || !x->pmod_shoup || x->beta == 0 || x->ql > x->qlp)
+      return hipErrorInvalidValue;
+  if (b.entries != a.entries || b.count != a.count || b.qlp != a.qlp || b.ql != a.ql || b.beta != a.beta ||
+      b.size_q != a.size_q || b.size_p != a.size_p)
+    return hipErrorInvalidValue;
+  if (a.qlp == 0 || a.count == 0) return hipSuccess;
+  if (n < kGalB || a.beta > 4) {  // the shapes without the register-resident form: two launches
+    hipError_t e = keyswitch_rotate_batch(a, n, s);
+    return e != hipSuccess ? e : keyswitch_rotate_batch(b, n, s);
+  }
+  const uint32_t log_n = __builtin_ctzll(n);
+  const uint32_t per = (a.qlp * static_cast<uint32_t>(n / kGalB) + 7) / 8 * 8;
+  const dim3 grid(2 * per);
+  switch (a.beta) {
+    case 1: ks_rotate_batch_full<1, true><<<grid, kBlock, 0, s>>>(pa, log_n); break;
+    case 2: ks_rotate_batch_full<2, true><<<grid, kBlock, 0, s>>>(pa, log_n); break;
+    case 3: ks_rotate_batch_full<3, true><<<grid, kBlock, 0, s>>>(pa, log_n); break;
+    default: ks_rotate_batch_full<4, true><<<grid, kBlock, 0, s>>>(pa, log_n); break;
   }
   return hipGetLastError();
 }

@@ -34,6 +34,7 @@
 #include "../host/keys.h"
 #include "../host/modulus.h"
 #include "../host/traffic.h"
+#include "../csrc/ckks.h"
 #include "../csrc/rns.h"
 #include "../csrc/ntt.h"
 
@@ -437,6 +438,74 @@ int main(int argc, char** argv) {
     std::printf("{\"done\": \"refapi\", \"ok\": %s}\n", g_ok ? "true" : "false");
     return g_ok ? 0 : 1;
   }
+  if (mode == "ltpair") {
+    // the linear-transform inner products of two ciphertexts: two lt_bsgs launches against one
+    // lt_bsgs_pair launch (the plaintexts shared through L2), at the CoeffToSlot level shape
+    // (Ql = 30, P = 10, g = 32, b = 8); outputs compared bit for bit
+    const size_t QlP = ctx.size_Q() + ctx.size_P(), words = 2 * QlP * N;
+    const int g = 32, b = 8;
+    hipStream_t s = ctx.stream();
+    phx::ChaChaKey key{};
+    for (int i = 0; i < 8; ++i) key.k[i] = 0x1234567u * (i + 1);
+    uint64_t nonce = 1;
+    std::vector<DeviceBuffer<uint64_t>> babies, pts;
+    for (int c = 0; c < 2 * g; ++c) {
+      babies.emplace_back(words, s);
+      PHX_CHECK(phx::sample_uniform(babies.back().get(), ctx.mod_QP().q, ctx.mod_QP().barrett, N, QlP, key, nonce++, s));
+      PHX_CHECK(phx::sample_uniform(babies.back().get() + QlP * N, ctx.mod_QP().q, ctx.mod_QP().barrett, N, QlP, key,
+                                    nonce++, s));
+    }
+    std::vector<const uint64_t*> ptr_host;
+    for (int k = 0; k < g * b; ++k) {
+      pts.emplace_back(QlP * N, s);
+      PHX_CHECK(phx::sample_uniform(pts.back().get(), ctx.mod_QP().q, ctx.mod_QP().barrett, N, QlP, key, nonce++, s));
+      ptr_host.push_back(pts.back().get());
+    }
+    DeviceBuffer<const uint64_t*> ptr_dev(ptr_host.size(), s);
+    PHX_CHECK(hipMemcpy(ptr_dev.get(), ptr_host.data(), ptr_host.size() * sizeof(void*), hipMemcpyHostToDevice));
+    std::vector<DeviceBuffer<uint64_t>> out1, out2;
+    for (int k = 0; k < 2 * b; ++k) {
+      out1.emplace_back(words, s);
+      out2.emplace_back(words, s);
+    }
+    phx::LtPairArgs pa;
+    for (int c = 0; c < 2; ++c) {
+      phx::LtArgs& la = pa.a[c];
+      la.g = g;
+      la.b = b;
+      la.Ql = static_cast<int>(ctx.size_Q());
+      la.P = static_cast<int>(ctx.size_P());
+      la.size_Q = static_cast<int>(ctx.size_Q());
+      la.pts = ptr_dev.get();
+      la.q = ctx.mod_QP().q;
+      la.barrett = ctx.mod_QP().barrett;
+      for (int j = 0; j < g; ++j) la.baby[j] = babies[c * g + j].get();
+    }
+    auto run = [&](bool pair, std::vector<DeviceBuffer<uint64_t>>& out) {
+      for (int c = 0; c < 2; ++c)
+        for (int i = 0; i < b; ++i) pa.a[c].out[i] = out[c * b + i].get();
+      if (pair) PHX_CHECK(phx::lt_bsgs_pair(pa, N, s));
+      else for (int c = 0; c < 2; ++c) PHX_CHECK(phx::lt_bsgs(pa.a[c], N, s));
+    };
+    hipEvent_t e0, e1;
+    PHX_CHECK(hipEventCreate(&e0));
+    PHX_CHECK(hipEventCreate(&e1));
+    for (int rep = 0; rep < 3; ++rep)
+      for (bool pair : {false, true}) {
+        run(pair, pair ? out2 : out1);  // warm
+        PHX_CHECK(hipEventRecord(e0, s));
+        for (int it = 0; it < 5; ++it) run(pair, pair ? out2 : out1);
+        PHX_CHECK(hipEventRecord(e1, s));
+        PHX_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        PHX_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        std::printf("{\"ltpair\": \"%s\", \"ms_per_pair\": %.3f}\n", pair ? "pair" : "two", ms / 5);
+      }
+    bool same = true;
+    for (int k = 0; k < 2 * b && same; ++k) same = out1[k].download(s) == out2[k].download(s);
+    report("ltpair_bitexact", same ? 0.0 : 1.0, 0.5, 0);
+    return g_ok ? 0 : 1;
+  }
   if (mode == "chebdepth") {
     // EvalChebyshevSeries through the reference's Paterson-Stockmeyer (host/chebyshev_ps.cpp) for
     // every degree 5..119 on three intervals: levels consumed (a pending rescale counts) against
@@ -751,7 +820,16 @@ int main(int argc, char** argv) {
   if (mode == "batch") {
     // C5 on one GPU: `iters` independent bootstraps, `lanes` of them side by side
     const int lanes = argc > 4 ? std::atoi(argv[4]) : 2;
-    std::vector<PhantomCiphertext> batch(static_cast<size_t>(std::max(1, iters)), ct);
+    // distinct inputs: fresh encryptions of fresh messages at the drained input's level and scale
+    std::vector<PhantomCiphertext> batch(static_cast<size_t>(std::max(1, iters)));
+    std::vector<std::vector<double>> xs(batch.size());
+    for (size_t i = 0; i < batch.size(); ++i) {
+      xs[i].resize(slots);
+      for (auto& v : xs[i]) v = dis(rng);
+      PhantomPlaintext p;
+      enc.encode(ctx, xs[i], ct.scale(), p, ct.chain_index());
+      sk.encrypt_symmetric(ctx, p, batch[i]);
+    }
     std::vector<PhantomCiphertext> warm = boot.EvalBootstrapBatch(
         std::vector<PhantomCiphertext>(batch.begin(), batch.begin() + std::min<size_t>(batch.size(), lanes)), ctx,
         lanes);
@@ -761,12 +839,21 @@ int main(int argc, char** argv) {
     PHX_CHECK(hipDeviceSynchronize());
     const double ms = now_ms() - a;
     double worst = 1e9;
-    for (const auto& o : outs) {
-      std::vector<std::complex<double>> z = decrypt_decode(ctx, sk, enc, o);
+    for (size_t i = 0; i < outs.size(); ++i) {
+      std::vector<std::complex<double>> z = decrypt_decode(ctx, sk, enc, outs[i]);
       std::vector<double> res(slots);
       for (size_t j = 0; j < slots; ++j) res[j] = z[j].real();
-      worst = std::min(worst, compute_bit_precision(x, res));
+      worst = std::min(worst, compute_bit_precision(xs[i], res));
     }
+    // the batch (lanes, two bootstraps in lockstep per lane) equals bootstrapping one at a time,
+    // bit for bit
+    bool same = true;
+    for (size_t i = 0; i < std::min<size_t>(outs.size(), 6); ++i) {
+      const PhantomCiphertext one = boot.EvalBootstrap(batch[i], ctx);
+      same &= one.to_host(ctx.stream()) == outs[i].to_host(ctx.stream()) && one.scale() == outs[i].scale() &&
+              one.chain_index() == outs[i].chain_index();
+    }
+    report("batch_equals_single_bitexact", same ? 0.0 : 1.0, 0.5, outs.empty() ? 0 : outs[0].chain_index());
     std::printf("{\"stage\": \"batch\", \"bootstraps\": %zu, \"lanes\": %d, \"ms_total\": %.2f, "
                 "\"bootstraps_per_s\": %.3f, \"min_avg_bits\": %.2f}\n",
                 outs.size(), lanes, ms, 1e3 * outs.size() / ms, worst);

@@ -913,80 +913,99 @@ const void* FHECKKSRNS::baby_table(const PhantomContext& cc, const LTLevel& lv, 
   return t.second.get();
 }
 
-PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const PhantomCiphertext& in,
-                                          const LTLevel& lv) const {
+// one linear-transform level in three stages (apply_level runs them for one ciphertext,
+// apply_level_pair for two with the inner products of both in one launch)
+struct LevelWork {
   PhantomCiphertext tmp;
-  const PhantomCiphertext& ct = AtLevel(cc, in, lv.chain - 1, sf_, tmp);
+  const PhantomCiphertext* ct = nullptr;
+  size_t Ql = 0, QlP = 0;
+  DeviceBuffer<uint64_t> digits, babies, giants;
+  phx::KsRotateBatchArgs ba;  // the baby steps' launch (level_babies with launch = false leaves it)
+  PhantomCiphertext acc;
+};
+
+void FHECKKSRNS::level_babies(const PhantomContext& cc, const PhantomCiphertext& in, const LTLevel& lv,
+                              LevelWork& w, bool launch) const {
+  w.ct = &AtLevel(cc, in, lv.chain - 1, sf_, w.tmp);
+  const PhantomCiphertext& ct = *w.ct;
   const size_t n = cc.poly_degree(), Ql = cc.get_context_data(ct.chain_index()).coeff_modulus_size();
   const size_t QlP = Ql + cc.size_P();
+  w.Ql = Ql;
+  w.QlP = QlP;
   hipStream_t s = cc.stream();
-  DeviceBuffer<uint64_t> digits = EvalFastRotationPrecompute(cc, ct);
+  w.digits = EvalFastRotationPrecompute(cc, ct);
   // every baby step in one launch (keyswitch_rotate_batch): the digits and c0 are read from HBM
   // once for the level, not once per rotation; baby j at babies + j 2 QlP n
   const size_t baby_words = 2 * QlP * n;
-  DeviceBuffer<uint64_t> babies(static_cast<size_t>(lv.g) * baby_words, s);
-  {
-    const RnsTool& rt = cc.get_context_data(ct.chain_index()).gpu_rns_tool();
-    phx::KsRotateBatchArgs ba;
-    ba.digits = digits.get();
-    ba.entries = static_cast<const phx::KsBatchEntry*>(baby_table(cc, lv, QlP));
-    ba.count = static_cast<uint32_t>(lv.g);
-    ba.qp = cc.mod_QP().q;
-    ba.qp_barrett = cc.mod_QP().barrett;
-    ba.ct = ct.data();
-    ba.pmod = rt.bigP_mod_q();
-    ba.pmod_shoup = rt.bigP_mod_q_shoup();
-    ba.out = babies.get();
-    ba.ql = static_cast<uint32_t>(Ql);
-    ba.qlp = static_cast<uint32_t>(QlP);
-    ba.size_q = static_cast<uint32_t>(cc.size_Q());
-    ba.size_p = static_cast<uint32_t>(cc.size_P());
-    ba.beta = static_cast<uint32_t>(rt.beta());
+  w.babies = DeviceBuffer<uint64_t>(static_cast<size_t>(lv.g) * baby_words, s);
+  const RnsTool& rt = cc.get_context_data(ct.chain_index()).gpu_rns_tool();
+  phx::KsRotateBatchArgs& ba = w.ba;
+  ba.digits = w.digits.get();
+  ba.entries = static_cast<const phx::KsBatchEntry*>(baby_table(cc, lv, QlP));
+  ba.count = static_cast<uint32_t>(lv.g);
+  ba.qp = cc.mod_QP().q;
+  ba.qp_barrett = cc.mod_QP().barrett;
+  ba.ct = ct.data();
+  ba.pmod = rt.bigP_mod_q();
+  ba.pmod_shoup = rt.bigP_mod_q_shoup();
+  ba.out = w.babies.get();
+  ba.ql = static_cast<uint32_t>(Ql);
+  ba.qlp = static_cast<uint32_t>(QlP);
+  ba.size_q = static_cast<uint32_t>(cc.size_Q());
+  ba.size_p = static_cast<uint32_t>(cc.size_P());
+  ba.beta = static_cast<uint32_t>(rt.beta());
+  if (launch) {
     hip_ok(phx::keyswitch_rotate_batch(ba, n, s), "linear transform baby steps");
-    static const bool shapes = std::getenv("PHX_BOOT_TRACE") != nullptr;
-    if (shapes)
-      std::fprintf(stderr, "[lt] chain %zu Ql %zu beta %zu D %d g %d b %d\n", lv.chain, Ql, rt.beta(), lv.D, lv.g, lv.b);
-    size_t rotations = 0;
-    for (int j = 0; j < lv.g; ++j) {
-      const long r = static_cast<long>(j - lv.center) * lv.stride, nn = static_cast<long>(n / 2);
-      rotations += ((r % nn) + nn) % nn != 0;
-    }
-    traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP * rotations, n));
-    // the digits and c0 read, the baby steps written
-    traffic::ciphertexts(traffic::limb_bytes(rt.beta() * QlP + Ql + 2 * QlP * static_cast<size_t>(lv.g), n));
+    w.digits.release();
   }
-  digits.release();
-  // every giant step's inner sum in one launch: giant 0 straight into the accumulator, giants
-  // 1 .. b-1 into one buffer [b - 1][2][QlP][n] so that their moddowns batch
-  const size_t ext_words = 2 * QlP * n;
-  const size_t G = static_cast<size_t>(lv.b - 1);
-  PhantomCiphertext acc;
-  acc.resize(2, QlP, n, s, false);
-  acc.set_chain_index(ct.chain_index());
-  acc.set_ntt_form(true);
-  DeviceBuffer<uint64_t> giants(std::max<size_t>(G, 1) * ext_words, s);
+  static const bool shapes = std::getenv("PHX_BOOT_TRACE") != nullptr;
+  if (shapes)
+    std::fprintf(stderr, "[lt] chain %zu Ql %zu beta %zu D %d g %d b %d\n", lv.chain, Ql, rt.beta(), lv.D, lv.g, lv.b);
+  size_t rotations = 0;
+  for (int j = 0; j < lv.g; ++j) {
+    const long r = static_cast<long>(j - lv.center) * lv.stride, nn = static_cast<long>(n / 2);
+    rotations += ((r % nn) + nn) % nn != 0;
+  }
+  traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP * rotations, n));
+  // the digits and c0 read, the baby steps written
+  traffic::ciphertexts(traffic::limb_bytes(rt.beta() * QlP + Ql + 2 * QlP * static_cast<size_t>(lv.g), n));
+  // giant 0's inner sum goes straight into the accumulator, giants 1 .. b-1 into one buffer
+  // [b - 1][2][QlP][n] so that their moddowns batch
+  w.acc.resize(2, QlP, n, s, false);
+  w.acc.set_chain_index(ct.chain_index());
+  w.acc.set_ntt_form(true);
+  w.giants = DeviceBuffer<uint64_t>(std::max<size_t>(static_cast<size_t>(lv.b - 1), 1) * 2 * QlP * n, s);
+}
+
+phx::LtArgs FHECKKSRNS::level_lt_args(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const {
+  const size_t n = cc.poly_degree(), baby_words = 2 * w.QlP * n, ext_words = 2 * w.QlP * n;
   phx::LtArgs la;
   la.g = lv.g;
   la.b = lv.b;
-  la.Ql = static_cast<int>(Ql);
+  la.Ql = static_cast<int>(w.Ql);
   la.P = static_cast<int>(cc.size_P());
   la.size_Q = static_cast<int>(cc.size_Q());
   la.pts = lv.d_pts.get();
   la.q = cc.mod_QP().q;
   la.barrett = cc.mod_QP().barrett;
-  for (int j = 0; j < lv.g; ++j) la.baby[j] = babies.get() + static_cast<size_t>(j) * baby_words;
-  la.out[0] = acc.data();
-  for (size_t i = 1; i <= G; ++i) la.out[i] = giants.get() + (i - 1) * ext_words;
-  hip_ok(phx::lt_bsgs(la, n, s), "linear transform inner products");
-  {
-    // the level's non-zero diagonals read once; the baby steps read and the inner sums written
-    // once; the input read once (by the modup) and the output written once (after the giant steps)
-    size_t nz = 0;
-    for (const auto& p : lv.pts) nz += p ? 1 : 0;
-    traffic::plaintexts(traffic::limb_bytes(nz * QlP, n));
-    traffic::ciphertexts(traffic::limb_bytes(2 * QlP * static_cast<size_t>(lv.g + lv.b), n));
-  }
-  babies.release();
+  for (int j = 0; j < lv.g; ++j) la.baby[j] = w.babies.get() + static_cast<size_t>(j) * baby_words;
+  la.out[0] = w.acc.data();
+  for (int i = 1; i < lv.b; ++i) la.out[i] = w.giants.get() + static_cast<size_t>(i - 1) * ext_words;
+  // the level's non-zero diagonals read once; the baby steps read and the inner sums written
+  // once; the input read once (by the modup) and the output written once (after the giant steps)
+  size_t nz = 0;
+  for (const auto& p : lv.pts) nz += p ? 1 : 0;
+  traffic::plaintexts(traffic::limb_bytes(nz * w.QlP, n));
+  traffic::ciphertexts(traffic::limb_bytes(2 * w.QlP * static_cast<size_t>(lv.g + lv.b), n));
+  return la;
+}
+
+PhantomCiphertext FHECKKSRNS::level_giants(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const {
+  const PhantomCiphertext& ct = *w.ct;
+  const size_t n = cc.poly_degree(), QlP = w.QlP, Ql = w.Ql, ext_words = 2 * QlP * n;
+  const size_t G = static_cast<size_t>(lv.b - 1);
+  hipStream_t s = cc.stream();
+  w.babies.release();
   if (G > 0) {
     // giant steps accumulate in the extended basis (one moddown at the end).  Their c1's come down
     // to Ql and into their modup digits in one batched pass (one launch per stage over all G,
@@ -996,17 +1015,49 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
     const RnsTool& rt = cc.get_context_data(ct.chain_index()).gpu_rns_tool();
     const size_t dwords = rt.beta() * QlP * n;
     DeviceBuffer<uint64_t> digits(G * dwords, s);
-    rt.moddown_modup(digits.get(), giants.get() + QlP * n, cc.gpu_rns_tables(), s, G, ext_words);
+    rt.moddown_modup(digits.get(), w.giants.get() + QlP * n, cc.gpu_rns_tables(), s, G, ext_words);
     for (size_t i = 1; i <= G; ++i)
-      EvalRotateExtAccumulateDigits(cc, ct.chain_index(), giants.get() + (i - 1) * ext_words,
+      EvalRotateExtAccumulateDigits(cc, ct.chain_index(), w.giants.get() + (i - 1) * ext_words,
                                     digits.get() + (i - 1) * dwords, galois_keys_,
-                                    static_cast<int>(static_cast<long>(lv.g) * static_cast<long>(i) * lv.stride), acc);
+                                    static_cast<int>(static_cast<long>(lv.g) * static_cast<long>(i) * lv.stride), w.acc);
   }
-  acc.set_scale(ct.scale() * sf_.at(lv.chain - 1));
-  acc.SetNoiseScaleDeg(2);
+  w.acc.set_scale(ct.scale() * sf_.at(lv.chain - 1));
+  w.acc.SetNoiseScaleDeg(2);
   // giant steps: each inner sum read once, the level's result written once
   traffic::ciphertexts(traffic::limb_bytes(2 * QlP * static_cast<size_t>(lv.b) + 2 * (Ql - 1), n));
-  return KeySwitchDownRescale(cc, acc);
+  w.giants.release();
+  return KeySwitchDownRescale(cc, w.acc);
+}
+
+PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const PhantomCiphertext& in,
+                                          const LTLevel& lv) const {
+  LevelWork w;
+  level_babies(cc, in, lv, w);
+  hip_ok(phx::lt_bsgs(level_lt_args(cc, lv, w), cc.poly_degree(), cc.stream()), "linear transform inner products");
+  return level_giants(cc, lv, w);
+}
+
+std::vector<PhantomCiphertext> FHECKKSRNS::apply_level_pair(const PhantomContext& cc, const PhantomCiphertext& a,
+                                                            const PhantomCiphertext& b, const LTLevel& lv) const {
+  LevelWork w[2];
+  level_babies(cc, a, lv, w[0], false);
+  level_babies(cc, b, lv, w[1], false);
+  hip_ok(phx::keyswitch_rotate_batch_pair(phx::KsRotateBatchPairArgs{{w[0].ba, w[1].ba}}, cc.poly_degree(), cc.stream()),
+         "linear transform baby steps (pair)");
+  w[0].digits.release();
+  w[1].digits.release();
+  phx::LtPairArgs pa;
+  pa.a[0] = level_lt_args(cc, lv, w[0]);
+  pa.a[1] = level_lt_args(cc, lv, w[1]);
+  if (lv.g == 32 && lv.b <= 8 && w[0].Ql == w[1].Ql) {
+    hip_ok(phx::lt_bsgs_pair(pa, cc.poly_degree(), cc.stream()), "linear transform inner products (pair)");
+  } else {
+    for (const phx::LtArgs& la : pa.a) hip_ok(phx::lt_bsgs(la, cc.poly_degree(), cc.stream()), "linear transform inner products");
+  }
+  std::vector<PhantomCiphertext> r;
+  r.push_back(level_giants(cc, lv, w[0]));
+  r.push_back(level_giants(cc, lv, w[1]));
+  return r;
 }
 
 PhantomCiphertext FHECKKSRNS::EvalCoeffsToSlots(const PhantomCiphertext& ct, const PhantomContext& cc,
@@ -1353,7 +1404,15 @@ std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<
     workers.emplace_back([&, t] {
       try {
         LaneGuard lane(cc, t);
-        for (size_t i = t; i < in.size(); i += k) out[i] = EvalBootstrap(in[i], cc, numSlots);
+        // two at a time in lockstep (shared plaintext reads, EvalMod on four lanes)
+        const Precom& pc = precom(numSlots, cc);
+        size_t i = t;
+        for (; i + k < in.size(); i += 2 * k) {
+          std::vector<PhantomCiphertext> r = bootstrap_pair(in[i], in[i + k], cc, pc);
+          out[i] = std::move(r[0]);
+          out[i + k] = std::move(r[1]);
+        }
+        if (i < in.size()) out[i] = EvalBootstrap(in[i], cc, numSlots);
       } catch (...) {
         err[t] = std::current_exception();
       }
@@ -1409,6 +1468,36 @@ PhantomCiphertext FHECKKSRNS::EvalBootstrap(const PhantomCiphertext& in, const P
   EvalMultConstInplace(cc, finalCiphertext, 1.0 / static_cast<double>(pow2), sf_);
   EvalModReduceInPlace(cc, finalCiphertext, 1);
   return finalCiphertext;
+}
+
+std::vector<PhantomCiphertext> FHECKKSRNS::bootstrap_pair(const PhantomCiphertext& a, const PhantomCiphertext& b,
+                                                          const PhantomContext& cc, const Precom& pc) const {
+  const uint32_t N = static_cast<uint32_t>(cc.poly_degree()), M = 2 * N;
+  if (pc.slots != N / 2) return {bootstrap_once(a, cc, pc), bootstrap_once(b, cc, pc)};
+  std::vector<PhantomCiphertext> x{RaiseWithCorrection(a, cc), RaiseWithCorrection(b, cc)};
+  for (const LTLevel& lv : pc.enc) x = apply_level_pair(cc, x[0], x[1], lv);
+  // the conjugate split of each; EvalMod of the four halves in lockstep
+  std::vector<PhantomCiphertext> halves(4);
+  for (int c = 0; c < 2; ++c) {
+    PhantomCiphertext& enc = x[c];
+    PhantomCiphertext conj = EvalConjFused(cc, enc, galois_keys_);
+    PhantomCiphertext enc_i = enc;
+    sub_inplace(cc, enc_i, conj);
+    add_inplace(cc, enc, conj);
+    MultByMonomialInPlace(cc, enc_i, 3 * M / 4);  // times -i
+    halves[2 * c] = std::move(enc);
+    halves[2 * c + 1] = std::move(enc_i);
+  }
+  halves = eval_mod_lanes(std::move(halves), cc);
+  for (int c = 0; c < 2; ++c) {
+    PhantomCiphertext im = std::move(halves[2 * c + 1]);
+    MultByMonomialInPlace(cc, im, M / 4);  // times i
+    x[c] = std::move(halves[2 * c]);
+    EvalAddAutoInplace(cc, x[c], im, sf_);
+  }
+  for (const LTLevel& lv : pc.dec) x = apply_level_pair(cc, x[0], x[1], lv);
+  for (PhantomCiphertext& d : x) MultByIntegerInPlace(cc, d, uint64_t(1) << correction_);
+  return x;
 }
 
 PhantomCiphertext FHECKKSRNS::bootstrap_once(const PhantomCiphertext& in, const PhantomContext& cc,

@@ -24,6 +24,7 @@
 #include "context.h"
 #include "encoder.h"
 #include "keys.h"
+#include "../csrc/ckks.h"
 
 namespace phantom {
 
@@ -59,6 +60,8 @@ class LeafTableCache {
   std::mutex mu_;
   std::map<std::vector<uint64_t>, DeviceBuffer<uint64_t>> tables_;
 };
+
+struct LevelWork;  // one linear-transform level's working buffers (bootstrap.cpp)
 
 class FHECKKSRNS {
  public:
@@ -224,6 +227,14 @@ class FHECKKSRNS {
                     std::vector<LTLevel>& out, bool encode) const;
   const Precom& precom(uint32_t numSlots, const PhantomContext& cc) const;
   PhantomCiphertext apply_level(const PhantomContext& cc, const PhantomCiphertext& ct, const LTLevel& lv) const;
+  void level_babies(const PhantomContext& cc, const PhantomCiphertext& in, const LTLevel& lv, LevelWork& w,
+                    bool launch = true) const;
+  phx::LtArgs level_lt_args(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const;
+  PhantomCiphertext level_giants(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const;
+  // apply_level of two ciphertexts in lockstep: the inner products of both in one launch that
+  // reads the level's plaintexts about once (lt_bsgs_pair); each result equals apply_level's
+  std::vector<PhantomCiphertext> apply_level_pair(const PhantomContext& cc, const PhantomCiphertext& a,
+                                                  const PhantomCiphertext& b, const LTLevel& lv) const;
   // the reference-signature precompute / evaluate pair (above): one direction's levels built from
   // a caller's roots, and the level structure re-attached to a caller's plaintext set
   std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>> precompute_dir(
@@ -247,6 +258,10 @@ class FHECKKSRNS {
                                                  const std::vector<double>& coeffs) const;
   void double_angle_lanes(std::vector<PhantomCiphertext>& v, const PhantomContext& cc, uint32_t numIter) const;
   PhantomCiphertext bootstrap_once(const PhantomCiphertext& ct, const PhantomContext& cc, const Precom& pc) const;
+  // bootstrap_once of two ciphertexts in lockstep (full packing): paired linear-transform levels,
+  // EvalMod on four lanes; each result equals bootstrap_once's, bit for bit
+  std::vector<PhantomCiphertext> bootstrap_pair(const PhantomCiphertext& a, const PhantomCiphertext& b,
+                                                const PhantomContext& cc, const Precom& pc) const;
 
   PhantomCKKSEncoder& encoder_;
   std::vector<double> sf_, sf_big_;

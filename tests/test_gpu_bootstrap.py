@@ -115,13 +115,17 @@ def test_bootstrapping_example_verbatim():
 
 
 def test_bootstrap_batch_on_stream_lanes():
-    """EvalBootstrapBatch: 6 bootstraps, 3 stream lanes side by side (C5's per-GPU path); every
-    output keeps the single-bootstrap precision."""
-    rc, lines, err = _run("batch", "16", "6", "3", timeout=115)
+    """EvalBootstrapBatch: 6 bootstraps of distinct inputs, 3 stream lanes side by side, two
+    bootstraps in lockstep per lane (C5's per-GPU path: paired linear-transform levels, EvalMod on
+    four lanes); every output keeps the single-bootstrap precision and equals EvalBootstrap of its
+    input bit for bit."""
+    rc, lines, err = _run("batch", "16", "6", "3", timeout=150)
     assert rc == 0, (lines, err)
     b = [l for l in lines if l.get("stage") == "batch"][0]
     assert b["bootstraps"] == 6 and b["lanes"] == 3, b
     assert b["min_avg_bits"] > 9.85, b
+    checks = {l["check"]: l for l in lines if "check" in l}
+    assert checks["batch_equals_single_bitexact"]["ok"], checks
 
 
 # ---- bootstrapping sessions through the C-ABI (include/phantom_amd.h phantom_boot_*) ------------

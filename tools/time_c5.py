@@ -1,0 +1,15 @@
+"""C5 throughput of a library variant: bench.c5_leg (256 bootstraps, 4 lanes, 8 verified) on the
+variant's ctypes binding.  usage: python tools/time_c5.py tools/variants/<name>/py"""
+import os
+import sys
+
+sys.path.insert(0, sys.argv[1])
+import phantom_amd as PA  # noqa: E402,F401  (the variant's binding, loaded first)
+import torch  # noqa: E402
+
+sys.path.insert(1, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+torch.cuda.set_device(0)
+r = bench.c5_leg(None, torch, 1, 0, 0, total=256, lanes=4, verify=8)
+print(os.path.basename(os.path.dirname(os.path.abspath(sys.argv[1]))), r["bootstraps_per_s"], r["min_avg_bits"], flush=True)
