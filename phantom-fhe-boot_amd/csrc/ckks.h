@@ -53,14 +53,16 @@ struct LtArgs {
   int g = 0, b = 0, Ql = 0, P = 0, size_Q = 0;
 };
 hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s);
-// lt_bsgs of two ciphertexts at one level through the same plaintexts (two bootstraps in
-// lockstep) in one launch, the two ciphertexts' blocks for the same elements on one XCD so that
-// the plaintexts are read from HBM about once for both.  a[0] and a[1] differ only in baby / out;
-// g == 32 and b <= 8 (the bootstrap's levels).  Each result equals its own lt_bsgs, bit for bit.
-struct LtPairArgs {
-  LtArgs a[2];
+// lt_bsgs of `count` (2..4) ciphertexts at one level through the same plaintexts (bootstraps in
+// lockstep) in one launch, the ciphertexts' blocks for the same elements on one XCD so that the
+// plaintexts are read from HBM about once for all.  a[0..count) differ only in baby / out; g == 32
+// and b <= 8 (the bootstrap's levels).  Each result equals its own lt_bsgs, bit for bit.
+constexpr int kLtGroupMax = 4;
+struct LtGroupArgs {
+  LtArgs a[kLtGroupMax];
+  int count = 0;
 };
-hipError_t lt_bsgs_pair(const LtPairArgs& pa, size_t n, hipStream_t s);
+hipError_t lt_bsgs_group(const LtGroupArgs& ga, size_t n, hipStream_t s);
 
 // ---- Chebyshev leaves: M linear combinations of the same K ciphertexts in one pass ----------
 //   out[m][t][l] = sum_k in[k][t][l] * coef[m][k][l] + (t == 0 ? cadd[m][l] : 0)   (mod q_l)

@@ -246,18 +246,19 @@ __global__ __launch_bounds__(kBlock, 2) void lt_bsgs_wide_kernel(LtArgs a, uint3
   lt_bsgs_wide<G, B>(a, log_n, total, blockIdx.x, gridDim.x, ptab);
 }
 
-// two ciphertexts through the same plaintexts (lt_bsgs_pair): the blocks of the two that cover
-// the same elements are dealt to one XCD 8 dispatches apart (blocks b and b + 8 share an XCD under
-// round-robin placement), so the second one's plaintext reads are served by that XCD's L2
+// `count` ciphertexts through the same plaintexts (lt_bsgs_group): the blocks of the ciphertexts
+// that cover the same elements are dealt to one XCD 8 dispatches apart (blocks b and b + 8 share an
+// XCD under round-robin placement), so the followers' plaintext reads are served by that XCD's L2
 template <int G, int B>
-__global__ __launch_bounds__(kBlock, 2) void lt_bsgs_pair_kernel(LtPairArgs pa, uint32_t log_n, size_t total) {
+__global__ __launch_bounds__(kBlock, 2) void lt_bsgs_group_kernel(LtGroupArgs ga, uint32_t log_n, size_t total) {
   extern __shared__ const uint64_t* ptab[];
-  const LtArgs& a0 = pa.a[0];
+  const LtArgs& a0 = ga.a[0];
   for (int k = threadIdx.x; k < a0.b * G; k += kBlock) ptab[k] = a0.pts[k];
   __syncthreads();
+  const uint32_t K = static_cast<uint32_t>(ga.count);
   const uint32_t b = blockIdx.x, x = b % 8, k = b / 8;
-  const uint32_t c = k % 2, blk = (k / 2) * 8 + x, nblk = gridDim.x / 2;
-  lt_bsgs_wide<G, B>(pa.a[c], log_n, total, blk, nblk, ptab);
+  const uint32_t c = k % K, blk = (k / K) * 8 + x, nblk = gridDim.x / K;
+  lt_bsgs_wide<G, B>(ga.a[c], log_n, total, blk, nblk, ptab);
 }
 
 template <bool MUL, bool ACC>
@@ -473,19 +474,21 @@ hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t lt_bsgs_pair(const LtPairArgs& pa, size_t n, hipStream_t s) {
-  const LtArgs& a = pa.a[0];
-  const LtArgs& b = pa.a[1];
-  if (a.g != 32 || a.b < 1 || a.b > 8 || !a.pts || b.g != a.g || b.b != a.b || b.pts != a.pts || b.Ql != a.Ql ||
-      b.P != a.P || b.size_Q != a.size_Q)
-    return hipErrorInvalidValue;
-  for (const LtArgs* x : {&a, &b})
-    for (int i = 0; i < x->b; ++i)
-      if (!x->out[i]) return hipErrorInvalidValue;
+hipError_t lt_bsgs_group(const LtGroupArgs& ga, size_t n, hipStream_t s) {
+  if (ga.count < 2 || ga.count > kLtGroupMax) return hipErrorInvalidValue;
+  const LtArgs& a = ga.a[0];
+  if (a.g != 32 || a.b < 1 || a.b > 8 || !a.pts) return hipErrorInvalidValue;
+  for (int c = 0; c < ga.count; ++c) {
+    const LtArgs& x = ga.a[c];
+    if (x.g != a.g || x.b != a.b || x.pts != a.pts || x.Ql != a.Ql || x.P != a.P || x.size_Q != a.size_Q)
+      return hipErrorInvalidValue;
+    for (int i = 0; i < x.b; ++i)
+      if (!x.out[i]) return hipErrorInvalidValue;
+  }
   const size_t total = n * static_cast<size_t>(a.Ql + a.P);
   const size_t lds = static_cast<size_t>(a.b) * a.g * sizeof(const uint64_t*);
   const int per = (grid_for(total) + 7) / 8 * 8;  // blocks per ciphertext, whole XCD rounds
-  lt_bsgs_pair_kernel<32, 8><<<2 * per, kBlock, lds, s>>>(pa, __builtin_ctzll(n), total);
+  lt_bsgs_group_kernel<32, 8><<<ga.count * per, kBlock, lds, s>>>(ga, __builtin_ctzll(n), total);
   return hipGetLastError();
 }
 

@@ -757,25 +757,25 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_kernel(KsRotateArgs a, uint3
 // every entry, so an entry reads only its key halves from HBM; those loads are issued for entry
 // k + 1 before entry k's barrier and gather, so they are in flight while the gather runs.
 //
-// PAIR: two ciphertexts' baby steps through the same keys (two bootstraps in lockstep) in one
-// launch; the two ciphertexts' workgroups of the same (limb, source block) are dealt to one XCD 8
-// dispatches apart (blocks b and b + 8 share an XCD under round-robin placement), so the second
-// reads the key halves from that XCD's L2.
-template <int BETA, bool PAIR>
-__global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchPairArgs pa, uint32_t log_n) {
+// GROUP: `count` ciphertexts' baby steps through the same keys (bootstraps in lockstep) in one
+// launch; the ciphertexts' workgroups of the same (limb, source block) are dealt to one XCD 8
+// dispatches apart (blocks b and b + 8 share an XCD under round-robin placement), so the followers
+// read the key halves from that XCD's L2.
+template <int BETA, bool GROUP>
+__global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGroupArgs pa, uint32_t log_n) {
   constexpr uint32_t bsz = kGalB;
   constexpr int PP = kGalB / 2 / kBlock;  // pairs per thread
   __shared__ uint64_t s0[2][kGalB], s1[2][kGalB];
   const uint32_t nb = (1u << log_n) / bsz;
   uint32_t bid = blockIdx.x;
   int c = 0;
-  if constexpr (PAIR) {
-    const uint32_t x = bid % 8, k = bid / 8;
-    c = static_cast<int>(k % 2);
-    bid = (k / 2) * 8 + x;
+  if constexpr (GROUP) {
+    const uint32_t K = static_cast<uint32_t>(pa.count), x = bid % 8, k = bid / 8;
+    c = static_cast<int>(k % K);
+    bid = (k / K) * 8 + x;
   }
   const KsRotateBatchArgs& a = pa.a[c];
-  if (PAIR && bid >= a.qlp * nb) return;  // the rounding of the pair grid (workgroup-uniform, no barrier passed)
+  if (GROUP && bid >= a.qlp * nb) return;  // the rounding of the group grid (workgroup-uniform, no barrier passed)
   const uint32_t l = bid / nb, sblk = bid % nb;
   const uint32_t twr = l >= a.ql ? a.size_q + (l - a.ql) : l;
   const uint64_t q = a.qp[twr], r0 = a.qp_barrett[2 * twr], r1 = a.qp_barrett[2 * twr + 1];
@@ -1231,37 +1231,40 @@ hipError_t keyswitch_rotate_batch(const KsRotateBatchArgs& a, size_t n, hipStrea
   const uint32_t log_n = __builtin_ctzll(n), bsz = static_cast<uint32_t>(std::min<size_t>(n, kGalB));
   const dim3 grid(static_cast<uint32_t>(a.qlp * (n / bsz)));
   switch (bsz == kGalB ? a.beta : 0) {
-    case 1: ks_rotate_batch_full<1, false><<<grid, kBlock, 0, s>>>(KsRotateBatchPairArgs{{a, a}}, log_n); break;
-    case 2: ks_rotate_batch_full<2, false><<<grid, kBlock, 0, s>>>(KsRotateBatchPairArgs{{a, a}}, log_n); break;
-    case 3: ks_rotate_batch_full<3, false><<<grid, kBlock, 0, s>>>(KsRotateBatchPairArgs{{a, a}}, log_n); break;
-    case 4: ks_rotate_batch_full<4, false><<<grid, kBlock, 0, s>>>(KsRotateBatchPairArgs{{a, a}}, log_n); break;
+    case 1: ks_rotate_batch_full<1, false><<<grid, kBlock, 0, s>>>(KsRotateBatchGroupArgs{{a}, 1}, log_n); break;
+    case 2: ks_rotate_batch_full<2, false><<<grid, kBlock, 0, s>>>(KsRotateBatchGroupArgs{{a}, 1}, log_n); break;
+    case 3: ks_rotate_batch_full<3, false><<<grid, kBlock, 0, s>>>(KsRotateBatchGroupArgs{{a}, 1}, log_n); break;
+    case 4: ks_rotate_batch_full<4, false><<<grid, kBlock, 0, s>>>(KsRotateBatchGroupArgs{{a}, 1}, log_n); break;
     default: ks_rotate_batch_kernel<<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
   }
   return hipGetLastError();
 }
 
-hipError_t keyswitch_rotate_batch_pair(const KsRotateBatchPairArgs& pa, size_t n, hipStream_t s) {
-  const KsRotateBatchArgs& a = pa.a[0];
-  const KsRotateBatchArgs& b = pa.a[1];
-  for (const KsRotateBatchArgs* x : {&a, &b})
-    if (!x->digits || !x->entries || !x->ct || !x->out || !x->pmod || !x->pmod_shoup || x->beta == 0 || x->ql > x->qlp)
+hipError_t keyswitch_rotate_batch_group(const KsRotateBatchGroupArgs& ga, size_t n, hipStream_t s) {
+  if (ga.count < 2 || ga.count > kKsGroupMax) return hipErrorInvalidValue;
+  const KsRotateBatchArgs& a = ga.a[0];
+  for (int c = 0; c < ga.count; ++c) {
+    const KsRotateBatchArgs& x = ga.a[c];
+    if (!x.digits || !x.entries || !x.ct || !x.out || !x.pmod || !x.pmod_shoup || x.beta == 0 || x.ql > x.qlp)
       return hipErrorInvalidValue;
-  if (b.entries != a.entries || b.count != a.count || b.qlp != a.qlp || b.ql != a.ql || b.beta != a.beta ||
-      b.size_q != a.size_q || b.size_p != a.size_p)
-    return hipErrorInvalidValue;
+    if (x.entries != a.entries || x.count != a.count || x.qlp != a.qlp || x.ql != a.ql || x.beta != a.beta ||
+        x.size_q != a.size_q || x.size_p != a.size_p)
+      return hipErrorInvalidValue;
+  }
   if (a.qlp == 0 || a.count == 0) return hipSuccess;
-  if (n < kGalB || a.beta > 4) {  // the shapes without the register-resident form: two launches
-    hipError_t e = keyswitch_rotate_batch(a, n, s);
-    return e != hipSuccess ? e : keyswitch_rotate_batch(b, n, s);
+  if (n < kGalB || a.beta > 4) {  // the shapes without the register-resident form: one launch each
+    for (int c = 0; c < ga.count; ++c)
+      if (hipError_t e = keyswitch_rotate_batch(ga.a[c], n, s)) return e;
+    return hipSuccess;
   }
   const uint32_t log_n = __builtin_ctzll(n);
   const uint32_t per = (a.qlp * static_cast<uint32_t>(n / kGalB) + 7) / 8 * 8;
-  const dim3 grid(2 * per);
+  const dim3 grid(static_cast<uint32_t>(ga.count) * per);
   switch (a.beta) {
-    case 1: ks_rotate_batch_full<1, true><<<grid, kBlock, 0, s>>>(pa, log_n); break;
-    case 2: ks_rotate_batch_full<2, true><<<grid, kBlock, 0, s>>>(pa, log_n); break;
-    case 3: ks_rotate_batch_full<3, true><<<grid, kBlock, 0, s>>>(pa, log_n); break;
-    default: ks_rotate_batch_full<4, true><<<grid, kBlock, 0, s>>>(pa, log_n); break;
+    case 1: ks_rotate_batch_full<1, true><<<grid, kBlock, 0, s>>>(ga, log_n); break;
+    case 2: ks_rotate_batch_full<2, true><<<grid, kBlock, 0, s>>>(ga, log_n); break;
+    case 3: ks_rotate_batch_full<3, true><<<grid, kBlock, 0, s>>>(ga, log_n); break;
+    default: ks_rotate_batch_full<4, true><<<grid, kBlock, 0, s>>>(ga, log_n); break;
   }
   return hipGetLastError();
 }

@@ -440,7 +440,7 @@ int main(int argc, char** argv) {
   }
   if (mode == "ltpair") {
     // the linear-transform inner products of two ciphertexts: two lt_bsgs launches against one
-    // lt_bsgs_pair launch (the plaintexts shared through L2), at the CoeffToSlot level shape
+    // lt_bsgs_group launch (the plaintexts shared through L2), at the CoeffToSlot level shape
     // (Ql = 30, P = 10, g = 32, b = 8); outputs compared bit for bit
     const size_t QlP = ctx.size_Q() + ctx.size_P(), words = 2 * QlP * N;
     const int g = 32, b = 8;
@@ -468,7 +468,8 @@ int main(int argc, char** argv) {
       out1.emplace_back(words, s);
       out2.emplace_back(words, s);
     }
-    phx::LtPairArgs pa;
+    phx::LtGroupArgs pa;
+    pa.count = 2;
     for (int c = 0; c < 2; ++c) {
       phx::LtArgs& la = pa.a[c];
       la.g = g;
@@ -484,7 +485,7 @@ int main(int argc, char** argv) {
     auto run = [&](bool pair, std::vector<DeviceBuffer<uint64_t>>& out) {
       for (int c = 0; c < 2; ++c)
         for (int i = 0; i < b; ++i) pa.a[c].out[i] = out[c * b + i].get();
-      if (pair) PHX_CHECK(phx::lt_bsgs_pair(pa, N, s));
+      if (pair) PHX_CHECK(phx::lt_bsgs_group(pa, N, s));
       else for (int c = 0; c < 2; ++c) PHX_CHECK(phx::lt_bsgs(pa.a[c], N, s));
     };
     hipEvent_t e0, e1;

@@ -1037,26 +1037,34 @@ PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const Phanto
   return level_giants(cc, lv, w);
 }
 
-std::vector<PhantomCiphertext> FHECKKSRNS::apply_level_pair(const PhantomContext& cc, const PhantomCiphertext& a,
-                                                            const PhantomCiphertext& b, const LTLevel& lv) const {
-  LevelWork w[2];
-  level_babies(cc, a, lv, w[0], false);
-  level_babies(cc, b, lv, w[1], false);
-  hip_ok(phx::keyswitch_rotate_batch_pair(phx::KsRotateBatchPairArgs{{w[0].ba, w[1].ba}}, cc.poly_degree(), cc.stream()),
-         "linear transform baby steps (pair)");
-  w[0].digits.release();
-  w[1].digits.release();
-  phx::LtPairArgs pa;
-  pa.a[0] = level_lt_args(cc, lv, w[0]);
-  pa.a[1] = level_lt_args(cc, lv, w[1]);
-  if (lv.g == 32 && lv.b <= 8 && w[0].Ql == w[1].Ql) {
-    hip_ok(phx::lt_bsgs_pair(pa, cc.poly_degree(), cc.stream()), "linear transform inner products (pair)");
+std::vector<PhantomCiphertext> FHECKKSRNS::apply_level_group(const PhantomContext& cc,
+                                                             const std::vector<const PhantomCiphertext*>& in,
+                                                             const LTLevel& lv) const {
+  const int K = static_cast<int>(in.size());
+  if (K < 2 || K > phx::kLtGroupMax) throw std::invalid_argument("apply_level_group: 2 to 4 ciphertexts");
+  std::vector<LevelWork> w(K);
+  phx::KsRotateBatchGroupArgs ka;
+  ka.count = K;
+  for (int c = 0; c < K; ++c) {
+    level_babies(cc, *in[c], lv, w[c], false);
+    ka.a[c] = w[c].ba;
+  }
+  hip_ok(phx::keyswitch_rotate_batch_group(ka, cc.poly_degree(), cc.stream()), "linear transform baby steps (group)");
+  for (LevelWork& x : w) x.digits.release();
+  phx::LtGroupArgs ga;
+  ga.count = K;
+  bool same_ql = true;
+  for (int c = 0; c < K; ++c) {
+    ga.a[c] = level_lt_args(cc, lv, w[c]);
+    same_ql &= w[c].Ql == w[0].Ql;
+  }
+  if (lv.g == 32 && lv.b <= 8 && same_ql) {
+    hip_ok(phx::lt_bsgs_group(ga, cc.poly_degree(), cc.stream()), "linear transform inner products (group)");
   } else {
-    for (const phx::LtArgs& la : pa.a) hip_ok(phx::lt_bsgs(la, cc.poly_degree(), cc.stream()), "linear transform inner products");
+    for (int c = 0; c < K; ++c) hip_ok(phx::lt_bsgs(ga.a[c], cc.poly_degree(), cc.stream()), "linear transform inner products");
   }
   std::vector<PhantomCiphertext> r;
-  r.push_back(level_giants(cc, lv, w[0]));
-  r.push_back(level_giants(cc, lv, w[1]));
+  for (int c = 0; c < K; ++c) r.push_back(level_giants(cc, lv, w[c]));
   return r;
 }
 
@@ -1404,15 +1412,22 @@ std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<
     workers.emplace_back([&, t] {
       try {
         LaneGuard lane(cc, t);
-        // two at a time in lockstep (shared plaintext reads, EvalMod on four lanes)
+        // up to kBootGroup of the lane's ciphertexts at a time in lockstep (shared plaintext and
+        // key reads, EvalMod on 2 x group lanes)
         const Precom& pc = precom(numSlots, cc);
-        size_t i = t;
-        for (; i + k < in.size(); i += 2 * k) {
-          std::vector<PhantomCiphertext> r = bootstrap_pair(in[i], in[i + k], cc, pc);
-          out[i] = std::move(r[0]);
-          out[i + k] = std::move(r[1]);
+        std::vector<size_t> mine;
+        for (size_t i = t; i < in.size(); i += k) mine.push_back(i);
+        for (size_t g0 = 0; g0 < mine.size(); g0 += kBootGroup) {
+          const size_t cnt = std::min(kBootGroup, mine.size() - g0);
+          if (cnt == 1) {
+            out[mine[g0]] = EvalBootstrap(in[mine[g0]], cc, numSlots);
+            continue;
+          }
+          std::vector<const PhantomCiphertext*> grp;
+          for (size_t m = 0; m < cnt; ++m) grp.push_back(&in[mine[g0 + m]]);
+          std::vector<PhantomCiphertext> r = bootstrap_group(grp, cc, pc);
+          for (size_t m = 0; m < cnt; ++m) out[mine[g0 + m]] = std::move(r[m]);
         }
-        if (i < in.size()) out[i] = EvalBootstrap(in[i], cc, numSlots);
       } catch (...) {
         err[t] = std::current_exception();
       }
@@ -1470,15 +1485,26 @@ PhantomCiphertext FHECKKSRNS::EvalBootstrap(const PhantomCiphertext& in, const P
   return finalCiphertext;
 }
 
-std::vector<PhantomCiphertext> FHECKKSRNS::bootstrap_pair(const PhantomCiphertext& a, const PhantomCiphertext& b,
-                                                          const PhantomContext& cc, const Precom& pc) const {
+std::vector<PhantomCiphertext> FHECKKSRNS::bootstrap_group(const std::vector<const PhantomCiphertext*>& in,
+                                                           const PhantomContext& cc, const Precom& pc) const {
   const uint32_t N = static_cast<uint32_t>(cc.poly_degree()), M = 2 * N;
-  if (pc.slots != N / 2) return {bootstrap_once(a, cc, pc), bootstrap_once(b, cc, pc)};
-  std::vector<PhantomCiphertext> x{RaiseWithCorrection(a, cc), RaiseWithCorrection(b, cc)};
-  for (const LTLevel& lv : pc.enc) x = apply_level_pair(cc, x[0], x[1], lv);
-  // the conjugate split of each; EvalMod of the four halves in lockstep
-  std::vector<PhantomCiphertext> halves(4);
-  for (int c = 0; c < 2; ++c) {
+  const size_t K = in.size();
+  if (pc.slots != N / 2 || K < 2) {
+    std::vector<PhantomCiphertext> r;
+    for (const PhantomCiphertext* c : in) r.push_back(bootstrap_once(*c, cc, pc));
+    return r;
+  }
+  std::vector<PhantomCiphertext> x;
+  for (const PhantomCiphertext* c : in) x.push_back(RaiseWithCorrection(*c, cc));
+  auto level = [&](const LTLevel& lv) {
+    std::vector<const PhantomCiphertext*> p;
+    for (const PhantomCiphertext& c : x) p.push_back(&c);
+    x = apply_level_group(cc, p, lv);
+  };
+  for (const LTLevel& lv : pc.enc) level(lv);
+  // the conjugate split of each; EvalMod of all 2K halves in lockstep
+  std::vector<PhantomCiphertext> halves(2 * K);
+  for (size_t c = 0; c < K; ++c) {
     PhantomCiphertext& enc = x[c];
     PhantomCiphertext conj = EvalConjFused(cc, enc, galois_keys_);
     PhantomCiphertext enc_i = enc;
@@ -1489,13 +1515,13 @@ std::vector<PhantomCiphertext> FHECKKSRNS::bootstrap_pair(const PhantomCiphertex
     halves[2 * c + 1] = std::move(enc_i);
   }
   halves = eval_mod_lanes(std::move(halves), cc);
-  for (int c = 0; c < 2; ++c) {
+  for (size_t c = 0; c < K; ++c) {
     PhantomCiphertext im = std::move(halves[2 * c + 1]);
     MultByMonomialInPlace(cc, im, M / 4);  // times i
     x[c] = std::move(halves[2 * c]);
     EvalAddAutoInplace(cc, x[c], im, sf_);
   }
-  for (const LTLevel& lv : pc.dec) x = apply_level_pair(cc, x[0], x[1], lv);
+  for (const LTLevel& lv : pc.dec) level(lv);
   for (PhantomCiphertext& d : x) MultByIntegerInPlace(cc, d, uint64_t(1) << correction_);
   return x;
 }

@@ -231,10 +231,11 @@ class FHECKKSRNS {
                     bool launch = true) const;
   phx::LtArgs level_lt_args(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const;
   PhantomCiphertext level_giants(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const;
-  // apply_level of two ciphertexts in lockstep: the inner products of both in one launch that
-  // reads the level's plaintexts about once (lt_bsgs_pair); each result equals apply_level's
-  std::vector<PhantomCiphertext> apply_level_pair(const PhantomContext& cc, const PhantomCiphertext& a,
-                                                  const PhantomCiphertext& b, const LTLevel& lv) const;
+  // apply_level of 2..4 ciphertexts in lockstep: their baby steps and inner products each in one
+  // launch that reads the level's keys / plaintexts about once for all; each result equals apply_level's
+  std::vector<PhantomCiphertext> apply_level_group(const PhantomContext& cc,
+                                                   const std::vector<const PhantomCiphertext*>& in,
+                                                   const LTLevel& lv) const;
   // the reference-signature precompute / evaluate pair (above): one direction's levels built from
   // a caller's roots, and the level structure re-attached to a caller's plaintext set
   std::vector<std::vector<std::shared_ptr<PhantomPlaintext>>> precompute_dir(
@@ -258,10 +259,11 @@ class FHECKKSRNS {
                                                  const std::vector<double>& coeffs) const;
   void double_angle_lanes(std::vector<PhantomCiphertext>& v, const PhantomContext& cc, uint32_t numIter) const;
   PhantomCiphertext bootstrap_once(const PhantomCiphertext& ct, const PhantomContext& cc, const Precom& pc) const;
-  // bootstrap_once of two ciphertexts in lockstep (full packing): paired linear-transform levels,
-  // EvalMod on four lanes; each result equals bootstrap_once's, bit for bit
-  std::vector<PhantomCiphertext> bootstrap_pair(const PhantomCiphertext& a, const PhantomCiphertext& b,
-                                                const PhantomContext& cc, const Precom& pc) const;
+  // bootstrap_once of 2..4 ciphertexts in lockstep (full packing): grouped linear-transform levels,
+  // EvalMod on 2 x group lanes; each result equals bootstrap_once's, bit for bit
+  static constexpr size_t kBootGroup = 4;
+  std::vector<PhantomCiphertext> bootstrap_group(const std::vector<const PhantomCiphertext*>& in,
+                                                 const PhantomContext& cc, const Precom& pc) const;
 
   PhantomCKKSEncoder& encoder_;
   std::vector<double> sf_, sf_big_;

@@ -115,14 +115,14 @@ def test_bootstrapping_example_verbatim():
 
 
 def test_bootstrap_batch_on_stream_lanes():
-    """EvalBootstrapBatch: 6 bootstraps of distinct inputs, 3 stream lanes side by side, two
-    bootstraps in lockstep per lane (C5's per-GPU path: paired linear-transform levels, EvalMod on
-    four lanes); every output keeps the single-bootstrap precision and equals EvalBootstrap of its
+    """EvalBootstrapBatch: 8 bootstraps of distinct inputs, 2 stream lanes side by side, four
+    bootstraps in lockstep per lane (C5's per-GPU path: grouped linear-transform levels, EvalMod on
+    eight lanes); every output keeps the single-bootstrap precision and equals EvalBootstrap of its
     input bit for bit."""
-    rc, lines, err = _run("batch", "16", "6", "3", timeout=150)
+    rc, lines, err = _run("batch", "16", "8", "2", timeout=150)
     assert rc == 0, (lines, err)
     b = [l for l in lines if l.get("stage") == "batch"][0]
-    assert b["bootstraps"] == 6 and b["lanes"] == 3, b
+    assert b["bootstraps"] == 8 and b["lanes"] == 2, b
     assert b["min_avg_bits"] > 9.85, b
     checks = {l["check"]: l for l in lines if "check" in l}
     assert checks["batch_equals_single_bitexact"]["ok"], checks

@@ -58,7 +58,8 @@ __device__ __forceinline__ void step(uint64_t& a, uint32_t b) {
   a = (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-template <int OP>
+// CH independent chains, 16 / CH dependent steps each per iteration (16 instructions)
+template <int OP, int CH>
 __global__ void __launch_bounds__(256) bench(uint64_t* sink, uint64_t* cycles, int iters, uint32_t seed) {
   uint64_t a[8];
 #pragma unroll
@@ -67,9 +68,9 @@ __global__ void __launch_bounds__(256) bench(uint64_t* sink, uint64_t* cycles, i
   const uint64_t t0 = clock64();
   for (int i = 0; i < iters; ++i) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < 16 / CH; ++u) {
 #pragma unroll
-      for (int c = 0; c < 8; ++c) step<OP>(a[c], b);
+      for (int c = 0; c < CH; ++c) step<OP>(a[c], b);
     }
   }
   const uint64_t t1 = clock64();
@@ -81,20 +82,20 @@ __global__ void __launch_bounds__(256) bench(uint64_t* sink, uint64_t* cycles, i
   if ((threadIdx.x & 63) == 0) cycles[gid / 64] = t1 - t0;
 }
 
-template <int OP>
+template <int OP, int CH = 8>
 static int run(int waves_per_simd, int cus, int iters) {
   const int blocks = cus * waves_per_simd;  // 256 threads = one wave per SIMD per block
   const size_t threads = static_cast<size_t>(blocks) * 256;
   uint64_t *sink = nullptr, *cyc = nullptr;
   CHECK(hipMalloc(&sink, threads * 8));
   CHECK(hipMalloc(&cyc, threads / 64 * 8));
-  hipLaunchKernelGGL(bench<OP>, dim3(blocks), dim3(256), 0, nullptr, sink, cyc, iters, 0x9E3779B9u);
+  hipLaunchKernelGGL((bench<OP, CH>), dim3(blocks), dim3(256), 0, nullptr, sink, cyc, iters, 0x9E3779B9u);
   CHECK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   CHECK(hipEventRecord(e0, nullptr));
-  hipLaunchKernelGGL(bench<OP>, dim3(blocks), dim3(256), 0, nullptr, sink, cyc, iters, 0x9E3779B9u);
+  hipLaunchKernelGGL((bench<OP, CH>), dim3(blocks), dim3(256), 0, nullptr, sink, cyc, iters, 0x9E3779B9u);
   CHECK(hipEventRecord(e1, nullptr));
   CHECK(hipDeviceSynchronize());
   float ms = 0;
@@ -105,9 +106,9 @@ static int run(int waves_per_simd, int cus, int iters) {
   for (uint64_t c : h) mean += static_cast<double>(c);
   mean /= h.size();
   const double per_wave = mean / (static_cast<double>(iters) * 16);
-  std::printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_instr_per_wave\": %.2f, "
+  std::printf("{\"op\": \"%s\", \"chains\": %d, \"waves_per_simd\": %d, \"cycles_per_instr_per_wave\": %.2f, "
               "\"cycles_per_instr_per_simd\": %.2f, \"kernel_ms\": %.3f}\n",
-              kNames[OP], waves_per_simd, per_wave, per_wave / waves_per_simd, ms);
+              kNames[OP], CH, waves_per_simd, per_wave, per_wave / waves_per_simd, ms);
   CHECK(hipFree(sink));
   CHECK(hipFree(cyc));
   return 0;
@@ -115,8 +116,16 @@ static int run(int waves_per_simd, int cus, int iters) {
 
 template <int OP>
 static int sweep(int cus, int iters) {
-  for (int w : {1, 2, 4})
+  for (int w : {1, 2, 3, 4, 6, 8})
     if (run<OP>(w, cus, iters)) return 1;
+  return 0;
+}
+// instruction-level parallelism inside one wave against waves per SIMD
+template <int OP>
+static int sweep_ilp(int cus, int iters) {
+  for (int w : {1, 2, 4}) {
+    if (run<OP, 1>(w, cus, iters) || run<OP, 2>(w, cus, iters) || run<OP, 4>(w, cus, iters)) return 1;
+  }
   return 0;
 }
 
@@ -134,5 +143,8 @@ int main() {
   rc |= sweep<BFI>(cus, iters);
   rc |= sweep<FMA_F64>(cus, iters);
   rc |= sweep<MUL_F64>(cus, iters);
+  rc |= sweep_ilp<MUL_LO>(cus, iters);
+  rc |= sweep_ilp<MAD_U64>(cus, iters);
+  rc |= sweep_ilp<ADD_U32>(cus, iters);
   return rc;
 }
