@@ -191,6 +191,14 @@ struct KsRotateArgs {
   bool accumulate = false;
 };
 hipError_t keyswitch_rotate(const KsRotateArgs& a, int mode, size_t n, hipStream_t s);
+// keyswitch_rotate of `count` (2..kKsGroupMax) ciphertexts by the same rotation (evk, perm) in one
+// launch, their workgroups of an output block on one XCD so that the key is read from HBM about
+// once for all; each result equals its own keyswitch_rotate, bit for bit
+struct KsRotateGroupArgs {
+  KsRotateArgs a[4];
+  int count = 1;
+};
+hipError_t keyswitch_rotate_group(const KsRotateGroupArgs& ga, int mode, size_t n, hipStream_t s);
 
 // Batched baby steps: keyswitch_rotate (mode 1) for several rotations of one ciphertext in ONE
 // launch.  A workgroup owns a SOURCE block (limb l, kGaloisBlock consecutive indices), reads the

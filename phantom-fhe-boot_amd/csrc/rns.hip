@@ -692,11 +692,23 @@ __global__ __launch_bounds__(kBlock) void galois_finish_kernel(GaloisFinishArgs 
   }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void ks_rotate_kernel(KsRotateArgs a, uint32_t log_n, uint32_t bsz) {
+// GROUP: the same rotation of `count` ciphertexts through one key in one launch (bootstraps in
+// lockstep), their workgroups of an output block on one XCD 8 dispatches apart so that the
+// followers read the key halves from that XCD's L2 (as ks_rotate_batch_full's GROUP form)
+template <int MODE, bool GROUP>
+__global__ __launch_bounds__(kBlock) void ks_rotate_kernel(KsRotateGroupArgs ga, uint32_t log_n, uint32_t bsz) {
   __shared__ uint64_t s0[kGalB], s1[kGalB];
   const uint32_t nb = (1u << log_n) / bsz;
-  const uint32_t l = blockIdx.x / nb, ob = blockIdx.x % nb;
+  uint32_t bid = blockIdx.x;
+  int c = 0;
+  if constexpr (GROUP) {
+    const uint32_t K = static_cast<uint32_t>(ga.count), x = bid % 8, k = bid / 8;
+    c = static_cast<int>(k % K);
+    bid = (k / K) * 8 + x;
+  }
+  const KsRotateArgs& a = ga.a[c];
+  if (GROUP && bid >= a.qlp * nb) return;  // the rounding of the group grid (workgroup-uniform, no barrier passed)
+  const uint32_t l = bid / nb, ob = bid % nb;
   const uint32_t twr = l >= a.ql ? a.size_q + (l - a.ql) : l;
   const uint64_t q = a.qp[twr], r0 = a.qp_barrett[2 * twr], r1 = a.qp_barrett[2 * twr + 1];
   const size_t n = size_t(1) << log_n;
@@ -1217,9 +1229,33 @@ hipError_t keyswitch_rotate(const KsRotateArgs& a, int mode, size_t n, hipStream
   const uint32_t log_n = __builtin_ctzll(n), bsz = static_cast<uint32_t>(std::min<size_t>(n, kGalB));
   const dim3 grid(static_cast<uint32_t>(a.qlp * (n / bsz)));
   switch (mode) {
-    case 0: ks_rotate_kernel<0><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
-    case 1: ks_rotate_kernel<1><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
-    default: ks_rotate_kernel<2><<<grid, kBlock, 0, s>>>(a, log_n, bsz); break;
+    case 0: ks_rotate_kernel<0, false><<<grid, kBlock, 0, s>>>(KsRotateGroupArgs{{a}, 1}, log_n, bsz); break;
+    case 1: ks_rotate_kernel<1, false><<<grid, kBlock, 0, s>>>(KsRotateGroupArgs{{a}, 1}, log_n, bsz); break;
+    default: ks_rotate_kernel<2, false><<<grid, kBlock, 0, s>>>(KsRotateGroupArgs{{a}, 1}, log_n, bsz); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t keyswitch_rotate_group(const KsRotateGroupArgs& ga, int mode, size_t n, hipStream_t s) {
+  if (ga.count < 2 || ga.count > kKsGroupMax || mode < 0 || mode > 2) return hipErrorInvalidValue;
+  const KsRotateArgs& a = ga.a[0];
+  for (int c = 0; c < ga.count; ++c) {
+    const KsRotateArgs& x = ga.a[c];
+    if (!x.digits || !x.evk || !x.out || !x.perm || x.beta == 0) return hipErrorInvalidValue;
+    if (mode > 0 && !x.c0) return hipErrorInvalidValue;
+    if (mode == 1 && (!x.pmod || !x.pmod_shoup)) return hipErrorInvalidValue;
+    if (x.evk != a.evk || x.perm != a.perm || x.qlp != a.qlp || x.ql != a.ql || x.beta != a.beta ||
+        x.size_q != a.size_q || x.size_p != a.size_p)
+      return hipErrorInvalidValue;
+  }
+  if (a.qlp == 0) return hipSuccess;
+  const uint32_t log_n = __builtin_ctzll(n), bsz = static_cast<uint32_t>(std::min<size_t>(n, kGalB));
+  const uint32_t per = (a.qlp * static_cast<uint32_t>(n / bsz) + 7) / 8 * 8;
+  const dim3 grid(static_cast<uint32_t>(ga.count) * per);
+  switch (mode) {
+    case 0: ks_rotate_kernel<0, true><<<grid, kBlock, 0, s>>>(ga, log_n, bsz); break;
+    case 1: ks_rotate_kernel<1, true><<<grid, kBlock, 0, s>>>(ga, log_n, bsz); break;
+    default: ks_rotate_kernel<2, true><<<grid, kBlock, 0, s>>>(ga, log_n, bsz); break;
   }
   return hipGetLastError();
 }

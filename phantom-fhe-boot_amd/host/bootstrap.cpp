@@ -1063,8 +1063,65 @@ std::vector<PhantomCiphertext> FHECKKSRNS::apply_level_group(const PhantomContex
   } else {
     for (int c = 0; c < K; ++c) hip_ok(phx::lt_bsgs(ga.a[c], cc.poly_degree(), cc.stream()), "linear transform inner products");
   }
+  return level_giants_group(cc, lv, w);
+}
+
+std::vector<PhantomCiphertext> FHECKKSRNS::level_giants_group(const PhantomContext& cc, const LTLevel& lv,
+                                                              std::vector<LevelWork>& w) const {
+  const size_t K = w.size(), n = cc.poly_degree(), QlP = w[0].QlP, Ql = w[0].Ql, ext_words = 2 * QlP * n;
+  const size_t G = static_cast<size_t>(lv.b - 1);
+  hipStream_t s = cc.stream();
+  bool same = true;
+  for (const LevelWork& x : w) same &= x.QlP == QlP && x.ct->chain_index() == w[0].ct->chain_index();
+  if (!same) {
+    std::vector<PhantomCiphertext> r;
+    for (LevelWork& x : w) r.push_back(level_giants(cc, lv, x));
+    return r;
+  }
+  for (LevelWork& x : w) x.babies.release();
+  if (G > 0) {
+    // as level_giants, with each giant rotation of the K ciphertexts in one launch that reads
+    // its key about once (keyswitch_rotate_group)
+    const RnsTool& rt = cc.get_context_data(w[0].ct->chain_index()).gpu_rns_tool();
+    const size_t dwords = rt.beta() * QlP * n;
+    std::vector<DeviceBuffer<uint64_t>> digits;
+    for (LevelWork& x : w) {
+      digits.emplace_back(G * dwords, s);
+      rt.moddown_modup(digits.back().get(), x.giants.get() + QlP * n, cc.gpu_rns_tables(), s, G, ext_words);
+    }
+    for (size_t i = 1; i <= G; ++i) {
+      const uint32_t elt = FindAutomorphismIndex2nComplex(
+          static_cast<int>(static_cast<long>(lv.g) * static_cast<long>(i) * lv.stride), n);
+      phx::KsRotateGroupArgs ga;
+      ga.count = static_cast<int>(K);
+      for (size_t c = 0; c < K; ++c) {
+        phx::KsRotateArgs& g = ga.a[c];
+        g.digits = digits[c].get() + (i - 1) * dwords;
+        g.evk = galois_keys_.get(elt).public_keys_ptr();
+        g.qp = cc.mod_QP().q;
+        g.qp_barrett = cc.mod_QP().barrett;
+        g.c0 = w[c].giants.get() + (i - 1) * ext_words;
+        g.out = w[c].acc.data();
+        g.perm = cc.galois_perm(elt);
+        g.ql = static_cast<uint32_t>(Ql);
+        g.qlp = static_cast<uint32_t>(QlP);
+        g.size_q = static_cast<uint32_t>(cc.size_Q());
+        g.size_p = static_cast<uint32_t>(cc.size_P());
+        g.beta = static_cast<uint32_t>(rt.beta());
+        g.accumulate = true;
+      }
+      hip_ok(phx::keyswitch_rotate_group(ga, 2, n, s), "giant step key switch + permute + accumulate (group)");
+      traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP, n));  // read once for the group
+    }
+  }
   std::vector<PhantomCiphertext> r;
-  for (int c = 0; c < K; ++c) r.push_back(level_giants(cc, lv, w[c]));
+  for (LevelWork& x : w) {
+    x.acc.set_scale(x.ct->scale() * sf_.at(lv.chain - 1));
+    x.acc.SetNoiseScaleDeg(2);
+    traffic::ciphertexts(traffic::limb_bytes(2 * QlP * static_cast<size_t>(lv.b) + 2 * (Ql - 1), n));
+    x.giants.release();
+    r.push_back(KeySwitchDownRescale(cc, x.acc));
+  }
   return r;
 }
 

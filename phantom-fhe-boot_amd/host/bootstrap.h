@@ -231,6 +231,8 @@ class FHECKKSRNS {
                     bool launch = true) const;
   phx::LtArgs level_lt_args(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const;
   PhantomCiphertext level_giants(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const;
+  std::vector<PhantomCiphertext> level_giants_group(const PhantomContext& cc, const LTLevel& lv,
+                                                    std::vector<LevelWork>& w) const;
   // apply_level of 2..4 ciphertexts in lockstep: their baby steps and inner products each in one
   // launch that reads the level's keys / plaintexts about once for all; each result equals apply_level's
   std::vector<PhantomCiphertext> apply_level_group(const PhantomContext& cc,
