@@ -392,7 +392,7 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, 
 # HBM bytes per forward-NTT launch (column + row pass) from PMC counters: FETCH_SIZE and
 # WRITE_SIZE collected in separate rocprofv3 --pmc passes over the same NTT shape
 # (tools/gpu_pmc_traffic.sh), gfx950 FETCH_SIZE correction applied (tools/pmc_traffic.py).
-PMC_TRAFFIC_FILE = "profiles/r03/ntt_pmc_traffic.json"
+PMC_TRAFFIC_FILE = "profiles/r04/ntt_pmc_traffic.json"
 
 
 def pmc_traffic():
