@@ -377,7 +377,7 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, 
         res = {
             "workload": f"C5: {total} independent C4 bootstraps (input chain index {chain}) sharded over {world} rank(s), "
                         "scatter -> EvalBootstrapBatch -> gather of serialized ciphertexts",
-            "bootstraps": total, "bootstraps_per_rank": per, "lanes_per_rank": lanes, "ranks": world,
+            "bootstraps": total, "bootstraps_per_rank": per, "lanes_per_rank": lanes, "lockstep_group": 4, "ranks": world,
             "bootstraps_per_s": round(total / max_s, 3), "max_rank_s": round(max_s, 3),
             "scatter_gather_bytes": total * (sin + sout),
             "verified": nver, "min_avg_bits": round(min(bits), 2), "mean_avg_bits": round(float(np.mean(bits)), 2),
