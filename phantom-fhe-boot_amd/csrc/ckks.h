@@ -53,14 +53,22 @@ struct LtArgs {
   int g = 0, b = 0, Ql = 0, P = 0, size_Q = 0;
 };
 hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s);
-// lt_bsgs of `count` (2..4) ciphertexts at one level through the same plaintexts (bootstraps in
-// lockstep) in one launch, the ciphertexts' blocks for the same elements on one XCD so that the
-// plaintexts are read from HBM about once for all.  a[0..count) differ only in baby / out; g == 32
-// and b <= 8 (the bootstrap's levels).  Each result equals its own lt_bsgs, bit for bit.
-constexpr int kLtGroupMax = 4;
+// lt_bsgs of `count` (2..kLtGroupMax) ciphertexts at one level through the same plaintexts
+// (bootstraps in lockstep) in one launch, the ciphertexts' blocks for the same elements on one XCD
+// so that the plaintexts are read from HBM about once for all.  Each ciphertext's babies are
+// contiguous (baby j at baby0[c] + j baby_stride words), its inner sum 0 goes to acc[c] and inner
+// sum i >= 1 to giant1[c] + (i - 1) giant_stride; g == 32, b <= 8 (the bootstrap's levels).  Each
+// result equals its own lt_bsgs, bit for bit.
+constexpr int kLtGroupMax = 8;
 struct LtGroupArgs {
-  LtArgs a[kLtGroupMax];
-  int count = 0;
+  const uint64_t* const* pts = nullptr;
+  const uint64_t* q = nullptr;
+  const uint64_t* barrett = nullptr;
+  int g = 0, b = 0, Ql = 0, P = 0, size_Q = 0, count = 0;
+  uint64_t baby_stride = 0, giant_stride = 0;
+  const uint64_t* baby0[kLtGroupMax] = {};
+  uint64_t* acc[kLtGroupMax] = {};
+  uint64_t* giant1[kLtGroupMax] = {};
 };
 hipError_t lt_bsgs_group(const LtGroupArgs& ga, size_t n, hipStream_t s);
 

@@ -174,8 +174,26 @@ __global__ __launch_bounds__(kBlock, 2) void lt_bsgs_kernel(LtArgs a, uint32_t l
 // Wide form for G = 32 baby steps (at most B giant steps): the babies are held 8 at a time and
 // every giant step's 128-bit sums stay in registers across the two halves, so each baby and each
 // plaintext is still read once (the register-resident form of lt_bsgs_kernel<32> spills).
-template <int G, int B>
-__device__ __forceinline__ void lt_bsgs_wide(const LtArgs& a, uint32_t log_n, size_t total, uint32_t block,
+// where the babies and the inner sums of one ciphertext live: LtArgs' pointer arrays, or the
+// group form's contiguous buffers (baby j at baby0 + j baby_stride, inner sum i >= 1 at
+// giant1 + (i - 1) giant_stride, inner sum 0 at acc)
+struct LtSingleSrc {
+  const LtArgs& a;
+  __device__ const uint64_t* baby(int j) const { return a.baby[j]; }
+  __device__ uint64_t* out(int i) const { return a.out[i]; }
+};
+struct LtGroupSrc {
+  const LtGroupArgs& a;
+  int c;
+  __device__ const uint64_t* baby(int j) const { return a.baby0[c] + static_cast<size_t>(j) * a.baby_stride; }
+  __device__ uint64_t* out(int i) const {
+    return i == 0 ? a.acc[c] : a.giant1[c] + static_cast<size_t>(i - 1) * a.giant_stride;
+  }
+};
+
+template <int G, int B, class Src>
+__device__ __forceinline__ void lt_bsgs_wide(const Src& src, int nb, int Ql, int size_Q, const uint64_t* qv,
+                                             const uint64_t* barrett, uint32_t log_n, size_t total, uint32_t block,
                                              uint32_t nblocks, const uint64_t* const* ptab) {
   constexpr uint64_t kM30 = (1ull << 30) - 1;
   constexpr int C = 8;
@@ -183,8 +201,8 @@ __device__ __forceinline__ void lt_bsgs_wide(const LtArgs& a, uint32_t log_n, si
   const size_t pstride = total;
   for (size_t e = block * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)nblocks * kBlock) {
     const int l = static_cast<int>(e >> log_n);
-    const int row = l < a.Ql ? l : a.size_Q + (l - a.Ql);
-    const uint64_t q = a.q[row], r0 = a.barrett[2 * row], r1 = a.barrett[2 * row + 1];
+    const int row = l < Ql ? l : size_Q + (l - Ql);
+    const uint64_t q = qv[row], r0 = barrett[2 * row], r1 = barrett[2 * row + 1];
     u128 acc[B][2];
 #pragma unroll
     for (int i = 0; i < B; ++i) acc[i][0] = acc[i][1] = u128{0, 0};
@@ -193,7 +211,8 @@ __device__ __forceinline__ void lt_bsgs_wide(const LtArgs& a, uint32_t log_n, si
       uint32_t xl[2][C], xh[2][C];
 #pragma unroll
       for (int j = 0; j < C; ++j) {
-        const uint64_t v0 = a.baby[c0 + j][e], v1 = a.baby[c0 + j][pstride + e];
+        const uint64_t* bj = src.baby(c0 + j);
+        const uint64_t v0 = bj[e], v1 = bj[pstride + e];
         xl[0][j] = static_cast<uint32_t>(v0 & kM30);
         xh[0][j] = static_cast<uint32_t>(v0 >> 30);
         xl[1][j] = static_cast<uint32_t>(v1 & kM30);
@@ -201,7 +220,7 @@ __device__ __forceinline__ void lt_bsgs_wide(const LtArgs& a, uint32_t log_n, si
       }
 #pragma unroll
       for (int i = 0; i < B; ++i) {
-        if (i >= a.b) break;
+        if (i >= nb) break;
         const uint64_t* const* prow = ptab + i * G + c0;
         uint64_t w[C];
 #pragma unroll
@@ -230,8 +249,8 @@ __device__ __forceinline__ void lt_bsgs_wide(const LtArgs& a, uint32_t log_n, si
     }
 #pragma unroll
     for (int i = 0; i < B; ++i) {
-      if (i >= a.b) break;
-      uint64_t* o = a.out[i];
+      if (i >= nb) break;
+      uint64_t* o = src.out(i);
       o[e] = barrett_reduce_128(acc[i][0], q, r0, r1);
       o[pstride + e] = barrett_reduce_128(acc[i][1], q, r0, r1);
     }
@@ -243,7 +262,7 @@ __global__ __launch_bounds__(kBlock, 2) void lt_bsgs_wide_kernel(LtArgs a, uint3
   extern __shared__ const uint64_t* ptab[];
   for (int k = threadIdx.x; k < a.b * G; k += kBlock) ptab[k] = a.pts[k];
   __syncthreads();
-  lt_bsgs_wide<G, B>(a, log_n, total, blockIdx.x, gridDim.x, ptab);
+  lt_bsgs_wide<G, B>(LtSingleSrc{a}, a.b, a.Ql, a.size_Q, a.q, a.barrett, log_n, total, blockIdx.x, gridDim.x, ptab);
 }
 
 // `count` ciphertexts through the same plaintexts (lt_bsgs_group): the blocks of the ciphertexts
@@ -252,13 +271,13 @@ __global__ __launch_bounds__(kBlock, 2) void lt_bsgs_wide_kernel(LtArgs a, uint3
 template <int G, int B>
 __global__ __launch_bounds__(kBlock, 2) void lt_bsgs_group_kernel(LtGroupArgs ga, uint32_t log_n, size_t total) {
   extern __shared__ const uint64_t* ptab[];
-  const LtArgs& a0 = ga.a[0];
-  for (int k = threadIdx.x; k < a0.b * G; k += kBlock) ptab[k] = a0.pts[k];
+  for (int k = threadIdx.x; k < ga.b * G; k += kBlock) ptab[k] = ga.pts[k];
   __syncthreads();
   const uint32_t K = static_cast<uint32_t>(ga.count);
   const uint32_t b = blockIdx.x, x = b % 8, k = b / 8;
   const uint32_t c = k % K, blk = (k / K) * 8 + x, nblk = gridDim.x / K;
-  lt_bsgs_wide<G, B>(ga.a[c], log_n, total, blk, nblk, ptab);
+  lt_bsgs_wide<G, B>(LtGroupSrc{ga, static_cast<int>(c)}, ga.b, ga.Ql, ga.size_Q, ga.q, ga.barrett, log_n, total, blk,
+                     nblk, ptab);
 }
 
 template <bool MUL, bool ACC>
@@ -475,18 +494,12 @@ hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s) {
 }
 
 hipError_t lt_bsgs_group(const LtGroupArgs& ga, size_t n, hipStream_t s) {
-  if (ga.count < 2 || ga.count > kLtGroupMax) return hipErrorInvalidValue;
-  const LtArgs& a = ga.a[0];
-  if (a.g != 32 || a.b < 1 || a.b > 8 || !a.pts) return hipErrorInvalidValue;
-  for (int c = 0; c < ga.count; ++c) {
-    const LtArgs& x = ga.a[c];
-    if (x.g != a.g || x.b != a.b || x.pts != a.pts || x.Ql != a.Ql || x.P != a.P || x.size_Q != a.size_Q)
-      return hipErrorInvalidValue;
-    for (int i = 0; i < x.b; ++i)
-      if (!x.out[i]) return hipErrorInvalidValue;
-  }
-  const size_t total = n * static_cast<size_t>(a.Ql + a.P);
-  const size_t lds = static_cast<size_t>(a.b) * a.g * sizeof(const uint64_t*);
+  if (ga.count < 2 || ga.count > kLtGroupMax || ga.g != 32 || ga.b < 1 || ga.b > 8 || !ga.pts || !ga.q || !ga.barrett)
+    return hipErrorInvalidValue;
+  for (int c = 0; c < ga.count; ++c)
+    if (!ga.baby0[c] || !ga.acc[c] || (ga.b > 1 && !ga.giant1[c])) return hipErrorInvalidValue;
+  const size_t total = n * static_cast<size_t>(ga.Ql + ga.P);
+  const size_t lds = static_cast<size_t>(ga.b) * ga.g * sizeof(const uint64_t*);
   const int per = (grid_for(total) + 7) / 8 * 8;  // blocks per ciphertext, whole XCD rounds
   lt_bsgs_group_kernel<32, 8><<<ga.count * per, kBlock, lds, s>>>(ga, __builtin_ctzll(n), total);
   return hipGetLastError();

@@ -194,8 +194,9 @@ hipError_t keyswitch_rotate(const KsRotateArgs& a, int mode, size_t n, hipStream
 // keyswitch_rotate of `count` (2..kKsGroupMax) ciphertexts by the same rotation (evk, perm) in one
 // launch, their workgroups of an output block on one XCD so that the key is read from HBM about
 // once for all; each result equals its own keyswitch_rotate, bit for bit
+constexpr int kKsGroupMax = 8;
 struct KsRotateGroupArgs {
-  KsRotateArgs a[4];
+  KsRotateArgs a[kKsGroupMax];
   int count = 1;
 };
 hipError_t keyswitch_rotate_group(const KsRotateGroupArgs& ga, int mode, size_t n, hipStream_t s);
@@ -228,7 +229,6 @@ hipError_t keyswitch_rotate_batch(const KsRotateBatchArgs& a, size_t n, hipStrea
 // in one launch, the ciphertexts' workgroups of a (limb, source block) on one XCD so that the keys
 // are read from HBM about once for all; a[0..count) differ only in digits / ct / out.  Each result
 // equals its own keyswitch_rotate_batch, bit for bit.
-constexpr int kKsGroupMax = 4;
 struct KsRotateBatchGroupArgs {
   KsRotateBatchArgs a[kKsGroupMax];
   int count = 1;

@@ -1041,7 +1041,8 @@ std::vector<PhantomCiphertext> FHECKKSRNS::apply_level_group(const PhantomContex
                                                              const std::vector<const PhantomCiphertext*>& in,
                                                              const LTLevel& lv) const {
   const int K = static_cast<int>(in.size());
-  if (K < 2 || K > phx::kLtGroupMax) throw std::invalid_argument("apply_level_group: 2 to 4 ciphertexts");
+  if (K < 2 || K > phx::kLtGroupMax || K > phx::kKsGroupMax)
+    throw std::invalid_argument("apply_level_group: 2 to 8 ciphertexts");
   std::vector<LevelWork> w(K);
   phx::KsRotateBatchGroupArgs ka;
   ka.count = K;
@@ -1051,17 +1052,34 @@ std::vector<PhantomCiphertext> FHECKKSRNS::apply_level_group(const PhantomContex
   }
   hip_ok(phx::keyswitch_rotate_batch_group(ka, cc.poly_degree(), cc.stream()), "linear transform baby steps (group)");
   for (LevelWork& x : w) x.digits.release();
-  phx::LtGroupArgs ga;
-  ga.count = K;
   bool same_ql = true;
+  std::vector<phx::LtArgs> la(K);
   for (int c = 0; c < K; ++c) {
-    ga.a[c] = level_lt_args(cc, lv, w[c]);
+    la[c] = level_lt_args(cc, lv, w[c]);
     same_ql &= w[c].Ql == w[0].Ql;
   }
   if (lv.g == 32 && lv.b <= 8 && same_ql) {
+    const size_t ext_words = 2 * w[0].QlP * cc.poly_degree();
+    phx::LtGroupArgs ga;
+    ga.pts = la[0].pts;
+    ga.q = la[0].q;
+    ga.barrett = la[0].barrett;
+    ga.g = la[0].g;
+    ga.b = la[0].b;
+    ga.Ql = la[0].Ql;
+    ga.P = la[0].P;
+    ga.size_Q = la[0].size_Q;
+    ga.count = K;
+    ga.baby_stride = ext_words;  // (the babies and inner sums are [2][QlP][n] ciphertexts, back to back)
+    ga.giant_stride = ext_words;
+    for (int c = 0; c < K; ++c) {
+      ga.baby0[c] = w[c].babies.get();
+      ga.acc[c] = w[c].acc.data();
+      ga.giant1[c] = w[c].giants.get();
+    }
     hip_ok(phx::lt_bsgs_group(ga, cc.poly_degree(), cc.stream()), "linear transform inner products (group)");
   } else {
-    for (int c = 0; c < K; ++c) hip_ok(phx::lt_bsgs(ga.a[c], cc.poly_degree(), cc.stream()), "linear transform inner products");
+    for (int c = 0; c < K; ++c) hip_ok(phx::lt_bsgs(la[c], cc.poly_degree(), cc.stream()), "linear transform inner products");
   }
   return level_giants_group(cc, lv, w);
 }
@@ -1450,8 +1468,26 @@ std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<
                                                               uint32_t numSlots) const {
   const int k = std::max(1, std::min({lanes, PhantomContext::kLanes, static_cast<int>(in.size())}));
   std::vector<PhantomCiphertext> out(in.size());
+  // ciphertexts t, t + k, ... of lane t, up to kBootGroup at a time in lockstep (shared plaintext
+  // and key reads, EvalMod on 2 x group lanes)
+  auto run_lane = [&](int t) {
+    const Precom& pc = precom(numSlots, cc);
+    std::vector<size_t> mine;
+    for (size_t i = t; i < in.size(); i += k) mine.push_back(i);
+    for (size_t g0 = 0; g0 < mine.size(); g0 += kBootGroup) {
+      const size_t cnt = std::min(kBootGroup, mine.size() - g0);
+      if (cnt == 1) {
+        out[mine[g0]] = EvalBootstrap(in[mine[g0]], cc, numSlots);
+        continue;
+      }
+      std::vector<const PhantomCiphertext*> grp;
+      for (size_t m = 0; m < cnt; ++m) grp.push_back(&in[mine[g0 + m]]);
+      std::vector<PhantomCiphertext> r = bootstrap_group(grp, cc, pc);
+      for (size_t m = 0; m < cnt; ++m) out[mine[g0 + m]] = std::move(r[m]);
+    }
+  };
   if (k == 1) {
-    for (size_t i = 0; i < in.size(); ++i) out[i] = EvalBootstrap(in[i], cc, numSlots);
+    run_lane(0);
     return out;
   }
   const hipStream_t s0 = cc.stream();
@@ -1469,22 +1505,7 @@ std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<
     workers.emplace_back([&, t] {
       try {
         LaneGuard lane(cc, t);
-        // up to kBootGroup of the lane's ciphertexts at a time in lockstep (shared plaintext and
-        // key reads, EvalMod on 2 x group lanes)
-        const Precom& pc = precom(numSlots, cc);
-        std::vector<size_t> mine;
-        for (size_t i = t; i < in.size(); i += k) mine.push_back(i);
-        for (size_t g0 = 0; g0 < mine.size(); g0 += kBootGroup) {
-          const size_t cnt = std::min(kBootGroup, mine.size() - g0);
-          if (cnt == 1) {
-            out[mine[g0]] = EvalBootstrap(in[mine[g0]], cc, numSlots);
-            continue;
-          }
-          std::vector<const PhantomCiphertext*> grp;
-          for (size_t m = 0; m < cnt; ++m) grp.push_back(&in[mine[g0 + m]]);
-          std::vector<PhantomCiphertext> r = bootstrap_group(grp, cc, pc);
-          for (size_t m = 0; m < cnt; ++m) out[mine[g0 + m]] = std::move(r[m]);
-        }
+        run_lane(t);
       } catch (...) {
         err[t] = std::current_exception();
       }

@@ -233,7 +233,7 @@ class FHECKKSRNS {
   PhantomCiphertext level_giants(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const;
   std::vector<PhantomCiphertext> level_giants_group(const PhantomContext& cc, const LTLevel& lv,
                                                     std::vector<LevelWork>& w) const;
-  // apply_level of 2..4 ciphertexts in lockstep: their baby steps and inner products each in one
+  // apply_level of 2..8 ciphertexts in lockstep: their baby steps and inner products each in one
   // launch that reads the level's keys / plaintexts about once for all; each result equals apply_level's
   std::vector<PhantomCiphertext> apply_level_group(const PhantomContext& cc,
                                                    const std::vector<const PhantomCiphertext*>& in,
@@ -261,7 +261,7 @@ class FHECKKSRNS {
                                                  const std::vector<double>& coeffs) const;
   void double_angle_lanes(std::vector<PhantomCiphertext>& v, const PhantomContext& cc, uint32_t numIter) const;
   PhantomCiphertext bootstrap_once(const PhantomCiphertext& ct, const PhantomContext& cc, const Precom& pc) const;
-  // bootstrap_once of 2..4 ciphertexts in lockstep (full packing): grouped linear-transform levels,
+  // bootstrap_once of 2..8 ciphertexts in lockstep (full packing): grouped linear-transform levels,
   // EvalMod on 2 x group lanes; each result equals bootstrap_once's, bit for bit
   static constexpr size_t kBootGroup = 4;
   std::vector<PhantomCiphertext> bootstrap_group(const std::vector<const PhantomCiphertext*>& in,

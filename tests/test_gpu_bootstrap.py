@@ -114,15 +114,26 @@ def test_bootstrapping_example_verbatim():
     assert float(vals["avg"]) > 9.0, vals
 
 
-def test_bootstrap_batch_on_stream_lanes():
-    """EvalBootstrapBatch: 8 bootstraps of distinct inputs, 2 stream lanes side by side, four
-    bootstraps in lockstep per lane (C5's per-GPU path: grouped linear-transform levels, EvalMod on
-    eight lanes); every output keeps the single-bootstrap precision and equals EvalBootstrap of its
-    input bit for bit."""
-    rc, lines, err = _run("batch", "16", "8", "2", timeout=150)
+def test_bootstrap_batch_one_lane():
+    """EvalBootstrapBatch on one lane: 8 bootstraps as two lockstep groups of four on the caller's
+    stream, every output equal to EvalBootstrap of its input bit for bit."""
+    rc, lines, err = _run("batch", "16", "8", "1", timeout=150)
     assert rc == 0, (lines, err)
     b = [l for l in lines if l.get("stage") == "batch"][0]
-    assert b["bootstraps"] == 8 and b["lanes"] == 2, b
+    assert b["bootstraps"] == 8 and b["lanes"] == 1 and b["min_avg_bits"] > 9.85, b
+    checks = {l["check"]: l for l in lines if "check" in l}
+    assert checks["batch_equals_single_bitexact"]["ok"], checks
+
+
+def test_bootstrap_batch_on_stream_lanes():
+    """EvalBootstrapBatch: 10 bootstraps of distinct inputs, 2 stream lanes side by side, each lane
+    bootstrapping its five as a lockstep group of four and a single one (C5's per-GPU path: grouped
+    linear-transform levels, EvalMod on eight lanes); every output keeps the single-bootstrap precision and equals
+    EvalBootstrap of its input bit for bit."""
+    rc, lines, err = _run("batch", "16", "10", "2", timeout=150)
+    assert rc == 0, (lines, err)
+    b = [l for l in lines if l.get("stage") == "batch"][0]
+    assert b["bootstraps"] == 10 and b["lanes"] == 2, b
     assert b["min_avg_bits"] > 9.85, b
     checks = {l["check"]: l for l in lines if "check" in l}
     assert checks["batch_equals_single_bitexact"]["ok"], checks
