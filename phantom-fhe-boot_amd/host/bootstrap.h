@@ -263,7 +263,10 @@ class FHECKKSRNS {
   PhantomCiphertext bootstrap_once(const PhantomCiphertext& ct, const PhantomContext& cc, const Precom& pc) const;
   // bootstrap_once of 2..8 ciphertexts in lockstep (full packing): grouped linear-transform levels,
   // EvalMod on 2 x group lanes; each result equals bootstrap_once's, bit for bit
-  static constexpr size_t kBootGroup = 4;
+#ifndef PHX_BOOT_GROUP
+#define PHX_BOOT_GROUP 4
+#endif
+  static constexpr size_t kBootGroup = PHX_BOOT_GROUP;
   std::vector<PhantomCiphertext> bootstrap_group(const std::vector<const PhantomCiphertext*>& in,
                                                  const PhantomContext& cc, const Precom& pc) const;
 

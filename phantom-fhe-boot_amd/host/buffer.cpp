@@ -65,7 +65,19 @@ void DevicePool::forget_stream(hipStream_t s) {
       }
 }
 
+// PHX_POOL_TRACE=1: one stderr line per out-of-memory release of the cache
+static bool pool_trace() {
+  static const bool on = [] {
+    const char* e = std::getenv("PHX_POOL_TRACE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 void DevicePool::release_cached_locked() {
+  size_t cached = 0, freed = 0;
+  for (auto& kv : free_) cached += kv.first.second * kv.second.size();
+  const size_t held0 = held_;
   for (auto& kv : free_) {
     std::vector<Block> keep;
     for (Block& b : kv.second) {
@@ -75,9 +87,14 @@ void DevicePool::release_cached_locked() {
       }
       if (b.ev) spare_.push_back(b.ev);
       (void)hipFree(b.p);
+      held_ -= kv.first.second;
+      freed += kv.first.second;
     }
     kv.second.swap(keep);
   }
+  if (pool_trace())
+    std::fprintf(stderr, "{\"pool_release\": true, \"held_MiB\": %zu, \"cached_MiB\": %zu, \"freed_MiB\": %zu}\n",
+                 held0 >> 20, cached >> 20, freed >> 20);
 }
 
 void* DevicePool::alloc(size_t bytes, hipStream_t s) {
@@ -86,8 +103,12 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
   const size_t c = size_class(bytes);
   {
     std::lock_guard<std::mutex> lk(mu_);
-    auto it = free_.find({dev, c});
-    if (it != free_.end()) {
+    // the exact class first; a large request may also take a cached block up to a quarter larger
+    // (the bootstrap's per-level buffers differ by a limb or two: without the slack each level
+    // keeps its own cached copies, and lockstep groups of them fill the GPU)
+    const size_t top = c >= kSlackMin ? c + c / 4 : c;
+    for (auto it = free_.lower_bound({dev, c}); it != free_.end() && it->first.first == dev && it->first.second <= top;
+         ++it) {
       auto& v = it->second;
       for (size_t i = v.size(); i-- > 0;) {
         Block& b = v[i];
@@ -96,7 +117,7 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
         void* p = b.p;
         if (b.ev) spare_.push_back(b.ev);
         v.erase(v.begin() + static_cast<long>(i));
-        live_[p] = c;
+        live_[p] = it->first.second;  // the block's own class: it returns there
         return p;
       }
     }
@@ -112,6 +133,7 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
   }
   std::lock_guard<std::mutex> lk(mu_);
   live_[p] = c;
+  held_ += c;
   return p;
 }
 
@@ -121,23 +143,24 @@ void DevicePool::free(void* p, size_t bytes, hipStream_t s, bool completed) {
   PHX_CHECK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(mu_);
   auto it = live_.find(p);
-  if (it == live_.end() || it->second != size_class(bytes)) {
+  if (it == live_.end() || it->second < size_class(bytes)) {
     std::fprintf(stderr, "DevicePool: free of %p (%zu bytes) that is not a live block (double free?)\n", p, bytes);
     std::abort();
   }
+  const size_t cls = it->second;
   live_.erase(it);
   Block b{p, s, nullptr};
 #ifdef PHX_GUARD
   // debug builds: poison the block in the freeing stream's order, so a stream that still reads it
   // after this free (a buffer freed on a stream other than its last user's) reads garbage and the
   // results show it
-  if (!completed) PHX_CHECK(hipMemsetAsync(p, 0xFF, size_class(bytes), s));
+  if (!completed) PHX_CHECK(hipMemsetAsync(p, 0xFF, cls, s));
 #endif
   if (!completed) {
     b.ev = take_event();
     PHX_CHECK(hipEventRecord(b.ev, s));
   }
-  free_[{dev, size_class(bytes)}].push_back(b);
+  free_[{dev, cls}].push_back(b);
 }
 
 }  // namespace phantom

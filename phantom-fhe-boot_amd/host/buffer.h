@@ -43,9 +43,11 @@ class DevicePool {
     hipEvent_t ev;  // null when known complete
   };
   std::mutex mu_;
+  static constexpr size_t kSlackMin = size_t(4) << 20;          // requests from here may take a block up to 1/4 larger
   std::map<std::pair<int, size_t>, std::vector<Block>> free_;  // (device, class) -> blocks
   std::map<void*, size_t> live_;                               // handed-out blocks (double-free check)
   std::vector<hipEvent_t> spare_;
+  size_t held_ = 0;  // bytes obtained from hipMalloc and not returned (live + cached)
   hipEvent_t take_event();
   void release_cached_locked();
 };

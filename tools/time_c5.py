@@ -12,4 +12,6 @@ import bench  # noqa: E402
 
 torch.cuda.set_device(0)
 r = bench.c5_leg(None, torch, 1, 0, 0, total=256, lanes=4, verify=8)
-print(os.path.basename(os.path.dirname(os.path.abspath(sys.argv[1]))), r["bootstraps_per_s"], r["min_avg_bits"], flush=True)
+free, total = torch.cuda.mem_get_info()
+print(os.path.basename(os.path.dirname(os.path.abspath(sys.argv[1]))), r["bootstraps_per_s"], r["min_avg_bits"],
+      "used_GiB %.1f" % ((total - free) / 2**30), flush=True)
