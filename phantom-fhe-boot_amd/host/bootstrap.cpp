@@ -1465,17 +1465,19 @@ static void trace(const PhantomContext& cc, const char* stage, const PhantomCiph
 
 std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<PhantomCiphertext>& in,
                                                               const PhantomContext& cc, int lanes,
-                                                              uint32_t numSlots) const {
+                                                              uint32_t numSlots, size_t group) const {
   const int k = std::max(1, std::min({lanes, PhantomContext::kLanes, static_cast<int>(in.size())}));
+  if (group < 1 || group > static_cast<size_t>(phx::kLtGroupMax))
+    throw std::invalid_argument("EvalBootstrapBatch: group must be 1.." + std::to_string(phx::kLtGroupMax));
   std::vector<PhantomCiphertext> out(in.size());
-  // ciphertexts t, t + k, ... of lane t, up to kBootGroup at a time in lockstep (shared plaintext
+  // ciphertexts t, t + k, ... of lane t, up to `group` at a time in lockstep (shared plaintext
   // and key reads, EvalMod on 2 x group lanes)
   auto run_lane = [&](int t) {
     const Precom& pc = precom(numSlots, cc);
     std::vector<size_t> mine;
     for (size_t i = t; i < in.size(); i += k) mine.push_back(i);
-    for (size_t g0 = 0; g0 < mine.size(); g0 += kBootGroup) {
-      const size_t cnt = std::min(kBootGroup, mine.size() - g0);
+    for (size_t g0 = 0; g0 < mine.size(); g0 += group) {
+      const size_t cnt = std::min(group, mine.size() - g0);
       if (cnt == 1) {
         out[mine[g0]] = EvalBootstrap(in[mine[g0]], cc, numSlots);
         continue;

@@ -106,7 +106,10 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
     // the exact class first; a large request may also take a cached block up to a quarter larger
     // (the bootstrap's per-level buffers differ by a limb or two: without the slack each level
     // keeps its own cached copies, and lockstep groups of them fill the GPU)
-    const size_t top = c >= kSlackMin ? c + c / 4 : c;
+#ifndef PHX_POOL_SLACK_Q
+#define PHX_POOL_SLACK_Q 1  // the slack in quarters of the request
+#endif
+    const size_t top = c >= kSlackMin ? c + c * PHX_POOL_SLACK_Q / 4 : c;
     for (auto it = free_.lower_bound({dev, c}); it != free_.end() && it->first.first == dev && it->first.second <= top;
          ++it) {
       auto& v = it->second;

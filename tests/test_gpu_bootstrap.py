@@ -139,6 +139,19 @@ def test_bootstrap_batch_on_stream_lanes():
     assert checks["batch_equals_single_bitexact"]["ok"], checks
 
 
+def test_bootstrap_batch_groups_of_eight():
+    """EvalBootstrapBatch with group = 8 (the grouped kernels' maximum, LtGroupArgs /
+    KsRotateBatchGroupArgs at 8 ciphertexts): 8 bootstraps as one lockstep group on one lane, then
+    11 on 2 lanes (groups of 6 and 5). Every output equals EvalBootstrap of its input bit for bit."""
+    for n, lanes in (("8", "1"), ("11", "2")):
+        rc, lines, err = _run("batch", "16", n, lanes, "8", timeout=150)
+        assert rc == 0, (lines, err)
+        b = [l for l in lines if l.get("stage") == "batch"][0]
+        assert b["bootstraps"] == int(n) and b["group"] == 8 and b["min_avg_bits"] > 9.85, b
+        checks = {l["check"]: l for l in lines if "check" in l}
+        assert checks["batch_equals_single_bitexact"]["ok"], checks
+
+
 # ---- bootstrapping sessions through the C-ABI (include/phantom_amd.h phantom_boot_*) ------------
 
 def _session_run(num_slots=0, iterations=1, precision=0, count=2, chain=26, lanes=2):
