@@ -225,9 +225,16 @@ int phantom_boot_output_bytes(phantom_boot_session* s, size_t* bytes) {
 
 int phantom_boot_run(phantom_boot_session* s, const uint8_t* dev_in, size_t in_stride, size_t count, uint8_t* dev_out,
                      size_t out_stride, int lanes) {
+  return phantom_boot_run_grouped(s, dev_in, in_stride, count, dev_out, out_stride, lanes,
+                                  static_cast<int>(FHECKKSRNS::kBootGroup));
+}
+
+int phantom_boot_run_grouped(phantom_boot_session* s, const uint8_t* dev_in, size_t in_stride, size_t count,
+                             uint8_t* dev_out, size_t out_stride, int lanes, int group) {
   PHX_CAPI_GUARD({
     auto& b = session(s);
     if ((!dev_in || !dev_out) && count) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (group < 1 || group > 8) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "group must be 1..8");
     std::vector<PhantomCiphertext> in;
     in.reserve(count);
     for (size_t i = 0; i < count; ++i) in.push_back(load_device(*b.ctx, dev_in + i * in_stride, in_stride));
@@ -235,7 +242,7 @@ int phantom_boot_run(phantom_boot_session* s, const uint8_t* dev_in, size_t in_s
     if (b.iterations > 1) {
       for (auto& c : in) out.push_back(b.boot->EvalBootstrap(c, *b.ctx, b.slots, b.iterations, b.precision));
     } else {
-      out = b.boot->EvalBootstrapBatch(in, *b.ctx, lanes, b.slots);
+      out = b.boot->EvalBootstrapBatch(in, *b.ctx, lanes, b.slots, static_cast<size_t>(group));
     }
     for (size_t i = 0; i < count; ++i) save_device(*b.ctx, out[i], dev_out + i * out_stride, out_stride);
     return PHANTOM_OK;

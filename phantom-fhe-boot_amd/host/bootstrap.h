@@ -98,6 +98,10 @@ class FHECKKSRNS {
   // bootstrap, scale the residual error up by 2^precision, bootstrap it and subtract.
   PhantomCiphertext EvalBootstrap(const PhantomCiphertext& ct, const PhantomContext& cc, uint32_t numSlots = 0,
                                   uint32_t numIterations = 1, uint32_t precision = 0) const;
+#ifndef PHX_BOOT_GROUP
+#define PHX_BOOT_GROUP 4
+#endif
+  static constexpr size_t kBootGroup = PHX_BOOT_GROUP;  // EvalBootstrapBatch's default lockstep group
   // a batch of independent bootstraps, `lanes` at a time side by side (each on its own thread
   // and stream lane, PhantomContext::kLanes at most), each lane `group` ciphertexts at a time in
   // lockstep (1..8; 8 gains ~1.5% at C5 for ~80 GiB more device memory); the results are ordered
@@ -266,10 +270,6 @@ class FHECKKSRNS {
   PhantomCiphertext bootstrap_once(const PhantomCiphertext& ct, const PhantomContext& cc, const Precom& pc) const;
   // bootstrap_once of 2..8 ciphertexts in lockstep (full packing): grouped linear-transform levels,
   // EvalMod on 2 x group lanes; each result equals bootstrap_once's, bit for bit
-#ifndef PHX_BOOT_GROUP
-#define PHX_BOOT_GROUP 4
-#endif
-  static constexpr size_t kBootGroup = PHX_BOOT_GROUP;
   std::vector<PhantomCiphertext> bootstrap_group(const std::vector<const PhantomCiphertext*>& in,
                                                  const PhantomContext& cc, const Precom& pc) const;
 

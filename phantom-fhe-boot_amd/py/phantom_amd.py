@@ -88,6 +88,7 @@ _SIGS = {
                                            ctypes.c_uint32, sz, ctypes.POINTER(sz), ctypes.POINTER(sz),
                                            ctypes.POINTER(sz)]),
     "phantom_boot_run": (ctypes.c_int, [vp, vp, sz, sz, vp, sz, ctypes.c_int]),
+    "phantom_boot_run_grouped": (ctypes.c_int, [vp, vp, sz, sz, vp, sz, ctypes.c_int, ctypes.c_int]),
     "phantom_boot_decrypt": (ctypes.c_int, [vp, vp, sz, vp]),
 }
 
@@ -252,8 +253,13 @@ class BootSession:
                                           ctypes.byref(b)))
         return b.value
 
-    def run(self, dev_in, in_stride, count, dev_out, out_stride, lanes=4):
-        check(load().phantom_boot_run(self.handle, dev_in, in_stride, count, dev_out, out_stride, lanes))
+    def run(self, dev_in, in_stride, count, dev_out, out_stride, lanes=4, group=None):
+        """group: ciphertexts per lane in lockstep (1..8); None = the library default (4)."""
+        if group is None:
+            check(load().phantom_boot_run(self.handle, dev_in, in_stride, count, dev_out, out_stride, lanes))
+        else:
+            check(load().phantom_boot_run_grouped(self.handle, dev_in, in_stride, count, dev_out, out_stride, lanes,
+                                                  group))
 
     def decrypt(self, dev_ptr, capacity):
         import numpy as np

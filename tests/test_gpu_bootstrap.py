@@ -198,6 +198,34 @@ def test_two_iteration_bootstrap_gains_precision():
     assert two[0] > 21.0 and two[0] > one[0] + 10.0, (one, two)
 
 
+def test_session_run_grouped_matches_default():
+    """phantom_boot_run_grouped: 9 bootstraps on 1 lane as a group of 8 and a single one, and on 2
+    lanes as groups of 2 (5 and 4 per lane), each byte-identical to phantom_boot_run's groups of 4;
+    a group outside 1..8 is PHANTOM_ERR_INVALID_ARGUMENT."""
+    import numpy as np
+    import torch
+    import phantom_amd as PA
+    sess = PA.BootSession(bytes(range(32)))
+    count, chain = 9, 26
+    vals = np.random.default_rng(0xB8).uniform(1.0, 5.0, size=(count, sess.slots))
+    sin, sout = sess.input_bytes(chain), sess.output_bytes()
+    dev_in = torch.empty((count, sin), dtype=torch.uint8, device="cuda")
+    assert sess.encrypt(vals, chain, dev_in.data_ptr(), sin) == sin
+    outs = []
+    for lanes, group in ((1, None), (1, 8), (2, 2)):
+        o = torch.zeros((count, sout), dtype=torch.uint8, device="cuda")
+        sess.run(dev_in.data_ptr(), sin, count, o.data_ptr(), sout, lanes, group)
+        torch.cuda.synchronize()
+        outs.append(o.cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    dev_out = outs[0].cuda()
+    bits = [PA.bit_precision(vals[i], sess.decrypt(dev_out[i].data_ptr(), sout)) for i in range(2)]
+    assert min(bits) > 9.85, bits
+    with pytest.raises(PA.PhantomError):
+        sess.run(dev_in.data_ptr(), sin, 1, dev_out.data_ptr(), sout, 1, 9)
+    sess.close()
+
+
 def test_bench_c5_leg_single_gpu():
     """bench.py's C5 leg at world size 1 with a small batch: encrypt on rank 0, scatter, batch
     bootstrap on lanes, gather, decrypt-check every result."""
