@@ -310,7 +310,8 @@ def job_throughput(units_per_rank, world, max_seconds):
     return units_per_rank * world / max_seconds
 
 
-def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, verify=None, key_seed=None):
+def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, verify=None, key_seed=None,
+           group=4):
     """Config C5: `total` independent C4 bootstraps sharded over the ranks, one
     process per GPU.  Every rank regenerates the same keys from a 32-byte seed rank 0 broadcasts
     (no key traffic).  Rank 0 encrypts the batch — 2^15 reals in [1, 5] per ciphertext at chain
@@ -348,7 +349,7 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, 
     warm_in = torch.empty((warm_n, sin), dtype=torch.uint8, device=dev)
     sess.encrypt(rng.uniform(1.0, 5.0, size=(warm_n, sess.slots)), chain, warm_in.data_ptr(), sin)
     warm_out = torch.empty((warm_n, sout), dtype=torch.uint8, device=dev)
-    sess.run(warm_in.data_ptr(), sin, warm_n, warm_out.data_ptr(), sout, lanes)
+    sess.run(warm_in.data_ptr(), sin, warm_n, warm_out.data_ptr(), sout, lanes, group)
     del warm_in, warm_out
     local_out = torch.empty((per, sout), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
@@ -358,7 +359,7 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, 
     t0 = time.perf_counter()
     local_in = shard.scatter_rows(dist, full, per, sin, dev)
     torch.cuda.synchronize()
-    sess.run(local_in.data_ptr(), sin, per, local_out.data_ptr(), sout, lanes)
+    sess.run(local_in.data_ptr(), sin, per, local_out.data_ptr(), sout, lanes, group)
     torch.cuda.synchronize()
     gathered = shard.gather_rows(dist, local_out, dev)
     torch.cuda.synchronize()
@@ -377,7 +378,7 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, 
         res = {
             "workload": f"C5: {total} independent C4 bootstraps (input chain index {chain}) sharded over {world} rank(s), "
                         "scatter -> EvalBootstrapBatch -> gather of serialized ciphertexts",
-            "bootstraps": total, "bootstraps_per_rank": per, "lanes_per_rank": lanes, "lockstep_group": 4, "ranks": world,
+            "bootstraps": total, "bootstraps_per_rank": per, "lanes_per_rank": lanes, "lockstep_group": group, "ranks": world,
             "bootstraps_per_s": round(total / max_s, 3), "max_rank_s": round(max_s, 3),
             "scatter_gather_bytes": total * (sin + sout),
             "verified": nver, "min_avg_bits": round(min(bits), 2), "mean_avg_bits": round(float(np.mean(bits)), 2),
@@ -434,6 +435,8 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (sharded bootstrap batch) leg")
     ap.add_argument("--c5-batch", type=int, default=1024, help="C5: bootstraps in the whole batch")
     ap.add_argument("--c5-lanes", type=int, default=4, help="C5: concurrent bootstraps per GPU")
+    ap.add_argument("--c5-group", type=int, default=4,
+                    help="C5: bootstraps per lane in lockstep (1..8; 8 holds ~80 GiB more device memory)")
     ap.add_argument("--c5-verify", type=int, default=None, help="C5: decrypt-check only the first K results")
     ap.add_argument("--c5-key-seed", default=None, help="C5: 64 hex digits of key seed (default: OS entropy)")
     args = ap.parse_args()
@@ -532,7 +535,8 @@ def main():
     c5 = None
     if not args.no_c5:
         c5 = c5_leg(dist if world > 1 else None, torch, world, rank, local_rank, total=args.c5_batch,
-                    lanes=args.c5_lanes, verify=args.c5_verify, key_seed=args.c5_key_seed)
+                    lanes=args.c5_lanes, verify=args.c5_verify, key_seed=args.c5_key_seed,
+                    group=args.c5_group)
 
     # parity spot-check of the last buffer state is done by tests/; here just sanity
     value = job_throughput(2 * BYTES_PER_TRANSFORM * args.steps, world, elapsed) / 1e9
