@@ -344,8 +344,9 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, 
     if rank == 0:
         full = torch.empty((total, sin), dtype=torch.uint8, device=dev)
         sess.encrypt(values, chain, full.data_ptr(), sin)
-    # warm-up on every rank (first-use allocations and code loading), untimed
-    warm_n = min(lanes, per)
+    # warm-up on every rank (first-use allocations and code loading), untimed: one full lockstep
+    # group per lane, so the grouped path's buffers are in the pool before the timed region
+    warm_n = min(lanes * group, per)
     warm_in = torch.empty((warm_n, sin), dtype=torch.uint8, device=dev)
     sess.encrypt(rng.uniform(1.0, 5.0, size=(warm_n, sess.slots)), chain, warm_in.data_ptr(), sin)
     warm_out = torch.empty((warm_n, sout), dtype=torch.uint8, device=dev)
