@@ -40,6 +40,7 @@ BYTES_PER_TRANSFORM = 16 * N * L  # 46,137,344
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 RING_BYTES = 512 << 20  # > 2 x the 256 MiB Infinity Cache: a buffer is cold again when the ring comes back to it
 FWD_LAUNCHES = 200  # forward launches behind the roofline's fwd_ms (independent of --steps)
+TWO_PASS_FLOOR_US = 17.5  # two read+write passes over the [44][65536] batch, no arithmetic
 
 
 def _oracle_ntt_rate(O, mods, threads, seconds):
@@ -386,6 +387,16 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, 
             "setup_s": round(setup_s, 2), "scaling": "strong",
             "keys": "regenerated on every rank from a broadcast 32-byte seed",
         }
+        # roofline per GPU: the reference schedule's key and diagonal bytes (c4_reference_bytes) read
+        # once per lockstep group (the grouped kernels share them through each XCD's L2), plus each
+        # bootstrap's own ciphertext I/O, over the measured per-GPU bootstrap rate
+        _, parts, _ = c4_reference_bytes(input_chain=chain)
+        per_boot = (parts["keys"] + parts["plaintexts"]) / max(1, group) + parts["ciphertexts"]
+        ach = per_boot * (total / max_s) / world / 1e9
+        res["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_bootstrap": int(per_boot),
+                           "source": "bench.c4_reference_bytes: (keys + diagonals) / lockstep group + ciphertext I/O "
+                                     "per bootstrap, per GPU"}
     del full, gathered, local_out
     sess.close()
     return res
@@ -586,6 +597,12 @@ def main():
                 "launch_gap_ms": round(fwd_ms - KERNEL_SUM_MS, 5) if KERNEL_SUM_MS else None,
                 "traffic": pmc_traffic(),
                 "traffic_source": PMC_TRAFFIC_FILE,
+                # the two-pass design's own ceiling: one read + write of the batch per pass, measured as
+                # a plain two-pass copy of the same tiles (17.5 us): 0.60 of 8 TB/s
+                # (9.6 us per forward) is beyond any two-pass transform
+                "two_pass_floor_us": TWO_PASS_FLOOR_US,
+                "two_pass_floor_frac": round(BYTES_PER_TRANSFORM / (TWO_PASS_FLOOR_US * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                "two_pass_floor_source": "profiles/r01/ubench_fused.txt, profiles/r02/ubench_stream.txt",
             },
         }
         if not args.no_c3:

@@ -141,7 +141,8 @@ int phantom_relinearize_rescale(const phantom_context *ctx, size_t chain_index, 
  * ([2][L-1][n]); bit-identical to phantom_relinearize_rescale on each.  The reference issues one
  * relinearize_inplace + rescale_to_next_inplace per product (src/evaluate.cu:1552-1647); EvalMod's
  * Chebyshev ladder and double angle (src/bootstrap.cu:1657-1668, src/evaluate.cu:3264-3535) run
- * their independent products this way. */
+ * their independent products this way.  Not in place: the output range
+ * [out, out + (count - 1) out_stride + 2 (L-1) n) must not meet the ct3 range (rejected). */
 int phantom_relinearize_rescale_batch(const phantom_context *ctx, size_t chain_index, const uint64_t *ct3,
                                       size_t ct3_stride, size_t count, uint64_t *out, size_t out_stride,
                                       const uint64_t *const *key_digits, size_t dnum, hipStream_t stream);
@@ -229,6 +230,31 @@ int phantom_fast_rotation_ext_batch(const phantom_context *ctx, size_t chain_ind
 int phantom_rotate_ext_accumulate(const phantom_context *ctx, size_t chain_index, uint64_t *ext,
                                   const uint64_t *const *key_digits, size_t dnum, uint32_t galois_elt, uint64_t *acc,
                                   int accumulate, hipStream_t stream);
+/* ---- lockstep groups: `group` (2..8) ciphertexts of one level through the same keys / plaintexts in
+ * ONE launch (a bootstrap batch, src/bootstrap.cu:1157-1405 run per ciphertext by the reference).
+ * The ciphertexts' workgroups for the same elements run on one XCD, so the shared operand is read
+ * from HBM about once per group; every result equals the single-ciphertext entry above on that
+ * ciphertext, bit for bit.
+ * phantom_lt_bsgs_group: phantom_lt_bsgs for ciphertext c with babies[c] + j baby_stride (words) as
+ * baby j; inner sum 0 goes to acc[c], inner sum i >= 1 to giants[c] + (i - 1) giant_stride.
+ * g must be 32 and b <= 8 (the bootstrap's CoeffToSlot / SlotToCoeff levels). */
+int phantom_lt_bsgs_group(const phantom_context *ctx, size_t chain_index, size_t group,
+                          const uint64_t *const *babies, size_t baby_stride, size_t g, const uint64_t *const *pts,
+                          size_t b, uint64_t *const *acc, uint64_t *const *giants, size_t giant_stride,
+                          hipStream_t stream);
+/* phantom_fast_rotation_ext_batch for ciphertext c = (cts[c], digits[c]) with outputs
+ * outs[c * count + k]; the entries (key_digits, galois_elts) are shared, and every ciphertext's outputs
+ * must sit at the same offsets from its first output (outs[c * count + k] - outs[c * count]). */
+int phantom_fast_rotation_ext_batch_group(const phantom_context *ctx, size_t chain_index, size_t group,
+                                          const uint64_t *const *cts, const uint64_t *const *digits,
+                                          const uint64_t *const *const *key_digits, size_t dnum,
+                                          const uint32_t *galois_elts, size_t count, uint64_t *const *outs,
+                                          hipStream_t stream);
+/* phantom_rotate_ext_accumulate of ext[c] into acc[c] for c < group by the same rotation key */
+int phantom_rotate_ext_accumulate_group(const phantom_context *ctx, size_t chain_index, size_t group,
+                                        uint64_t *const *ext, const uint64_t *const *key_digits, size_t dnum,
+                                        uint32_t galois_elt, uint64_t *const *acc, int accumulate,
+                                        hipStream_t stream);
 /* tensor_prod_2x2 with MulAddRescale's linear epilogue: out [3][Ql][n] = f (ct1 x ct2), then
  * out[p] += c t[p] for p < 2 (t[p] at t + p t_stride; f, c: host residues per limb or NULL) */
 int phantom_tensor_lin(const phantom_context *ctx, size_t chain_index, const uint64_t *ct1, const uint64_t *ct2,

@@ -186,6 +186,143 @@ int phantom_rotate_ext_accumulate(const phantom_context* ctx, size_t chain_index
   });
 }
 
+int phantom_lt_bsgs_group(const phantom_context* ctx, size_t chain_index, size_t group,
+                          const uint64_t* const* babies, size_t baby_stride, size_t g, const uint64_t* const* pts,
+                          size_t b, uint64_t* const* acc, uint64_t* const* giants, size_t giant_stride,
+                          hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    if (!babies || !pts || !acc || (b > 1 && !giants)) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (group < 2 || group > static_cast<size_t>(phx::kLtGroupMax))
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "group must hold 2 to 8 ciphertexts");
+    if (g != 32 || b < 1 || b > 8) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "grouped inner sums need g = 32, b <= 8");
+    const size_t ext_words = 2 * (rt.size_Ql() + pc.size_P()) * pc.poly_degree();
+    if (baby_stride < ext_words || (b > 1 && giant_stride < ext_words))
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "stride below one extended-basis ciphertext");
+    phx::LtGroupArgs a;
+    a.g = static_cast<int>(g);
+    a.b = static_cast<int>(b);
+    a.Ql = static_cast<int>(rt.size_Ql());
+    a.P = static_cast<int>(pc.size_P());
+    a.size_Q = static_cast<int>(pc.size_Q());
+    a.q = pc.mod_QP().q;
+    a.barrett = pc.mod_QP().barrett;
+    a.count = static_cast<int>(group);
+    a.baby_stride = baby_stride;
+    a.giant_stride = giant_stride;
+    for (size_t c = 0; c < group; ++c) {
+      if (!babies[c] || !acc[c] || (b > 1 && !giants[c])) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+      a.baby0[c] = babies[c];
+      a.acc[c] = acc[c];
+      a.giant1[c] = b > 1 ? giants[c] : acc[c];
+    }
+    phantom::DeviceBuffer<const uint64_t*> table;
+    table.upload(std::vector<const uint64_t*>(pts, pts + g * b), stream);
+    a.pts = table.get();
+    const hipError_t e = phx::lt_bsgs_group(a, pc.poly_degree(), stream);
+    PHX_CHECK(hipStreamSynchronize(stream));  // the pointer table is freed on return
+    return from_hip(e);
+  });
+}
+
+int phantom_fast_rotation_ext_batch_group(const phantom_context* ctx, size_t chain_index, size_t group,
+                                          const uint64_t* const* cts, const uint64_t* const* digits,
+                                          const uint64_t* const* const* key_digits, size_t dnum,
+                                          const uint32_t* galois_elts, size_t count, uint64_t* const* outs,
+                                          hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (count == 0) return PHANTOM_OK;
+    if (!cts || !digits || !key_digits || !galois_elts || !outs) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (group < 2 || group > static_cast<size_t>(phx::kKsGroupMax))
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "group must hold 2 to 8 ciphertexts");
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    const size_t n = pc.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + pc.size_P();
+    std::vector<phx::KsBatchEntry> e(count);
+    for (size_t k = 0; k < count; ++k) {
+      if (key_digits[k]) {
+        e[k].evk = phantom_capi_key_array(ctx, key_digits[k], dnum, rt.beta());
+        e[k].perm = pc.galois_perm(galois_elts[k]);
+        e[k].binv = pc.galois_block_inv(galois_elts[k]);
+      }
+    }
+    for (size_t c = 0; c < group; ++c) {
+      if (!cts[c] || !digits[c]) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+      for (size_t k = 0; k < count; ++k) {
+        uint64_t* const o = outs[c * count + k];
+        if (!o) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null output");
+        const int64_t off = o - outs[c * count];
+        if (c == 0) e[k].out_off = off;
+        else if (off != e[k].out_off)
+          return fail(PHANTOM_ERR_INVALID_ARGUMENT, "every ciphertext's outputs must sit at the same offsets");
+      }
+    }
+    phantom::DeviceBuffer<phx::KsBatchEntry> table;
+    table.upload(e, stream);
+    phx::KsRotateBatchGroupArgs ga;
+    ga.count = static_cast<int>(group);
+    for (size_t c = 0; c < group; ++c) {
+      phx::KsRotateBatchArgs& a = ga.a[c];
+      a.digits = digits[c];
+      a.entries = table.get();
+      a.count = static_cast<uint32_t>(count);
+      a.qp = pc.mod_QP().q;
+      a.qp_barrett = pc.mod_QP().barrett;
+      a.ct = cts[c];
+      a.pmod = rt.bigP_mod_q();
+      a.pmod_shoup = rt.bigP_mod_q_shoup();
+      a.out = outs[c * count];
+      a.ql = static_cast<uint32_t>(Ql);
+      a.qlp = static_cast<uint32_t>(QlP);
+      a.size_q = static_cast<uint32_t>(pc.size_Q());
+      a.size_p = static_cast<uint32_t>(pc.size_P());
+      a.beta = static_cast<uint32_t>(rt.beta());
+    }
+    const hipError_t err = phx::keyswitch_rotate_batch_group(ga, n, stream);
+    PHX_CHECK(hipStreamSynchronize(stream));  // the entry table is freed on return
+    return from_hip(err);
+  });
+}
+
+int phantom_rotate_ext_accumulate_group(const phantom_context* ctx, size_t chain_index, size_t group,
+                                        uint64_t* const* ext, const uint64_t* const* key_digits, size_t dnum,
+                                        uint32_t galois_elt, uint64_t* const* acc, int accumulate,
+                                        hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    if (!ext || !acc) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (group < 2 || group > static_cast<size_t>(phx::kKsGroupMax))
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "group must hold 2 to 8 ciphertexts");
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    const size_t n = pc.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + pc.size_P();
+    const uint64_t* const* evk = phantom_capi_key_array(ctx, key_digits, dnum, rt.beta());
+    const size_t dwords = rt.beta() * QlP * n;
+    phantom::DeviceBuffer<uint64_t> digits(group * dwords, stream);
+    phx::KsRotateGroupArgs ga;
+    ga.count = static_cast<int>(group);
+    for (size_t c = 0; c < group; ++c) {
+      if (!ext[c] || !acc[c]) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+      rt.moddown_modup(digits.get() + c * dwords, ext[c] + QlP * n, pc.gpu_rns_tables(), stream);
+      phx::KsRotateArgs& g = ga.a[c];
+      g.digits = digits.get() + c * dwords;
+      g.evk = evk;
+      g.qp = pc.mod_QP().q;
+      g.qp_barrett = pc.mod_QP().barrett;
+      g.c0 = ext[c];
+      g.out = acc[c];
+      g.perm = pc.galois_perm(galois_elt);
+      g.ql = static_cast<uint32_t>(Ql);
+      g.qlp = static_cast<uint32_t>(QlP);
+      g.size_q = static_cast<uint32_t>(pc.size_Q());
+      g.size_p = static_cast<uint32_t>(pc.size_P());
+      g.beta = static_cast<uint32_t>(rt.beta());
+      g.accumulate = accumulate != 0;
+    }
+    return from_hip(phx::keyswitch_rotate_group(ga, 2, n, stream));
+  });
+}
+
 int phantom_tensor_lin(const phantom_context* ctx, size_t chain_index, const uint64_t* ct1, const uint64_t* ct2,
                        uint64_t* out, const uint64_t* f, const uint64_t* t, size_t t_stride, const uint64_t* c,
                        hipStream_t stream) {

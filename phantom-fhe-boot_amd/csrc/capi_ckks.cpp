@@ -154,6 +154,12 @@ int phantom_relinearize_rescale_batch(const phantom_context* ctx, size_t chain_i
       return fail(PHANTOM_ERR_INVALID_ARGUMENT, "bad batch (1 <= count <= 16)");
     if (count > 1 && (ct3_stride < 3 * L * n || out_stride < 2 * (L - 1) * n))
       return fail(PHANTOM_ERR_INVALID_ARGUMENT, "batch strides overlap");
+    // not in place: the finish reads c0 / c1 of every ct3 ([3][L][n]) while it writes the outputs
+    // ([2][L-1][n]) in another layout, so an output range must not meet an input range
+    const uintptr_t in0 = reinterpret_cast<uintptr_t>(ct3), out0 = reinterpret_cast<uintptr_t>(out);
+    const uintptr_t in1 = in0 + ((count - 1) * ct3_stride + 3 * L * n) * sizeof(uint64_t);
+    const uintptr_t out1 = out0 + ((count - 1) * out_stride + 2 * (L - 1) * n) * sizeof(uint64_t);
+    if (out0 < in1 && in0 < out1) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "output overlaps the input (not in place)");
     auto* c = const_cast<phantom_context*>(ctx);
     const uint64_t* const* evk = c->device_key_array(key_digits, dnum, rt.beta());
     std::vector<uint64_t*> outs(count);

@@ -225,7 +225,7 @@ struct KsRotateBatchArgs {
   uint32_t ql = 0, qlp = 0, size_q = 0, size_p = 0, beta = 0;
 };
 hipError_t keyswitch_rotate_batch(const KsRotateBatchArgs& a, size_t n, hipStream_t s);
-// keyswitch_rotate_batch of `count` (2..4) ciphertexts at one level through the same entries (keys)
+// keyswitch_rotate_batch of `count` (2..kKsGroupMax) ciphertexts at one level through the same entries (keys)
 // in one launch, the ciphertexts' workgroups of a (limb, source block) on one XCD so that the keys
 // are read from HBM about once for all; a[0..count) differ only in digits / ct / out.  Each result
 // equals its own keyswitch_rotate_batch, bit for bit.

@@ -841,6 +841,42 @@ int main(int argc, char** argv) {
     return g_ok ? 0 : 1;
   }
 
+  if (mode == "prof") {
+    // kernel-trace windows for rocprofv3 (tools/prof_windows.py cuts the trace at idle gaps of more
+    // than 20 ms): warm-up, then exactly ONE warm bootstrap, then ONE lockstep group of `iters`
+    // (default 4) bootstraps on one lane, each between device synchronisations and 100 ms sleeps
+    const size_t group = static_cast<size_t>(std::max(2, std::min(iters, 8)));
+    std::vector<PhantomCiphertext> batch(group);
+    for (size_t i = 0; i < group; ++i) {
+      std::vector<double> xi(slots);
+      for (auto& v : xi) v = dis(rng);
+      PhantomPlaintext p;
+      enc.encode(ctx, xi, ct.scale(), p, ct.chain_index());
+      sk.encrypt_symmetric(ctx, p, batch[i]);
+    }
+    auto gap = [] {
+      PHX_CHECK(hipDeviceSynchronize());
+      const double t = now_ms();
+      while (now_ms() - t < 100.0) {
+      }
+    };
+    for (int w = 0; w < 2; ++w) (void)boot.EvalBootstrap(ct, ctx);
+    (void)boot.EvalBootstrapBatch(batch, ctx, 1, 0, group);
+    gap();
+    double a = now_ms();
+    PhantomCiphertext one = boot.EvalBootstrap(ct, ctx);
+    PHX_CHECK(hipDeviceSynchronize());
+    const double ms1 = now_ms() - a;
+    gap();
+    a = now_ms();
+    std::vector<PhantomCiphertext> outs = boot.EvalBootstrapBatch(batch, ctx, 1, 0, group);
+    PHX_CHECK(hipDeviceSynchronize());
+    const double msg = now_ms() - a;
+    gap();
+    std::printf("{\"stage\": \"prof\", \"single_ms\": %.2f, \"group\": %zu, \"group_ms\": %.2f}\n", ms1, group, msg);
+    return 0;
+  }
+
   if (mode == "batch") {
     // C5 on one GPU: `iters` independent bootstraps, `lanes` of them side by side
     const int lanes = argc > 4 ? std::atoi(argv[4]) : 2;

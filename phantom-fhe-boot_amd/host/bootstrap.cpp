@@ -1466,7 +1466,10 @@ static void trace(const PhantomContext& cc, const char* stage, const PhantomCiph
 std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<PhantomCiphertext>& in,
                                                               const PhantomContext& cc, int lanes,
                                                               uint32_t numSlots, size_t group) const {
-  const int k = std::max(1, std::min({lanes, PhantomContext::kLanes, static_cast<int>(in.size())}));
+  // a call from one of this function's own lane threads (a nested batch) runs serially on the
+  // caller's lane: its lane streams are already in use by the outer batch
+  static thread_local bool on_lane = false;
+  const int k = on_lane ? 1 : std::max(1, std::min({lanes, PhantomContext::kLanes, static_cast<int>(in.size())}));
   if (group < 1 || group > static_cast<size_t>(phx::kLtGroupMax))
     throw std::invalid_argument("EvalBootstrapBatch: group must be 1.." + std::to_string(phx::kLtGroupMax));
   std::vector<PhantomCiphertext> out(in.size());
@@ -1507,6 +1510,7 @@ std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<
     workers.emplace_back([&, t] {
       try {
         LaneGuard lane(cc, t);
+        on_lane = true;
         run_lane(t);
       } catch (...) {
         err[t] = std::current_exception();

@@ -98,10 +98,10 @@ class FHECKKSRNS {
   // bootstrap, scale the residual error up by 2^precision, bootstrap it and subtract.
   PhantomCiphertext EvalBootstrap(const PhantomCiphertext& ct, const PhantomContext& cc, uint32_t numSlots = 0,
                                   uint32_t numIterations = 1, uint32_t precision = 0) const;
-#ifndef PHX_BOOT_GROUP
-#define PHX_BOOT_GROUP 4
-#endif
-  static constexpr size_t kBootGroup = PHX_BOOT_GROUP;  // EvalBootstrapBatch's default lockstep group
+  // EvalBootstrapBatch's default lockstep group (a run-time choice: the group argument below,
+  // phantom_boot_run_grouped at the C-ABI)
+  static constexpr size_t kBootGroup = 4;
+  static_assert(kBootGroup >= 1 && kBootGroup <= 8, "lockstep groups hold 1 to phx::kLtGroupMax ciphertexts");
   // a batch of independent bootstraps, `lanes` at a time side by side (each on its own thread
   // and stream lane, PhantomContext::kLanes at most), each lane `group` ciphertexts at a time in
   // lockstep (1..8; 8 gains ~1.5% at C5 for ~80 GiB more device memory); the results are ordered

@@ -74,6 +74,14 @@ _SIGS = {
                                                        ctypes.POINTER(ctypes.c_uint32), sz, ctypes.POINTER(vp), vp]),
     "phantom_rotate_ext_accumulate": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, ctypes.c_uint32, vp,
                                                      ctypes.c_int, vp]),
+    "phantom_lt_bsgs_group": (ctypes.c_int, [vp, sz, sz, ctypes.POINTER(vp), sz, sz, ctypes.POINTER(vp), sz,
+                                             ctypes.POINTER(vp), ctypes.POINTER(vp), sz, vp]),
+    "phantom_fast_rotation_ext_batch_group": (ctypes.c_int, [vp, sz, sz, ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                                             ctypes.POINTER(ctypes.POINTER(vp)), sz,
+                                                             ctypes.POINTER(ctypes.c_uint32), sz, ctypes.POINTER(vp),
+                                                             vp]),
+    "phantom_rotate_ext_accumulate_group": (ctypes.c_int, [vp, sz, sz, ctypes.POINTER(vp), ctypes.POINTER(vp), sz,
+                                                           ctypes.c_uint32, ctypes.POINTER(vp), ctypes.c_int, vp]),
     "phantom_tensor_lin": (ctypes.c_int, [vp, sz, vp, vp, vp, vp, vp, sz, vp, vp]),
     "phantom_lin_comb": (ctypes.c_int, [vp, sz, vp, sz, vp, vp, sz, sz, vp, vp]),
     "phantom_mul_scalar": (ctypes.c_int, [vp, sz, vp, sz, vp, vp, vp, sz, vp]),

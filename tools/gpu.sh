@@ -51,6 +51,18 @@ step_pmc() {
        -- ${PMC_CMD:?PMC_CMD unset} > "$OUT/pmc$i.log" 2>&1) || { echo "pmc pass $i failed"; tail -5 "$OUT/pmc$i.log"; return 1; }
   done
 }
+step_profboot() {  # kernel trace of ONE warm bootstrap and ONE lockstep group of $GROUP, one CSV per window
+  (cd /tmp && timeout -k 10 ${T_STATS:-300} rocprofv3 --kernel-trace --output-format csv -d "$OUT/profboot" -o run \
+     -- "$GRAFT_REPO_ROOT/phantom-fhe-boot_amd/bin/bootstrapping_example" prof 16 ${GROUP:-4} > "$OUT/profboot.log" 2>&1)
+  local rc=$?; tail -2 "$OUT/profboot.log"; [ $rc -eq 0 ] || return $rc
+  $PY tools/prof_windows.py "$(find "$OUT/profboot" -name '*kernel_trace.csv' | head -1)" "$OUT/boot_window"
+}
+step_profpmc() {  # FETCH_SIZE per dispatch over the same run (lt_bsgs_wide vs lt_bsgs_group)
+  (cd /tmp && timeout -s KILL ${T_PMC:-240} rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv \
+     -d "$OUT/profpmc" -o run -- "$GRAFT_REPO_ROOT/phantom-fhe-boot_amd/bin/bootstrapping_example" prof 16 ${GROUP:-4} \
+     > "$OUT/profpmc.log" 2>&1) || { tail -5 "$OUT/profpmc.log"; return 1; }
+  $PY tools/lt_fetch.py "$OUT/profpmc" > "$OUT/lt_fetch.json" && cat "$OUT/lt_fetch.json"
+}
 step_traffic() {
   PMC_SETS="FETCH_SIZE;WRITE_SIZE" step_pmc || return 1
   mkdir -p "$OUT/traffic" && mv "$OUT/pmc1" "$OUT/traffic/p1" && mv "$OUT/pmc2" "$OUT/traffic/p2"

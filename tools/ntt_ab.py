@@ -5,6 +5,8 @@ back-to-back means, and a checksum of the forward output (equal = bit-identical)
 round-trip flag.  NTT_BITS=60 uses the 40-limb C4 chain (integer path), 50 the C2 batch.
 
   python tools/ntt_ab.py <py dir of build A> <py dir of build B> ...
+A build may carry environment settings: <py dir>@NAME=value,NAME2=value (e.g. a run-time knob of one
+library).  NTT_REP=k repeats the moduli k times (a k times larger launch of the same primes).
 """
 import json
 import os
@@ -22,6 +24,8 @@ if os.environ.get("NTT_BITS", "50") == "60":
     mods = PA.coeff_modulus_create(N, [60] + [59] * 29 + [60] * 10)
 else:
     mods = PA.coeff_modulus_create(N, [60] + [50] * 44 + [60] * 15)[:L]
+mods = mods * int(os.environ.get("NTT_REP", "1"))
+L = len(mods)
 t = PA.NttTables(N, mods)
 rng = np.random.default_rng(1)
 base = np.concatenate([rng.integers(0, q, size=N, dtype=np.uint64) for q in mods])
@@ -70,7 +74,10 @@ def main():
     res = {d: [] for d in dirs}
     for rep in range(int(os.environ.get("REPS", "3"))):
         for d in dirs:
-            out = subprocess.run([sys.executable, "-c", CODE, d], capture_output=True, text=True, timeout=240)
+            path, _, envs = d.partition("@")
+            env = dict(os.environ)
+            env.update(dict(kv.split("=", 1) for kv in envs.split(",") if kv))
+            out = subprocess.run([sys.executable, "-c", CODE, path], capture_output=True, text=True, timeout=240, env=env)
             line = [l for l in out.stdout.splitlines() if l.startswith("RESULT")]
             if not line:
                 print(d, "ERROR", out.stderr[-600:], flush=True)
