@@ -355,6 +355,7 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, 
     del warm_in, warm_out
     local_out = torch.empty((per, sout), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
+    PA.pool_reset_peak()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -370,6 +371,7 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, 
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     max_s = max_over_ranks(dist, [elapsed], "cuda")[0]
+    pool = PA.pool_stats()  # the engine's device allocator on this rank (batch buffers are torch's)
     res = None
     if rank == 0:
         nver = total if verify is None else min(verify, total)
@@ -386,6 +388,8 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, 
             "verified": nver, "min_avg_bits": round(min(bits), 2), "mean_avg_bits": round(float(np.mean(bits)), 2),
             "setup_s": round(setup_s, 2), "scaling": "strong",
             "keys": "regenerated on every rank from a broadcast 32-byte seed",
+            "rank0_pool_GiB": {"held": round(pool["held"] / 2**30, 2), "peak_held": round(pool["peak_held"] / 2**30, 2),
+                               "peak_live": round(pool["peak_live"] / 2**30, 2)},
         }
         # roofline per GPU: the reference schedule's key and diagonal bytes (c4_reference_bytes) read
         # once per lockstep group (the grouped kernels share them through each XCD's L2), plus each

@@ -334,6 +334,11 @@ int phantom_switch_modulus_raise(const phantom_context *ctx, const uint64_t *in_
  * out[2] ciphertext operand / result bytes — the numerator of the bootstrap's roofline */
 int phantom_traffic_read(uint64_t *out);
 int phantom_traffic_reset(void);
+/* The engine's device allocator (host/buffer.h DevicePool, the reference's cudaMallocAsync pool with
+ * an unbounded release threshold, src/context.cu:127-131): out[0] bytes held from the driver,
+ * out[1] bytes live (handed out), out[2] peak live and out[3] peak held since the last reset. */
+int phantom_pool_stats(uint64_t *out);
+int phantom_pool_reset_peak(void);
 /* EvalMod's Chebyshev interpolant (host only): out[degree + 1] = coefficients c of
  * (2 pi)^(-2^-r) cos(2 pi (K y - 1/4) / 2^r) on [-1, 1], r = double_angle_iterations, with
  * p(y) = sum_k c_k T_k(y) (c_0 NOT halved; the reference's tables g_coefficientsUniform/Sparse,

@@ -116,6 +116,21 @@ int phantom_traffic_reset(void) {
   return PHANTOM_OK;
 }
 
+int phantom_pool_stats(uint64_t* out) {
+  if (!out) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+  const phantom::DevicePool::Stats st = phantom::DevicePool::instance().stats();
+  out[0] = st.held;
+  out[1] = st.live;
+  out[2] = st.peak_live;
+  out[3] = st.peak_held;
+  return PHANTOM_OK;
+}
+
+int phantom_pool_reset_peak(void) {
+  phantom::DevicePool::instance().reset_peak();
+  return PHANTOM_OK;
+}
+
 int phantom_eval_mod_coefficients(uint32_t K, uint32_t double_angle_iterations, int degree, double* out) {
   PHX_CAPI_GUARD({
     if (!out || degree < 1 || degree > 1024 || K < 1) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "bad arguments");

@@ -1,4 +1,7 @@
 #include "buffer.h"
+
+#include <algorithm>
+#include <iterator>
 #include "traffic.h"
 
 namespace phantom {
@@ -22,14 +25,9 @@ DevicePool& DevicePool::instance() {
 }
 
 size_t DevicePool::size_class(size_t bytes) {
-  if (bytes <= 512) return 512;
-  if (bytes < (size_t(1) << 20)) {
-    size_t c = 512;
-    while (c < bytes) c <<= 1;
-    return c;
-  }
-  const size_t g = size_t(2) << 20;  // 2 MiB granules above 1 MiB
-  return (bytes + g - 1) / g * g;
+  size_t c = 512;
+  while (c < bytes) c <<= 1;
+  return c;
 }
 
 hipEvent_t DevicePool::take_event() {
@@ -53,16 +51,113 @@ static bool event_done(hipEvent_t e) {
   return false;
 }
 
+void DevicePool::drop_done(Pending& pend) {
+  for (size_t i = pend.size(); i-- > 0;)
+    if (event_done(pend[i].second)) {
+      spare_.push_back(pend[i].second);
+      pend.erase(pend.begin() + static_cast<long>(i));
+    }
+}
+
+// a block whose last uses were on `s` (stream order) or have completed may be reused on `s`
+bool DevicePool::ready_for(Pending& pend, hipStream_t s) {
+  bool ready = true;
+  for (size_t i = pend.size(); i-- > 0;) {
+    if (pend[i].first == s) continue;
+    if (event_done(pend[i].second)) {
+      spare_.push_back(pend[i].second);
+      pend.erase(pend.begin() + static_cast<long>(i));
+    } else {
+      ready = false;
+    }
+  }
+  return ready;
+}
+
+void DevicePool::insert_free(Block* b) { by_size_.emplace(std::make_pair(b->chunk->dev, b->size), b); }
+
+void DevicePool::erase_free(Block* b) {
+  auto r = by_size_.equal_range({b->chunk->dev, b->size});
+  for (auto it = r.first; it != r.second; ++it)
+    if (it->second == b) {
+      by_size_.erase(it);
+      return;
+    }
+}
+
+void DevicePool::note_live(long delta) {
+  st_.live = static_cast<size_t>(static_cast<long>(st_.live) + delta);
+  if (st_.live > st_.peak_live) st_.peak_live = st_.live;
+  if (st_.held > st_.peak_held) st_.peak_held = st_.held;
+}
+
+// best fit among the free blocks of the device that are ready for `s`; splits off the rest
+void* DevicePool::carve(int dev, size_t c, hipStream_t s) {
+  for (auto it = by_size_.lower_bound({dev, c}); it != by_size_.end() && it->first.first == dev; ++it) {
+    Block* b = it->second;
+    if (!ready_for(b->pending, s)) continue;
+    by_size_.erase(it);
+    if (b->size > c) {  // the remainder stays free with the pending uses of the whole block
+      Block rest;
+      rest.chunk = b->chunk;
+      rest.off = b->off + c;
+      rest.size = b->size - c;
+      rest.pending = std::move(b->pending);
+      Block* r = &b->chunk->blocks.emplace(rest.off, std::move(rest)).first->second;
+      insert_free(r);
+      b->size = c;
+    }
+    for (auto& pe : b->pending) spare_.push_back(pe.second);  // (all on `s`: stream order covers them)
+    b->pending.clear();
+    b->free = false;
+    b->req = c;
+    void* p = b->chunk->base + b->off;
+    live_[p] = b;
+    note_live(static_cast<long>(c));
+    return p;
+  }
+  return nullptr;
+}
+
+DevicePool::Chunk* DevicePool::grow(int dev, size_t c) {
+  const size_t sz = std::max(c, kChunk);
+  void* p = nullptr;
+  if (hipMalloc(&p, sz) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  Chunk* ch = new Chunk();
+  ch->base = static_cast<char*>(p);
+  ch->size = sz;
+  ch->dev = dev;
+  Block b;
+  b.chunk = ch;
+  b.off = 0;
+  b.size = sz;
+  insert_free(&ch->blocks.emplace(0, std::move(b)).first->second);
+  chunks_.push_back(ch);
+  st_.held += sz;
+  return ch;
+}
+
 void DevicePool::forget_stream(hipStream_t s) {
   std::lock_guard<std::mutex> lk(mu_);
-  for (auto& kv : free_)
-    for (Block& b : kv.second)
+  for (auto& kv : small_free_)
+    for (Small& b : kv.second)
       if (b.stream == s) {
         // the caller has synchronised s: its blocks are free for any stream from now on
         if (b.ev) spare_.push_back(b.ev);
         b.ev = nullptr;
         b.stream = nullptr;
       }
+  for (auto& kv : by_size_) {
+    Pending& pend = kv.second->pending;
+    for (size_t i = pend.size(); i-- > 0;)
+      if (pend[i].first == s) {
+        spare_.push_back(pend[i].second);
+        pend.erase(pend.begin() + static_cast<long>(i));
+      }
+  }
 }
 
 // PHX_POOL_TRACE=1: one stderr line per out-of-memory release of the cache
@@ -74,53 +169,76 @@ static bool pool_trace() {
   return on;
 }
 
+// frees the cached small blocks and the arena chunks that are wholly free, whose uses completed
 void DevicePool::release_cached_locked() {
-  size_t cached = 0, freed = 0;
-  for (auto& kv : free_) cached += kv.first.second * kv.second.size();
-  const size_t held0 = held_;
-  for (auto& kv : free_) {
-    std::vector<Block> keep;
-    for (Block& b : kv.second) {
+  const size_t held0 = st_.held;
+  size_t freed = 0;
+  for (auto& kv : small_free_) {
+    std::vector<Small> keep;
+    for (Small& b : kv.second) {
       if (b.ev && !event_done(b.ev)) {
         keep.push_back(b);
         continue;
       }
       if (b.ev) spare_.push_back(b.ev);
       (void)hipFree(b.p);
-      held_ -= kv.first.second;
+      st_.held -= kv.first.second;
       freed += kv.first.second;
     }
     kv.second.swap(keep);
   }
+  for (size_t i = chunks_.size(); i-- > 0;) {
+    Chunk* ch = chunks_[i];
+    if (ch->blocks.size() != 1) continue;
+    Block& b = ch->blocks.begin()->second;
+    if (!b.free) continue;
+    drop_done(b.pending);
+    if (!b.pending.empty()) continue;
+    erase_free(&b);
+    (void)hipFree(ch->base);
+    st_.held -= ch->size;
+    freed += ch->size;
+    delete ch;
+    chunks_.erase(chunks_.begin() + static_cast<long>(i));
+  }
   if (pool_trace())
-    std::fprintf(stderr, "{\"pool_release\": true, \"held_MiB\": %zu, \"cached_MiB\": %zu, \"freed_MiB\": %zu}\n",
-                 held0 >> 20, cached >> 20, freed >> 20);
+    std::fprintf(stderr, "{\"pool_release\": true, \"held_MiB\": %zu, \"freed_MiB\": %zu, \"live_MiB\": %zu}\n",
+                 held0 >> 20, freed >> 20, st_.live >> 20);
 }
 
 void* DevicePool::alloc(size_t bytes, hipStream_t s) {
   int dev = 0;
   PHX_CHECK(hipGetDevice(&dev));
+  if (bytes >= kArenaMin) {
+    const size_t c = (bytes + kGrain - 1) / kGrain * kGrain;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (void* p = carve(dev, c, s)) return p;
+    if (grow(dev, c)) return carve(dev, c, s);
+    // out of device memory: return wholly free chunks and cached small blocks, then wait for every
+    // pending use so that all free blocks coalesce into reusable space
+    release_cached_locked();
+    if (grow(dev, c)) return carve(dev, c, s);
+    PHX_CHECK(hipDeviceSynchronize());
+    if (void* p = carve(dev, c, s)) return p;
+    release_cached_locked();
+    if (!grow(dev, c)) PHX_CHECK(hipErrorOutOfMemory);
+    return carve(dev, c, s);
+  }
   const size_t c = size_class(bytes);
   {
     std::lock_guard<std::mutex> lk(mu_);
-    // the exact class first; a large request may also take a cached block up to a quarter larger
-    // (the bootstrap's per-level buffers differ by a limb or two: without the slack each level
-    // keeps its own cached copies, and lockstep groups of them fill the GPU)
-#ifndef PHX_POOL_SLACK_Q
-#define PHX_POOL_SLACK_Q 1  // the slack in quarters of the request
-#endif
-    const size_t top = c >= kSlackMin ? c + c * PHX_POOL_SLACK_Q / 4 : c;
-    for (auto it = free_.lower_bound({dev, c}); it != free_.end() && it->first.first == dev && it->first.second <= top;
-         ++it) {
+    auto it = small_free_.find({dev, c});
+    if (it != small_free_.end()) {
       auto& v = it->second;
       for (size_t i = v.size(); i-- > 0;) {
-        Block& b = v[i];
+        Small& b = v[i];
         const bool ready = !b.ev || b.stream == s || event_done(b.ev);
         if (!ready) continue;
         void* p = b.p;
         if (b.ev) spare_.push_back(b.ev);
         v.erase(v.begin() + static_cast<long>(i));
-        live_[p] = it->first.second;  // the block's own class: it returns there
+        small_live_[p] = c;
+        note_live(static_cast<long>(c));
         return p;
       }
     }
@@ -135,35 +253,96 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
     PHX_CHECK(hipMalloc(&p, c));
   }
   std::lock_guard<std::mutex> lk(mu_);
-  live_[p] = c;
-  held_ += c;
+  small_live_[p] = c;
+  st_.held += c;
+  note_live(static_cast<long>(c));
   return p;
 }
 
 void DevicePool::free(void* p, size_t bytes, hipStream_t s, bool completed) {
   if (!p) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  if (bytes >= kArenaMin) {
+    auto it = live_.find(p);
+    const size_t c = (bytes + kGrain - 1) / kGrain * kGrain;
+    if (it == live_.end() || it->second->req != c) {
+      std::fprintf(stderr, "DevicePool: free of %p (%zu bytes) that is not a live block of that size (double free?)\n",
+                   p, bytes);
+      std::abort();
+    }
+    Block* b = it->second;
+    live_.erase(it);
+    note_live(-static_cast<long>(b->size));
+#ifdef PHX_GUARD
+    // debug builds: poison the block in the freeing stream's order, so a stream that still reads it
+    // after this free (a buffer freed on a stream other than its last user's) reads garbage and the
+    // results show it
+    if (!completed) PHX_CHECK(hipMemsetAsync(p, 0xFF, b->size, s));
+#endif
+    b->free = true;
+    b->req = 0;
+    if (!completed) {
+      hipEvent_t ev = take_event();
+      PHX_CHECK(hipEventRecord(ev, s));
+      b->pending.emplace_back(s, ev);
+    }
+    // coalesce with free neighbours (their pending uses move into the merged block)
+    auto& blocks = b->chunk->blocks;
+    auto me = blocks.find(b->off);
+    if (me != blocks.begin()) {
+      auto prev = std::prev(me);
+      if (prev->second.free) {
+        Block* pb = &prev->second;
+        erase_free(pb);
+        pb->size += b->size;
+        for (auto& pe : b->pending) pb->pending.push_back(pe);
+        blocks.erase(me);
+        b = pb;
+        me = prev;
+      }
+    }
+    auto nx = std::next(me);
+    if (nx != blocks.end() && nx->second.free) {
+      Block* nb = &nx->second;
+      erase_free(nb);
+      b->size += nb->size;
+      for (auto& pe : nb->pending) b->pending.push_back(pe);
+      blocks.erase(nx);
+    }
+    drop_done(b->pending);
+    insert_free(b);
+    return;
+  }
   int dev = 0;
   PHX_CHECK(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lk(mu_);
-  auto it = live_.find(p);
-  if (it == live_.end() || it->second < size_class(bytes)) {
+  auto it = small_live_.find(p);
+  if (it == small_live_.end() || it->second != size_class(bytes)) {
     std::fprintf(stderr, "DevicePool: free of %p (%zu bytes) that is not a live block (double free?)\n", p, bytes);
     std::abort();
   }
   const size_t cls = it->second;
-  live_.erase(it);
-  Block b{p, s, nullptr};
+  small_live_.erase(it);
+  note_live(-static_cast<long>(cls));
+  Small b{p, s, nullptr};
 #ifdef PHX_GUARD
-  // debug builds: poison the block in the freeing stream's order, so a stream that still reads it
-  // after this free (a buffer freed on a stream other than its last user's) reads garbage and the
-  // results show it
   if (!completed) PHX_CHECK(hipMemsetAsync(p, 0xFF, cls, s));
 #endif
   if (!completed) {
     b.ev = take_event();
     PHX_CHECK(hipEventRecord(b.ev, s));
   }
-  free_[{dev, cls}].push_back(b);
+  small_free_[{dev, cls}].push_back(b);
+}
+
+DevicePool::Stats DevicePool::stats() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return st_;
+}
+
+void DevicePool::reset_peak() {
+  std::lock_guard<std::mutex> lk(mu_);
+  st_.peak_live = st_.live;
+  st_.peak_held = st_.held;
 }
 
 }  // namespace phantom

@@ -19,37 +19,80 @@ namespace phantom {
 
 // Caching device allocator.  A freed block is kept with an event recorded on the stream that
 // freed it; it is handed out again to the same stream at once (stream order protects it) or
-// to another stream once that event has completed.  Blocks are never returned to the driver.
+// to another stream once that event has completed.  Blocks are never returned to the driver
+// (except to satisfy a failed hipMalloc).
 // Replaces hipMallocAsync / hipFreeAsync: with ROCm 7.2's stream-ordered pool, reused blocks
 // were observed to still be in use (key-switching keys and ciphertexts corrupted; reproduced by
 // examples/bootstrapping_example ops, gone with synchronous allocation).
+//  * Small requests (< kArenaMin) are cached by power-of-two size class.
+//  * Large requests are carved best-fit out of arena chunks (kChunk, or the request when larger)
+//    in kGrain units; a block is split on allocation and coalesced with free neighbours on free,
+//    the merged block carrying every pending (stream, event) of its parts.  Held memory then tracks
+//    the live set instead of one cached copy per distinct size (the bootstrap's per-level buffers
+//    differ by a limb or two).
 class DevicePool {
  public:
   static DevicePool& instance();
   void* alloc(size_t bytes, hipStream_t s);
   // completed: the caller has synchronised the device (no event needed)
   void free(void* p, size_t bytes, hipStream_t s, bool completed = false);
-  // size class of a request (blocks are reused only within a class)
-  static size_t size_class(size_t bytes);
   // stream `s` is about to be destroyed and has been synchronised: its cached blocks become
   // plain free blocks (a later stream may reuse the handle value; an event recorded on a
   // destroyed stream must not be queried)
   void forget_stream(hipStream_t s);
+  struct Stats {
+    size_t held = 0;       // bytes obtained from hipMalloc and not returned
+    size_t live = 0;       // bytes handed out and not freed
+    size_t peak_live = 0;  // maximum of `live` since the last reset_peak()
+    size_t peak_held = 0;
+  };
+  Stats stats();
+  void reset_peak();
+  static constexpr size_t kArenaMin = size_t(1) << 20;  // requests from here are carved from the arena
+  static constexpr size_t kGrain = size_t(64) << 10;    // arena block granularity
+  static constexpr size_t kChunk = size_t(1) << 30;     // arena growth step
 
  private:
-  struct Block {
+  using Pending = std::vector<std::pair<hipStream_t, hipEvent_t>>;  // uses a block may still have
+  struct Small {
     void* p;
     hipStream_t stream;
     hipEvent_t ev;  // null when known complete
   };
+  struct Chunk;
+  struct Block {
+    Chunk* chunk = nullptr;
+    size_t off = 0, size = 0;
+    bool free = true;
+    size_t req = 0;  // live blocks: the rounded request they were handed out for
+    Pending pending;
+  };
+  struct Chunk {
+    char* base = nullptr;
+    size_t size = 0;
+    int dev = 0;
+    std::map<size_t, Block> blocks;  // by offset, covering the chunk
+  };
   std::mutex mu_;
-  static constexpr size_t kSlackMin = size_t(4) << 20;          // requests from here may take a block up to 1/4 larger
-  std::map<std::pair<int, size_t>, std::vector<Block>> free_;  // (device, class) -> blocks
-  std::map<void*, size_t> live_;                               // handed-out blocks (double-free check)
+  // small blocks: (device, class) -> cached blocks
+  std::map<std::pair<int, size_t>, std::vector<Small>> small_free_;
+  std::map<void*, size_t> small_live_;  // handed-out small block -> its class
+  // arena
+  std::vector<Chunk*> chunks_;
+  std::multimap<std::pair<int, size_t>, Block*> by_size_;  // free arena blocks by (device, size)
+  std::map<void*, Block*> live_;                           // handed-out arena blocks
   std::vector<hipEvent_t> spare_;
-  size_t held_ = 0;  // bytes obtained from hipMalloc and not returned (live + cached)
+  Stats st_;
+  static size_t size_class(size_t bytes);
   hipEvent_t take_event();
+  bool ready_for(Pending& pend, hipStream_t s);  // drops completed uses
+  void drop_done(Pending& pend);
+  void insert_free(Block* b);
+  void erase_free(Block* b);
+  void* carve(int dev, size_t c, hipStream_t s);
+  Chunk* grow(int dev, size_t c);
   void release_cached_locked();
+  void note_live(long delta);
 };
 
 template <typename T>

@@ -66,6 +66,8 @@ _SIGS = {
     "phantom_boot_session_destroy": (ctypes.c_int, [vp]),
     "phantom_traffic_read": (ctypes.c_int, [vp]),
     "phantom_traffic_reset": (ctypes.c_int, []),
+    "phantom_pool_stats": (ctypes.c_int, [vp]),
+    "phantom_pool_reset_peak": (ctypes.c_int, []),
     "phantom_lt_bsgs": (ctypes.c_int, [vp, sz, ctypes.POINTER(vp), sz, ctypes.POINTER(vp), sz, ctypes.POINTER(vp), vp]),
     "phantom_keyswitch_ext": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_fast_rotation_ext": (ctypes.c_int, [vp, sz, vp, vp, ctypes.POINTER(vp), sz, ctypes.c_uint32, ctypes.c_int,
@@ -285,6 +287,17 @@ class BootSession:
             self.close()
         except Exception:
             pass
+
+
+def pool_stats():
+    """the device allocator's {held, live, peak_live, peak_held} bytes (phantom_pool_stats)"""
+    out = (ctypes.c_uint64 * 4)()
+    check(load().phantom_pool_stats(out))
+    return dict(zip(("held", "live", "peak_live", "peak_held"), (int(x) for x in out)))
+
+
+def pool_reset_peak():
+    check(load().phantom_pool_reset_peak())
 
 
 def traffic():

@@ -18,8 +18,12 @@ lib = PA.load()
 # BITS=60: 44 60-bit primes (the integer Shoup path every C4 bootstrap limb takes)
 if os.environ.get("BITS", "50") == "60":
     mods = PA.coeff_modulus_create(N, [60] * L)
+elif os.environ.get("BITS") == "c4":  # the 40-limb C4 chain (Q = {60, 29 x 59}, P = 10 x 60)
+    mods = PA.coeff_modulus_create(N, [60] + [59] * 29 + [60] * 10)
 else:
     mods = PA.coeff_modulus_create(N, [60] + [50] * 44 + [60] * 15)[:L]
+mods = mods * int(os.environ.get("REP", "1"))  # REP times as many limbs (the same primes) per launch
+L = len(mods)
 t = PA.NttTables(N, mods)
 rng = np.random.default_rng(1)
 base = np.concatenate([rng.integers(0, q, size=N, dtype=np.uint64) for q in mods])
