@@ -311,8 +311,8 @@ def job_throughput(units_per_rank, world, max_seconds):
     return units_per_rank * world / max_seconds
 
 
-def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=4, chain=26, verify=None, key_seed=None,
-           group=4):
+def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=3, chain=26, verify=None, key_seed=None,
+           group=8):
     """Config C5: `total` independent C4 bootstraps sharded over the ranks, one
     process per GPU.  Every rank regenerates the same keys from a 32-byte seed rank 0 broadcasts
     (no key traffic).  Rank 0 encrypts the batch — 2^15 reals in [1, 5] per ciphertext at chain
@@ -450,9 +450,10 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (bootstrap latency) leg")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (sharded bootstrap batch) leg")
     ap.add_argument("--c5-batch", type=int, default=1024, help="C5: bootstraps in the whole batch")
-    ap.add_argument("--c5-lanes", type=int, default=4, help="C5: concurrent bootstraps per GPU")
-    ap.add_argument("--c5-group", type=int, default=4,
-                    help="C5: bootstraps per lane in lockstep (1..8; 8 holds ~80 GiB more device memory)")
+    ap.add_argument("--c5-lanes", type=int, default=3, help="C5: stream lanes per GPU (each runs lockstep groups)")
+    ap.add_argument("--c5-group", type=int, default=8,
+                    help="C5: bootstraps per lane in lockstep (1..8); 3 x 8 holds ~86 GiB, 4 x 8 ~107 GiB, "
+                         "2 x 4 ~56 GiB (profiles/r05/c5_pool/)")
     ap.add_argument("--c5-verify", type=int, default=None, help="C5: decrypt-check only the first K results")
     ap.add_argument("--c5-key-seed", default=None, help="C5: 64 hex digits of key seed (default: OS entropy)")
     args = ap.parse_args()

@@ -100,11 +100,12 @@ class FHECKKSRNS {
                                   uint32_t numIterations = 1, uint32_t precision = 0) const;
   // EvalBootstrapBatch's default lockstep group (a run-time choice: the group argument below,
   // phantom_boot_run_grouped at the C-ABI)
-  static constexpr size_t kBootGroup = 4;
+  static constexpr size_t kBootGroup = 8;
   static_assert(kBootGroup >= 1 && kBootGroup <= 8, "lockstep groups hold 1 to phx::kLtGroupMax ciphertexts");
   // a batch of independent bootstraps, `lanes` at a time side by side (each on its own thread
   // and stream lane, PhantomContext::kLanes at most), each lane `group` ciphertexts at a time in
-  // lockstep (1..8; 8 gains ~1.5% at C5 for ~80 GiB more device memory); the results are ordered
+  // lockstep (1..8; groups of 8 on 3 lanes: 56.8/s holding 86 GiB, groups of 4 on 4 lanes: 55.6/s
+  // holding 79 GiB, profiles/r05/c5_pool/); the results are ordered
   // on cc.stream()
   std::vector<PhantomCiphertext> EvalBootstrapBatch(const std::vector<PhantomCiphertext>& in,
                                                     const PhantomContext& cc, int lanes, uint32_t numSlots = 0,

@@ -91,11 +91,17 @@ void DevicePool::note_live(long delta) {
   if (st_.held > st_.peak_held) st_.peak_held = st_.held;
 }
 
-// best fit among the free blocks of the device that are ready for `s`; splits off the rest
-void* DevicePool::carve(int dev, size_t c, hipStream_t s) {
+// best fit among the free blocks of the device that are ready for `s`; splits off the rest.  With
+// `wait`, the best fit among all free blocks: `s` is made to wait (on the device) for the pending
+// uses of the block on other streams, as a stream-ordered allocator reuses another stream's block.
+void* DevicePool::carve(int dev, size_t c, hipStream_t s, bool wait) {
   for (auto it = by_size_.lower_bound({dev, c}); it != by_size_.end() && it->first.first == dev; ++it) {
     Block* b = it->second;
-    if (!ready_for(b->pending, s)) continue;
+    if (!ready_for(b->pending, s)) {
+      if (!wait) continue;
+      for (auto& pe : b->pending)
+        if (pe.first != s) PHX_CHECK(hipStreamWaitEvent(s, pe.second, 0));
+    }
     by_size_.erase(it);
     if (b->size > c) {  // the remainder stays free with the pending uses of the whole block
       Block rest;
@@ -213,11 +219,18 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
     const size_t c = (bytes + kGrain - 1) / kGrain * kGrain;
     std::lock_guard<std::mutex> lk(mu_);
     if (void* p = carve(dev, c, s)) return p;
+    // Free blocks that are still in use by other streams: once the cached space exceeds the slack,
+    // reuse one behind a device-side wait instead of growing (the held memory then tracks the live
+    // set plus the slack; the lanes of a batch wait at most for another lane's last use of a block)
+    const size_t cached = st_.held - st_.live;
+    if (cached > std::max(kSlackMin, st_.live / 8))
+      if (void* p = carve(dev, c, s, true)) return p;
     if (grow(dev, c)) return carve(dev, c, s);
     // out of device memory: return wholly free chunks and cached small blocks, then wait for every
     // pending use so that all free blocks coalesce into reusable space
     release_cached_locked();
     if (grow(dev, c)) return carve(dev, c, s);
+    if (void* p = carve(dev, c, s, true)) return p;
     PHX_CHECK(hipDeviceSynchronize());
     if (void* p = carve(dev, c, s)) return p;
     release_cached_locked();

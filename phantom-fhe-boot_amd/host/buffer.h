@@ -51,6 +51,7 @@ class DevicePool {
   static constexpr size_t kArenaMin = size_t(1) << 20;  // requests from here are carved from the arena
   static constexpr size_t kGrain = size_t(64) << 10;    // arena block granularity
   static constexpr size_t kChunk = size_t(1) << 30;     // arena growth step
+  static constexpr size_t kSlackMin = size_t(2) << 30;  // cached arena space kept before waiting on reuse
 
  private:
   using Pending = std::vector<std::pair<hipStream_t, hipEvent_t>>;  // uses a block may still have
@@ -89,7 +90,7 @@ class DevicePool {
   void drop_done(Pending& pend);
   void insert_free(Block* b);
   void erase_free(Block* b);
-  void* carve(int dev, size_t c, hipStream_t s);
+  void* carve(int dev, size_t c, hipStream_t s, bool wait = false);
   Chunk* grow(int dev, size_t c);
   void release_cached_locked();
   void note_live(long delta);
