@@ -85,8 +85,12 @@ C3_BYTES = (4 * 45 + 3 * 2 * 60 + 2 * 44) * N * 8  # 329,252,8
 def c3_leg(PA, lib, torch, steps=20, warmup=3):
     """Config C3: HE multiply + relinearize + rescale at N=2^16, Q = {60, 44x50},
     P = 15x60 (dnum 3), ciphertexts at chain index 1 (45 limbs), uniform random ciphertexts and
-    key digits (parity of these ops is bit-exact, tests/test_gpu_ckks.py).  Per-op HIP-event time
-    on the stream the kernels run on, averaged over `steps`."""
+    key digits (parity of these ops is bit-exact, tests/test_gpu_ckks.py).
+    total_ms: `steps` back-to-back multiply -> relinearize -> rescale sequences between one pair of
+    HIP events on the stream the kernels run on, per sequence.  ms: each op alone, `steps` calls back
+    to back between one event pair, per call.  (An event pair around every op adds ~10 us of event
+    processing to each op on the device timeline: rocprofv3 traces of that form show a ~10 us idle
+    gap at every op boundary and none inside an op, profiles/r05/c3/.)"""
     mods = PA.coeff_modulus_create(N, C3_BITS)
     ctx = PA.Context(N, mods, 15)
     ql = mods[:45]
@@ -112,22 +116,26 @@ def c3_leg(PA, lib, torch, steps=20, warmup=3):
         for f in ops.values():
             PA.check(f())
     torch.cuda.synchronize()
-    ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-          for k in ops}
-    for i in range(steps):
-        for k, f in ops.items():
-            ev[k][i][0].record(stream)
-            PA.check(f())
-            ev[k][i][1].record(stream)
-    torch.cuda.synchronize()
-    ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
-    total = sum(ms.values())
+
+    def timed(fns):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(steps):
+            for f in fns:
+                PA.check(f())
+        b.record(stream)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / steps
+
+    total = timed(list(ops.values()))
+    ms = {k: timed([f]) for k, f in ops.items()}
     ctx.close()
     achieved = C3_BYTES / (total * 1e-3) / 1e9
     return {
         "workload": "C3: multiply + relinearize + rescale_to_next, N=65536, 45->44 limbs, P=15, dnum=3",
         "ms": {k: round(v, 4) for k, v in ms.items()},
         "total_ms": round(total, 4),
+        "sum_of_ops_ms": round(sum(ms.values()), 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes": C3_BYTES},
     }
@@ -375,10 +383,14 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=3, chain=26, 
     res = None
     if rank == 0:
         nver = total if verify is None else min(verify, total)
-        bits = []
+        bits, flat, low = [], [], 0
         for i in range(nver):
-            got = sess.decrypt(gathered[i].data_ptr(), sout)
+            got = np.asarray(sess.decrypt(gathered[i].data_ptr(), sout), dtype=np.float64)
             bits.append(PA.bit_precision(values[i], got))
+            # the same with the error's mean over the slots removed: the bootstrap's precision tail is
+            # a constant offset of every slot (coefficient 0); what is left is the rest
+            flat.append(PA.bit_precision(values[i], got - np.mean(got - values[i])))
+            low += bits[-1] < 9.6
         res = {
             "workload": f"C5: {total} independent C4 bootstraps (input chain index {chain}) sharded over {world} rank(s), "
                         "scatter -> EvalBootstrapBatch -> gather of serialized ciphertexts",
@@ -386,6 +398,7 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=3, chain=26, 
             "bootstraps_per_s": round(total / max_s, 3), "max_rank_s": round(max_s, 3),
             "scatter_gather_bytes": total * (sin + sout),
             "verified": nver, "min_avg_bits": round(min(bits), 2), "mean_avg_bits": round(float(np.mean(bits)), 2),
+            "min_offset_free_bits": round(min(flat), 2), "below_9_6_bits": low,
             "setup_s": round(setup_s, 2), "scaling": "strong",
             "keys": "regenerated on every rank from a broadcast 32-byte seed",
             "rank0_pool_GiB": {"held": round(pool["held"] / 2**30, 2), "peak_held": round(pool["peak_held"] / 2**30, 2),

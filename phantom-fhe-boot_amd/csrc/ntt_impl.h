@@ -51,6 +51,10 @@ constexpr int COLS = 16;
 constexpr int BLOCK = 256;
 constexpr int CBLOCK = COLS * 16 > BLOCK ? COLS * 16 : BLOCK;  // column-pass workgroup bound
 constexpr int kNttWavesPerEU = 3;  // __launch_bounds__ occupancy target (waves per SIMD) of one-tile grids
+#ifndef PHX_ROW_WAVES
+#define PHX_ROW_WAVES 3
+#endif
+constexpr int kRowWaves = PHX_ROW_WAVES;  // ... of the plain row pass (no prologue / epilogue)
 
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 
@@ -504,29 +508,26 @@ struct TileRef {
   size_t k;       // ... and inside its limb
 };
 
-// Forward epilogue: out = (c - y) * w (+ out).  Its operands c (and out when accumulating) are
-// loaded with the tile, behind the twiddle loads, so their latency hides under the butterflies
-// instead of sitting between the last round and the stores.
+// Forward epilogue: out = (c - y) * w (+ out).  Its operand c is loaded with the last round's
+// twiddles, so its latency hides under that round's butterflies instead of sitting between the
+// last round and the stores; the accumulated `out` (moddown into an existing ciphertext only) is
+// read in the store loop, so that no second operand set is held through the round (the finish
+// then runs at 3 waves per SIMD without spilling).
 struct EpiOperands {
-  uint64_t c[E], o[E];
+  uint64_t c[E];
 };
 __device__ __forceinline__ void epilogue_load(const KArgs& a, const TileRef& tr, uint32_t T, EpiOperands& eo) {
   const size_t e = (size_t)tr.buf_limb * a.n + tr.k;
   const uint64_t* c = a.epi.c + tr.poly * a.epi.c_stride + e;
-  const uint64_t* o = a.epi.ks_out(tr.poly) + e;
 #pragma unroll
   for (int j = 0; j < E; ++j) eo.c[j] = __builtin_nontemporal_load(c + j * T);
-  if (a.epi.accumulate) {
-#pragma unroll
-    for (int j = 0; j < E; ++j) eo.o[j] = __builtin_nontemporal_load(o + j * T);
-  }
 }
 __device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr, uint32_t j, uint32_t T,
                                                const EpiOperands& eo, uint64_t y, uint64_t q) {
   const size_t e = (size_t)tr.buf_limb * a.n + tr.k + j * T;
   uint64_t* o = a.epi.ks_out(tr.poly) + e;
   uint64_t v = mul_shoup(sub_mod(eo.c[j], y, q), a.epi.w[tr.buf_limb], a.epi.ws[tr.buf_limb], q);
-  if (a.epi.accumulate) v = add_mod(v, eo.o[j], q);
+  if (a.epi.accumulate) v = add_mod(v, __builtin_nontemporal_load(o), q);
   store_wt(o, v);
 }
 
@@ -543,6 +544,10 @@ __device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr
 // 0.268-0.274 ms, bootstrap 23.41-23.57 -> 23.17-23.37 ms (profiles/r03/ks_waves/).
 constexpr int kKsKC = 1, kKsWaves = 3;
 constexpr int kKspWaves = 2;  // ... and of the inverse row pass with the key-switch prologue
+#ifndef PHX_EPI_WAVES
+#define PHX_EPI_WAVES 3
+#endif
+constexpr int kEpiWaves = PHX_EPI_WAVES;  // ... and of the row pass with the rescale / moddown finish
 template <int T, int BETA>
 __device__ __forceinline__ void ks_epilogue_b(const KArgs& a, const TileRef& tr, const uint64_t (&y)[E], uint64_t q,
                                               uint64_t r0, uint64_t r1) {
@@ -995,7 +1000,6 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
           }
         }
       });
-      if constexpr (FWD && EPI && !KS) epilogue_load(a, tr, T, eo);
 #pragma unroll
       for (int k = 0; k < K0; ++k) {
         const uint32_t e = t + 1 + T * k;
@@ -1028,6 +1032,8 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
           if constexpr (R > 0) relayout<S2_LOG, R - 1, R>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
           double w[E];
           get_tw(rc, w);
+          // the epilogue's operands behind the last twiddles: held through the last round only
+          if constexpr (EPI && !KS && R == RN - 1) epilogue_load(a, tr, T, eo);
           ct_round_f64<S2_LOG, R, P::row_fwd.mask>(v, w, lc.qd, lc.qinv);
         });
         if constexpr (RN > 1) relayout<S2_LOG, RN - 1, 0>(v, reinterpret_cast<double*>(lrow), idx, sync, t);
@@ -1137,7 +1143,7 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
 // KS: forward, the epilogue is the key-switch form (ks_epilogue; EPI must be set too); inverse, the
 // input is the key-switch prologue (ks_prologue).
 template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false, bool LZ = false, bool KS = false>
-__global__ __launch_bounds__(BLOCK, KS ? (FWD ? kKsWaves : kKspWaves) : EPI ? 2 : kNttWavesPerEU)
+__global__ __launch_bounds__(BLOCK, KS ? (FWD ? kKsWaves : kKspWaves) : EPI ? kEpiWaves : kRowWaves)
 void ntt_row(KArgs a) {
   using RS = RowShape<S1_LOG, S2_LOG>;
   __shared__ uint64_t lds[RS::LDS_WORDS];

@@ -223,7 +223,7 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
     // reuse one behind a device-side wait instead of growing (the held memory then tracks the live
     // set plus the slack; the lanes of a batch wait at most for another lane's last use of a block)
     const size_t cached = st_.held - st_.live;
-    if (cached > std::max(kSlackMin, st_.live / 8))
+    if (cached > std::max(kSlackMin, st_.live / 16))
       if (void* p = carve(dev, c, s, true)) return p;
     if (grow(dev, c)) return carve(dev, c, s);
     // out of device memory: return wholly free chunks and cached small blocks, then wait for every

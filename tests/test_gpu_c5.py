@@ -1,16 +1,24 @@
 """Config C5 at one rank's share of the 8-GPU job: 128 = 1024 / 8 independent
 bootstraps through bench.py's c5_leg — fresh OS-entropy keys from a 32-byte seed (as every rank
-regenerates them), session encryption at chain index 26, EvalBootstrapBatch on 4 stream lanes, the
-serialized results decrypted and every one of the 128 checked with compute_bit_precision
-(bootstrapping_example.cu:17-41, which the reference only prints, :118-198).
+regenerates them), session encryption at chain index 26, EvalBootstrapBatch on 3 stream lanes in
+lockstep groups of 8 (bench.py's defaults), the serialized results decrypted and every one of the
+128 checked with compute_bit_precision (bootstrapping_example.cu:17-41, which the reference only
+prints, :118-198).
 
-Gate: min over the 128 > 7.5 bits, mean > 9.9.  Measured with fresh keys: mean 9.97-10.04; the
-low tail (8.11-8.8 over 1024, 8.28 over 960 in profiles/r04/tail/) is CoeffToSlot's slot 0 alone:
-it appears when coefficient 0 or N/2 of the raised plaintext has overflow I = 0 (about 1.3% of
-ciphertexts), with an offset of 1.8e-5 s(zeta) (s(zeta) = the secret at the slot's root, a
-Gaussian of sigma 148 per component over keys); a 4-sigma key gives 7.7 bits
-(tests/test_gpu_precision_tail.py).  The wall time of the leg is written to gpurun_out/c5_rank_share.json so the driver's
-8-rank bench is known to fit its timeout."""
+Gates, set by the mechanism of the precision tail (tests/test_gpu_precision_tail.py):
+  - offset-free precision > 11.0 bits for every bootstrap: the same measure with the error's mean
+    over the slots removed.  The bootstrap's error is a constant offset of every slot
+    (coefficient 0: the sine's cubic term, -0.0027, and the key-dependent slot-0 term when that
+    slot's overflow is 0); everything else is at 12.0-12.3 bits over 1024 bootstraps
+    (profiles/r05/c5_precision/).  A regression anywhere but coefficient 0 fails this gate.
+  - mean > 9.9 bits and at most 5% of the bootstraps below 9.6 bits (the slot-0 events are ~1.3%);
+  - min > 7.5 bits: the coefficient-0 tail alone, 1.8e-5 |s(zeta)| for a key whose s(zeta) (the
+    secret at the slot's root, Gaussian of sigma ~148 per component) is 4 sigma out.  Measured
+    minima over 1024: 8.11-9.68.  The advisor's 8.5 would fail for 2-3 sigma keys on a slot-0
+    event, a property of the reference's parameters that the engine restates bit for bit, not a
+    regression; the offset-free gate above is the tight one.
+The wall time of the leg is written to gpurun_out/c5_rank_share.json so the driver's 8-rank bench
+is known to fit its timeout."""
 import json
 import os
 import sys
@@ -29,11 +37,13 @@ def test_c5_one_rank_share_128_bootstraps_all_verified():
     import bench
     torch.cuda.set_device(0)
     t0 = time.perf_counter()
-    res = bench.c5_leg(None, torch, 1, 0, 0, total=128, lanes=4)
+    res = bench.c5_leg(None, torch, 1, 0, 0, total=128)
     wall = time.perf_counter() - t0
     rec = {"wall_s": round(wall, 2), **res}
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "c5_rank_share.json"), "w") as f:
         json.dump(rec, f)
     assert res["bootstraps"] == 128 and res["verified"] == 128, rec
-    assert res["min_avg_bits"] > 7.5 and res["mean_avg_bits"] > 9.9, rec
+    assert res["min_offset_free_bits"] > 11.0, rec
+    assert res["mean_avg_bits"] > 9.9 and res["below_9_6_bits"] <= 128 // 20, rec
+    assert res["min_avg_bits"] > 7.5, rec
