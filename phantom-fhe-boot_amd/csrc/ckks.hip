@@ -171,9 +171,6 @@ __global__ __launch_bounds__(kBlock, 2) void lt_bsgs_kernel(LtArgs a, uint32_t l
   }
 }
 
-// Wide form for G = 32 baby steps (at most B giant steps): the babies are held 8 at a time and
-// every giant step's 128-bit sums stay in registers across the two halves, so each baby and each
-// plaintext is still read once (the register-resident form of lt_bsgs_kernel<32> spills).
 // where the babies and the inner sums of one ciphertext live: LtArgs' pointer arrays, or the
 // group form's contiguous buffers (baby j at baby0 + j baby_stride, inner sum i >= 1 at
 // giant1 + (i - 1) giant_stride, inner sum 0 at acc)
@@ -191,93 +188,209 @@ struct LtGroupSrc {
   }
 };
 
-template <int G, int B, class Src>
-__device__ __forceinline__ void lt_bsgs_wide(const Src& src, int nb, int Ql, int size_Q, const uint64_t* qv,
-                                             const uint64_t* barrett, uint32_t log_n, size_t total, uint32_t block,
-                                             uint32_t nblocks, const uint64_t* const* ptab) {
+// G = 32 baby steps, at most 8 giant steps (the bootstrap's CoeffToSlot / SlotToCoeff levels):
+// one workgroup = 8 waves over one tile of 64 E elements (E consecutive elements per lane, one
+// 8E-byte load per lane), wave i computing giant step i.  The tile's 64 baby rows (32 babies x 2
+// polynomials) are staged once in LDS as 30-bit halves (32 E KB); each wave then streams only its
+// own 32 plaintexts, 4 at a time, double-buffered: chunk c + 1's loads are in flight while chunk
+// c's products run, and chunk 0's over the staging barrier.  The register-resident form this
+// replaces held all 8 giant steps' 128-bit sums per lane (220 VGPRs, 8 waves per CU) and read HBM
+// at 4.7 TB/s.  Each baby and each plaintext is still read from HBM once; the sums are exact
+// 128-bit values, so every result is bit-identical to lt_bsgs_kernel's.
+#ifndef PHX_LT_EPL
+#define PHX_LT_EPL 2
+#endif
+constexpr int kLtWaves = 8, kLtChunk = 4, kLtEpl = PHX_LT_EPL;
+static_assert(kLtEpl == 1 || kLtEpl == 2, "1 or 2 elements per lane");
+
+template <int E>
+struct LtVec;  // E consecutive u64 of one lane
+template <>
+struct LtVec<1> {
+  uint64_t v[1];
+};
+template <>
+struct LtVec<2> {
+  uint64_t v[2];
+};
+
+template <int E>
+__device__ __forceinline__ LtVec<E> lt_ld(const uint64_t* p) {
+  LtVec<E> r;
+  if constexpr (E == 2) {
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    const u64x2 x = *(const __attribute__((address_space(1))) u64x2*)p;
+    r.v[0] = x.x;
+    r.v[1] = x.y;
+  } else {
+    r.v[0] = *(const __attribute__((address_space(1))) uint64_t*)p;
+  }
+  return r;
+}
+
+using LtPtr = const __attribute__((address_space(4))) uint64_t*;
+
+// chunk c (plaintexts 4c .. 4c + 3) of this wave's giant step
+template <int E>
+__device__ __forceinline__ void lt_load_chunk(LtVec<E> (&w)[kLtChunk], const __attribute__((address_space(4))) LtPtr* prow,
+                                              int c, size_t e) {
+#pragma unroll
+  for (int j = 0; j < kLtChunk; ++j) w[j] = lt_ld<E>((const uint64_t*)prow[c * kLtChunk + j] + e);
+}
+
+// the four 64-bit partial sums of x * w per element and polynomial, x and w split in 30-bit halves
+struct LtPart {
+  uint64_t ll, m1, m2, hh;
+};
+
+// part += sum_j baby(4c + j) * w[j], the babies from LDS (< 2^60 each partial product, at most 8
+// chunks... folded every 2 chunks: <= 8 products per partial sum, < 2^63).  The memory clobbers
+// (IR) and scheduling barriers (machine code) keep this chunk's LDS reads and products inside it,
+// and binding the partial sums to the closing asm stops the products being deferred: hoisted to
+// the top of the kernel the LDS reads alone cost 128 VGPRs.
+template <int E>
+__device__ __forceinline__ void lt_chunk_products(LtPart (&part)[E][2], const LtVec<E> (&w)[kLtChunk],
+                                                  const uint2 (*xs)[64 * E], int c, int lane) {
   constexpr uint64_t kM30 = (1ull << 30) - 1;
-  constexpr int C = 8;
-  static_assert(G % C == 0, "whole chunks of babies");
-  const size_t pstride = total;
-  for (size_t e = block * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)nblocks * kBlock) {
-    const int l = static_cast<int>(e >> log_n);
-    const int row = l < Ql ? l : size_Q + (l - Ql);
-    const uint64_t q = qv[row], r0 = barrett[2 * row], r1 = barrett[2 * row + 1];
-    u128 acc[B][2];
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < B; ++i) acc[i][0] = acc[i][1] = u128{0, 0};
+  for (int jj = 0; jj < kLtChunk; ++jj) {
+    const int j = c * kLtChunk + jj;
 #pragma unroll
-    for (int c0 = 0; c0 < G; c0 += C) {
-      uint32_t xl[2][C], xh[2][C];
-#pragma unroll
-      for (int j = 0; j < C; ++j) {
-        const uint64_t* bj = src.baby(c0 + j);
-        const uint64_t v0 = bj[e], v1 = bj[pstride + e];
-        xl[0][j] = static_cast<uint32_t>(v0 & kM30);
-        xh[0][j] = static_cast<uint32_t>(v0 >> 30);
-        xl[1][j] = static_cast<uint32_t>(v1 & kM30);
-        xh[1][j] = static_cast<uint32_t>(v1 >> 30);
+    for (int t = 0; t < 2; ++t) {
+      uint2 x[E];
+      if constexpr (E == 2) {
+        const uint4 xx = *reinterpret_cast<const uint4*>(&xs[2 * j + t][2 * lane]);
+        x[0] = make_uint2(xx.x, xx.y);
+        x[1] = make_uint2(xx.z, xx.w);
+      } else {
+        x[0] = xs[2 * j + t][lane];
       }
 #pragma unroll
-      for (int i = 0; i < B; ++i) {
-        if (i >= nb) break;
-        const uint64_t* const* prow = ptab + i * G + c0;
-        uint64_t w[C];
-#pragma unroll
-        for (int j = 0; j < C; ++j) w[j] = ((const __attribute__((address_space(1))) uint64_t*)prow[j])[e];
-        __builtin_amdgcn_sched_barrier(0);
-        uint64_t ll[2] = {0, 0}, m1[2] = {0, 0}, m2[2] = {0, 0}, hh[2] = {0, 0};
-#pragma unroll
-        for (int j = 0; j < C; ++j) {
-          const uint32_t wl = static_cast<uint32_t>(w[j] & kM30), wh = static_cast<uint32_t>(w[j] >> 30);
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            ll[t] += static_cast<uint64_t>(xl[t][j]) * wl;
-            m1[t] += static_cast<uint64_t>(xl[t][j]) * wh;
-            m2[t] += static_cast<uint64_t>(xh[t][j]) * wl;
-            hh[t] += static_cast<uint64_t>(xh[t][j]) * wh;
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          add128(acc[i][t], u128{ll[t], 0});
-          add128(acc[i][t], u128{m1[t] << 30, m1[t] >> 34});
-          add128(acc[i][t], u128{m2[t] << 30, m2[t] >> 34});
-          add128(acc[i][t], u128{hh[t] << 60, hh[t] >> 4});
-        }
+      for (int k = 0; k < E; ++k) {
+        const uint32_t wl = static_cast<uint32_t>(w[jj].v[k] & kM30), wh = static_cast<uint32_t>(w[jj].v[k] >> 30);
+        LtPart& P = part[k][t];
+        P.ll += static_cast<uint64_t>(x[k].x) * wl;
+        P.m1 += static_cast<uint64_t>(x[k].x) * wh;
+        P.m2 += static_cast<uint64_t>(x[k].y) * wl;
+        P.hh += static_cast<uint64_t>(x[k].y) * wh;
       }
     }
+  }
 #pragma unroll
-    for (int i = 0; i < B; ++i) {
-      if (i >= nb) break;
-      uint64_t* o = src.out(i);
-      o[e] = barrett_reduce_128(acc[i][0], q, r0, r1);
-      o[pstride + e] = barrett_reduce_128(acc[i][1], q, r0, r1);
+  for (int k = 0; k < E; ++k)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      LtPart& P = part[k][t];
+      asm volatile("" : "+v"(P.ll), "+v"(P.m1), "+v"(P.m2), "+v"(P.hh)::"memory");
+    }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int E>
+__device__ __forceinline__ void lt_fold(u128 (&acc)[E][2], LtPart (&part)[E][2]) {
+#pragma unroll
+  for (int k = 0; k < E; ++k)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      LtPart& P = part[k][t];
+      add128(acc[k][t], u128{P.ll, 0});
+      add128(acc[k][t], u128{P.m1 << 30, P.m1 >> 34});
+      add128(acc[k][t], u128{P.m2 << 30, P.m2 >> 34});
+      add128(acc[k][t], u128{P.hh << 60, P.hh >> 4});
+      P = LtPart{0, 0, 0, 0};
+      // folded here, not all at the end (which would keep every fold's partial sums live)
+      asm volatile("" : "+v"(acc[k][t].lo), "+v"(acc[k][t].hi));
+    }
+}
+
+template <int E, class Src>
+__device__ __forceinline__ void lt_bsgs_tile(const Src& src, int nb, int Ql, int size_Q, const uint64_t* qv,
+                                             const uint64_t* barrett, uint32_t log_n, size_t total, size_t tile,
+                                             const uint64_t* const* pts) {
+  constexpr int G = 32, T = 64 * E, NC = G / kLtChunk;
+  constexpr uint64_t kM30 = (1ull << 30) - 1;
+  __shared__ uint2 xs[2 * G][T];  // row 2j + t: baby j, polynomial t, as {low 30, high 30} bits
+  // a memory clobber ahead of the loads: it keeps them where they are written
+  asm volatile("" ::: "memory");
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const size_t e = tile * T + static_cast<size_t>(lane) * E;
+  // staging: wave wv loads polynomial wv & 1 of babies (wv >> 1) + 4r, r < 8 (rows wv + 8r)
+  LtVec<E> v[8];
+  const size_t poff = static_cast<size_t>(wv & 1) * total + e;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) v[r] = lt_ld<E>(src.baby((wv >> 1) + 4 * r) + poff);
+  __builtin_amdgcn_sched_barrier(0);  // the babies' loads first: the staging writes wait for them only
+  // waves past the last giant step repeat the last one (its plaintexts come from L2, and they
+  // store the same values to the same places): with a branch around their loads and products the
+  // backend sinks the plaintext loads past the barrier, or makes the staging writes wait for them
+  const int wi = wv < nb ? wv : nb - 1;
+  const __attribute__((address_space(4))) LtPtr* prow = (const __attribute__((address_space(4))) LtPtr*)(pts + wi * G);
+  LtVec<E> wbuf[2][kLtChunk];
+  lt_load_chunk<E>(wbuf[0], prow, 0, e);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int k = 0; k < E; ++k)
+      xs[wv + 8 * r][lane * E + k] =
+          make_uint2(static_cast<uint32_t>(v[r].v[k] & kM30), static_cast<uint32_t>(v[r].v[k] >> 30));
+  // LDS writes done, then the workgroup barrier; the plaintext loads stay in flight (a
+  // __syncthreads would also drain vmcnt)
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt and expcnt unconstrained
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  u128 acc[E][2];
+  LtPart part[E][2];
+#pragma unroll
+  for (int k = 0; k < E; ++k)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      acc[k][t] = u128{0, 0};
+      part[k][t] = LtPart{0, 0, 0, 0};
+    }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (c + 1 < NC) lt_load_chunk<E>(wbuf[(c + 1) & 1], prow, c + 1, e);
+    lt_chunk_products<E>(part, wbuf[c & 1], xs, c, lane);
+    if (c & 1) lt_fold<E>(acc, part);  // 8 products per partial sum
+  }
+  const int l = static_cast<int>((tile * T) >> log_n);
+  const int row = l < Ql ? l : size_Q + (l - Ql);
+  const uint64_t q = qv[row], r0 = barrett[2 * row], r1 = barrett[2 * row + 1];
+  uint64_t* o = src.out(wi);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if constexpr (E == 2) {
+      *reinterpret_cast<ulong2*>(o + t * total + e) =
+          make_ulong2(barrett_reduce_128(acc[0][t], q, r0, r1), barrett_reduce_128(acc[1][t], q, r0, r1));
+    } else {
+      o[t * total + e] = barrett_reduce_128(acc[0][t], q, r0, r1);
     }
   }
 }
 
-template <int G, int B>
-__global__ __launch_bounds__(kBlock, 2) void lt_bsgs_wide_kernel(LtArgs a, uint32_t log_n, size_t total) {
-  extern __shared__ const uint64_t* ptab[];
-  for (int k = threadIdx.x; k < a.b * G; k += kBlock) ptab[k] = a.pts[k];
-  __syncthreads();
-  lt_bsgs_wide<G, B>(LtSingleSrc{a}, a.b, a.Ql, a.size_Q, a.q, a.barrett, log_n, total, blockIdx.x, gridDim.x, ptab);
+template <int E>
+__global__ __launch_bounds__(64 * kLtWaves) void lt_bsgs_tile_kernel(LtArgs a, uint32_t log_n, size_t total) {
+  lt_bsgs_tile<E>(LtSingleSrc{a}, a.b, a.Ql, a.size_Q, a.q, a.barrett, log_n, total, blockIdx.x, a.pts);
 }
 
-// `count` ciphertexts through the same plaintexts (lt_bsgs_group): the blocks of the ciphertexts
-// that cover the same elements are dealt to one XCD 8 dispatches apart (blocks b and b + 8 share an
-// XCD under round-robin placement), so the followers' plaintext reads are served by that XCD's L2
-template <int G, int B>
-__global__ __launch_bounds__(kBlock, 2) void lt_bsgs_group_kernel(LtGroupArgs ga, uint32_t log_n, size_t total) {
-  extern __shared__ const uint64_t* ptab[];
-  for (int k = threadIdx.x; k < ga.b * G; k += kBlock) ptab[k] = ga.pts[k];
-  __syncthreads();
+// `count` ciphertexts through the same plaintexts (lt_bsgs_group): the workgroups of the
+// ciphertexts that cover the same tile are dealt to one XCD 8 dispatches apart (workgroups w and
+// w + 8 share an XCD under round-robin placement), so the followers' plaintext reads are served by
+// that XCD's L2
+template <int E>
+__global__ __launch_bounds__(64 * kLtWaves) void lt_bsgs_group_kernel(LtGroupArgs ga, uint32_t log_n, size_t total) {
   const uint32_t K = static_cast<uint32_t>(ga.count);
   const uint32_t b = blockIdx.x, x = b % 8, k = b / 8;
-  const uint32_t c = k % K, blk = (k / K) * 8 + x, nblk = gridDim.x / K;
-  lt_bsgs_wide<G, B>(LtGroupSrc{ga, static_cast<int>(c)}, ga.b, ga.Ql, ga.size_Q, ga.q, ga.barrett, log_n, total, blk,
-                     nblk, ptab);
+  const uint32_t c = k % K, tile = (k / K) * 8 + x;
+  if (static_cast<size_t>(tile) * 64 * E >= total) return;  // the grid rounds the tiles up to whole XCD rounds
+  lt_bsgs_tile<E>(LtGroupSrc{ga, static_cast<int>(c)}, ga.b, ga.Ql, ga.size_Q, ga.q, ga.barrett, log_n, total, tile,
+                  ga.pts);
 }
 
 template <bool MUL, bool ACC>
@@ -485,7 +598,8 @@ hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s) {
     case 8: lt_bsgs_kernel<8><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
     case 16: lt_bsgs_kernel<16><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
     case 32:
-      if (a.b <= 8) lt_bsgs_wide_kernel<32, 8><<<grid, kBlock, lds, s>>>(a, log_n, total);
+      if (a.b <= kLtWaves && n >= 64 * kLtEpl)
+        lt_bsgs_tile_kernel<kLtEpl><<<static_cast<unsigned>(total / (64 * kLtEpl)), 64 * kLtWaves, 0, s>>>(a, log_n, total);
       else lt_bsgs_kernel<32><<<grid, kBlock, lds, s>>>(a, log_n, total);
       break;
     default: return hipErrorInvalidValue;
@@ -498,10 +612,11 @@ hipError_t lt_bsgs_group(const LtGroupArgs& ga, size_t n, hipStream_t s) {
     return hipErrorInvalidValue;
   for (int c = 0; c < ga.count; ++c)
     if (!ga.baby0[c] || !ga.acc[c] || (ga.b > 1 && !ga.giant1[c])) return hipErrorInvalidValue;
+  if (n < 64 * kLtEpl) return hipErrorInvalidValue;
   const size_t total = n * static_cast<size_t>(ga.Ql + ga.P);
-  const size_t lds = static_cast<size_t>(ga.b) * ga.g * sizeof(const uint64_t*);
-  const int per = (grid_for(total) + 7) / 8 * 8;  // blocks per ciphertext, whole XCD rounds
-  lt_bsgs_group_kernel<32, 8><<<ga.count * per, kBlock, lds, s>>>(ga, __builtin_ctzll(n), total);
+  const size_t per = (total / (64 * kLtEpl) + 7) / 8 * 8;  // workgroups per ciphertext, whole XCD rounds
+  lt_bsgs_group_kernel<kLtEpl>
+      <<<static_cast<unsigned>(ga.count * per), 64 * kLtWaves, 0, s>>>(ga, __builtin_ctzll(n), total);
   return hipGetLastError();
 }
 

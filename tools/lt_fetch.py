@@ -1,5 +1,5 @@
 """HBM read bytes of the linear transforms' inner-product kernels in `bootstrapping_example prof`
-(one warm bootstrap, then one lockstep group): the last 4 lt_bsgs_wide dispatches (the single
+(one warm bootstrap, then one lockstep group): the last 4 lt_bsgs_wide / lt_bsgs_tile dispatches (the single
 bootstrap's 4 levels) against the last 4 lt_bsgs_group dispatches (the group's 4 levels), from a
 rocprofv3 --pmc FETCH_SIZE pass (gfx950: bytes = 2 x FETCH_SIZE x 1024, MI355X_MICROARCH.md §HBM).
 
@@ -18,7 +18,7 @@ def main(root, group=4):
             if r["Counter_Name"] != "FETCH_SIZE":
                 continue
             name = r["Kernel_Name"]
-            kind = "single" if "lt_bsgs_wide_kernel" in name else "group" if "lt_bsgs_group_kernel" in name else None
+            kind = "single" if ("lt_bsgs_wide_kernel" in name or "lt_bsgs_tile_kernel" in name) else "group" if "lt_bsgs_group_kernel" in name else None
             if kind:
                 rows.append((int(r["Dispatch_Id"]), kind, 2 * 1024 * float(r["Counter_Value"]),
                              int(r.get("Grid_Size", 0) or 0)))
