@@ -113,7 +113,10 @@ int main(int argc, char** argv) {
   double t0 = now_ms();
   PhantomContext ctx(parms);
   // "tail" draws fresh OS-entropy keys
-  const uint64_t key_seed = mode == "tail" ? 0 : 0x5EED;
+  // (TAIL_KEY_SEED=s: seeded keys s, s + 1, .. instead, so that two library builds see the same
+  // keys and ciphertexts: tools/diag_centred.sh)
+  const char* tail_seed = std::getenv("TAIL_KEY_SEED");
+  const uint64_t key_seed = mode == "tail" ? (tail_seed ? std::strtoull(tail_seed, nullptr, 0) : 0) : 0x5EED;
   PhantomSecretKey sk = key_seed ? PhantomSecretKey::for_testing(ctx, key_seed) : PhantomSecretKey(ctx);
   PhantomCKKSEncoder enc(ctx);
   const std::vector<double> sf = precompute_scaling_factors(ctx, scale);
@@ -727,7 +730,7 @@ int main(int argc, char** argv) {
     const int nkeys = argc > 4 ? std::max(1, std::atoi(argv[4])) : 1;
     for (int key = 0; key < nkeys; ++key) {
     if (key > 0) {
-      sk = PhantomSecretKey(ctx);
+      sk = key_seed ? PhantomSecretKey::for_testing(ctx, key_seed + key) : PhantomSecretKey(ctx);
       boot.EvalMultKeyGen(sk, ctx);
       boot.EvalBootstrapKeyGen(sk, ctx);
     }
@@ -740,7 +743,10 @@ int main(int argc, char** argv) {
       std::printf("{\"key\": %d, \"s_zeta\": [%.2f, %.2f], \"hamming\": %zu}\n", key, sz.real(), sz.imag(),
                   static_cast<size_t>(std::count_if(sc.begin(), sc.end(), [](int8_t v) { return v != 0; })));
     }
-    for (int it = 0; it < std::max(1, iters); ++it) {
+    // TAIL_ONLY_I0=1: bootstrap only ciphertexts whose slot 0 has overflow I = 0 in coefficient 0
+    // or N/2 (the ~1.3% that expose the slot-0 offset), drawing up to 400 per kept one
+    const bool only_i0 = std::getenv("TAIL_ONLY_I0") != nullptr;
+    for (int it = 0, tries = 0; it < std::max(1, iters); ++it) {
       std::vector<double> xt(slots);
       for (auto& v : xt) v = dis(rng);
       PhantomPlaintext pin;
@@ -760,6 +766,11 @@ int main(int argc, char** argv) {
         const __int128 d = ((__int128)r[N + k] - t0 % (__int128)q1 + 2 * (__int128)q1) % (__int128)q1;
         I[k] = static_cast<int>(centered(static_cast<uint64_t>(d * q0inv % (__int128)q1), q1));
         if (std::abs(I[k]) > max_i) { max_i = std::abs(I[k]); arg_i = k; }
+      }
+      if (only_i0 && I[0] != 0 && I[N / 2] != 0) {
+        if (++tries > 400 * std::max(1, iters)) break;
+        --it;
+        continue;
       }
       PhantomCiphertext o = boot.EvalBootstrap(cin, ctx);
       // the same input bootstrapped again must give the same ciphertext bit for bit (the

@@ -7,9 +7,69 @@
 
 #include "numth.h"
 
+#ifndef PHX_DIAG_CENTRED
+#define PHX_DIAG_CENTRED 0
+#endif
+#if PHX_DIAG_CENTRED
+#include <cstdio>
+#include "../csrc/ckks.h"
+#endif
+
 namespace phantom {
 
 using namespace phantom::arith;
+
+#if PHX_DIAG_CENTRED
+// DIAGNOSTIC BUILD ONLY (-DPHX_DIAG_CENTRED=1, tools/diag_centred.sh): never
+// part of the product, which divides exactly as the reference does (floor division by a
+// non-centred remainder, src/rns.cu:1160-1184, and the fast conversion without overflow
+// correction, src/rns_bconv.cu:791-843).  Here every division of an NTT-form input by D (rescale:
+// D = q_last; moddown: D = P; moddown + rescale: D = q_last P) is made mean-unbiased by adding H to
+// every coefficient first: floor((c + H) / D) - u with u the conversion's overflow, E[u] =
+// (ibase - 1) / 2, so H = (ibase / 2) D for an even input base and ((ibase - 1) / 2) D + floor(D/2)
+// for an odd one (the rescale's single limb: floor(q_last / 2), plain centred rounding).  In NTT form,
+// limb l += (H mod m_l) NTT_l(1, 1, ..., 1).  The fused key-switch forms never materialise their
+// input, so this build needs PHX_KS_EPI=0.  PHX_DIAG_CENTRED=2: the rescales only; =3: the moddowns
+// (and the fused moddown + rescale) only.
+constexpr bool kDiagRescale = PHX_DIAG_CENTRED != 3, kDiagModdown = PHX_DIAG_CENTRED != 2;
+namespace {
+void diag_unbias(uint64_t* x, size_t polys, size_t poly_stride, const std::vector<uint64_t>& mods, int split,
+                 size_t size_Q, const std::vector<uint64_t>& divisor, size_t ibase, size_t n, const phx::NttTables& ntt,
+                 hipStream_t s) {
+  const size_t L = mods.size();
+  std::vector<uint64_t> c(L), cs(L);
+  for (size_t l = 0; l < L; ++l) {
+    const uint64_t m = mods[l];
+    uint64_t d = 1 % m;
+    for (uint64_t q : divisor) d = mul_mod(d, q % m, m);
+    uint64_t h = mul_mod((ibase / 2) % m, d, m);
+    if (ibase % 2) h = (h + mul_mod((d + m - 1) % m, (m + 1) / 2, m)) % m;  // + floor(D / 2) = (D - 1) / 2
+    c[l] = h;
+    cs[l] = shoup(h, m);
+  }
+  DeviceBuffer<uint64_t> ones(L * n, s), dq(L, s), dc(L, s), dcs(L, s);
+  ones.upload(std::vector<uint64_t>(L * n, 1), s);
+  dq.upload(mods, s);
+  dc.upload(c, s);
+  dcs.upload(cs, s);
+  phx::LimbMap map;
+  map.num_limbs = (int)L;
+  map.split = split;
+  map.first_a = 0;
+  map.first_b = (int)size_Q;
+  hip_ok(phx::ntt_forward(ntt, ones.get(), ones.get(), map, s), "diag NTT(1)");
+  for (size_t p = 0; p < polys; ++p)
+    hip_ok(phx::mul_scalar_add(ones.get(), dc.get(), dcs.get(), x + p * poly_stride, x + p * poly_stride, dq.get(), n, L, s),
+           "diag unbias");
+  PHX_CHECK(hipStreamSynchronize(s));
+  static bool said = false;
+  if (!said) {
+    said = true;
+    std::fprintf(stderr, "[diag] PHX_DIAG_CENTRED build: divisions made mean-unbiased (not the product)\n");
+  }
+}
+}  // namespace
+#endif
 
 void DeviceBaseConverter::init(const std::vector<uint64_t>& in, const std::vector<uint64_t>& out, hipStream_t s) {
   ibase = in;
@@ -296,6 +356,14 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
                           size_t polys, const uint64_t* tmu, const uint64_t* const* evk) const {
   // every stage runs once over all `polys` polynomials (ct [polys][Ql][n], cx [polys][QlP][n])
   const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_;
+#if PHX_DIAG_CENTRED
+  if (tmu) throw std::runtime_error("PHX_DIAG_CENTRED build: run with PHX_KS_EPI=0");
+  if (kDiagModdown) {
+    std::vector<uint64_t> mods(base_Ql_);
+    mods.insert(mods.end(), base_P_.begin(), base_P_.end());
+    diag_unbias(cx, polys, size_QlP * n_, mods, (int)size_Ql, size_Q_, base_P_, size_P_, n_, ntt, s);
+  }
+#endif
   const int np = static_cast<int>(polys);
   uint64_t* cp = cx + size_Ql * n_;
   phx::LimbMap pm;
@@ -362,6 +430,13 @@ void RnsTool::moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTabl
   if (size_P_ == 0) throw std::invalid_argument("no special primes");
   if (count < 1 || (count > 1 && c1_stride < size_QlP * n_)) throw std::invalid_argument("moddown_modup: bad batch");
   const int nc = static_cast<int>(count);
+#if PHX_DIAG_CENTRED
+  if (kDiagModdown) {
+    std::vector<uint64_t> mods(base_Ql_);
+    mods.insert(mods.end(), base_P_.begin(), base_P_.end());
+    diag_unbias(c1, count, count > 1 ? c1_stride : 0, mods, (int)size_Ql, size_Q_, base_P_, size_P_, n_, ntt, s);
+  }
+#endif
   phx::LimbMap all;
   all.num_limbs = (int)size_QlP;
   all.split = (int)size_Ql;
@@ -391,6 +466,15 @@ void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables&
   const size_t size_Ql = base_Ql_.size(), size_QlP = size_Ql + size_P_;
   if (size_Ql < 2 || size_P_ == 0) throw std::invalid_argument("end of modulus switching chain reached");
   const size_t Ln = size_Ql - 1;
+#if PHX_DIAG_CENTRED
+  if (ks) throw std::runtime_error("PHX_DIAG_CENTRED build: run with PHX_KS_EPI=0");
+  if (kDiagModdown) {
+    std::vector<uint64_t> mods(base_Ql_), div(base_P_);
+    mods.insert(mods.end(), base_P_.begin(), base_P_.end());
+    div.push_back(base_Ql_.back());
+    diag_unbias(cx, polys, size_QlP * n_, mods, (int)size_Ql, size_Q_, div, size_P_ + 1, n_, ntt, s);
+  }
+#endif
   const int np = static_cast<int>(polys);
   // the dropped limbs q_last, p_0 .. p_{P-1} are contiguous in the extended buffer
   uint64_t* dropped = cx + Ln * n_;
@@ -467,6 +551,12 @@ void RnsTool::rescale_ntt_to(const uint64_t* in, uint64_t* const* outs, size_t c
   if (cts < 1 || cts > static_cast<size_t>(phx::kMaxKsProds)) throw std::invalid_argument("rescale: bad batch");
   const size_t Ln = L - 1, polys = 2 * cts;
   const int np = static_cast<int>(polys);
+#if PHX_DIAG_CENTRED
+  DeviceBuffer<uint64_t> diag_in(polys * L * n_, s);
+  PHX_CHECK(hipMemcpyAsync(diag_in.get(), in, polys * L * n_ * 8, hipMemcpyDeviceToDevice, s));
+  if (kDiagRescale) diag_unbias(diag_in.get(), polys, L * n_, base_Ql_, (int)L, size_Q_, {base_Ql_.back()}, 1, n_, ntt, s);
+  in = diag_in.get();
+#endif
   uint64_t* last = ws_->get(s, Workspace::kRescaleLast, polys * n_);
   hip_ok(phx::ntt_inverse(ntt, in + Ln * n_, last, phx::LimbMap::contiguous(1, (int)Ln).batched(np, L * n_, n_),
                           nullptr, nullptr, s),
@@ -492,6 +582,12 @@ void RnsTool::rescale_ntt(const uint64_t* in, uint64_t* out, size_t polys, const
   if (L < 2) throw std::invalid_argument("end of modulus switching chain reached");
   const size_t Ln = L - 1;
   const int np = static_cast<int>(polys);
+#if PHX_DIAG_CENTRED
+  DeviceBuffer<uint64_t> diag_in(polys * L * n_, s);
+  PHX_CHECK(hipMemcpyAsync(diag_in.get(), in, polys * L * n_ * 8, hipMemcpyDeviceToDevice, s));
+  if (kDiagRescale) diag_unbias(diag_in.get(), polys, L * n_, base_Ql_, (int)L, size_Q_, {base_Ql_.back()}, 1, n_, ntt, s);
+  in = diag_in.get();
+#endif
   uint64_t* last = ws_->get(s, Workspace::kRescaleLast, polys * n_);
   // all polynomials in one launch per stage
   hip_ok(phx::ntt_inverse(ntt, in + Ln * n_, last, phx::LimbMap::contiguous(1, (int)Ln).batched(np, L * n_, n_),
