@@ -47,7 +47,7 @@ step_pmc() {
   IFS=';' read -ra sets <<< "${PMC_SETS:?PMC_SETS unset}"
   for set in "${sets[@]}"; do
     i=$((i+1))
-    (cd /tmp && timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $set --output-format csv -d "$OUT/pmc$i" -o run \
+    (cd /tmp && timeout -s KILL ${T_PMC:-90} rocprofv3 --kernel-trace --pmc $set --output-format csv -d "$OUT/pmc$i" -o run \
        -- ${PMC_CMD:?PMC_CMD unset} > "$OUT/pmc$i.log" 2>&1) || { echo "pmc pass $i failed"; tail -5 "$OUT/pmc$i.log"; return 1; }
   done
 }
