@@ -255,6 +255,15 @@ int phantom_rotate_ext_accumulate_group(const phantom_context *ctx, size_t chain
                                         uint64_t *const *ext, const uint64_t *const *key_digits, size_t dnum,
                                         uint32_t galois_elt, uint64_t *const *acc, int accumulate,
                                         hipStream_t stream);
+/* one linear-transform level's baby steps and inner sums in ONE kernel, the babies never written
+ * (round 5): for ciphertext c < group (1..8), outs[c * b + i] [2][Ql+P][n] = sum_{j<32} baby_j(c) *
+ * pts[i 32 + j] for i < b <= 8, where baby_j(c) is phantom_fast_rotation_ext_batch's output k = j for
+ * cts[c] / digits[c] (key_digits[j] NULL: the identity) - equal bit for bit to that call followed by
+ * phantom_lt_bsgs.  The ciphertexts share the keys and plaintexts (read from HBM about once). */
+int phantom_lt_level_fused(const phantom_context *ctx, size_t chain_index, size_t group, const uint64_t *const *cts,
+                           const uint64_t *const *digits, const uint64_t *const *const *key_digits, size_t dnum,
+                           const uint32_t *galois_elts, const uint64_t *const *pts, size_t b, uint64_t *const *outs,
+                           hipStream_t stream);
 /* tensor_prod_2x2 with MulAddRescale's linear epilogue: out [3][Ql][n] = f (ct1 x ct2), then
  * out[p] += c t[p] for p < 2 (t[p] at t + p t_stride; f, c: host residues per limb or NULL) */
 int phantom_tensor_lin(const phantom_context *ctx, size_t chain_index, const uint64_t *ct1, const uint64_t *ct2,

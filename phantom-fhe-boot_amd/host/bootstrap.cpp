@@ -925,7 +925,7 @@ struct LevelWork {
 };
 
 void FHECKKSRNS::level_babies(const PhantomContext& cc, const PhantomCiphertext& in, const LTLevel& lv,
-                              LevelWork& w, bool launch) const {
+                              LevelWork& w, bool launch, bool alloc_babies) const {
   w.ct = &AtLevel(cc, in, lv.chain - 1, sf_, w.tmp);
   const PhantomCiphertext& ct = *w.ct;
   const size_t n = cc.poly_degree(), Ql = cc.get_context_data(ct.chain_index()).coeff_modulus_size();
@@ -937,7 +937,7 @@ void FHECKKSRNS::level_babies(const PhantomContext& cc, const PhantomCiphertext&
   // every baby step in one launch (keyswitch_rotate_batch): the digits and c0 are read from HBM
   // once for the level, not once per rotation; baby j at babies + j 2 QlP n
   const size_t baby_words = 2 * QlP * n;
-  w.babies = DeviceBuffer<uint64_t>(static_cast<size_t>(lv.g) * baby_words, s);
+  if (alloc_babies) w.babies = DeviceBuffer<uint64_t>(static_cast<size_t>(lv.g) * baby_words, s);
   const RnsTool& rt = cc.get_context_data(ct.chain_index()).gpu_rns_tool();
   phx::KsRotateBatchArgs& ba = w.ba;
   ba.digits = w.digits.get();
@@ -967,8 +967,9 @@ void FHECKKSRNS::level_babies(const PhantomContext& cc, const PhantomCiphertext&
     rotations += ((r % nn) + nn) % nn != 0;
   }
   traffic::keys(traffic::limb_bytes(rt.beta() * 2 * QlP * rotations, n));
-  // the digits and c0 read, the baby steps written
-  traffic::ciphertexts(traffic::limb_bytes(rt.beta() * QlP + Ql + 2 * QlP * static_cast<size_t>(lv.g), n));
+  // the digits and c0 read, the baby steps written (not in the fused form)
+  traffic::ciphertexts(
+      traffic::limb_bytes(rt.beta() * QlP + Ql + (alloc_babies ? 2 * QlP * static_cast<size_t>(lv.g) : 0), n));
   // giant 0's inner sum goes straight into the accumulator, giants 1 .. b-1 into one buffer
   // [b - 1][2][QlP][n] so that their moddowns batch
   w.acc.resize(2, QlP, n, s, false);
@@ -1029,9 +1030,49 @@ PhantomCiphertext FHECKKSRNS::level_giants(const PhantomContext& cc, const LTLev
   return KeySwitchDownRescale(cc, w.acc);
 }
 
+bool FHECKKSRNS::level_fused(const PhantomContext& cc, const LTLevel& lv) const {
+  static const bool on = [] {  // opt-in: measured slower than the two launches (profiles/r05/ks_lt_fused/)
+    const char* e = std::getenv("PHX_LT_FUSED");
+    return e && e[0] == '1';
+  }();
+  const size_t n = cc.poly_degree();
+  return on && lv.g == 32 && lv.b <= phx::kKsLtMaxB && n >= 1024;
+}
+
+phx::KsLtArgs FHECKKSRNS::level_fused_args(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const {
+  const size_t n = cc.poly_degree(), ext_words = 2 * w.QlP * n;
+  phx::KsLtArgs A;
+  A.ks = w.ba;
+  A.pts = lv.d_pts.get();
+  A.b = lv.b;
+  A.out[0] = w.acc.data();
+  for (int i = 1; i < lv.b; ++i) A.out[i] = w.giants.get() + static_cast<size_t>(i - 1) * ext_words;
+  size_t nz = 0;
+  for (const auto& p : lv.pts) nz += p ? 1 : 0;
+  traffic::plaintexts(traffic::limb_bytes(nz * w.QlP, n));
+  traffic::ciphertexts(traffic::limb_bytes(2 * w.QlP * static_cast<size_t>(lv.b), n));  // the inner sums written
+  return A;
+}
+
 PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const PhantomCiphertext& in,
                                           const LTLevel& lv) const {
   LevelWork w;
+  if (level_fused(cc, lv)) {
+    level_babies(cc, in, lv, w, false, false);
+    if (w.ba.beta > 4) {  // (the fused kernel's digit bound) the two launches instead
+      w.babies = DeviceBuffer<uint64_t>(static_cast<size_t>(lv.g) * 2 * w.QlP * cc.poly_degree(), cc.stream());
+      w.ba.out = w.babies.get();
+      hip_ok(phx::keyswitch_rotate_batch(w.ba, cc.poly_degree(), cc.stream()), "linear transform baby steps");
+      w.digits.release();
+      hip_ok(phx::lt_bsgs(level_lt_args(cc, lv, w), cc.poly_degree(), cc.stream()), "linear transform inner products");
+      return level_giants(cc, lv, w);
+    }
+    phx::KsLtGroupArgs ga;
+    ga.a[0] = level_fused_args(cc, lv, w);
+    hip_ok(phx::ks_lt_fused(ga, cc.poly_degree(), cc.stream()), "linear transform baby steps + inner products");
+    w.digits.release();
+    return level_giants(cc, lv, w);
+  }
   level_babies(cc, in, lv, w);
   hip_ok(phx::lt_bsgs(level_lt_args(cc, lv, w), cc.poly_degree(), cc.stream()), "linear transform inner products");
   return level_giants(cc, lv, w);
@@ -1044,10 +1085,26 @@ std::vector<PhantomCiphertext> FHECKKSRNS::apply_level_group(const PhantomContex
   if (K < 2 || K > phx::kLtGroupMax || K > phx::kKsGroupMax)
     throw std::invalid_argument("apply_level_group: 2 to 8 ciphertexts");
   std::vector<LevelWork> w(K);
+  // the fused form (one launch, no babies in HBM) when the K levels share a shape
+  const bool try_fused = level_fused(cc, lv);
+  for (int c = 0; c < K; ++c) level_babies(cc, *in[c], lv, w[c], false, !try_fused);
+  bool fused = try_fused;
+  for (int c = 0; c < K; ++c) fused &= w[c].ba.beta <= 4 && w[c].QlP == w[0].QlP;
+  if (fused) {
+    phx::KsLtGroupArgs ga;
+    ga.count = K;
+    for (int c = 0; c < K; ++c) ga.a[c] = level_fused_args(cc, lv, w[c]);
+    hip_ok(phx::ks_lt_fused(ga, cc.poly_degree(), cc.stream()), "linear transform baby steps + inner products (group)");
+    for (LevelWork& x : w) x.digits.release();
+    return level_giants_group(cc, lv, w);
+  }
   phx::KsRotateBatchGroupArgs ka;
   ka.count = K;
   for (int c = 0; c < K; ++c) {
-    level_babies(cc, *in[c], lv, w[c], false);
+    if (try_fused) {  // shapes differ: the babies after all
+      w[c].babies = DeviceBuffer<uint64_t>(static_cast<size_t>(lv.g) * 2 * w[c].QlP * cc.poly_degree(), cc.stream());
+      w[c].ba.out = w[c].babies.get();
+    }
     ka.a[c] = w[c].ba;
   }
   hip_ok(phx::keyswitch_rotate_batch_group(ka, cc.poly_degree(), cc.stream()), "linear transform baby steps (group)");

@@ -84,6 +84,9 @@ _SIGS = {
                                                              vp]),
     "phantom_rotate_ext_accumulate_group": (ctypes.c_int, [vp, sz, sz, ctypes.POINTER(vp), ctypes.POINTER(vp), sz,
                                                            ctypes.c_uint32, ctypes.POINTER(vp), ctypes.c_int, vp]),
+    "phantom_lt_level_fused": (ctypes.c_int, [vp, sz, sz, ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                              ctypes.POINTER(ctypes.POINTER(vp)), sz, ctypes.POINTER(ctypes.c_uint32),
+                                              ctypes.POINTER(vp), sz, ctypes.POINTER(vp), vp]),
     "phantom_tensor_lin": (ctypes.c_int, [vp, sz, vp, vp, vp, vp, vp, sz, vp, vp]),
     "phantom_lin_comb": (ctypes.c_int, [vp, sz, vp, sz, vp, vp, sz, sz, vp, vp]),
     "phantom_mul_scalar": (ctypes.c_int, [vp, sz, vp, sz, vp, vp, vp, sz, vp]),
