@@ -264,6 +264,14 @@ int phantom_lt_level_fused(const phantom_context *ctx, size_t chain_index, size_
                            const uint64_t *const *digits, const uint64_t *const *const *key_digits, size_t dnum,
                            const uint32_t *galois_elts, const uint64_t *const *pts, size_t b, uint64_t *const *outs,
                            hipStream_t stream);
+/* the EvalMod products' tensors in ONE launch (count <= 8 jobs at one level, L = Ql limbs each):
+ * out[k] [3][L][n] = factors[k] (ct1[k] x ct2[k]), then out[k][p] += c[k] t[k][p] for p < 2 when t[k]
+ * (t[k][p] at t[k] + p t_stride; c[k] host residues per limb), then out[k][0] += consts[k] when
+ * consts[k] (host residues per limb); factors[k] >= 1 */
+int phantom_tensor_lin_batch(const phantom_context *ctx, size_t chain_index, size_t count, const uint64_t *const *ct1,
+                             const uint64_t *const *ct2, uint64_t *const *out, const uint64_t *factors,
+                             const uint64_t *const *t, size_t t_stride, const uint64_t *const *c,
+                             const uint64_t *const *consts, hipStream_t stream);
 /* tensor_prod_2x2 with MulAddRescale's linear epilogue: out [3][Ql][n] = f (ct1 x ct2), then
  * out[p] += c t[p] for p < 2 (t[p] at t + p t_stride; f, c: host residues per limb or NULL) */
 int phantom_tensor_lin(const phantom_context *ctx, size_t chain_index, const uint64_t *ct1, const uint64_t *ct2,

@@ -407,6 +407,45 @@ int phantom_tensor_lin(const phantom_context* ctx, size_t chain_index, const uin
   });
 }
 
+int phantom_tensor_lin_batch(const phantom_context* ctx, size_t chain_index, size_t count, const uint64_t* const* ct1,
+                             const uint64_t* const* ct2, uint64_t* const* out, const uint64_t* factors,
+                             const uint64_t* const* t, size_t t_stride, const uint64_t* const* c,
+                             const uint64_t* const* consts, hipStream_t stream) {
+  PHX_CAPI_GUARD({
+    const auto& pc = phantom_capi_context(ctx);
+    const auto& rt = tool_at(pc, chain_index);
+    const size_t L = rt.size_Ql();
+    if (!ct1 || !ct2 || !out || !factors) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (count < 1 || count > static_cast<size_t>(phx::kTensorBatchMax) ||
+        count * 2 * L > static_cast<size_t>(phx::kTensorBatchLimbWords))
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "too many jobs for one launch at this level");
+    const auto& mods = rt.base_Ql();
+    phx::TensorLinBatchArgs a;
+    a.q = pc.mod_QP().q;
+    a.barrett = pc.mod_QP().barrett;
+    a.L = static_cast<uint32_t>(L);
+    a.count = static_cast<uint32_t>(count);
+    for (size_t k = 0; k < count; ++k) {
+      phx::TensorLinJob& J = a.job[k];
+      J.ct1 = ct1[k];
+      J.ct2 = ct2[k];
+      J.out = out[k];
+      J.factor = factors[k];
+      J.t = t ? t[k] : nullptr;
+      J.t_stride = J.t ? t_stride : 0;
+      J.has_const = consts && consts[k] ? 1 : 0;
+      uint64_t* cl = a.limb + k * 2 * L;
+      if (J.t) {
+        if (!c || !c[k]) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "a term needs its constants");
+        for (size_t l = 0; l < L; ++l) cl[l] = c[k][l] % mods[l];
+      }
+      if (J.has_const)
+        for (size_t l = 0; l < L; ++l) cl[L + l] = consts[k][l] % mods[l];
+    }
+    return from_hip(phx::tensor_lin_batch(a, pc.poly_degree(), stream));
+  });
+}
+
 int phantom_lin_comb(const phantom_context* ctx, size_t chain_index, uint64_t* d, size_t d_polys, const uint64_t* ca,
                      const uint64_t* t, size_t t_polys, size_t t_stride, const uint64_t* cb, hipStream_t stream) {
   PHX_CAPI_GUARD({

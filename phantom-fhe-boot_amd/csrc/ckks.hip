@@ -506,33 +506,73 @@ __global__ __launch_bounds__(kBlock) void tensor_lin_kernel(TensorLinArgs a, uin
   }
 }
 
-// tensor_lin over the products of one batch: grid row blockIdx.y = product (see ckks.h)
+// tensor_lin over the products of one batch: grid row blockIdx.y = product (see ckks.h).  Two
+// elements per thread and 16-byte accesses; the factor 2 (the EvalMod products' only factor
+// besides 1) is a modular doubling instead of a 128-bit product and Barrett reduction.
+typedef uint64_t tl_u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ tl_u64x2 tl_ld2(const uint64_t* p) {
+  return *(const __attribute__((address_space(1))) tl_u64x2*)p;
+}
+__device__ __forceinline__ void tl_st2(uint64_t* p, uint64_t x, uint64_t y) {
+  tl_u64x2 v;
+  v.x = x;
+  v.y = y;
+  *(__attribute__((address_space(1))) tl_u64x2*)p = v;
+}
+
 __global__ __launch_bounds__(kBlock) void tensor_lin_batch_kernel(TensorLinBatchArgs a, uint32_t log_n, size_t total) {
   const uint32_t k = blockIdx.y;
   const TensorLinJob& J = a.job[k];
   const uint64_t* cl = a.limb + static_cast<size_t>(k) * 2 * a.L;
   const size_t stride = total;
-  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
-    const uint32_t l = static_cast<uint32_t>(e >> log_n);
+  const bool dbl = J.factor == 2, scaled = J.factor != 1;  // product-uniform branches
+  for (size_t e = 2 * (blockIdx.x * (size_t)kBlock + threadIdx.x); e < total; e += 2 * (size_t)gridDim.x * kBlock) {
+    const uint32_t l = static_cast<uint32_t>(e >> log_n);  // (n even: the pair shares a limb)
     const uint64_t q = a.q[l], r0 = a.barrett[2 * l], r1 = a.barrett[2 * l + 1];
-    const uint64_t a0 = J.ct1[e], a1 = J.ct1[stride + e], b0 = J.ct2[e], b1 = J.ct2[stride + e];
-    u128 c1 = mul_wide(a0, b1);
-    add128(c1, mul_wide(a1, b0));
-    uint64_t d0 = mul_mod(a0, b0, q, r0, r1), d1 = barrett_reduce_128(c1, q, r0, r1), d2 = mul_mod(a1, b1, q, r0, r1);
-    if (J.factor != 1) {  // product-uniform branches
-      d0 = mul_mod(d0, J.factor, q, r0, r1);
-      d1 = mul_mod(d1, J.factor, q, r0, r1);
-      d2 = mul_mod(d2, J.factor, q, r0, r1);
+    const tl_u64x2 A0 = tl_ld2(J.ct1 + e), A1 = tl_ld2(J.ct1 + stride + e);
+    const tl_u64x2 B0 = tl_ld2(J.ct2 + e), B1 = tl_ld2(J.ct2 + stride + e);
+    tl_u64x2 T0, T1;
+    if (J.t) {
+      T0 = tl_ld2(J.t + e);
+      T1 = tl_ld2(J.t + J.t_stride + e);
+    }
+    uint64_t d[3][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint64_t a0 = A0[u], a1 = A1[u], b0 = B0[u], b1 = B1[u];
+      u128 c1 = mul_wide(a0, b1);
+      add128(c1, mul_wide(a1, b0));
+      d[0][u] = mul_mod(a0, b0, q, r0, r1);
+      d[1][u] = barrett_reduce_128(c1, q, r0, r1);
+      d[2][u] = mul_mod(a1, b1, q, r0, r1);
+    }
+    if (dbl) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) d[p][u] = add_mod(d[p][u], d[p][u], q);
+    } else if (scaled) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) d[p][u] = mul_mod(d[p][u], J.factor, q, r0, r1);
     }
     if (J.t) {
       const uint64_t c = cl[l];
-      d0 = add_mod(d0, mul_mod(J.t[e], c, q, r0, r1), q);
-      d1 = add_mod(d1, mul_mod(J.t[J.t_stride + e], c, q, r0, r1), q);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        d[0][u] = add_mod(d[0][u], mul_mod(T0[u], c, q, r0, r1), q);
+        d[1][u] = add_mod(d[1][u], mul_mod(T1[u], c, q, r0, r1), q);
+      }
     }
-    if (J.has_const) d0 = add_mod(d0, cl[a.L + l], q);
-    J.out[e] = d0;
-    J.out[stride + e] = d1;
-    J.out[2 * stride + e] = d2;
+    if (J.has_const) {
+      const uint64_t cc = cl[a.L + l];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) d[0][u] = add_mod(d[0][u], cc, q);
+    }
+    tl_st2(J.out + e, d[0][0], d[0][1]);
+    tl_st2(J.out + stride + e, d[1][0], d[1][1]);
+    tl_st2(J.out + 2 * stride + e, d[2][0], d[2][1]);
   }
 }
 

@@ -88,6 +88,8 @@ _SIGS = {
                                               ctypes.POINTER(ctypes.POINTER(vp)), sz, ctypes.POINTER(ctypes.c_uint32),
                                               ctypes.POINTER(vp), sz, ctypes.POINTER(vp), vp]),
     "phantom_tensor_lin": (ctypes.c_int, [vp, sz, vp, vp, vp, vp, vp, sz, vp, vp]),
+    "phantom_tensor_lin_batch": (ctypes.c_int, [vp, sz, sz, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                                vp, ctypes.POINTER(vp), sz, ctypes.POINTER(vp), ctypes.POINTER(vp), vp]),
     "phantom_lin_comb": (ctypes.c_int, [vp, sz, vp, sz, vp, vp, sz, sz, vp, vp]),
     "phantom_mul_scalar": (ctypes.c_int, [vp, sz, vp, sz, vp, vp, vp, sz, vp]),
     "phantom_leaf_combine": (ctypes.c_int, [vp, sz, ctypes.POINTER(vp), vp, sz, vp, vp, ctypes.POINTER(vp), sz, vp]),

@@ -187,6 +187,43 @@ def test_tensor_lin(c4, rng, with_f, with_t):
     assert np.array_equal(to_host(dout), want)
 
 
+@pytest.mark.parametrize("chain", [4, 16])
+def test_tensor_lin_batch(c4, rng, chain):
+    """the EvalMod products' batched tensors (tensor_lin_batch_kernel: 2 elements per thread, the
+    factor 2 as a modular doubling) == or_tensor_lin per job: factors 1, 2 and 3, with and without
+    a term and a constant"""
+    ql = c4.ql(chain)
+    L = len(ql)
+    mods = O.arr(ql)
+    tl = c4.ql(chain - 2)
+    jobs = [(1, True, True), (2, True, False), (2, False, True), (3, True, True), (1, False, False), (2, True, True)]
+    cnt = len(jobs)
+    A = [_rand(rng, ql, 2) for _ in range(cnt)]
+    B = [_rand(rng, ql, 2) for _ in range(cnt)]
+    T = [_rand(rng, tl, 2) for _ in range(cnt)]
+    C = [O.arr([int(x) % q for x, q in zip(rng.integers(0, 2 ** 62, size=L, dtype=np.uint64), ql)]) for _ in range(cnt)]
+    K = [O.arr([int(x) % q for x, q in zip(rng.integers(0, 2 ** 62, size=L, dtype=np.uint64), ql)]) for _ in range(cnt)]
+    dA, dB, dT = [to_dev(x) for x in A], [to_dev(x) for x in B], [to_dev(x) for x in T]
+    dout = [to_dev(np.zeros(3 * L * N, dtype=np.uint64)) for _ in range(cnt)]
+    vp = lambda xs: PA.ptr_array(list(xs))
+    facs = O.arr([f for f, _, _ in jobs])
+    PA.check(_lib().phantom_tensor_lin_batch(
+        c4.handle, chain, cnt, vp(ptr(x) for x in dA), vp(ptr(x) for x in dB), vp(ptr(x) for x in dout),
+        facs.ctypes.data, vp(ptr(dT[k]) if jobs[k][1] else 0 for k in range(cnt)), len(tl) * N,
+        vp(C[k].ctypes.data if jobs[k][1] else 0 for k in range(cnt)),
+        vp(K[k].ctypes.data if jobs[k][2] else 0 for k in range(cnt)), stream()))
+    for k, (f, with_t, with_c) in enumerate(jobs):
+        want = np.zeros(3 * L * N, dtype=np.uint64)
+        fr = O.arr([f % q for q in ql])
+        O.lib().or_tensor_lin(O.P(A[k]), O.P(B[k]), O.P(want), N, L, O.P(mods), O.P(fr) if f != 1 else None,
+                              O.P(T[k]) if with_t else None, len(tl) * N, O.P(C[k]) if with_t else None)
+        if with_c:
+            w0 = want[:L * N].reshape(L, N)
+            for l in range(L):
+                w0[l] = (w0[l] + np.uint64(K[k][l])) % np.uint64(ql[l])
+        assert np.array_equal(to_host(dout[k]), want), k
+
+
 def test_lin_comb_and_mul_scalar(c4, rng):
     chain = 20
     ql = c4.ql(chain)
