@@ -393,6 +393,18 @@ __global__ __launch_bounds__(64 * kLtWaves) void lt_bsgs_group_kernel(LtGroupArg
                   ga.pts);
 }
 
+// 16-byte global accesses of two consecutive elements
+typedef uint64_t tl_u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ tl_u64x2 tl_ld2(const uint64_t* p) {
+  return *(const __attribute__((address_space(1))) tl_u64x2*)p;
+}
+__device__ __forceinline__ void tl_st2(uint64_t* p, uint64_t x, uint64_t y) {
+  tl_u64x2 v;
+  v.x = x;
+  v.y = y;
+  *(__attribute__((address_space(1))) tl_u64x2*)p = v;
+}
+
 template <bool MUL, bool ACC>
 __global__ __launch_bounds__(kBlock) void scalar_v_kernel(const uint64_t* in, size_t in_stride, LimbScalars c,
                                                           const uint64_t* acc, uint64_t* out, const uint64_t* q,
@@ -400,12 +412,20 @@ __global__ __launch_bounds__(kBlock) void scalar_v_kernel(const uint64_t* in, si
   in += blockIdx.y * in_stride;
   out += blockIdx.y * total;
   if constexpr (ACC) acc += blockIdx.y * total;
-  for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
+  // two elements per thread, 16-byte accesses (n even: a pair shares its limb)
+  for (size_t e = 2 * (blockIdx.x * (size_t)kBlock + threadIdx.x); e < total; e += 2 * (size_t)gridDim.x * kBlock) {
     const uint32_t l = static_cast<uint32_t>(e >> log_n);
-    const uint64_t ql = q[l];
-    uint64_t v = MUL ? mul_shoup(in[e], c.v[l], c.vs[l], ql) : add_mod(in[e], c.v[l], ql);
-    if constexpr (ACC) v = add_mod(v, acc[e], ql);
-    out[e] = v;
+    const uint64_t ql = q[l], cv = c.v[l];
+    const tl_u64x2 x = tl_ld2(in + e);
+    uint64_t v[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) v[u] = MUL ? mul_shoup(x[u], cv, c.vs[l], ql) : add_mod(x[u], cv, ql);
+    if constexpr (ACC) {
+      const tl_u64x2 y = tl_ld2(acc + e);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) v[u] = add_mod(v[u], y[u], ql);
+    }
+    tl_st2(out + e, v[0], v[1]);
   }
 }
 
@@ -509,16 +529,6 @@ __global__ __launch_bounds__(kBlock) void tensor_lin_kernel(TensorLinArgs a, uin
 // tensor_lin over the products of one batch: grid row blockIdx.y = product (see ckks.h).  Two
 // elements per thread and 16-byte accesses; the factor 2 (the EvalMod products' only factor
 // besides 1) is a modular doubling instead of a 128-bit product and Barrett reduction.
-typedef uint64_t tl_u64x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ tl_u64x2 tl_ld2(const uint64_t* p) {
-  return *(const __attribute__((address_space(1))) tl_u64x2*)p;
-}
-__device__ __forceinline__ void tl_st2(uint64_t* p, uint64_t x, uint64_t y) {
-  tl_u64x2 v;
-  v.x = x;
-  v.y = y;
-  *(__attribute__((address_space(1))) tl_u64x2*)p = v;
-}
 
 __global__ __launch_bounds__(kBlock) void tensor_lin_batch_kernel(TensorLinBatchArgs a, uint32_t log_n, size_t total) {
   const uint32_t k = blockIdx.y;
