@@ -200,7 +200,11 @@ struct LtGroupSrc {
 #ifndef PHX_LT_EPL
 #define PHX_LT_EPL 2
 #endif
-constexpr int kLtWaves = 8, kLtChunk = 4, kLtEpl = PHX_LT_EPL;
+#ifndef PHX_LT_DEPTH
+#define PHX_LT_DEPTH 2
+#endif
+constexpr int kLtWaves = 8, kLtChunk = 4, kLtEpl = PHX_LT_EPL, kLtDepth = PHX_LT_DEPTH;
+static_assert(kLtDepth >= 2 && kLtDepth <= 4, "2 to 4 plaintext chunks in flight");
 static_assert(kLtEpl == 1 || kLtEpl == 2, "1 or 2 elements per lane");
 
 template <int E>
@@ -328,8 +332,10 @@ __device__ __forceinline__ void lt_bsgs_tile(const Src& src, int nb, int Ql, int
   // backend sinks the plaintext loads past the barrier, or makes the staging writes wait for them
   const int wi = wv < nb ? wv : nb - 1;
   const __attribute__((address_space(4))) LtPtr* prow = (const __attribute__((address_space(4))) LtPtr*)(pts + wi * G);
-  LtVec<E> wbuf[2][kLtChunk];
-  lt_load_chunk<E>(wbuf[0], prow, 0, e);
+  constexpr int D = kLtDepth;  // plaintext chunks in flight
+  LtVec<E> wbuf[D][kLtChunk];
+#pragma unroll
+  for (int c = 0; c + 1 < D; ++c) lt_load_chunk<E>(wbuf[c], prow, c, e);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int r = 0; r < 8; ++r)
@@ -355,8 +361,8 @@ __device__ __forceinline__ void lt_bsgs_tile(const Src& src, int nb, int Ql, int
     }
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    if (c + 1 < NC) lt_load_chunk<E>(wbuf[(c + 1) & 1], prow, c + 1, e);
-    lt_chunk_products<E>(part, wbuf[c & 1], xs, c, lane);
+    if (c + D - 1 < NC) lt_load_chunk<E>(wbuf[(c + D - 1) % D], prow, c + D - 1, e);
+    lt_chunk_products<E>(part, wbuf[c % D], xs, c, lane);
     if (c & 1) lt_fold<E>(acc, part);  // 8 products per partial sum
   }
   const int l = static_cast<int>((tile * T) >> log_n);

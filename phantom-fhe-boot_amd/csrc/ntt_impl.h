@@ -455,9 +455,14 @@ __device__ __forceinline__ LimbCtx limb_ctx(const KArgs& a, int row) {
 // L2 at once instead of sitting dirty until the end-of-kernel write-back.  Measured on the
 // column/row pass access patterns (tools/ubench_fused.hip, profiles/r01/ubench_fused.txt):
 // -2 us per pass at [44][65536].  Plain relaxed atomic stores carry no ordering.
+// every buffer these kernels touch is global memory: the explicit global address space keeps a
+// pointer the compiler cannot trace to a kernel argument (a key digit read from a pointer table)
+// off FLAT instructions, which count in lgkmcnt too and so make every LDS wait also wait for them
+using GU64 = __attribute__((address_space(1))) uint64_t;
 __device__ __forceinline__ void store_wt(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((GU64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ uint64_t gload_nt(const uint64_t* p) { return __builtin_nontemporal_load((const GU64*)p); }
 
 __device__ __forceinline__ double centered_f64(uint64_t w, uint64_t q) {
   return w > (q >> 1) ? -u52_to_f64(q - w) : u52_to_f64(w);
@@ -569,11 +574,11 @@ __device__ __forceinline__ void ks_epilogue_b(const KArgs& a, const TileRef& tr,
     for (int d = 0; d < BETA; ++d)
 #pragma unroll
       for (int i = 0; i < KC; ++i) {
-        tb[s][d][i] = __builtin_nontemporal_load(tm + d * a.epi.tmu_stride + (c * KC + i) * T);
-        kb[s][d][i] = __builtin_nontemporal_load(kp[d] + (c * KC + i) * T);
+        tb[s][d][i] = gload_nt(tm + d * a.epi.tmu_stride + (c * KC + i) * T);
+        kb[s][d][i] = gload_nt(kp[d] + (c * KC + i) * T);
       }
 #pragma unroll
-    for (int i = 0; i < KC; ++i) ob[s][i] = __builtin_nontemporal_load(third + (c * KC + i) * T);
+    for (int i = 0; i < KC; ++i) ob[s][i] = gload_nt(third + (c * KC + i) * T);
   };
   load(0, 0);
   static_for<NC>([&](auto cc) {
@@ -627,11 +632,11 @@ __device__ __forceinline__ void ks_prologue_b(const KArgs& a, const TileRef& tr,
     for (int d = 0; d < BETA; ++d)
 #pragma unroll
       for (int i = 0; i < KC; ++i) {
-        tb[s][d][i] = __builtin_nontemporal_load(tm + d * a.epi.tmu_stride + (c * KC + i) * T);
-        kb[s][d][i] = __builtin_nontemporal_load(kp[d] + (c * KC + i) * T);
+        tb[s][d][i] = gload_nt(tm + d * a.epi.tmu_stride + (c * KC + i) * T);
+        kb[s][d][i] = gload_nt(kp[d] + (c * KC + i) * T);
       }
 #pragma unroll
-    for (int i = 0; i < KC; ++i) ob[s][i] = __builtin_nontemporal_load(ad + (c * KC + i) * T);
+    for (int i = 0; i < KC; ++i) ob[s][i] = gload_nt(ad + (c * KC + i) * T);
   };
   load(0, 0);
   static_for<NC>([&](auto cc) {

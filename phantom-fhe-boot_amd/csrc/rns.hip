@@ -40,15 +40,25 @@ dim3 poly_grid(size_t work_items, size_t polys) {
 
 using u64x2 = ulonglong2;
 
-__device__ __forceinline__ u64x2 ld2(const uint64_t* p) { return *reinterpret_cast<const u64x2*>(p); }
+// 16-byte accesses, always to global memory: the explicit address space keeps a pointer the compiler
+// cannot trace to a kernel argument (a key digit read from a pointer table) off FLAT instructions,
+// which count in lgkmcnt too, so that every LDS wait would also wait for them
+typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+using GV2 = __attribute__((address_space(1))) v2u64;
+__device__ __forceinline__ u64x2 ld2(const uint64_t* p) {
+  const v2u64 v = *(const GV2*)p;
+  return make_ulonglong2(v.x, v.y);
+}
 // streamed-once operands (keys): nontemporal 16-byte load
 __device__ __forceinline__ u64x2 ld2_nt(const uint64_t* p) {
-  typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
-  const v2u64 v = __builtin_nontemporal_load(reinterpret_cast<const v2u64*>(p));
+  const v2u64 v = __builtin_nontemporal_load((const GV2*)p);
   return make_ulonglong2(v.x, v.y);
 }
 __device__ __forceinline__ void st2(uint64_t* p, uint64_t a, uint64_t b) {
-  *reinterpret_cast<u64x2*>(p) = make_ulonglong2(a, b);
+  v2u64 v;
+  v.x = a;
+  v.y = b;
+  *(GV2*)p = v;
 }
 
 // generic binary elementwise over [L][n] with per-limb modulus
@@ -761,6 +771,25 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_kernel(KsRotateGroupArgs ga,
   (void)n;
 }
 
+// a pointer every lane holds the same value of (read from LDS), in scalar registers
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return reinterpret_cast<T*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+// workgroup barrier after this wave's LDS writes (lgkmcnt(0)), leaving its global loads in flight
+// (a __syncthreads also waits for every outstanding load); the memory clobbers keep the compiler
+// from moving LDS accesses across it
+__device__ __forceinline__ void ks_lt_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt unconstrained
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // keyswitch_rotate_batch: workgroup = (limb l, source block sblk); entry k's products go to LDS
 // buffer k & 1 (one barrier per entry: an entry's gather from buffer k & 1 finishes before any
 // thread passes entry k + 1's barrier, so entry k + 2 may overwrite it).
@@ -773,6 +802,7 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_kernel(KsRotateGroupArgs ga,
 // launch; the ciphertexts' workgroups of the same (limb, source block) are dealt to one XCD 8
 // dispatches apart (blocks b and b + 8 share an XCD under round-robin placement), so the followers
 // read the key halves from that XCD's L2.
+constexpr uint32_t kKsBatchFullMax = 64;  // entries of one ks_rotate_batch_full launch
 template <int BETA, bool GROUP>
 __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGroupArgs pa, uint32_t log_n) {
   constexpr uint32_t bsz = kGalB;
@@ -809,12 +839,55 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGrou
       pc0[p] = make_ulonglong2(mul_shoup(c0.x, w, ws, q), mul_shoup(c0.y, w, ws, q));
     }
   }
+  // the key-switched entries compacted in LDS (the identity entries, P (c0, c1) unpermuted, are
+  // written first), so the loop below has no branch around its loads: a branch would make the
+  // compiler wait for every load in flight where the paths join
+  __shared__ const uint64_t* kp[kKsBatchFullMax][BETA];
+  __shared__ const uint32_t* pp[kKsBatchFullMax];
+  __shared__ uint32_t bi[kKsBatchFullMax];
+  __shared__ int64_t oo[kKsBatchFullMax];
+  __shared__ int nks;
+  if (threadIdx.x < 64) {
+    const uint32_t k = threadIdx.x;
+    const bool live = k < a.count;
+    const KsBatchEntry en = a.entries[live ? k : 0];
+    const bool ks = live && en.evk != nullptr;
+    const uint64_t m = __ballot(ks);
+    const int pos = __popcll(m & ((1ull << threadIdx.x) - 1));
+    if (ks) {
+      pp[pos] = en.perm;
+      bi[pos] = en.binv[sblk];
+      oo[pos] = en.out_off;
+#pragma unroll
+      for (int b = 0; b < BETA; ++b) kp[pos][b] = en.evk[b];
+    }
+    if (threadIdx.x == 0) nks = __popcll(m);
+  }
+  for (uint32_t k = 0; k < a.count; ++k) {  // identity entries (workgroup-uniform; nothing in flight yet)
+    const KsBatchEntry en = a.entries[k];
+    if (en.evk) continue;
+    uint64_t* out = a.out + en.out_off;
+#pragma unroll
+    for (int p = 0; p < PP; ++p) {
+      const size_t j = j0 + 2 * (threadIdx.x + p * kBlock);
+      uint64_t v1x = 0, v1y = 0;
+      if (addc) {
+        const u64x2 c1 = ld2(a.ct + ql_n + lbase + j);
+        v1x = mul_shoup(c1.x, w, ws, q);
+        v1y = mul_shoup(c1.y, w, ws, q);
+      }
+      st2(out + lbase + j, pc0[p].x, pc0[p].y);
+      st2(out + qlp_n + lbase + j, v1x, v1y);
+    }
+  }
+  __syncthreads();
+  const int nk = __builtin_amdgcn_readfirstlane(nks);
+  if (nk == 0) return;  // workgroup-uniform, no barrier below
   u64x2 k0[PP][BETA], k1[PP][BETA];
-  auto load_keys = [&](const KsBatchEntry& e) {
-    if (!e.evk) return;
+  auto load_keys = [&](int k) {
 #pragma unroll
     for (int b = 0; b < BETA; ++b) {
-      const uint64_t* key = e.evk[b];
+      const uint64_t* key = uniform_ptr(kp[k][b]);
 #pragma unroll
       for (int p = 0; p < PP; ++p) {
         const size_t j = j0 + 2 * (threadIdx.x + p * kBlock);
@@ -823,67 +896,48 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGrou
       }
     }
   };
-  KsBatchEntry e = a.entries[0];
-  load_keys(e);
-  for (uint32_t k = 0; k < a.count; ++k) {
+  load_keys(0);
+  constexpr int GM = bsz / kBlock;  // gathered outputs per thread
+  for (int k = 0; k < nk; ++k) {
     uint64_t* t0 = s0[k & 1];
     uint64_t* t1 = s1[k & 1];
-    const bool ks = e.evk != nullptr;
+    // the gather's permutation first: loads are waited for in issue order, so one issued after
+    // the next entry's keys would make the gather wait for those keys too
+    const uint32_t ob = bi[k];
+    const __attribute__((address_space(1))) uint32_t* pm =
+        (const __attribute__((address_space(1))) uint32_t*)uniform_ptr(pp[k]) + (size_t)ob * bsz;
+    uint32_t src[GM];
+#pragma unroll
+    for (int m = 0; m < GM; ++m) src[m] = pm[threadIdx.x + m * kBlock];
+    asm volatile("" ::: "memory");  // (issued here, not sunk to their use after the key loads)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int p = 0; p < PP; ++p) {
       const uint32_t i = threadIdx.x + p * kBlock;
-      uint64_t v0x, v0y, v1x, v1y;
-      if (ks) {
-        u128 a0x{0, 0}, a0y{0, 0}, a1x{0, 0}, a1y{0, 0};
+      u128 a0x{0, 0}, a0y{0, 0}, a1x{0, 0}, a1y{0, 0};
 #pragma unroll
-        for (int b = 0; b < BETA; ++b) {
-          add128(a0x, mul_wide(dg[p][b].x, k0[p][b].x));
-          add128(a0y, mul_wide(dg[p][b].y, k0[p][b].y));
-          add128(a1x, mul_wide(dg[p][b].x, k1[p][b].x));
-          add128(a1y, mul_wide(dg[p][b].y, k1[p][b].y));
-        }
-        v0x = add_mod(barrett_reduce_128(a0x, q, r0, r1), pc0[p].x, q);
-        v0y = add_mod(barrett_reduce_128(a0y, q, r0, r1), pc0[p].y, q);
-        v1x = barrett_reduce_128(a1x, q, r0, r1);
-        v1y = barrett_reduce_128(a1y, q, r0, r1);
-      } else {  // identity: P (c0, c1) on the Ql limbs, zero on P's
-        v0x = pc0[p].x;
-        v0y = pc0[p].y;
-        v1x = v1y = 0;
-        if (addc) {
-          const u64x2 c1 = ld2(a.ct + ql_n + lbase + j0 + 2 * i);
-          v1x = mul_shoup(c1.x, w, ws, q);
-          v1y = mul_shoup(c1.y, w, ws, q);
-        }
+      for (int b = 0; b < BETA; ++b) {
+        add128(a0x, mul_wide(dg[p][b].x, k0[p][b].x));
+        add128(a0y, mul_wide(dg[p][b].y, k0[p][b].y));
+        add128(a1x, mul_wide(dg[p][b].x, k1[p][b].x));
+        add128(a1y, mul_wide(dg[p][b].y, k1[p][b].y));
       }
-      t0[2 * i] = v0x;
-      t0[2 * i + 1] = v0y;
-      t1[2 * i] = v1x;
-      t1[2 * i + 1] = v1y;
+      t0[2 * i] = add_mod(barrett_reduce_128(a0x, q, r0, r1), pc0[p].x, q);
+      t0[2 * i + 1] = add_mod(barrett_reduce_128(a0y, q, r0, r1), pc0[p].y, q);
+      t1[2 * i] = barrett_reduce_128(a1x, q, r0, r1);
+      t1[2 * i + 1] = barrett_reduce_128(a1y, q, r0, r1);
     }
-    const KsBatchEntry cur = e;
-    if (k + 1 < a.count) {
-      e = a.entries[k + 1];
-      load_keys(e);  // in flight during this entry's barrier and gather
-    }
-    __syncthreads();
-    uint64_t* out = a.out + cur.out_off;
-    if (ks) {
-      const uint32_t ob = cur.binv[sblk];
-      const uint32_t* pm = cur.perm + (size_t)ob * bsz;
+    // the next entry's keys (the last one's again at the end: L2 hits) in flight over the barrier
+    // and the gather
+    __builtin_amdgcn_sched_barrier(0);
+    load_keys(min(k + 1, nk - 1));
+    ks_lt_barrier();
+    uint64_t* out = a.out + oo[k] + lbase + (size_t)ob * bsz;
 #pragma unroll
-      for (uint32_t i = threadIdx.x; i < bsz; i += kBlock) {
-        const uint32_t src = pm[i] & (bsz - 1);
-        const size_t d = lbase + (size_t)ob * bsz + i;
-        out[d] = t0[src];
-        out[qlp_n + d] = t1[src];
-      }
-    } else {
-#pragma unroll
-      for (uint32_t i = threadIdx.x; i < bsz; i += kBlock) {
-        out[lbase + j0 + i] = t0[i];
-        out[qlp_n + lbase + j0 + i] = t1[i];
-      }
+    for (int m = 0; m < GM; ++m) {
+      const uint32_t i = threadIdx.x + m * kBlock;
+      out[i] = t0[src[m] & (bsz - 1)];
+      out[qlp_n + i] = t1[src[m] & (bsz - 1)];
     }
   }
 }
@@ -898,22 +952,6 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGrou
 // The next baby's key-switch inputs and permutation, and the plaintexts, are loaded one baby
 // ahead; the barrier is a raw s_barrier after lgkmcnt(0), so those loads stay in flight over it.
 constexpr int kKsLtTile = 256, kKsLtWaves = 8, kKsLtG = 32;
-
-// a pointer every lane holds the same value of (read from LDS), in scalar registers
-template <class T>
-__device__ __forceinline__ T* uniform_ptr(T* p) {
-  const uint64_t v = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
-  return reinterpret_cast<T*>((static_cast<uint64_t>(hi) << 32) | lo);
-}
-
-__device__ __forceinline__ void ks_lt_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt unconstrained
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 template <int BETA, bool GROUP>
 __global__ __launch_bounds__(kKsLtWaves * 64) void ks_lt_kernel(KsLtGroupArgs ga, uint32_t log_n) {
@@ -1479,7 +1517,7 @@ hipError_t keyswitch_rotate_batch(const KsRotateBatchArgs& a, size_t n, hipStrea
   if (a.qlp == 0 || a.count == 0) return hipSuccess;
   const uint32_t log_n = __builtin_ctzll(n), bsz = static_cast<uint32_t>(std::min<size_t>(n, kGalB));
   const dim3 grid(static_cast<uint32_t>(a.qlp * (n / bsz)));
-  switch (bsz == kGalB ? a.beta : 0) {
+  switch (bsz == kGalB && a.count <= kKsBatchFullMax ? a.beta : 0) {
     case 1: ks_rotate_batch_full<1, false><<<grid, kBlock, 0, s>>>(KsRotateBatchGroupArgs{{a}, 1}, log_n); break;
     case 2: ks_rotate_batch_full<2, false><<<grid, kBlock, 0, s>>>(KsRotateBatchGroupArgs{{a}, 1}, log_n); break;
     case 3: ks_rotate_batch_full<3, false><<<grid, kBlock, 0, s>>>(KsRotateBatchGroupArgs{{a}, 1}, log_n); break;
@@ -1501,7 +1539,7 @@ hipError_t keyswitch_rotate_batch_group(const KsRotateBatchGroupArgs& ga, size_t
       return hipErrorInvalidValue;
   }
   if (a.qlp == 0 || a.count == 0) return hipSuccess;
-  if (n < kGalB || a.beta > 4) {  // the shapes without the register-resident form: one launch each
+  if (n < kGalB || a.beta > 4 || a.count > kKsBatchFullMax) {  // the shapes without the register-resident form: one launch each
     for (int c = 0; c < ga.count; ++c)
       if (hipError_t e = keyswitch_rotate_batch(ga.a[c], n, s)) return e;
     return hipSuccess;
