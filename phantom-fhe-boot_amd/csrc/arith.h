@@ -77,6 +77,44 @@ __device__ __forceinline__ uint64_t barrett_reduce_64(uint64_t x, uint64_t q, ui
   return csub(x - mulhi(x, r1) * q, q);
 }
 
+// ---- 30-bit split accumulation: sum_i x_i y_i = LL + MM 2^30 + HH 2^60 with x = xh 2^30 + xl and
+// y = yh 2^30 + yl (x, y < 2^60), every partial product below 2^60, reduced once at the end ----
+struct SplitRed {
+  uint64_t c30, c30s, c60, c60s;  // 2^30 mod q, 2^60 mod q and their Shoup quotients
+};
+// floor(w 2^64 / q) for w < q from the Barrett ratio floor(2^128 / q) = {r0, r1} (an estimate at
+// most 2 low, corrected exactly)
+__device__ __forceinline__ uint64_t shoup_from_barrett(uint64_t w, uint64_t q, uint64_t r0, uint64_t r1) {
+  uint64_t s = w * r1 + mulhi(w, r0);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    // remainder w 2^64 - s q (< 3q, so its high word is 0 or 1)
+    const u128 p = mul_wide(s, q);
+    const uint64_t rlo = 0 - p.lo, rhi = w - p.hi - (p.lo != 0);
+    if (rhi != 0 || rlo >= q) ++s;
+  }
+  return s;
+}
+__device__ __forceinline__ SplitRed split_red(uint64_t q, uint64_t r0, uint64_t r1) {
+  SplitRed k;
+  k.c30 = (1ull << 30) % q;
+  k.c60 = (1ull << 60) % q;
+  k.c30s = shoup_from_barrett(k.c30, q, r0, r1);
+  k.c60s = shoup_from_barrett(k.c60, q, r0, r1);
+  return k;
+}
+// (ll + mm 2^30 + hh 2^60) mod q for q < 2^60, canonical (r1 = floor(2^64 / q), the high word of
+// the Barrett ratio): three lazy residues in [0, 2q) (a 64-bit Barrett step and two Shoup
+// products), their sum below 6q < 2^63, one more Barrett step to [0, 2q), one conditional subtraction
+__device__ __forceinline__ uint64_t split_reduce(uint64_t ll, uint64_t mm, uint64_t hh, const SplitRed& k, uint64_t q,
+                                                 uint64_t r1) {
+  const uint64_t a = ll - mulhi(ll, r1) * q;
+  const uint64_t b = mm * k.c30 - mulhi(mm, k.c30s) * q;
+  const uint64_t c = hh * k.c60 - mulhi(hh, k.c60s) * q;
+  const uint64_t s = a + b + c;
+  return csub(s - mulhi(s, r1) * q, q);
+}
+
 __device__ __forceinline__ uint64_t mul_mod(uint64_t a, uint64_t b, uint64_t q, uint64_t r0, uint64_t r1) {
   return barrett_reduce_128(mul_wide(a, b), q, r0, r1);
 }

@@ -827,12 +827,25 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGrou
   const size_t j0 = (size_t)sblk * bsz;
   const bool addc = l < a.ql;
   const uint64_t w = addc ? a.pmod[l] : 0, ws = addc ? a.pmod_shoup[l] : 0;
-  u64x2 dg[PP][BETA], pc0[PP];
+  // the digits split in 30-bit halves once (every entry's products use them), the products
+  // accumulated as 30-bit partial sums (ll, mm, hh below 2^62, 2^63, 2^62 for BETA <= 4) and
+  // reduced once per output (split_reduce) instead of 128-bit sums and a Barrett reduction
+  static_assert(BETA <= 4, "split partial sums");
+  constexpr uint64_t kM30 = (1ull << 30) - 1;
+  const SplitRed sr = split_red(q, r0, r1);
+  uint32_t dl[PP][BETA][2], dh[PP][BETA][2];
+  u64x2 pc0[PP];
 #pragma unroll
   for (int p = 0; p < PP; ++p) {
     const size_t j = j0 + 2 * (threadIdx.x + p * kBlock);
 #pragma unroll
-    for (int b = 0; b < BETA; ++b) dg[p][b] = ld2(a.digits + b * qlp_n + lbase + j);
+    for (int b = 0; b < BETA; ++b) {
+      const u64x2 d = ld2(a.digits + b * qlp_n + lbase + j);
+      dl[p][b][0] = static_cast<uint32_t>(d.x & kM30);
+      dh[p][b][0] = static_cast<uint32_t>(d.x >> 30);
+      dl[p][b][1] = static_cast<uint32_t>(d.y & kM30);
+      dh[p][b][1] = static_cast<uint32_t>(d.y >> 30);
+    }
     pc0[p] = make_ulonglong2(0, 0);
     if (addc) {
       const u64x2 c0 = ld2(a.ct + lbase + j);
@@ -891,8 +904,10 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGrou
 #pragma unroll
       for (int p = 0; p < PP; ++p) {
         const size_t j = j0 + 2 * (threadIdx.x + p * kBlock);
-        k0[p][b] = ld2_nt(key + kbase + j);
-        k1[p][b] = ld2_nt(key + qp_n + kbase + j);
+        // single: the keys are read once (nontemporal); GROUP: the followers on this XCD read
+        // them again from L2, so they keep the default policy
+        k0[p][b] = GROUP ? ld2(key + kbase + j) : ld2_nt(key + kbase + j);
+        k1[p][b] = GROUP ? ld2(key + qp_n + kbase + j) : ld2_nt(key + qp_n + kbase + j);
       }
     }
   };
@@ -914,18 +929,25 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGrou
 #pragma unroll
     for (int p = 0; p < PP; ++p) {
       const uint32_t i = threadIdx.x + p * kBlock;
-      u128 a0x{0, 0}, a0y{0, 0}, a1x{0, 0}, a1y{0, 0};
+      uint64_t ll[2][2] = {{0, 0}, {0, 0}}, mm[2][2] = {{0, 0}, {0, 0}}, hh[2][2] = {{0, 0}, {0, 0}};
 #pragma unroll
       for (int b = 0; b < BETA; ++b) {
-        add128(a0x, mul_wide(dg[p][b].x, k0[p][b].x));
-        add128(a0y, mul_wide(dg[p][b].y, k0[p][b].y));
-        add128(a1x, mul_wide(dg[p][b].x, k1[p][b].x));
-        add128(a1y, mul_wide(dg[p][b].y, k1[p][b].y));
+        const uint64_t kv[2][2] = {{k0[p][b].x, k0[p][b].y}, {k1[p][b].x, k1[p][b].y}};
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const uint32_t kl = static_cast<uint32_t>(kv[t][u] & kM30), kh = static_cast<uint32_t>(kv[t][u] >> 30);
+            ll[t][u] += static_cast<uint64_t>(dl[p][b][u]) * kl;
+            mm[t][u] += static_cast<uint64_t>(dl[p][b][u]) * kh;
+            mm[t][u] += static_cast<uint64_t>(dh[p][b][u]) * kl;
+            hh[t][u] += static_cast<uint64_t>(dh[p][b][u]) * kh;
+          }
       }
-      t0[2 * i] = add_mod(barrett_reduce_128(a0x, q, r0, r1), pc0[p].x, q);
-      t0[2 * i + 1] = add_mod(barrett_reduce_128(a0y, q, r0, r1), pc0[p].y, q);
-      t1[2 * i] = barrett_reduce_128(a1x, q, r0, r1);
-      t1[2 * i + 1] = barrett_reduce_128(a1y, q, r0, r1);
+      t0[2 * i] = add_mod(split_reduce(ll[0][0], mm[0][0], hh[0][0], sr, q, r1), pc0[p].x, q);
+      t0[2 * i + 1] = add_mod(split_reduce(ll[0][1], mm[0][1], hh[0][1], sr, q, r1), pc0[p].y, q);
+      t1[2 * i] = split_reduce(ll[1][0], mm[1][0], hh[1][0], sr, q, r1);
+      t1[2 * i + 1] = split_reduce(ll[1][1], mm[1][1], hh[1][1], sr, q, r1);
     }
     // the next entry's keys (the last one's again at the end: L2 hits) in flight over the barrier
     // and the gather

@@ -1,4 +1,4 @@
-"""C5 throughput of a library variant: bench.c5_leg (256 bootstraps, 4 lanes, 8 verified) on the
+"""C5 throughput of a library variant: bench.c5_leg (C5_TOTAL bootstraps, default 384, on C5_LANES lanes, default 3, 8 verified) on the
 variant's ctypes binding.  usage: python tools/time_c5.py tools/variants/<name>/py"""
 import os
 import sys
@@ -11,7 +11,8 @@ sys.path.insert(1, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 torch.cuda.set_device(0)
-r = bench.c5_leg(None, torch, 1, 0, 0, total=256, lanes=4, verify=8)
+lanes = int(os.environ.get("C5_LANES", "3"))
+r = bench.c5_leg(None, torch, 1, 0, 0, total=int(os.environ.get("C5_TOTAL", "384")), lanes=lanes, verify=8)
 free, total = torch.cuda.mem_get_info()
 print(os.path.basename(os.path.dirname(os.path.abspath(sys.argv[1]))), r["bootstraps_per_s"], r["min_avg_bits"],
       "used_GiB %.1f" % ((total - free) / 2**30), flush=True)
