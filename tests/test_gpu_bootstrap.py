@@ -194,8 +194,11 @@ def test_two_iteration_bootstrap_gains_precision():
     bootstrap removes most of the first one's error."""
     one, _ = _session_run(count=1)
     two, _ = _session_run(iterations=2, precision=8, count=1)
-    # measured on MI355X: 10.0 -> 22.5 bits (precision 6 / 8 / 10: 20.5 / 22.5 / 20.5)
-    assert two[0] > 21.0 and two[0] > one[0] + 10.0, (one, two)
+    # measured on MI355X over 48 fresh encryptions each (the encryptor draws OS entropy;
+    # profiles/r05/two_iter/dist_48.jsonl): one iteration 9.84-10.13 bits, median 9.99; two
+    # iterations at precision 8: 20.24-22.57, median 22.47, 2 of 48 below 21 (the first
+    # iteration's slot-0 tail, DESIGN.md §3 Precision, carried into the correction)
+    assert two[0] > 19.5 and two[0] > one[0] + 9.0, (one, two)
 
 
 def test_session_run_grouped_matches_default():
