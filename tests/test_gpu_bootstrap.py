@@ -196,8 +196,8 @@ def test_two_iteration_bootstrap_gains_precision():
     two, _ = _session_run(iterations=2, precision=8, count=1)
     # measured on MI355X over 48 fresh encryptions each (the encryptor draws OS entropy;
     # profiles/r05/two_iter/dist_48.jsonl): one iteration 9.84-10.13 bits, median 9.99; two
-    # iterations at precision 8: 20.24-22.57, median 22.47, 2 of 48 below 21 (the first
-    # iteration's slot-0 tail, DESIGN.md §3 Precision, carried into the correction)
+    # iterations at precision 8: 20.24-22.57, median 22.47, 2 of 48 below 21 (the low two not
+    # traced further)
     assert two[0] > 19.5 and two[0] > one[0] + 9.0, (one, two)
 
 
