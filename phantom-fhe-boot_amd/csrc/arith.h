@@ -81,6 +81,7 @@ __device__ __forceinline__ uint64_t barrett_reduce_64(uint64_t x, uint64_t q, ui
 // y = yh 2^30 + yl (x, y < 2^60), every partial product below 2^60, reduced once at the end ----
 struct SplitRed {
   uint64_t c30, c30s, c60, c60s;  // 2^30 mod q, 2^60 mod q and their Shoup quotients
+  uint64_t nq, nq2;               // -q, -2q mod 2^64
 };
 // floor(w 2^64 / q) for w < q from the Barrett ratio floor(2^128 / q) = {r0, r1} (an estimate at
 // most 2 low, corrected exactly)
@@ -95,19 +96,28 @@ __device__ __forceinline__ uint64_t shoup_from_barrett(uint64_t w, uint64_t q, u
   }
   return s;
 }
+// a uniform 64-bit value in scalar registers (every lane holds the same value)
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+// the constants of one modulus, for a workgroup-uniform q (kept in scalar registers)
 __device__ __forceinline__ SplitRed split_red(uint64_t q, uint64_t r0, uint64_t r1) {
   SplitRed k;
-  k.c30 = (1ull << 30) % q;
-  k.c60 = (1ull << 60) % q;
-  k.c30s = shoup_from_barrett(k.c30, q, r0, r1);
-  k.c60s = shoup_from_barrett(k.c60, q, r0, r1);
+  k.c30 = uniform_u64((1ull << 30) % q);
+  k.c60 = uniform_u64((1ull << 60) % q);
+  k.c30s = uniform_u64(shoup_from_barrett(k.c30, q, r0, r1));
+  k.c60s = uniform_u64(shoup_from_barrett(k.c60, q, r0, r1));
+  k.nq = uniform_u64(0 - q);
+  k.nq2 = uniform_u64(0 - (q << 1));
   return k;
 }
-// (ll + mm 2^30 + hh 2^60) mod q for q < 2^60, canonical (r1 = floor(2^64 / q), the high word of
-// the Barrett ratio): three lazy residues in [0, 2q) (a 64-bit Barrett step and two Shoup
-// products), their sum below 6q < 2^63, one more Barrett step to [0, 2q), one conditional subtraction
-__device__ __forceinline__ uint64_t split_reduce(uint64_t ll, uint64_t mm, uint64_t hh, const SplitRed& k, uint64_t q,
-                                                 uint64_t r1) {
+
+// split_reduce (below) with exact high products: three lazy residues in [0, 2q), their sum below
+// 6q, one more Barrett step and one conditional subtraction.  More instructions, fewer registers.
+__device__ __forceinline__ uint64_t split_reduce_exact(uint64_t ll, uint64_t mm, uint64_t hh, const SplitRed& k,
+                                                       uint64_t q, uint64_t r1) {
   const uint64_t a = ll - mulhi(ll, r1) * q;
   const uint64_t b = mm * k.c30 - mulhi(mm, k.c30s) * q;
   const uint64_t c = hh * k.c60 - mulhi(hh, k.c60s) * q;
@@ -188,6 +198,23 @@ __device__ __forceinline__ uint64_t csub_n(uint64_t x, uint64_t m, uint64_t nm) 
 // a w mod q in [0, 4q) (as mul_shoup_lazy4 below), given nq = -q mod 2^64: a w + Q' (-q)
 __device__ __forceinline__ uint64_t mul_shoup_lazy4(uint64_t a, uint64_t w, uint64_t ws, uint64_t q) {
   return a * w + mulhi_approx(a, ws) * opaque(0 - q);
+}
+
+// (ll + mm 2^30 + hh 2^60) mod q for q < 2^60, canonical (SplitRed above; r1 = floor(2^64 / q), the
+// high word of the Barrett ratio).  Three lazy residues with the approximate quotient (mulhi_approx,
+// at most 2 low): a 64-bit Barrett step on ll and Shoup products for mm 2^30 and hh 2^60, each in
+// [0, 4q); their sum below 12q < 2^64; one more Barrett step to [0, 4q) and two carry-free
+// conditional subtractions.  No VCC carries and no zero-extended 64-bit high products.
+__device__ __forceinline__ uint64_t split_reduce(uint64_t ll, uint64_t mm, uint64_t hh, const SplitRed& k, uint64_t q,
+                                                 uint64_t r1) {
+  const uint64_t nq = k.nq;
+  const uint64_t a = ll + mulhi_approx(ll, r1) * nq;
+  const uint64_t b = mm * k.c30 + mulhi_approx(mm, k.c30s) * nq;
+  const uint64_t c = hh * k.c60 + mulhi_approx(hh, k.c60s) * nq;
+  uint64_t s = add64(add64(a, b), c);
+  s = s + mulhi_approx(s, r1) * nq;
+  s = csub_n(s, q << 1, k.nq2);
+  return csub_n(s, q, nq);
 }
 
 // forward CT butterfly: x, y in [0, 8q) -> [0, 8q)

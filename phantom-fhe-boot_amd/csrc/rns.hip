@@ -944,10 +944,15 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGrou
             hh[t][u] += static_cast<uint64_t>(dh[p][b][u]) * kh;
           }
       }
-      t0[2 * i] = add_mod(split_reduce(ll[0][0], mm[0][0], hh[0][0], sr, q, r1), pc0[p].x, q);
-      t0[2 * i + 1] = add_mod(split_reduce(ll[0][1], mm[0][1], hh[0][1], sr, q, r1), pc0[p].y, q);
-      t1[2 * i] = split_reduce(ll[1][0], mm[1][0], hh[1][0], sr, q, r1);
-      t1[2 * i + 1] = split_reduce(ll[1][1], mm[1][1], hh[1][1], sr, q, r1);
+      // GROUP (keys from L2, issue-bound): the approximate-quotient form, fewer instructions at
+      // 132 VGPRs; single (HBM-bound): the exact form at 128 VGPRs keeps 4 waves per SIMD
+      auto red = [&](uint64_t x, uint64_t y, uint64_t z) {
+        return GROUP ? split_reduce(x, y, z, sr, q, r1) : split_reduce_exact(x, y, z, sr, q, r1);
+      };
+      t0[2 * i] = add_mod(red(ll[0][0], mm[0][0], hh[0][0]), pc0[p].x, q);
+      t0[2 * i + 1] = add_mod(red(ll[0][1], mm[0][1], hh[0][1]), pc0[p].y, q);
+      t1[2 * i] = red(ll[1][0], mm[1][0], hh[1][0]);
+      t1[2 * i + 1] = red(ll[1][1], mm[1][1], hh[1][1]);
     }
     // the next entry's keys (the last one's again at the end: L2 hits) in flight over the barrier
     // and the gather
