@@ -114,8 +114,9 @@ __device__ __forceinline__ SplitRed split_red(uint64_t q, uint64_t r0, uint64_t 
   return k;
 }
 
-// split_reduce (below) with exact high products: three lazy residues in [0, 2q), their sum below
-// 6q, one more Barrett step and one conditional subtraction.  More instructions, fewer registers.
+// split_reduce (below) with exact high products, for q < 2^61: three lazy residues in [0, 2q), their
+// sum below 6q < 2^64, one more Barrett step and one conditional subtraction.  More instructions,
+// fewer registers.
 __device__ __forceinline__ uint64_t split_reduce_exact(uint64_t ll, uint64_t mm, uint64_t hh, const SplitRed& k,
                                                        uint64_t q, uint64_t r1) {
   const uint64_t a = ll - mulhi(ll, r1) * q;
@@ -200,7 +201,7 @@ __device__ __forceinline__ uint64_t mul_shoup_lazy4(uint64_t a, uint64_t w, uint
   return a * w + mulhi_approx(a, ws) * opaque(0 - q);
 }
 
-// (ll + mm 2^30 + hh 2^60) mod q for q < 2^60, canonical (SplitRed above; r1 = floor(2^64 / q), the
+// (ll + mm 2^30 + hh 2^60) mod q for q < 2^60 (the lazy sum below 12q must fit 64 bits), canonical (SplitRed above; r1 = floor(2^64 / q), the
 // high word of the Barrett ratio).  Three lazy residues with the approximate quotient (mulhi_approx,
 // at most 2 low): a 64-bit Barrett step on ll and Shoup products for mm 2^30 and hh 2^60, each in
 // [0, 4q); their sum below 12q < 2^64; one more Barrett step to [0, 4q) and two carry-free

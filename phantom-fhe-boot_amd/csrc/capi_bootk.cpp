@@ -337,6 +337,7 @@ int phantom_fast_rotation_ext_batch_group(const phantom_context* ctx, size_t cha
       a.size_q = static_cast<uint32_t>(pc.size_Q());
       a.size_p = static_cast<uint32_t>(pc.size_P());
       a.beta = static_cast<uint32_t>(rt.beta());
+      a.q60 = phantom::below_2_60(pc.key_moduli());
     }
     const hipError_t err = phx::keyswitch_rotate_batch_group(ga, n, stream);
     PHX_CHECK(hipStreamSynchronize(stream));  // the entry table is freed on return

@@ -223,6 +223,9 @@ struct KsRotateBatchArgs {
   const uint64_t* pmod_shoup = nullptr;
   uint64_t* out = nullptr;                 // base of the outputs; must not alias digits / ct
   uint32_t ql = 0, qlp = 0, size_q = 0, size_p = 0, beta = 0;
+  // every key modulus is below 2^60 (set from the context): the grouped kernel may then reduce
+  // with approximate quotients (lazy sums below 12q); otherwise it takes the exact form
+  uint32_t q60 = 0;
 };
 hipError_t keyswitch_rotate_batch(const KsRotateBatchArgs& a, size_t n, hipStream_t s);
 // keyswitch_rotate_batch of `count` (2..kKsGroupMax) ciphertexts at one level through the same entries (keys)

@@ -803,7 +803,10 @@ __device__ __forceinline__ void ks_lt_barrier() {
 // dispatches apart (blocks b and b + 8 share an XCD under round-robin placement), so the followers
 // read the key halves from that XCD's L2.
 constexpr uint32_t kKsBatchFullMax = 64;  // entries of one ks_rotate_batch_full launch
-template <int BETA, bool GROUP>
+// FAST (GROUP launches over moduli below 2^60, KsRotateBatchArgs::q60): the approximate-quotient
+// reduction.  The grouped kernel reads its keys from L2 and is issue-bound, so fewer instructions
+// pay there; the single kernel is HBM-bound and keeps the exact form at 128 VGPRs (4 waves per SIMD).
+template <int BETA, bool GROUP, bool FAST = false>
 __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGroupArgs pa, uint32_t log_n) {
   constexpr uint32_t bsz = kGalB;
   constexpr int PP = kGalB / 2 / kBlock;  // pairs per thread
@@ -944,10 +947,8 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGrou
             hh[t][u] += static_cast<uint64_t>(dh[p][b][u]) * kh;
           }
       }
-      // GROUP (keys from L2, issue-bound): the approximate-quotient form, fewer instructions at
-      // 132 VGPRs; single (HBM-bound): the exact form at 128 VGPRs keeps 4 waves per SIMD
       auto red = [&](uint64_t x, uint64_t y, uint64_t z) {
-        return GROUP ? split_reduce(x, y, z, sr, q, r1) : split_reduce_exact(x, y, z, sr, q, r1);
+        return FAST ? split_reduce(x, y, z, sr, q, r1) : split_reduce_exact(x, y, z, sr, q, r1);
       };
       t0[2 * i] = add_mod(red(ll[0][0], mm[0][0], hh[0][0]), pc0[p].x, q);
       t0[2 * i + 1] = add_mod(red(ll[0][1], mm[0][1], hh[0][1]), pc0[p].y, q);
@@ -1574,12 +1575,19 @@ hipError_t keyswitch_rotate_batch_group(const KsRotateBatchGroupArgs& ga, size_t
   const uint32_t log_n = __builtin_ctzll(n);
   const uint32_t per = (a.qlp * static_cast<uint32_t>(n / kGalB) + 7) / 8 * 8;
   const dim3 grid(static_cast<uint32_t>(ga.count) * per);
+  bool fast = true;
+  for (int c = 0; c < ga.count; ++c) fast = fast && ga.a[c].q60 != 0;
+#define PHX_KSBF_GROUP(B)                                                              \
+  case B:                                                                              \
+    if (fast) ks_rotate_batch_full<B, true, true><<<grid, kBlock, 0, s>>>(ga, log_n);  \
+    else ks_rotate_batch_full<B, true, false><<<grid, kBlock, 0, s>>>(ga, log_n);      \
+    break;
   switch (a.beta) {
-    case 1: ks_rotate_batch_full<1, true><<<grid, kBlock, 0, s>>>(ga, log_n); break;
-    case 2: ks_rotate_batch_full<2, true><<<grid, kBlock, 0, s>>>(ga, log_n); break;
-    case 3: ks_rotate_batch_full<3, true><<<grid, kBlock, 0, s>>>(ga, log_n); break;
-    default: ks_rotate_batch_full<4, true><<<grid, kBlock, 0, s>>>(ga, log_n); break;
+    PHX_KSBF_GROUP(1) PHX_KSBF_GROUP(2) PHX_KSBF_GROUP(3)
+    default:
+    PHX_KSBF_GROUP(4)
   }
+#undef PHX_KSBF_GROUP
   return hipGetLastError();
 }
 

@@ -954,6 +954,7 @@ void FHECKKSRNS::level_babies(const PhantomContext& cc, const PhantomCiphertext&
   ba.size_q = static_cast<uint32_t>(cc.size_Q());
   ba.size_p = static_cast<uint32_t>(cc.size_P());
   ba.beta = static_cast<uint32_t>(rt.beta());
+  ba.q60 = below_2_60(cc.key_moduli());
   if (launch) {
     hip_ok(phx::keyswitch_rotate_batch(ba, n, s), "linear transform baby steps");
     w.digits.release();

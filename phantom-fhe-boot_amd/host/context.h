@@ -117,6 +117,13 @@ class LaneScope {
   }
 };
 
+// 1 when every modulus is below 2^60 (the grouped baby-step kernel's approximate reduction)
+inline uint32_t below_2_60(const std::vector<uint64_t>& moduli) {
+  for (uint64_t q : moduli)
+    if (q >> 60) return 0;
+  return 1;
+}
+
 class PhantomContext {
  public:
   // stream: where setup work and the façade's operations run; nullptr = a stream owned by the

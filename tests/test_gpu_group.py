@@ -123,6 +123,51 @@ def test_fast_rotation_ext_batch_group(c4, rng, chain, count, group):
             assert np.array_equal(got[k * W:(k + 1) * W], want), (c, k)
 
 
+@pytest.mark.parametrize("bits,chain,group", [(61, 1, 2), (61, 3, 4), (59, 1, 4), (59, 4, 2)])
+def test_fast_rotation_ext_batch_group_moduli_and_beta(rng, bits, chain, group):
+    """the grouped baby steps' two reductions at their partial-sum bounds: N = 4096, 8 + 2 moduli
+    of `bits` bits, so beta = 4 at chain 1 (all of Q).  61-bit moduli take the exact form (a lazy sum below
+    6q), moduli below 2^60 the approximate-quotient form (below 12q); both == or_fast_rotation_ext
+    / or_keyswitch_ext per ciphertext and rotation"""
+    n, size_p = 1 << 12, 2
+    mods = O.coeff_modulus_create(n, [bits] * 10)
+    ctx = PA.Context(n, mods, size_p)
+    ql = ctx.ql(chain)
+    em = ql + ctx.moduli[ctx.size_Q:]
+    W = 2 * len(em) * n
+    beta = -(-len(ql) // size_p)
+    dnum = -(-ctx.size_Q // size_p)
+    count = 5
+    cts = [np.concatenate([O.random_limbs(rng, n, ql) for _ in range(2)]) for _ in range(group)]
+    digits = [np.concatenate([O.random_limbs(rng, n, em) for _ in range(beta)]) for _ in range(group)]
+    elts = [pow(5, 3 * k + 1, 2 * n) for k in range(count)]
+    elts[-1] = 2 * n - 1
+    keys = [[np.concatenate([O.random_limbs(rng, n, ctx.moduli) for _ in range(2)]) for _ in range(dnum)]
+            for _ in range(2)]
+    dkeys = [[to_dev(x) for x in ks] for ks in keys]
+    dcts, ddig = [to_dev(x) for x in cts], [to_dev(x) for x in digits]
+    douts = [to_dev(np.full(count * W, 5, dtype=np.uint64)) for _ in range(group)]
+    key_arrays = [None if k == 0 else _vp(ptr(x) for x in dkeys[k % 2]) for k in range(count)]
+    kk = (ctypes.POINTER(ctypes.c_void_p) * count)(*[ctypes.cast(a, ctypes.POINTER(ctypes.c_void_p)) if a is not None
+                                                     else None for a in key_arrays])
+    el = (ctypes.c_uint32 * count)(*elts)
+    outs = [ptr(douts[c]) + 8 * k * W for c in range(group) for k in range(count)]
+    PA.check(_lib().phantom_fast_rotation_ext_batch_group(ctx.handle, chain, group, _vp(ptr(x) for x in dcts),
+                                                          _vp(ptr(x) for x in ddig), kk, dnum, el, count, _vp(outs),
+                                                          stream()))
+    pm = O.P(O.arr(ctx.moduli))
+    for c in range(group):
+        got = to_host(douts[c])
+        for k in range(count):
+            want = np.zeros(W, dtype=np.uint64)
+            if k == 0:
+                O.lib().or_keyswitch_ext(O.P(cts[c]), O.P(want), n, len(ql), ctx.size_Q, ctx.size_P, pm)
+            else:
+                O.lib().or_fast_rotation_ext(O.P(cts[c]), O.P(digits[c]), O.ptrs(keys[k % 2]), elts[k], 1, O.P(want),
+                                             n, len(ql), ctx.size_Q, ctx.size_P, pm)
+            assert np.array_equal(got[k * W:(k + 1) * W], want), (bits, c, k)
+
+
 def test_fast_rotation_ext_batch_group_rejects_ragged_offsets(c4, rng):
     """every ciphertext's outputs must sit at the entry offsets of ciphertext 0"""
     chain, count, group = 17, 2, 2
