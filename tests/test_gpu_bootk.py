@@ -104,12 +104,16 @@ def test_fast_rotation_ext(c4, rng, chain, elt_kind, add_first):
 
 
 @pytest.mark.parametrize("shape,chain,count,identity_at", [("c4", 1, 9, 4), ("c4", 3, 4, None), ("c4", 17, 32, 16),
-                                                             ("n512", 1, 7, 2)])
+                                                             ("n512", 1, 7, 2), ("q61", 1, 5, 0)])
 def test_fast_rotation_ext_batch(c4, rng, shape, chain, count, identity_at):
     """one launch of `count` baby steps == the per-rotation EvalFastRotationExt / KeySwitchExt
-    (c4: full 1024-index blocks, beta 3 / 2; n512: the any-size kernel, beta 4)"""
+    (c4: full 1024-index blocks, beta 3 / 2; n512: the any-size kernel, beta 4; q61: the full
+    kernel at N = 4096 with 61-bit moduli and beta 4, the split partial sums' bounds)"""
     if shape == "c4":
         ctx, n, size_p = c4, N, SIZE_P
+    elif shape == "q61":
+        n, size_p = 1 << 12, 2
+        ctx = PA.Context(n, O.coeff_modulus_create(n, [61] * 10), size_p)
     else:
         n, size_p = 512, 2
         ctx = PA.Context(n, O.coeff_modulus_create(n, [50] * 10), size_p)
