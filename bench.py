@@ -380,6 +380,8 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=3, chain=26, 
     elapsed = time.perf_counter() - t0
     max_s = max_over_ranks(dist, [elapsed], "cuda")[0]
     pool = PA.pool_stats()  # the engine's device allocator on this rank (batch buffers are torch's)
+    # every rank's wall time and pool figures, so a multi-rank line shows any imbalance
+    ranks = shard.gather_stats(dist, [elapsed, pool["held"] / 2**30, pool["peak_live"] / 2**30], dev)
     res = None
     if rank == 0:
         nver = total if verify is None else min(verify, total)
@@ -403,6 +405,11 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=3, chain=26, 
             "keys": "regenerated on every rank from a broadcast 32-byte seed",
             "rank0_pool_GiB": {"held": round(pool["held"] / 2**30, 2), "peak_held": round(pool["peak_held"] / 2**30, 2),
                                "peak_live": round(pool["peak_live"] / 2**30, 2)},
+            "per_rank": {"wall_s": [round(r[0], 3) for r in ranks],
+                         "min_wall_s": round(min(r[0] for r in ranks), 3),
+                         "max_wall_s": round(max(r[0] for r in ranks), 3),
+                         "pool_held_GiB": [round(r[1], 2) for r in ranks],
+                         "pool_peak_live_GiB": [round(r[2], 2) for r in ranks]},
         }
         # roofline per GPU: the reference schedule's key and diagonal bytes (c4_reference_bytes) read
         # once per lockstep group (the grouped kernels share them through each XCD's L2), plus each

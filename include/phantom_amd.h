@@ -255,15 +255,6 @@ int phantom_rotate_ext_accumulate_group(const phantom_context *ctx, size_t chain
                                         uint64_t *const *ext, const uint64_t *const *key_digits, size_t dnum,
                                         uint32_t galois_elt, uint64_t *const *acc, int accumulate,
                                         hipStream_t stream);
-/* one linear-transform level's baby steps and inner sums in ONE kernel, the babies never written
- * (round 5): for ciphertext c < group (1..8), outs[c * b + i] [2][Ql+P][n] = sum_{j<32} baby_j(c) *
- * pts[i 32 + j] for i < b <= 8, where baby_j(c) is phantom_fast_rotation_ext_batch's output k = j for
- * cts[c] / digits[c] (key_digits[j] NULL: the identity) - equal bit for bit to that call followed by
- * phantom_lt_bsgs.  The ciphertexts share the keys and plaintexts (read from HBM about once). */
-int phantom_lt_level_fused(const phantom_context *ctx, size_t chain_index, size_t group, const uint64_t *const *cts,
-                           const uint64_t *const *digits, const uint64_t *const *const *key_digits, size_t dnum,
-                           const uint32_t *galois_elts, const uint64_t *const *pts, size_t b, uint64_t *const *outs,
-                           hipStream_t stream);
 /* the EvalMod products' tensors in ONE launch (count <= 8 jobs at one level, L = Ql limbs each):
  * out[k] [3][L][n] = factors[k] (ct1[k] x ct2[k]), then out[k][p] += c[k] t[k][p] for p < 2 when t[k]
  * (t[k][p] at t[k] + p t_stride; c[k] host residues per limb), then out[k][0] += consts[k] when

@@ -63,6 +63,7 @@ int phantom_lt_bsgs(const phantom_context* ctx, size_t chain_index, const uint64
     a.size_Q = static_cast<int>(pc.size_Q());
     a.q = pc.mod_QP().q;
     a.barrett = pc.mod_QP().barrett;
+    a.q60 = phantom::below_2_60(pc.key_moduli());
     for (size_t j = 0; j < g; ++j) a.baby[j] = babies[j];
     for (size_t i = 0; i < b; ++i) a.out[i] = outs[i];
     phantom::DeviceBuffer<const uint64_t*> table;
@@ -71,65 +72,6 @@ int phantom_lt_bsgs(const phantom_context* ctx, size_t chain_index, const uint64
     const hipError_t e = phx::lt_bsgs(a, pc.poly_degree(), stream);
     PHX_CHECK(hipStreamSynchronize(stream));  // the pointer table is freed on return
     return from_hip(e);
-  });
-}
-
-int phantom_lt_level_fused(const phantom_context* ctx, size_t chain_index, size_t group, const uint64_t* const* cts,
-                           const uint64_t* const* digits, const uint64_t* const* const* key_digits, size_t dnum,
-                           const uint32_t* galois_elts, const uint64_t* const* pts, size_t b, uint64_t* const* outs,
-                           hipStream_t stream) {
-  PHX_CAPI_GUARD({
-    constexpr size_t g = 32;
-    if (!cts || !digits || !key_digits || !galois_elts || !pts || !outs)
-      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
-    if (group < 1 || group > static_cast<size_t>(phx::kKsGroupMax))
-      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "group must hold 1 to 8 ciphertexts");
-    if (b < 1 || b > static_cast<size_t>(phx::kKsLtMaxB)) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "giant steps must be 1..8");
-    const auto& pc = phantom_capi_context(ctx);
-    const auto& rt = tool_at(pc, chain_index);
-    const size_t n = pc.poly_degree(), Ql = rt.size_Ql(), QlP = Ql + pc.size_P();
-    if (rt.beta() > 4 || n < 1024) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "the fused level needs beta <= 4, n >= 1024");
-    std::vector<phx::KsBatchEntry> e(g);
-    for (size_t k = 0; k < g; ++k) {
-      if (key_digits[k]) {
-        e[k].evk = phantom_capi_key_array(ctx, key_digits[k], dnum, rt.beta());
-        e[k].perm = pc.galois_perm(galois_elts[k]);
-        e[k].binv = pc.galois_block_inv(galois_elts[k]);
-      }
-    }
-    phantom::DeviceBuffer<phx::KsBatchEntry> table;
-    table.upload(e, stream);
-    phantom::DeviceBuffer<const uint64_t*> ptab;
-    ptab.upload(std::vector<const uint64_t*>(pts, pts + g * b), stream);
-    phx::KsLtGroupArgs ga;
-    ga.count = static_cast<int>(group);
-    for (size_t c = 0; c < group; ++c) {
-      if (!cts[c] || !digits[c]) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null ciphertext");
-      phx::KsLtArgs& A = ga.a[c];
-      phx::KsRotateBatchArgs& a = A.ks;
-      a.digits = digits[c];
-      a.entries = table.get();
-      a.count = static_cast<uint32_t>(g);
-      a.qp = pc.mod_QP().q;
-      a.qp_barrett = pc.mod_QP().barrett;
-      a.ct = cts[c];
-      a.pmod = rt.bigP_mod_q();
-      a.pmod_shoup = rt.bigP_mod_q_shoup();
-      a.ql = static_cast<uint32_t>(Ql);
-      a.qlp = static_cast<uint32_t>(QlP);
-      a.size_q = static_cast<uint32_t>(pc.size_Q());
-      a.size_p = static_cast<uint32_t>(pc.size_P());
-      a.beta = static_cast<uint32_t>(rt.beta());
-      A.pts = ptab.get();
-      A.b = static_cast<int>(b);
-      for (size_t i = 0; i < b; ++i) {
-        if (!outs[c * b + i]) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null output");
-        A.out[i] = outs[c * b + i];
-      }
-    }
-    const hipError_t err = phx::ks_lt_fused(ga, n, stream);
-    PHX_CHECK(hipStreamSynchronize(stream));  // the entry and pointer tables are freed on return
-    return from_hip(err);
   });
 }
 
@@ -267,6 +209,7 @@ int phantom_lt_bsgs_group(const phantom_context* ctx, size_t chain_index, size_t
     a.size_Q = static_cast<int>(pc.size_Q());
     a.q = pc.mod_QP().q;
     a.barrett = pc.mod_QP().barrett;
+    a.q60 = phantom::below_2_60(pc.key_moduli());
     a.count = static_cast<int>(group);
     a.baby_stride = baby_stride;
     a.giant_stride = giant_stride;

@@ -51,6 +51,10 @@ struct LtArgs {
   const uint64_t* q;           // full QP chain
   const uint64_t* barrett;     // [QP][2]
   int g = 0, b = 0, Ql = 0, P = 0, size_Q = 0;
+  // every modulus of the chain below 2^60 (phantom::below_2_60): the 30-bit split partial sums
+  // may then take 8 (tile kernels) or 16 (lt_bsgs_kernel) products before folding; otherwise a
+  // high-half product reaches 2^62 and the sums fold every 4 products (0 is always safe)
+  uint32_t q60 = 0;
 };
 hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s);
 // lt_bsgs of `count` (2..kLtGroupMax) ciphertexts at one level through the same plaintexts
@@ -65,6 +69,7 @@ struct LtGroupArgs {
   const uint64_t* q = nullptr;
   const uint64_t* barrett = nullptr;
   int g = 0, b = 0, Ql = 0, P = 0, size_Q = 0, count = 0;
+  uint32_t q60 = 0;  // as LtArgs::q60
   uint64_t baby_stride = 0, giant_stride = 0;
   const uint64_t* baby0[kLtGroupMax] = {};
   uint64_t* acc[kLtGroupMax] = {};

@@ -104,12 +104,14 @@ __global__ __launch_bounds__(kBlock) void mul_scalar_add_kernel(const uint64_t* 
 // One element (limb l, coefficient k) per thread and grid-stride step.  Babies are split into
 // 30-bit halves once; each giant step issues all G plaintext loads together (the pointer row
 // is one scalar block: no branches between the loads) and accumulates the 4 partial products
-// of every term in 64-bit sums — each is a sum of <= 16 products of 30-bit values, < 2^64 —
-// folded to 128 bits every 16 terms and Barrett-reduced once per output.
-template <int G>
+// of every term in 64-bit sums, folded to 128 bits every kChunk terms and Barrett-reduced once
+// per output.  Inputs below q < 2^60 split into halves below 2^30, so 16 products stay below
+// 2^64; with a 61-bit modulus the high halves reach 2^31 (products up to 2^62) and only 4 fit
+// (Q60 = LtArgs::q60).
+template <int G, bool Q60>
 __global__ __launch_bounds__(kBlock, 2) void lt_bsgs_kernel(LtArgs a, uint32_t log_n, size_t total) {
   constexpr uint64_t kM30 = (1ull << 30) - 1;
-  constexpr int kChunk = 16;
+  constexpr int kChunk = Q60 ? 16 : 4;
   // the [b][g] plaintext pointer table, staged in LDS once per workgroup (a global read of it
   // per giant step would add a memory round trip before the plaintext loads can issue)
   extern __shared__ const uint64_t* ptab[];
@@ -247,8 +249,9 @@ struct LtPart {
   uint64_t ll, m1, m2, hh;
 };
 
-// part += sum_j baby(4c + j) * w[j], the babies from LDS (< 2^60 each partial product, at most 8
-// chunks... folded every 2 chunks: <= 8 products per partial sum, < 2^63).  The memory clobbers
+// part += sum_j baby(4c + j) * w[j], the babies from LDS.  Folded every 2 chunks (8 products per
+// partial sum) when every modulus is below 2^60 (each product < 2^60, the sum < 2^63), every chunk
+// otherwise (61-bit moduli: a high-half product < 2^62, 4 of them < 2^64).  The memory clobbers
 // (IR) and scheduling barriers (machine code) keep this chunk's LDS reads and products inside it,
 // and binding the partial sums to the closing asm stops the products being deferred: hoisted to
 // the top of the kernel the LDS reads alone cost 128 VGPRs.
@@ -309,7 +312,7 @@ __device__ __forceinline__ void lt_fold(u128 (&acc)[E][2], LtPart (&part)[E][2])
     }
 }
 
-template <int E, class Src>
+template <int E, bool Q60, class Src>
 __device__ __forceinline__ void lt_bsgs_tile(const Src& src, int nb, int Ql, int size_Q, const uint64_t* qv,
                                              const uint64_t* barrett, uint32_t log_n, size_t total, size_t tile,
                                              const uint64_t* const* pts) {
@@ -363,7 +366,7 @@ __device__ __forceinline__ void lt_bsgs_tile(const Src& src, int nb, int Ql, int
   for (int c = 0; c < NC; ++c) {
     if (c + D - 1 < NC) lt_load_chunk<E>(wbuf[(c + D - 1) % D], prow, c + D - 1, e);
     lt_chunk_products<E>(part, wbuf[c % D], xs, c, lane);
-    if (c & 1) lt_fold<E>(acc, part);  // 8 products per partial sum
+    if ((c & 1) || !Q60) lt_fold<E>(acc, part);  // 8 (q < 2^60) or 4 products per partial sum
   }
   const int l = static_cast<int>((tile * T) >> log_n);
   const int row = l < Ql ? l : size_Q + (l - Ql);
@@ -380,22 +383,22 @@ __device__ __forceinline__ void lt_bsgs_tile(const Src& src, int nb, int Ql, int
   }
 }
 
-template <int E>
+template <int E, bool Q60>
 __global__ __launch_bounds__(64 * kLtWaves) void lt_bsgs_tile_kernel(LtArgs a, uint32_t log_n, size_t total) {
-  lt_bsgs_tile<E>(LtSingleSrc{a}, a.b, a.Ql, a.size_Q, a.q, a.barrett, log_n, total, blockIdx.x, a.pts);
+  lt_bsgs_tile<E, Q60>(LtSingleSrc{a}, a.b, a.Ql, a.size_Q, a.q, a.barrett, log_n, total, blockIdx.x, a.pts);
 }
 
 // `count` ciphertexts through the same plaintexts (lt_bsgs_group): the workgroups of the
 // ciphertexts that cover the same tile are dealt to one XCD 8 dispatches apart (workgroups w and
 // w + 8 share an XCD under round-robin placement), so the followers' plaintext reads are served by
 // that XCD's L2
-template <int E>
+template <int E, bool Q60>
 __global__ __launch_bounds__(64 * kLtWaves) void lt_bsgs_group_kernel(LtGroupArgs ga, uint32_t log_n, size_t total) {
   const uint32_t K = static_cast<uint32_t>(ga.count);
   const uint32_t b = blockIdx.x, x = b % 8, k = b / 8;
   const uint32_t c = k % K, tile = (k / K) * 8 + x;
   if (static_cast<size_t>(tile) * 64 * E >= total) return;  // the grid rounds the tiles up to whole XCD rounds
-  lt_bsgs_tile<E>(LtGroupSrc{ga, static_cast<int>(c)}, ga.b, ga.Ql, ga.size_Q, ga.q, ga.barrett, log_n, total, tile,
+  lt_bsgs_tile<E, Q60>(LtGroupSrc{ga, static_cast<int>(c)}, ga.b, ga.Ql, ga.size_Q, ga.q, ga.barrett, log_n, total, tile,
                   ga.pts);
 }
 
@@ -647,19 +650,29 @@ hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s) {
   const uint32_t log_n = __builtin_ctzll(n);
   const int grid = grid_for(total);
   const size_t lds = static_cast<size_t>(a.b) * a.g * sizeof(const uint64_t*);
-  switch (a.g) {
-    case 1: lt_bsgs_kernel<1><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
-    case 2: lt_bsgs_kernel<2><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
-    case 4: lt_bsgs_kernel<4><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
-    case 8: lt_bsgs_kernel<8><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
-    case 16: lt_bsgs_kernel<16><<<grid, kBlock, lds, s>>>(a, log_n, total); break;
-    case 32:
-      if (a.b <= kLtWaves && n >= 64 * kLtEpl)
-        lt_bsgs_tile_kernel<kLtEpl><<<static_cast<unsigned>(total / (64 * kLtEpl)), 64 * kLtWaves, 0, s>>>(a, log_n, total);
-      else lt_bsgs_kernel<32><<<grid, kBlock, lds, s>>>(a, log_n, total);
-      break;
-    default: return hipErrorInvalidValue;
+  const bool tile = a.g == 32 && a.b <= kLtWaves && n >= 64 * kLtEpl;
+#define PHX_LT_CASES(Q)                                                                                         \
+  switch (a.g) {                                                                                                \
+    case 1: lt_bsgs_kernel<1, Q><<<grid, kBlock, lds, s>>>(a, log_n, total); break;                            \
+    case 2: lt_bsgs_kernel<2, Q><<<grid, kBlock, lds, s>>>(a, log_n, total); break;                            \
+    case 4: lt_bsgs_kernel<4, Q><<<grid, kBlock, lds, s>>>(a, log_n, total); break;                            \
+    case 8: lt_bsgs_kernel<8, Q><<<grid, kBlock, lds, s>>>(a, log_n, total); break;                            \
+    case 16: lt_bsgs_kernel<16, Q><<<grid, kBlock, lds, s>>>(a, log_n, total); break;                          \
+    case 32:                                                                                                    \
+      if (tile)                                                                                                 \
+        lt_bsgs_tile_kernel<kLtEpl, Q>                                                                          \
+            <<<static_cast<unsigned>(total / (64 * kLtEpl)), 64 * kLtWaves, 0, s>>>(a, log_n, total);           \
+      else                                                                                                      \
+        lt_bsgs_kernel<32, Q><<<grid, kBlock, lds, s>>>(a, log_n, total);                                       \
+      break;                                                                                                    \
+    default: return hipErrorInvalidValue;                                                                       \
   }
+  if (a.q60) {
+    PHX_LT_CASES(true)
+  } else {
+    PHX_LT_CASES(false)
+  }
+#undef PHX_LT_CASES
   return hipGetLastError();
 }
 
@@ -671,8 +684,11 @@ hipError_t lt_bsgs_group(const LtGroupArgs& ga, size_t n, hipStream_t s) {
   if (n < 64 * kLtEpl) return hipErrorInvalidValue;
   const size_t total = n * static_cast<size_t>(ga.Ql + ga.P);
   const size_t per = (total / (64 * kLtEpl) + 7) / 8 * 8;  // workgroups per ciphertext, whole XCD rounds
-  lt_bsgs_group_kernel<kLtEpl>
-      <<<static_cast<unsigned>(ga.count * per), 64 * kLtWaves, 0, s>>>(ga, __builtin_ctzll(n), total);
+  const unsigned grid = static_cast<unsigned>(ga.count * per);
+  if (ga.q60)
+    lt_bsgs_group_kernel<kLtEpl, true><<<grid, 64 * kLtWaves, 0, s>>>(ga, __builtin_ctzll(n), total);
+  else
+    lt_bsgs_group_kernel<kLtEpl, false><<<grid, 64 * kLtWaves, 0, s>>>(ga, __builtin_ctzll(n), total);
   return hipGetLastError();
 }
 

@@ -238,26 +238,6 @@ struct KsRotateBatchGroupArgs {
 };
 hipError_t keyswitch_rotate_batch_group(const KsRotateBatchGroupArgs& ga, size_t n, hipStream_t s);
 
-// One linear-transform level's baby steps and inner sums in one kernel (round 5): baby j is entry
-// j of `ks` (keyswitch_rotate_batch, ks.count = 32 entries; ks.out unused), formed in LDS per tile
-// and never written to HBM; inner sum i = sum_j baby_j pts[i 32 + j] goes to out[i] ([2][QlP][n]),
-// i < b <= 8.  Each inner sum equals keyswitch_rotate_batch followed by lt_bsgs, bit for bit (the
-// same products, an exact 128-bit sum, one Barrett reduction).  `count` (1..kKsGroupMax) ciphertexts
-// at one level through the same entries and plaintexts: their workgroups of a (limb, tile) run 8
-// dispatches apart on one XCD, so keys and plaintexts are read from HBM about once for all.
-constexpr int kKsLtMaxB = 8;
-struct KsLtArgs {
-  KsRotateBatchArgs ks;
-  const uint64_t* const* pts = nullptr;  // device [b][32]
-  uint64_t* out[kKsLtMaxB] = {};
-  int b = 0;
-};
-struct KsLtGroupArgs {
-  KsLtArgs a[kKsGroupMax];
-  int count = 1;
-};
-hipError_t ks_lt_fused(const KsLtGroupArgs& ga, size_t n, hipStream_t s);
-
 struct GaloisFinishArgs {
   const uint64_t* cx;
   const uint64_t* c0;

@@ -970,203 +970,6 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGrou
   }
 }
 
-// ks_lt_fused (rns.h): workgroup = 8 waves over one tile of T = 256 output indices of one limb.
-// Per baby j: waves 0-3 form polynomial 0 of the key-switch product for the tile's source range
-// (the NTT-domain automorphism maps every aligned 256-index range onto one aligned 256-index
-// range, as the 1,024-index blocks of keyswitch_rotate_batch: perm[e] & ~255 is the same for the
-// tile) and waves 4-7 polynomial 1, into LDS; after one barrier every wave gathers both permuted
-// baby values of its 64 indices and accumulates them into 4 of the 8 giant steps' 128-bit sums
-// (waves 0-3: giant steps 0-3, waves 4-7: 4-7), each product of < 2^120 and 32 of them < 2^125.
-// The next baby's key-switch inputs and permutation, and the plaintexts, are loaded one baby
-// ahead; the barrier is a raw s_barrier after lgkmcnt(0), so those loads stay in flight over it.
-constexpr int kKsLtTile = 256, kKsLtWaves = 8, kKsLtG = 32;
-
-template <int BETA, bool GROUP>
-__global__ __launch_bounds__(kKsLtWaves * 64) void ks_lt_kernel(KsLtGroupArgs ga, uint32_t log_n) {
-  constexpr int T = kKsLtTile, G = kKsLtG;
-  using GPtr = const __attribute__((address_space(1))) uint64_t*;
-  using CPtr = const __attribute__((address_space(4))) uint64_t*;
-  __shared__ uint2 buf[2][2][T];              // [baby & 1][polynomial][source index - base]: {low 30, high 30 bits}
-  __shared__ const uint64_t* kptr[G][BETA];   // the key-switched babies' key digits, compacted
-  __shared__ const uint32_t* pptr[G];         // ... and permutations
-  __shared__ int bidx[G];                     // ... and baby indices (plaintext column)
-  __shared__ int ident, nks;                  // the identity baby's index (-1 if none), the key-switched count
-  const uint32_t n = 1u << log_n, tiles = n >> 8;
-  uint32_t bid = blockIdx.x;
-  int c = 0;
-  if constexpr (GROUP) {
-    const uint32_t K = static_cast<uint32_t>(ga.count), xcd = bid % 8, k = bid / 8;
-    c = static_cast<int>(k % K);
-    bid = (k / K) * 8 + xcd;
-  }
-  const KsLtArgs& A = ga.a[c];
-  const KsRotateBatchArgs& a = A.ks;
-  if (GROUP && bid >= a.qlp * tiles) return;  // the rounding of the group grid (workgroup-uniform)
-  const uint32_t l = bid / tiles, tile = bid % tiles;
-  if (threadIdx.x < 64) {  // wave 0 compacts the entries: key-switched babies first, in order
-    const bool live = threadIdx.x < G;
-    const KsBatchEntry en = a.entries[live ? threadIdx.x : 0];
-    const bool ks = live && en.evk != nullptr;
-    const uint64_t m = __ballot(ks);
-    const int pos = __popcll(m & ((1ull << threadIdx.x) - 1));
-    if (ks) {
-      pptr[pos] = en.perm;
-      bidx[pos] = static_cast<int>(threadIdx.x);
-#pragma unroll
-      for (int b = 0; b < BETA; ++b) kptr[pos][b] = en.evk[b];
-    }
-    const uint64_t idm = __ballot(live && en.evk == nullptr);
-    if (threadIdx.x == 0) {
-      ident = idm ? __ffsll(static_cast<long long>(idm)) - 1 : -1;
-      nks = __popcll(m);
-    }
-  }
-  __syncthreads();
-  const int nk = __builtin_amdgcn_readfirstlane(nks), id = __builtin_amdgcn_readfirstlane(ident);
-  const uint32_t lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t h = w >> 2, x = (w & 3) * 64 + lane;  // h: this wave's polynomial (key switch) and half of the giant steps
-  const uint32_t twr = l >= a.ql ? a.size_q + (l - a.ql) : l;
-  const uint64_t q = a.qp[twr], r0 = a.qp_barrett[2 * twr], r1 = a.qp_barrett[2 * twr + 1];
-  const bool inq = l < a.ql;
-  const uint64_t pw = inq ? a.pmod[l] : 0, pws = inq ? a.pmod_shoup[l] : 0;
-  const uint64_t pc = h == 0 ? pw : 0, pcs = h == 0 ? pws : 0;  // P c0 joins polynomial 0 only
-  const size_t qlp_n = (size_t)a.qlp << log_n, qp_n = (size_t)(a.size_q + a.size_p) << log_n;
-  const size_t lbase = (size_t)l << log_n, kbase = (size_t)twr << log_n;
-  const size_t cbase = (size_t)(inq ? l : 0) << log_n;  // c0 / c1 rows (a P limb reads row 0, times 0)
-  const uint32_t el = tile * T + x;  // this thread's output index within the limb
-  const int nb = A.b;
-  const __attribute__((address_space(4))) CPtr* ptab = (const __attribute__((address_space(4))) CPtr*)A.pts;
-  // plaintext of giant step 4h + ii (clamped to the last: its products are computed, not stored) for baby j
-  auto pt = [&](int ii, int j) {
-    const int i = min(static_cast<int>(4 * h) + ii, nb - 1);
-    return ((GPtr)(ptab[i * G + j] + lbase))[el];
-  };
-  u128 acc[4][2];
-  {  // the identity baby, P (c0, c1) on the Ql limbs, unpermuted (a zero factor when there is none)
-    const int j = id >= 0 ? id : 0;
-    const uint64_t f = id >= 0 ? pw : 0, fs = id >= 0 ? pws : 0;
-    uint64_t bv[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) bv[t] = mul_shoup(((GPtr)a.ct)[(size_t)t * a.ql * n + cbase + el], f, fs, q);
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const uint64_t wv = pt(ii, j);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) acc[ii][t] = mul_wide(bv[t], wv);
-    }
-  }
-  // ---- the key-switched babies, their inputs one baby ahead
-  if (nk == 0) {
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const int i = static_cast<int>(4 * h) + ii;
-      if (i >= nb) break;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) A.out[i][(size_t)t * qlp_n + lbase + el] = barrett_reduce_128(acc[ii][t], q, r0, r1);
-    }
-    return;
-  }
-  // one baby's inputs: its key-switch operands at this thread's source index, its plaintexts, and
-  // its permutation at this thread's output index.  Two sets alternate (a 2x unrolled loop), so no
-  // register holding a load in flight is ever copied (a copy would wait for the load).
-  struct St {
-    uint64_t dg[BETA], kv[BETA], c0, w[4];
-    uint32_t p;
-  };
-  // every load below is a wave-uniform base (made scalar) plus a 32-bit lane index, so it issues as
-  // global_load saddr + voffset with no 64-bit address arithmetic per lane
-  auto load_perm = [&](int k) {
-    return ((const __attribute__((address_space(1))) uint32_t*)uniform_ptr(pptr[k]))[el];
-  };
-  GPtr dig[BETA];
-#pragma unroll
-  for (int b = 0; b < BETA; ++b) dig[b] = (GPtr)(a.digits + b * qlp_n + lbase);
-  const GPtr c0row = (GPtr)(a.ct + cbase);
-  auto issue = [&](St& S, int k, uint32_t perm) {
-    S.p = perm;
-    const uint32_t src = (perm & ~uint32_t(T - 1)) + x;  // this thread's source index
-#pragma unroll
-    for (int b = 0; b < BETA; ++b) {
-      S.dg[b] = dig[b][src];
-      S.kv[b] = ((GPtr)(uniform_ptr(kptr[k][b]) + h * qp_n + kbase))[src];
-    }
-    S.c0 = c0row[src];
-    const int j = __builtin_amdgcn_readfirstlane(bidx[k]);
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii) S.w[ii] = pt(ii, j);
-  };
-  // the products with this wave's 4 plaintexts in 30-bit halves (x = xh 2^30 + xl, w likewise):
-  // per product ll += xl wl, mm += xl wh + xh wl, hh += xh wh, each partial sum of at most 2 babies'
-  // products below 2^62, folded into the 128-bit sums after every second baby
-  constexpr uint64_t kM30 = (1ull << 30) - 1;
-  uint64_t ll[4][2], mm[4][2], hh[4][2];
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-    for (int t = 0; t < 2; ++t) ll[ii][t] = mm[ii][t] = hh[ii][t] = 0;
-  auto fold = [&] {
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        add128(acc[ii][t], u128{ll[ii][t], 0});
-        add128(acc[ii][t], u128{mm[ii][t] << 30, mm[ii][t] >> 34});
-        add128(acc[ii][t], u128{hh[ii][t] << 60, hh[ii][t] >> 4});
-        ll[ii][t] = mm[ii][t] = hh[ii][t] = 0;
-      }
-  };
-  // baby k (inputs in S): its key-switch product of polynomial h into LDS, baby k + 1's inputs into
-  // N (pn: perm of k + 1, loaded a step ago; refreshed with perm of k + 2), one barrier, then the
-  // gather of both polynomials' baby values and their products with this wave's 4 plaintexts
-  auto step = [&](int k, St& S, St& N, uint32_t& pn) {
-    {
-      u128 v{0, 0};
-#pragma unroll
-      for (int b = 0; b < BETA; ++b) add128(v, mul_wide(S.dg[b], S.kv[b]));
-      const uint64_t y = add_mod(barrett_reduce_128(v, q, r0, r1), mul_shoup(S.c0, pc, pcs, q), q);
-      buf[k & 1][h][x] = make_uint2(static_cast<uint32_t>(y & kM30), static_cast<uint32_t>(y >> 30));
-    }
-    issue(N, min(k + 1, nk - 1), pn);
-    pn = load_perm(min(k + 2, nk - 1));
-    ks_lt_barrier();
-    uint2 bv[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) bv[t] = buf[k & 1][t][S.p & (T - 1)];
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const uint32_t wl = static_cast<uint32_t>(S.w[ii] & kM30), wh = static_cast<uint32_t>(S.w[ii] >> 30);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        ll[ii][t] += static_cast<uint64_t>(bv[t].x) * wl;
-        mm[ii][t] += static_cast<uint64_t>(bv[t].x) * wh;
-        mm[ii][t] += static_cast<uint64_t>(bv[t].y) * wl;
-        hh[ii][t] += static_cast<uint64_t>(bv[t].y) * wh;
-      }
-    }
-  };
-  St sa, sb;
-  uint32_t pn = load_perm(min(1, nk - 1));
-  issue(sa, 0, load_perm(0));
-  int k = 0;
-  for (; k + 1 < nk; k += 2) {
-    step(k, sa, sb, pn);
-    step(k + 1, sb, sa, pn);
-    fold();
-  }
-  if (k < nk) {
-    step(k, sa, sb, pn);
-    fold();
-  }
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii) {
-    const int i = static_cast<int>(4 * h) + ii;
-    if (i >= nb) break;
-    uint64_t* o = A.out[i];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) o[(size_t)t * qlp_n + lbase + el] = barrett_reduce_128(acc[ii][t], q, r0, r1);
-  }
-}
-
 // any block size / beta: per entry, the digits and c0 re-read (L1 / L2 hits after the first)
 __global__ __launch_bounds__(kBlock) void ks_rotate_batch_kernel(KsRotateBatchArgs a, uint32_t log_n, uint32_t bsz) {
   __shared__ uint64_t s0[2][kGalB], s1[2][kGalB];
@@ -1588,37 +1391,6 @@ hipError_t keyswitch_rotate_batch_group(const KsRotateBatchGroupArgs& ga, size_t
     PHX_KSBF_GROUP(4)
   }
 #undef PHX_KSBF_GROUP
-  return hipGetLastError();
-}
-
-hipError_t ks_lt_fused(const KsLtGroupArgs& ga, size_t n, hipStream_t s) {
-  if (ga.count < 1 || ga.count > kKsGroupMax || n < kGalB || n % kKsLtTile) return hipErrorInvalidValue;
-  const KsRotateBatchArgs& a = ga.a[0].ks;
-  for (int c = 0; c < ga.count; ++c) {
-    const KsLtArgs& A = ga.a[c];
-    const KsRotateBatchArgs& x = A.ks;
-    if (!x.digits || !x.entries || !x.ct || !x.pmod || !x.pmod_shoup || !x.qp || !x.qp_barrett || x.beta < 1 ||
-        x.beta > 4 || x.ql > x.qlp || x.count != static_cast<uint32_t>(kKsLtG) || !A.pts || A.b < 1 ||
-        A.b > kKsLtMaxB)
-      return hipErrorInvalidValue;
-    if (x.entries != a.entries || x.qlp != a.qlp || x.ql != a.ql || x.beta != a.beta || x.size_q != a.size_q ||
-        x.size_p != a.size_p || A.pts != ga.a[0].pts || A.b != ga.a[0].b)
-      return hipErrorInvalidValue;
-    for (int i = 0; i < A.b; ++i)
-      if (!A.out[i]) return hipErrorInvalidValue;
-  }
-  if (a.qlp == 0) return hipSuccess;
-  const uint32_t log_n = __builtin_ctzll(n), tiles = static_cast<uint32_t>(n / kKsLtTile);
-  const bool group = ga.count > 1;
-  const uint32_t per = group ? (a.qlp * tiles + 7) / 8 * 8 : a.qlp * tiles;
-  const dim3 grid(static_cast<uint32_t>(ga.count) * per), block(kKsLtWaves * 64);
-#define PHX_KSLT(B)                                                       \
-  case B:                                                                 \
-    if (group) ks_lt_kernel<B, true><<<grid, block, 0, s>>>(ga, log_n);   \
-    else ks_lt_kernel<B, false><<<grid, block, 0, s>>>(ga, log_n);        \
-    break;
-  switch (a.beta) { PHX_KSLT(1) PHX_KSLT(2) PHX_KSLT(3) PHX_KSLT(4) }
-#undef PHX_KSLT
   return hipGetLastError();
 }
 

@@ -476,6 +476,7 @@ int main(int argc, char** argv) {
       la[c].pts = ptr_dev.get();
       la[c].q = ctx.mod_QP().q;
       la[c].barrett = ctx.mod_QP().barrett;
+      la[c].q60 = below_2_60(ctx.key_moduli());
     }
     // the group form takes contiguous babies / inner sums: one buffer per ciphertext
     DeviceBuffer<uint64_t> bcat0(static_cast<size_t>(g) * words, s), bcat1(static_cast<size_t>(g) * words, s);
@@ -497,6 +498,7 @@ int main(int argc, char** argv) {
     pa.Ql = la[0].Ql;
     pa.P = la[0].P;
     pa.size_Q = la[0].size_Q;
+    pa.q60 = la[0].q60;
     pa.count = 2;
     pa.baby_stride = words;
     pa.giant_stride = words;

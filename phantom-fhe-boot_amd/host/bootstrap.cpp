@@ -990,6 +990,7 @@ phx::LtArgs FHECKKSRNS::level_lt_args(const PhantomContext& cc, const LTLevel& l
   la.pts = lv.d_pts.get();
   la.q = cc.mod_QP().q;
   la.barrett = cc.mod_QP().barrett;
+  la.q60 = below_2_60(cc.key_moduli());
   for (int j = 0; j < lv.g; ++j) la.baby[j] = w.babies.get() + static_cast<size_t>(j) * baby_words;
   la.out[0] = w.acc.data();
   for (int i = 1; i < lv.b; ++i) la.out[i] = w.giants.get() + static_cast<size_t>(i - 1) * ext_words;
@@ -1031,49 +1032,9 @@ PhantomCiphertext FHECKKSRNS::level_giants(const PhantomContext& cc, const LTLev
   return KeySwitchDownRescale(cc, w.acc);
 }
 
-bool FHECKKSRNS::level_fused(const PhantomContext& cc, const LTLevel& lv) const {
-  static const bool on = [] {  // opt-in: measured slower than the two launches (profiles/r05/ks_lt_fused/)
-    const char* e = std::getenv("PHX_LT_FUSED");
-    return e && e[0] == '1';
-  }();
-  const size_t n = cc.poly_degree();
-  return on && lv.g == 32 && lv.b <= phx::kKsLtMaxB && n >= 1024;
-}
-
-phx::KsLtArgs FHECKKSRNS::level_fused_args(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const {
-  const size_t n = cc.poly_degree(), ext_words = 2 * w.QlP * n;
-  phx::KsLtArgs A;
-  A.ks = w.ba;
-  A.pts = lv.d_pts.get();
-  A.b = lv.b;
-  A.out[0] = w.acc.data();
-  for (int i = 1; i < lv.b; ++i) A.out[i] = w.giants.get() + static_cast<size_t>(i - 1) * ext_words;
-  size_t nz = 0;
-  for (const auto& p : lv.pts) nz += p ? 1 : 0;
-  traffic::plaintexts(traffic::limb_bytes(nz * w.QlP, n));
-  traffic::ciphertexts(traffic::limb_bytes(2 * w.QlP * static_cast<size_t>(lv.b), n));  // the inner sums written
-  return A;
-}
-
 PhantomCiphertext FHECKKSRNS::apply_level(const PhantomContext& cc, const PhantomCiphertext& in,
                                           const LTLevel& lv) const {
   LevelWork w;
-  if (level_fused(cc, lv)) {
-    level_babies(cc, in, lv, w, false, false);
-    if (w.ba.beta > 4) {  // (the fused kernel's digit bound) the two launches instead
-      w.babies = DeviceBuffer<uint64_t>(static_cast<size_t>(lv.g) * 2 * w.QlP * cc.poly_degree(), cc.stream());
-      w.ba.out = w.babies.get();
-      hip_ok(phx::keyswitch_rotate_batch(w.ba, cc.poly_degree(), cc.stream()), "linear transform baby steps");
-      w.digits.release();
-      hip_ok(phx::lt_bsgs(level_lt_args(cc, lv, w), cc.poly_degree(), cc.stream()), "linear transform inner products");
-      return level_giants(cc, lv, w);
-    }
-    phx::KsLtGroupArgs ga;
-    ga.a[0] = level_fused_args(cc, lv, w);
-    hip_ok(phx::ks_lt_fused(ga, cc.poly_degree(), cc.stream()), "linear transform baby steps + inner products");
-    w.digits.release();
-    return level_giants(cc, lv, w);
-  }
   level_babies(cc, in, lv, w);
   hip_ok(phx::lt_bsgs(level_lt_args(cc, lv, w), cc.poly_degree(), cc.stream()), "linear transform inner products");
   return level_giants(cc, lv, w);
@@ -1086,28 +1047,10 @@ std::vector<PhantomCiphertext> FHECKKSRNS::apply_level_group(const PhantomContex
   if (K < 2 || K > phx::kLtGroupMax || K > phx::kKsGroupMax)
     throw std::invalid_argument("apply_level_group: 2 to 8 ciphertexts");
   std::vector<LevelWork> w(K);
-  // the fused form (one launch, no babies in HBM) when the K levels share a shape
-  const bool try_fused = level_fused(cc, lv);
-  for (int c = 0; c < K; ++c) level_babies(cc, *in[c], lv, w[c], false, !try_fused);
-  bool fused = try_fused;
-  for (int c = 0; c < K; ++c) fused &= w[c].ba.beta <= 4 && w[c].QlP == w[0].QlP;
-  if (fused) {
-    phx::KsLtGroupArgs ga;
-    ga.count = K;
-    for (int c = 0; c < K; ++c) ga.a[c] = level_fused_args(cc, lv, w[c]);
-    hip_ok(phx::ks_lt_fused(ga, cc.poly_degree(), cc.stream()), "linear transform baby steps + inner products (group)");
-    for (LevelWork& x : w) x.digits.release();
-    return level_giants_group(cc, lv, w);
-  }
+  for (int c = 0; c < K; ++c) level_babies(cc, *in[c], lv, w[c], false);
   phx::KsRotateBatchGroupArgs ka;
   ka.count = K;
-  for (int c = 0; c < K; ++c) {
-    if (try_fused) {  // shapes differ: the babies after all
-      w[c].babies = DeviceBuffer<uint64_t>(static_cast<size_t>(lv.g) * 2 * w[c].QlP * cc.poly_degree(), cc.stream());
-      w[c].ba.out = w[c].babies.get();
-    }
-    ka.a[c] = w[c].ba;
-  }
+  for (int c = 0; c < K; ++c) ka.a[c] = w[c].ba;
   hip_ok(phx::keyswitch_rotate_batch_group(ka, cc.poly_degree(), cc.stream()), "linear transform baby steps (group)");
   for (LevelWork& x : w) x.digits.release();
   bool same_ql = true;
@@ -1127,6 +1070,7 @@ std::vector<PhantomCiphertext> FHECKKSRNS::apply_level_group(const PhantomContex
     ga.Ql = la[0].Ql;
     ga.P = la[0].P;
     ga.size_Q = la[0].size_Q;
+    ga.q60 = la[0].q60;
     ga.count = K;
     ga.baby_stride = ext_words;  // (the babies and inner sums are [2][QlP][n] ciphertexts, back to back)
     ga.giant_stride = ext_words;
@@ -1532,21 +1476,26 @@ std::vector<PhantomCiphertext> FHECKKSRNS::EvalBootstrapBatch(const std::vector<
     throw std::invalid_argument("EvalBootstrapBatch: group must be 1.." + std::to_string(phx::kLtGroupMax));
   std::vector<PhantomCiphertext> out(in.size());
   // ciphertexts t, t + k, ... of lane t, up to `group` at a time in lockstep (shared plaintext
-  // and key reads, EvalMod on 2 x group lanes)
+  // and key reads, EvalMod on 2 x group lanes).  A lane's m ciphertexts form ceil(m / group)
+  // groups of near-equal size (43 at group 8: 8 + 5 x 7, not 5 x 8 + 3), so no lane ends on a
+  // small group that shares its key and plaintext reads among few ciphertexts
   auto run_lane = [&](int t) {
     const Precom& pc = precom(numSlots, cc);
     std::vector<size_t> mine;
     for (size_t i = t; i < in.size(); i += k) mine.push_back(i);
-    for (size_t g0 = 0; g0 < mine.size(); g0 += group) {
-      const size_t cnt = std::min(group, mine.size() - g0);
+    const size_t ng = (mine.size() + group - 1) / group;
+    for (size_t gi = 0, g0 = 0; gi < ng; ++gi) {
+      const size_t cnt = mine.size() / ng + (gi < mine.size() % ng ? 1 : 0);
+      const size_t at = g0;
+      g0 += cnt;
       if (cnt == 1) {
-        out[mine[g0]] = EvalBootstrap(in[mine[g0]], cc, numSlots);
+        out[mine[at]] = EvalBootstrap(in[mine[at]], cc, numSlots);
         continue;
       }
       std::vector<const PhantomCiphertext*> grp;
-      for (size_t m = 0; m < cnt; ++m) grp.push_back(&in[mine[g0 + m]]);
+      for (size_t m = 0; m < cnt; ++m) grp.push_back(&in[mine[at + m]]);
       std::vector<PhantomCiphertext> r = bootstrap_group(grp, cc, pc);
-      for (size_t m = 0; m < cnt; ++m) out[mine[g0 + m]] = std::move(r[m]);
+      for (size_t m = 0; m < cnt; ++m) out[mine[at + m]] = std::move(r[m]);
     }
   };
   if (k == 1) {

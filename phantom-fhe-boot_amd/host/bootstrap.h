@@ -238,11 +238,6 @@ class FHECKKSRNS {
   void level_babies(const PhantomContext& cc, const PhantomCiphertext& in, const LTLevel& lv, LevelWork& w,
                     bool launch = true, bool alloc_babies = true) const;
   phx::LtArgs level_lt_args(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const;
-  // the fused form of level_babies + lt_bsgs (phx::ks_lt_fused: the babies never reach HBM), for
-  // g = 32, b <= 8, beta <= 4 when PHX_LT_FUSED=1 (it saves the babies' memory but is VALU-bound:
-  // slower than the two launches, profiles/r05/ks_lt_fused/)
-  bool level_fused(const PhantomContext& cc, const LTLevel& lv) const;
-  phx::KsLtArgs level_fused_args(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const;
   PhantomCiphertext level_giants(const PhantomContext& cc, const LTLevel& lv, LevelWork& w) const;
   std::vector<PhantomCiphertext> level_giants_group(const PhantomContext& cc, const LTLevel& lv,
                                                     std::vector<LevelWork>& w) const;

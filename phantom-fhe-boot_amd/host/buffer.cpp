@@ -51,6 +51,16 @@ static bool event_done(hipEvent_t e) {
   return false;
 }
 
+void DevicePool::add_use(Pending& pend, Use u) {
+  for (Use& x : pend)
+    if (x.first == u.first) {
+      if (u.seq > x.seq) std::swap(x, u);
+      spare_.push_back(u.second);  // the older of the two
+      return;
+    }
+  pend.push_back(u);
+}
+
 void DevicePool::drop_done(Pending& pend) {
   for (size_t i = pend.size(); i-- > 0;)
     if (event_done(pend[i].second)) {
@@ -125,13 +135,23 @@ void* DevicePool::carve(int dev, size_t c, hipStream_t s, bool wait) {
   return nullptr;
 }
 
-DevicePool::Chunk* DevicePool::grow(int dev, size_t c) {
+// hipMalloc of a 1 GiB chunk takes milliseconds: the other lanes' threads keep allocating and
+// freeing meanwhile (the caller re-runs carve after the chunk is added, so a block freed in
+// between is also found)
+DevicePool::Chunk* DevicePool::grow(int dev, size_t c, std::unique_lock<std::mutex>& lk) {
   const size_t sz = std::max(c, kChunk);
   void* p = nullptr;
-  if (hipMalloc(&p, sz) != hipSuccess) {
+  lk.unlock();
+  const hipError_t r = hipMalloc(&p, sz);
+  lk.lock();
+  if (r != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
   }
+  return add_chunk(dev, p, sz);
+}
+
+DevicePool::Chunk* DevicePool::add_chunk(int dev, void* p, size_t sz) {
   Chunk* ch = new Chunk();
   ch->base = static_cast<char*>(p);
   ch->size = sz;
@@ -217,7 +237,7 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
   PHX_CHECK(hipGetDevice(&dev));
   if (bytes >= kArenaMin) {
     const size_t c = (bytes + kGrain - 1) / kGrain * kGrain;
-    std::lock_guard<std::mutex> lk(mu_);
+    std::unique_lock<std::mutex> lk(mu_);
     if (void* p = carve(dev, c, s)) return p;
     // Free blocks that are still in use by other streams: once the cached space exceeds the slack,
     // reuse one behind a device-side wait instead of growing (the held memory then tracks the live
@@ -225,16 +245,16 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
     const size_t cached = st_.held - st_.live;
     if (cached > std::max(kSlackMin, st_.live / 16))
       if (void* p = carve(dev, c, s, true)) return p;
-    if (grow(dev, c)) return carve(dev, c, s);
+    if (grow(dev, c, lk)) return carve(dev, c, s);
     // out of device memory: return wholly free chunks and cached small blocks, then wait for every
     // pending use so that all free blocks coalesce into reusable space
     release_cached_locked();
-    if (grow(dev, c)) return carve(dev, c, s);
+    if (grow(dev, c, lk)) return carve(dev, c, s);
     if (void* p = carve(dev, c, s, true)) return p;
     PHX_CHECK(hipDeviceSynchronize());
     if (void* p = carve(dev, c, s)) return p;
     release_cached_locked();
-    if (!grow(dev, c)) PHX_CHECK(hipErrorOutOfMemory);
+    if (!grow(dev, c, lk)) PHX_CHECK(hipErrorOutOfMemory);
     return carve(dev, c, s);
   }
   const size_t c = size_class(bytes);
@@ -297,7 +317,7 @@ void DevicePool::free(void* p, size_t bytes, hipStream_t s, bool completed) {
     if (!completed) {
       hipEvent_t ev = take_event();
       PHX_CHECK(hipEventRecord(ev, s));
-      b->pending.emplace_back(s, ev);
+      add_use(b->pending, Use{s, ev, ++seq_});
     }
     // coalesce with free neighbours (their pending uses move into the merged block)
     auto& blocks = b->chunk->blocks;
@@ -308,7 +328,7 @@ void DevicePool::free(void* p, size_t bytes, hipStream_t s, bool completed) {
         Block* pb = &prev->second;
         erase_free(pb);
         pb->size += b->size;
-        for (auto& pe : b->pending) pb->pending.push_back(pe);
+        for (const Use& u : b->pending) add_use(pb->pending, u);
         blocks.erase(me);
         b = pb;
         me = prev;
@@ -319,7 +339,7 @@ void DevicePool::free(void* p, size_t bytes, hipStream_t s, bool completed) {
       Block* nb = &nx->second;
       erase_free(nb);
       b->size += nb->size;
-      for (auto& pe : nb->pending) b->pending.push_back(pe);
+      for (const Use& u : nb->pending) add_use(b->pending, u);
       blocks.erase(nx);
     }
     drop_done(b->pending);

@@ -54,7 +54,14 @@ class DevicePool {
   static constexpr size_t kSlackMin = size_t(2) << 30;  // cached arena space kept before waiting on reuse
 
  private:
-  using Pending = std::vector<std::pair<hipStream_t, hipEvent_t>>;  // uses a block may still have
+  // uses a block may still have: at most one per stream, the newest (an event recorded later on a
+  // stream completes after every earlier one there, so it alone covers the stream's uses)
+  struct Use {
+    hipStream_t first;
+    hipEvent_t second;
+    uint64_t seq;  // record order (seq_)
+  };
+  using Pending = std::vector<Use>;
   struct Small {
     void* p;
     hipStream_t stream;
@@ -83,15 +90,18 @@ class DevicePool {
   std::multimap<std::pair<int, size_t>, Block*> by_size_;  // free arena blocks by (device, size)
   std::map<void*, Block*> live_;                           // handed-out arena blocks
   std::vector<hipEvent_t> spare_;
+  uint64_t seq_ = 0;
   Stats st_;
   static size_t size_class(size_t bytes);
   hipEvent_t take_event();
   bool ready_for(Pending& pend, hipStream_t s);  // drops completed uses
   void drop_done(Pending& pend);
+  void add_use(Pending& pend, Use u);  // keeps the newest use per stream
+  Chunk* add_chunk(int dev, void* p, size_t sz);
   void insert_free(Block* b);
   void erase_free(Block* b);
   void* carve(int dev, size_t c, hipStream_t s, bool wait = false);
-  Chunk* grow(int dev, size_t c);
+  Chunk* grow(int dev, size_t c, std::unique_lock<std::mutex>& lk);  // hipMalloc with lk released
   void release_cached_locked();
   void note_live(long delta);
 };

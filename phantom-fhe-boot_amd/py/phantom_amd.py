@@ -84,9 +84,6 @@ _SIGS = {
                                                              vp]),
     "phantom_rotate_ext_accumulate_group": (ctypes.c_int, [vp, sz, sz, ctypes.POINTER(vp), ctypes.POINTER(vp), sz,
                                                            ctypes.c_uint32, ctypes.POINTER(vp), ctypes.c_int, vp]),
-    "phantom_lt_level_fused": (ctypes.c_int, [vp, sz, sz, ctypes.POINTER(vp), ctypes.POINTER(vp),
-                                              ctypes.POINTER(ctypes.POINTER(vp)), sz, ctypes.POINTER(ctypes.c_uint32),
-                                              ctypes.POINTER(vp), sz, ctypes.POINTER(vp), vp]),
     "phantom_tensor_lin": (ctypes.c_int, [vp, sz, vp, vp, vp, vp, vp, sz, vp, vp]),
     "phantom_tensor_lin_batch": (ctypes.c_int, [vp, sz, sz, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
                                                 vp, ctypes.POINTER(vp), sz, ctypes.POINTER(vp), ctypes.POINTER(vp), vp]),
@@ -269,7 +266,8 @@ class BootSession:
         return b.value
 
     def run(self, dev_in, in_stride, count, dev_out, out_stride, lanes=4, group=None):
-        """group: ciphertexts per lane in lockstep (1..8); None = the library default (4)."""
+        """group: at most this many ciphertexts per lane in lockstep (1..8; a lane's m ciphertexts form
+        ceil(m / group) groups of near-equal size); None = the library default (8)."""
         if group is None:
             check(load().phantom_boot_run(self.handle, dev_in, in_stride, count, dev_out, out_stride, lanes))
         else:

@@ -88,3 +88,16 @@ def gather_rows(dist, local, device):
         return out
     dist.gather(local, None, dst=0)
     return None
+
+
+def gather_stats(dist, values, device):
+    """Every rank's list of floats -> the per-rank lists in rank order, on every rank (an all-gather
+    of one small float64 tensor; at world 1 just [values])."""
+    import torch
+    world, _ = _world(dist)
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if world == 1:
+        return [t.tolist()]
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [p.tolist() for p in parts]

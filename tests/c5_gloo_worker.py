@@ -113,6 +113,9 @@ def main():
         ok &= written == out_bytes
         out[j] = torch.from_numpy(row.copy())
     gathered = shard.gather_rows(dist, out, "cpu")
+    # bench.py's per-rank C5 figures (wall time, pool): every rank sees every rank's values in order
+    stats = shard.gather_stats(dist, [1.5 + rank, 10.0 * rank], "cpu")
+    ok &= stats == [[1.5 + r, 10.0 * r] for r in range(world)]
     if rank == 0:
         for i in range(total):
             h, d = deserialize(lib, gathered[i].numpy())

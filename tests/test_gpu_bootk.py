@@ -72,6 +72,27 @@ def test_lt_bsgs(c4, rng, chain, g, b):
         assert np.array_equal(to_host(douts[i]), want[i]), i
 
 
+@pytest.mark.parametrize("bits,g,b", [(61, 32, 8), (61, 16, 4), (61, 32, 3), (59, 32, 8)])
+def test_lt_bsgs_moduli(rng, bits, g, b):
+    """the inner sums' 30-bit split partial sums at their bounds: N = 4096, 8 + 2 moduli of `bits`
+    bits.  61-bit moduli make a high-half product reach 2^62, so the sums fold every 4 products
+    (LtArgs::q60 = 0); below 2^60 every 8 (tile kernel) or 16 (lt_bsgs_kernel).  == or_lt_bsgs"""
+    n, size_p, chain = 1 << 12, 2, 1
+    ctx = PA.Context(n, O.coeff_modulus_create(n, [bits] * 10), size_p)
+    em = ctx.ql(chain) + ctx.moduli[ctx.size_Q:]
+    rand = lambda polys: np.concatenate([O.random_limbs(rng, n, em) for _ in range(polys)])
+    babies = [rand(2) for _ in range(g)]
+    pts = [rand(1) for _ in range(g * b)]
+    db, dp = [to_dev(x) for x in babies], [to_dev(x) for x in pts]
+    douts = [to_dev(np.zeros(2 * len(em) * n, dtype=np.uint64)) for _ in range(b)]
+    PA.check(_lib().phantom_lt_bsgs(ctx.handle, chain, _vp(db), g, _vp(dp), b, _vp(douts), stream()))
+    want = [np.zeros(2 * len(em) * n, dtype=np.uint64) for _ in range(b)]
+    O.lib().or_lt_bsgs(O.ptrs(babies), g, O.ptrs(pts), b, O.ptrs(want), n, len(ctx.ql(chain)), ctx.size_Q,
+                       ctx.size_P, O.P(O.arr(ctx.moduli)))
+    for i in range(b):
+        assert np.array_equal(to_host(douts[i]), want[i]), (bits, i)
+
+
 @pytest.mark.parametrize("chain", [1, 17])
 def test_keyswitch_ext(c4, rng, chain):
     ql = c4.ql(chain)

@@ -84,6 +84,35 @@ def test_lt_bsgs_group(c4, rng, chain, b, group):
             assert np.array_equal(giants[(i - 1) * W:i * W], want[i]), (c, i)
 
 
+@pytest.mark.parametrize("bits,b,group", [(61, 8, 2), (61, 3, 4), (59, 8, 4)])
+def test_lt_bsgs_group_moduli(rng, bits, b, group):
+    """grouped inner sums at the split partial sums' bounds: N = 4096, 8 + 2 moduli of `bits` bits
+    (61-bit: folded every 4 products, LtGroupArgs::q60 = 0) == or_lt_bsgs per ciphertext"""
+    n, size_p, chain, g = 1 << 12, 2, 1, 32
+    ctx = PA.Context(n, O.coeff_modulus_create(n, [bits] * 10), size_p)
+    em = ctx.ql(chain) + ctx.moduli[ctx.size_Q:]
+    W = 2 * len(em) * n
+    rand = lambda polys: np.concatenate([O.random_limbs(rng, n, em) for _ in range(polys)])
+    babies = [[rand(2) for _ in range(g)] for _ in range(group)]
+    pts = [rand(1) for _ in range(g * b)]
+    dbabies = [to_dev(np.concatenate(bs)) for bs in babies]
+    dpts = [to_dev(x) for x in pts]
+    dacc = [to_dev(np.full(W, 3, dtype=np.uint64)) for _ in range(group)]
+    dgiant = [to_dev(np.full(max(b - 1, 1) * W, 9, dtype=np.uint64)) for _ in range(group)]
+    PA.check(_lib().phantom_lt_bsgs_group(ctx.handle, chain, group, _vp(ptr(x) for x in dbabies), W, g,
+                                          _vp(ptr(x) for x in dpts), b, _vp(ptr(x) for x in dacc),
+                                          _vp(ptr(x) for x in dgiant), W, stream()))
+    mods = O.P(O.arr(ctx.moduli))
+    for c in range(group):
+        want = [np.zeros(W, dtype=np.uint64) for _ in range(b)]
+        O.lib().or_lt_bsgs(O.ptrs(babies[c]), g, O.ptrs(pts), b, O.ptrs(want), n, len(ctx.ql(chain)), ctx.size_Q,
+                           ctx.size_P, mods)
+        assert np.array_equal(to_host(dacc[c]), want[0]), (bits, c, 0)
+        giants = to_host(dgiant[c])
+        for i in range(1, b):
+            assert np.array_equal(giants[(i - 1) * W:i * W], want[i]), (bits, c, i)
+
+
 @pytest.mark.parametrize("chain,count,group", [(2, 32, 2), (3, 12, 4), (17, 32, 2), (18, 12, 8)])
 def test_fast_rotation_ext_batch_group(c4, rng, chain, count, group):
     """the baby steps of `group` ciphertexts in one launch == per ciphertext and rotation
@@ -203,43 +232,3 @@ def test_rotate_ext_accumulate_group(c4, rng, chain, group, accumulate):
         O.lib().or_rotate_ext_accumulate(O.P(exts[c].copy()), O.ptrs(keys), elt, O.P(want), accumulate, N,
                                          len(c4.ql(chain)), c4.size_Q, c4.size_P, mods)
         assert np.array_equal(to_host(dacc[c]), want), c
-
-
-@pytest.mark.parametrize("chain,b,group", [(2, 8, 1), (3, 8, 2), (17, 8, 4), (18, 3, 8), (2, 5, 8)])
-def test_lt_level_fused(c4, rng, chain, b, group):
-    """phantom_lt_level_fused (baby steps formed per tile in LDS, never written) == the two
-    oracle-checked launches it replaces, phantom_fast_rotation_ext_batch then phantom_lt_bsgs, per
-    ciphertext: identity baby at 16, a conjugation among the rotations, 3 key sets round robin,
-    plaintexts from a pool with one zero diagonal, distinct inputs per ciphertext"""
-    g = 32
-    ql, em = c4.ql(chain), _ext_mods(c4, chain)
-    W = 2 * len(em) * N
-    beta = -(-len(ql) // SIZE_P)
-    dnum = -(-c4.size_Q // SIZE_P)
-    cts = [to_dev(_rand(rng, ql, 2)) for _ in range(group)]
-    digits = [to_dev(_rand(rng, em, beta)) for _ in range(group)]
-    elts = [pow(5, 7 * j + 3, 2 * N) for j in range(g)]
-    elts[29] = 2 * N - 1
-    identity_at = 16
-    keysets = [_keys(rng, c4) for _ in range(3)]
-    key_arrays = [None if j == identity_at else _vp(ptr(x) for x in keysets[j % 3][1]) for j in range(g)]
-    kk = (ctypes.POINTER(ctypes.c_void_p) * g)(*[ctypes.cast(a, ctypes.POINTER(ctypes.c_void_p)) if a is not None
-                                                 else None for a in key_arrays])
-    el = (ctypes.c_uint32 * g)(*elts)
-    pool = [to_dev(_rand(rng, em)) for _ in range(12)]
-    pool[3] = to_dev(np.zeros(len(em) * N, dtype=np.uint64))
-    pts = [ptr(pool[(5 * u + 1) % len(pool)]) for u in range(g * b)]
-    douts = [to_dev(np.full(W, 7, dtype=np.uint64)) for _ in range(group * b)]
-    PA.check(_lib().phantom_lt_level_fused(c4.handle, chain, group, _vp(ptr(x) for x in cts),
-                                           _vp(ptr(x) for x in digits), kk, dnum, el, _vp(pts), b,
-                                           _vp(ptr(x) for x in douts), stream()))
-    t = torch()
-    babies = t.empty(g * W, dtype=t.int64, device="cuda")
-    ref = [to_dev(np.zeros(W, dtype=np.uint64)) for _ in range(b)]
-    for c in range(group):
-        PA.check(_lib().phantom_fast_rotation_ext_batch(c4.handle, chain, ptr(cts[c]), ptr(digits[c]), kk, dnum, el, g,
-                                                        _vp(ptr(babies) + 8 * j * W for j in range(g)), stream()))
-        PA.check(_lib().phantom_lt_bsgs(c4.handle, chain, _vp(ptr(babies) + 8 * j * W for j in range(g)), g,
-                                        _vp(pts), b, _vp(ptr(x) for x in ref), stream()))
-        for i in range(b):
-            assert t.equal(douts[c * b + i], ref[i]), (c, i)
