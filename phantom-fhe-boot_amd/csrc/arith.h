@@ -81,7 +81,7 @@ __device__ __forceinline__ uint64_t barrett_reduce_64(uint64_t x, uint64_t q, ui
 // y = yh 2^30 + yl (x, y < 2^60), every partial product below 2^60, reduced once at the end ----
 struct SplitRed {
   uint64_t c30, c30s, c60, c60s;  // 2^30 mod q, 2^60 mod q and their Shoup quotients
-  uint64_t nq, nq2;               // -q, -2q mod 2^64
+  uint64_t nq, nq2, nq4;          // -q, -2q, -4q mod 2^64
 };
 // floor(w 2^64 / q) for w < q from the Barrett ratio floor(2^128 / q) = {r0, r1} (an estimate at
 // most 2 low, corrected exactly)
@@ -111,6 +111,7 @@ __device__ __forceinline__ SplitRed split_red(uint64_t q, uint64_t r0, uint64_t 
   k.c60s = uniform_u64(shoup_from_barrett(k.c60, q, r0, r1));
   k.nq = uniform_u64(0 - q);
   k.nq2 = uniform_u64(0 - (q << 1));
+  k.nq4 = uniform_u64(0 - (q << 2));
   return k;
 }
 
@@ -214,6 +215,25 @@ __device__ __forceinline__ uint64_t split_reduce(uint64_t ll, uint64_t mm, uint6
   const uint64_t c = hh * k.c60 + mulhi_approx(hh, k.c60s) * nq;
   uint64_t s = add64(add64(a, b), c);
   s = s + mulhi_approx(s, r1) * nq;
+  s = csub_n(s, q << 1, k.nq2);
+  return csub_n(s, q, nq);
+}
+
+// split_reduce with the three partial sums folded into two first: L = ll + (mm mod 2^30) 2^30 and
+// H = hh + floor(mm / 2^30), both below 2^63 (ll, hh < 2^62 and mm < 2^63 for BETA <= 4), so the
+// value is L + H 2^60.  A 64-bit Barrett step on L and a Shoup product H (2^60 mod q), each in
+// [0, 4q) with approximate quotients, their sum below 8q < 2^63 and three carry-free conditional
+// subtractions: 15 multiplies instead of 30.  q < 2^60.
+__device__ __forceinline__ uint64_t split_reduce2(uint64_t ll, uint64_t mm, uint64_t hh, const SplitRed& k, uint64_t q,
+                                                  uint64_t r1) {
+  constexpr uint64_t kM30 = (1ull << 30) - 1;
+  const uint64_t nq = k.nq;
+  const uint64_t L = add64(ll, (mm & kM30) << 30);
+  const uint64_t H = add64(hh, mm >> 30);
+  const uint64_t a = L + mulhi_approx(L, r1) * nq;
+  const uint64_t b = H * k.c60 + mulhi_approx(H, k.c60s) * nq;
+  uint64_t s = add64(a, b);
+  s = csub_n(s, q << 2, k.nq4);
   s = csub_n(s, q << 1, k.nq2);
   return csub_n(s, q, nq);
 }

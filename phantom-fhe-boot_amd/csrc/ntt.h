@@ -36,6 +36,7 @@ struct NttTables {
   double* row_a_inv = nullptr;   // the same factors of itw (inverses of the forward ones)
   double* row_b_inv = nullptr;
   bool lazy16 = false;           // every modulus < 2^60: forward integer passes use the 16q lazy range
+  bool int_only = false;         // every modulus >= 2^50: no limb takes the FP64 path
 };
 
 // log2 of the column-pass size S1 for a given log2(n) (the row pass handles the rest)

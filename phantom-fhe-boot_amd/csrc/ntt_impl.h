@@ -553,6 +553,17 @@ constexpr int kKspWaves = 2;  // ... and of the inverse row pass with the key-sw
 #define PHX_EPI_WAVES 3
 #endif
 constexpr int kEpiWaves = PHX_EPI_WAVES;  // ... and of the row pass with the rescale / moddown finish
+// Integer-only launches (IO: every modulus of the table >= 2^50, and < 2^60 for the lazy ranges;
+// every limb of the bootstrap chain) instantiate the kernels without the FP64 branch, whose FP64
+// twiddles and factors otherwise set the register allocation of the whole kernel: every integer
+// pass then fits 4 waves per SIMD without spilling (column 104-110 VGPRs, row 108-128; the mixed
+// row passes hold 138-161 at 3 waves).  40-limb C4-chain forward 31.2 -> 30.3 us, 120 limbs
+// 78.3 -> 75.2, bootstrap 22.5 -> 21.9 ms, C5 +2% (profiles/r06/ntt_io/).  5 waves on the column
+// pass (93 VGPRs with an unpadded, swizzled 32 KB tile) measured slower: 34.6 us.
+#ifndef PHX_NTT_IO
+#define PHX_NTT_IO 1
+#endif
+constexpr int kIoColWaves = 4, kIoRowWaves = 4, kIoEpiWaves = 4, kIoKsWaves = 4, kIoKspWaves = 4;
 template <int T, int BETA>
 __device__ __forceinline__ void ks_epilogue_b(const KArgs& a, const TileRef& tr, const uint64_t (&y)[E], uint64_t q,
                                               uint64_t r0, uint64_t r1) {
@@ -776,7 +787,7 @@ template <int S1_LOG>
 constexpr int col_lds_words() { return (Sub<S1_LOG>::S + Sub<S1_LOG>::S / 16) * COLS; }
 
 // One column tile (the calling workgroup's threads tid < NT; `lds`: col_lds_words words).
-template <int S1_LOG, int S2_LOG, bool FWD, bool BCV, bool LZ>
+template <int S1_LOG, int S2_LOG, bool FWD, bool BCV, bool LZ, bool IO>
 __device__ __forceinline__ void col_tile(const KArgs& a, int tile, uint64_t* lds, [[maybe_unused]] int sslot) {
   using SB = Sub<S1_LOG>;
   using P = Plan<S1_LOG, S2_LOG>;
@@ -803,7 +814,7 @@ __device__ __forceinline__ void col_tile(const KArgs& a, int tile, uint64_t* lds
 #pragma unroll
       for (int j = 0; j < E; ++j) x[j] = barrett_reduce_64(x[j], lc.q, r1);
     }
-    if (lc.f64) {
+    if (!IO && lc.f64) {
       const double* tab = a.col + (size_t)tr.row * SB::S;
       double w[RN][E];
       static_for<RN>([&](auto rc) {
@@ -887,8 +898,8 @@ __device__ __forceinline__ void col_tile(const KArgs& a, int tile, uint64_t* lds
   }
 }
 
-template <int S1_LOG, int S2_LOG, bool FWD, bool BCV = false, bool LZ = false>
-__global__ __launch_bounds__(CBLOCK, BCV ? 2 : kNttWavesPerEU) void ntt_col(KArgs a) {
+template <int S1_LOG, int S2_LOG, bool FWD, bool BCV = false, bool LZ = false, bool IO = false>
+__global__ __launch_bounds__(CBLOCK, BCV ? 2 : IO ? kIoColWaves : kNttWavesPerEU) void ntt_col(KArgs a) {
   constexpr int NT = COLS * Sub<S1_LOG>::T, CT = (1 << S2_LOG) / COLS;
   __shared__ uint64_t lds[col_lds_words<S1_LOG>()];
   if (threadIdx.x >= NT) return;  // no barrier involves the idle threads' absence (NT is a multiple of 64)
@@ -896,7 +907,7 @@ __global__ __launch_bounds__(CBLOCK, BCV ? 2 : kNttWavesPerEU) void ntt_col(KArg
   if (tile >= a.limbs * CT) return;
   [[maybe_unused]] const int sslot = blockIdx.x * (CBLOCK / 64) + threadIdx.x / 64;
   if constexpr (FWD && !BCV) PHX_STAMP(sslot, 0, false);
-  col_tile<S1_LOG, S2_LOG, FWD, BCV, LZ>(a, tile, lds, sslot);
+  col_tile<S1_LOG, S2_LOG, FWD, BCV, LZ, IO>(a, tile, lds, sslot);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -949,7 +960,7 @@ struct RowShape {
 };
 
 // One row item (the calling wave's RW rows; lds: RowShape::LDS_WORDS words, tw0: RowShape::TW0).
-template <int S1_LOG, int S2_LOG, bool FWD, bool EPI, bool LZ, bool KS>
+template <int S1_LOG, int S2_LOG, bool FWD, bool EPI, bool LZ, bool KS, bool IO>
 __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds, double* tw0,
                                          [[maybe_unused]] int sslot) {
   using SB = Sub<S2_LOG>;
@@ -975,7 +986,7 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
     const LimbCtx lc = limb_ctx(a, tr.row);
     uint64_t* dst = a.out + tr.off;
     [[maybe_unused]] EpiOperands eo;
-    if (lc.f64) {
+    if (!IO && lc.f64) {
       const double* A = a.row_a + ((size_t)tr.row * S1 + r) * 16;
       const double* Bt = a.row_b + (size_t)tr.row * S2;
       // raw factors: round 0 (e = t + 1 + T k < 2^ER0) and every later round's slots
@@ -1147,8 +1158,9 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
 // give it the registers to do so without spilling (168 VGPRs at three waves spilled 47).
 // KS: forward, the epilogue is the key-switch form (ks_epilogue; EPI must be set too); inverse, the
 // input is the key-switch prologue (ks_prologue).
-template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false, bool LZ = false, bool KS = false>
-__global__ __launch_bounds__(BLOCK, KS ? (FWD ? kKsWaves : kKspWaves) : EPI ? kEpiWaves : kRowWaves)
+template <int S1_LOG, int S2_LOG, bool FWD, bool EPI = false, bool LZ = false, bool KS = false, bool IO = false>
+__global__ __launch_bounds__(BLOCK, IO ? (KS ? (FWD ? kIoKsWaves : kIoKspWaves) : EPI ? kIoEpiWaves : kIoRowWaves)
+                                      : KS ? (FWD ? kKsWaves : kKspWaves) : EPI ? kEpiWaves : kRowWaves)
 void ntt_row(KArgs a) {
   using RS = RowShape<S1_LOG, S2_LOG>;
   __shared__ uint64_t lds[RS::LDS_WORDS];
@@ -1163,7 +1175,7 @@ void ntt_row(KArgs a) {
   const int sslot = 0;
 #endif
   if constexpr (FWD && !EPI) PHX_STAMP(sslot, 0, false);
-  row_item<S1_LOG, S2_LOG, FWD, EPI, LZ, KS>(a, item, lds, tw0, sslot);
+  row_item<S1_LOG, S2_LOG, FWD, EPI, LZ, KS, IO>(a, item, lds, tw0, sslot);
 }
 // ---------------------------------------------------------------------------------------
 // 1-D path for small transforms, n = 2^8 .. 2^11 (the reference's radix-2 fnwt_1d / inwt_1d,
@@ -1270,15 +1282,23 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   const dim3 grid_c(col_tiles), grid_r(row_groups);
   // column tiles of small transforms need fewer than BLOCK threads (rounded up to a wavefront)
   const dim3 block_c(std::max(64, COLS * Sub<S1_LOG>::T)), block_r(BLOCK);
+  // integer-only instantiations (IO) for degrees >= 2^14 (the bootstrap's): the FP64 branch is
+  // compiled out, so the kernels' registers are the integer path's alone
+  constexpr bool kIO = PHX_NTT_IO && S1_LOG + S2_LOG >= 14;
   if (!inverse) {
     NttEpilogue epi_row = a.epi;
     a.epi = NttEpilogue{};  // the column pass stores its intermediate
     // one lazy range for the whole launch: both passes must agree on the intermediate's bound
     const bool lz = tb.lazy16;
-    if (bcv && lz)
+    const bool io = kIO && lz && tb.int_only;
+    if (bcv && io)
+      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true, true, true, kIO>), grid_c, block_c, 0, stream, a);
+    else if (bcv && lz)
       hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true, true, true>), grid_c, block_c, 0, stream, a);
     else if (bcv)
       hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true, true, false>), grid_c, block_c, 0, stream, a);
+    else if (io)
+      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true, false, true, kIO>), grid_c, block_c, 0, stream, a);
     else if (lz)
       hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, true, false, true>), grid_c, block_c, 0, stream, a);
     else
@@ -1288,14 +1308,20 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
     a.map.in_outer = a.map.out_outer;
     a.bcast = nullptr;  // the row pass reads the intermediate
     a.epi = epi_row;
-    if (a.epi.out && a.epi.ks_beta > 0 && lz)
+    if (a.epi.out && a.epi.ks_beta > 0 && io)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true, true, true, kIO>), grid_r, block_r, 0, stream, a);
+    else if (a.epi.out && a.epi.ks_beta > 0 && lz)
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true, true, true>), grid_r, block_r, 0, stream, a);
     else if (a.epi.out && a.epi.ks_beta > 0)
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true, false, true>), grid_r, block_r, 0, stream, a);
+    else if (a.epi.out && io)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true, true, false, kIO>), grid_r, block_r, 0, stream, a);
     else if (a.epi.out && lz)
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true, true>), grid_r, block_r, 0, stream, a);
     else if (a.epi.out)
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, true, false>), grid_r, block_r, 0, stream, a);
+    else if (io)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, false, true, false, kIO>), grid_r, block_r, 0, stream, a);
     else if (lz)
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, true, false, true>), grid_r, block_r, 0, stream, a);
     else
@@ -1303,10 +1329,15 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
   } else {
     // one lazy range for the whole launch, as forward
     const bool lz = tb.lazy16;
-    if (a.epi.ks_beta > 0 && lz)
+    const bool io = kIO && lz && tb.int_only;
+    if (a.epi.ks_beta > 0 && io)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false, false, true, true, kIO>), grid_r, block_r, 0, stream, a);
+    else if (a.epi.ks_beta > 0 && lz)
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false, false, true, true>), grid_r, block_r, 0, stream, a);
     else if (a.epi.ks_beta > 0)
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false, false, false, true>), grid_r, block_r, 0, stream, a);
+    else if (io)
+      hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false, false, true, false, kIO>), grid_r, block_r, 0, stream, a);
     else if (lz)
       hipLaunchKernelGGL((ntt_row<S1_LOG, S2_LOG, false, false, true>), grid_r, block_r, 0, stream, a);
     else
@@ -1316,7 +1347,9 @@ hipError_t launch(const NttTables& tb, const uint64_t* in, uint64_t* out, const 
     a.map.in_outer = a.map.out_outer;
     a.copy = NttCopy{};  // the row pass made the copy
     a.epi = NttEpilogue{};  // ... and consumed the key-switch prologue
-    if (lz)
+    if (io)
+      hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false, false, true, kIO>), grid_c, block_c, 0, stream, a);
+    else if (lz)
       hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false, false, true>), grid_c, block_c, 0, stream, a);
     else
       hipLaunchKernelGGL((ntt_col<S1_LOG, S2_LOG, false>), grid_c, block_c, 0, stream, a);

@@ -803,11 +803,15 @@ __device__ __forceinline__ void ks_lt_barrier() {
 // dispatches apart (blocks b and b + 8 share an XCD under round-robin placement), so the followers
 // read the key halves from that XCD's L2.
 constexpr uint32_t kKsBatchFullMax = 64;  // entries of one ks_rotate_batch_full launch
+#ifndef PHX_KS_RED
+#define PHX_KS_RED 2  // FAST reduction: 2 = split_reduce2 (two folded terms), 1 = split_reduce (three)
+#endif
 // FAST (GROUP launches over moduli below 2^60, KsRotateBatchArgs::q60): the approximate-quotient
 // reduction.  The grouped kernel reads its keys from L2 and is issue-bound, so fewer instructions
 // pay there; the single kernel is HBM-bound and keeps the exact form at 128 VGPRs (4 waves per SIMD).
 template <int BETA, bool GROUP, bool FAST = false>
-__global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGroupArgs pa, uint32_t log_n) {
+__global__ __launch_bounds__(kBlock, BETA <= 3 ? 4 : 3) void ks_rotate_batch_full(KsRotateBatchGroupArgs pa,
+                                                                                   uint32_t log_n) {
   constexpr uint32_t bsz = kGalB;
   constexpr int PP = kGalB / 2 / kBlock;  // pairs per thread
   __shared__ uint64_t s0[2][kGalB], s1[2][kGalB];
@@ -948,7 +952,9 @@ __global__ __launch_bounds__(kBlock) void ks_rotate_batch_full(KsRotateBatchGrou
           }
       }
       auto red = [&](uint64_t x, uint64_t y, uint64_t z) {
-        return FAST ? split_reduce(x, y, z, sr, q, r1) : split_reduce_exact(x, y, z, sr, q, r1);
+        if constexpr (FAST && PHX_KS_RED == 2) return split_reduce2(x, y, z, sr, q, r1);
+        else if constexpr (FAST) return split_reduce(x, y, z, sr, q, r1);
+        else return split_reduce_exact(x, y, z, sr, q, r1);
       };
       t0[2 * i] = add_mod(red(ll[0][0], mm[0][0], hh[0][0]), pc0[p].x, q);
       t0[2 * i + 1] = add_mod(red(ll[0][1], mm[0][1], hh[0][1]), pc0[p].y, q);

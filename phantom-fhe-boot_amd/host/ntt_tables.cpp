@@ -42,6 +42,8 @@ DeviceNttTables::DeviceNttTables(size_t n, const std::vector<uint64_t>& moduli, 
   t_.log_n = log2_exact(n);
   t_.lazy16 = true;
   for (uint64_t q : moduli) t_.lazy16 &= q < (uint64_t(1) << 60);
+  t_.int_only = true;
+  for (uint64_t q : moduli) t_.int_only &= q >= (uint64_t(1) << 50);
   t_.num_moduli = L;
   if (t_.log_n < 3 || t_.log_n > 17) throw std::invalid_argument("unsupported polynomial degree");
 
