@@ -319,8 +319,21 @@ def job_throughput(units_per_rank, world, max_seconds):
     return units_per_rank * world / max_seconds
 
 
-def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=3, chain=26, verify=None, key_seed=None,
-           group=8):
+def c5_shape(per, lanes=None, group=None):
+    """Lanes x lockstep group for `per` bootstraps on one GPU (explicit values win).  Groups of 8
+    share the most key and diagonal reads; 3 lanes fill one bootstrap's serial tails best, at 1,024
+    and at the 8-GPU job's 128 per rank alike (profiles/r06/c5_share/: 128 per rank at 3 x 8 60.7-61.1/s,
+    2 x 8 60.1-60.5, 4 x 8 60.6, 4 x 4 59.1).  Each lane's m ciphertexts form ceil(m / group) groups
+    of near-equal size (EvalBootstrapBatch), so no lane ends on a small group; with fewer than a group
+    per lane the lanes shrink instead."""
+    group = 8 if group is None else group
+    if lanes is None:
+        lanes = max(1, min(3, -(-per // group)))
+    return lanes, group
+
+
+def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=None, chain=26, verify=None, key_seed=None,
+           group=None):
     """Config C5: `total` independent C4 bootstraps sharded over the ranks, one
     process per GPU.  Every rank regenerates the same keys from a 32-byte seed rank 0 broadcasts
     (no key traffic).  Rank 0 encrypts the batch — 2^15 reals in [1, 5] per ciphertext at chain
@@ -335,6 +348,7 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=3, chain=26, 
     if total % world:
         raise ValueError(f"C5 batch {total} does not divide over {world} ranks")
     per = total // world
+    lanes, group = c5_shape(per, lanes, group)
     dev = torch.device("cuda", local_rank)
     # fresh OS entropy by default; a fixed seed (--c5-key-seed) makes the keys, and with them the
     # per-ciphertext precision, reproducible
@@ -470,10 +484,11 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (bootstrap latency) leg")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (sharded bootstrap batch) leg")
     ap.add_argument("--c5-batch", type=int, default=1024, help="C5: bootstraps in the whole batch")
-    ap.add_argument("--c5-lanes", type=int, default=3, help="C5: stream lanes per GPU (each runs lockstep groups)")
-    ap.add_argument("--c5-group", type=int, default=8,
-                    help="C5: bootstraps per lane in lockstep (1..8); 3 x 8 holds ~86 GiB, 4 x 8 ~107 GiB, "
-                         "2 x 4 ~56 GiB (profiles/r05/c5_pool/)")
+    ap.add_argument("--c5-lanes", type=int, default=None,
+                    help="C5: stream lanes per GPU (each runs lockstep groups); default from the per-rank count (c5_shape)")
+    ap.add_argument("--c5-group", type=int, default=None,
+                    help="C5: at most this many bootstraps per lane in lockstep (1..8, default 8); 3 x 8 holds ~86 GiB, "
+                         "4 x 8 ~107 GiB, 2 x 4 ~56 GiB (profiles/r05/c5_pool/)")
     ap.add_argument("--c5-verify", type=int, default=None, help="C5: decrypt-check only the first K results")
     ap.add_argument("--c5-key-seed", default=None, help="C5: 64 hex digits of key seed (default: OS entropy)")
     args = ap.parse_args()

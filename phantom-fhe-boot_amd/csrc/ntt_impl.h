@@ -678,6 +678,11 @@ __device__ __forceinline__ void ks_prologue(const KArgs& a, const TileRef& tr, u
 // Row-pass block order of the key-switch epilogue: the polynomials' blocks of one row group are
 // dealt to one XCD back to back (blocks b and b + 8 share an XCD under round-robin placement;
 // speed only, any placement is correct), so the second polynomial reads tmu from that XCD's L2.
+// PHX_ROW_DEAL: the same order for every batched row pass, whose later polynomials then read the
+// row group's twiddles (the same limb's table rows) from L2.
+#ifndef PHX_ROW_DEAL
+#define PHX_ROW_DEAL 1
+#endif
 __device__ __forceinline__ int ks_row_block(const KArgs& a, int b, int waves, int groups) {
   const int polys = a.map.polys;
   if (polys < 2 || (a.limbs_per_poly * groups) % waves != 0) return b;
@@ -1166,7 +1171,7 @@ void ntt_row(KArgs a) {
   __shared__ uint64_t lds[RS::LDS_WORDS];
   __shared__ double tw0[RS::TW0];
   const int wave = threadIdx.x / 64;
-  const int blk = KS ? ks_row_block(a, blockIdx.x, RS::WAVES, RS::GROUPS) : (int)blockIdx.x;
+  const int blk = (KS || PHX_ROW_DEAL) ? ks_row_block(a, blockIdx.x, RS::WAVES, RS::GROUPS) : (int)blockIdx.x;
   const int item = __builtin_amdgcn_readfirstlane(blk * RS::WAVES + wave);
   if (item >= a.limbs * RS::GROUPS) return;  // no workgroup barrier in this kernel
 #if PHX_NTT_STAMP

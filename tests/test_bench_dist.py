@@ -61,6 +61,16 @@ def test_single_process_helpers_without_a_group():
     assert bench.job_throughput(10, 1, 2.0) == 5.0
 
 
+def test_c5_shape_from_the_per_rank_count():
+    """bench.c5_shape: groups of 8 on 3 lanes at the 1-GPU and 8-GPU per-rank counts, fewer lanes
+    below one group per lane, explicit values kept"""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.c5_shape(1024) == (3, 8) and bench.c5_shape(128) == (3, 8)
+    assert bench.c5_shape(8) == (1, 8) and bench.c5_shape(12) == (2, 8) and bench.c5_shape(1) == (1, 8)
+    assert bench.c5_shape(128, lanes=2) == (2, 8) and bench.c5_shape(128, group=4) == (3, 4)
+
+
 def test_c5_spawn_scatter_gather_two_ranks_gloo():
     """bench.py's C5 data path end to end on host buffers: shard.spawn_ranks starts 2 ranks with the
     rendezvous environment (what `bench.py --gpus 2` does without a launcher), rank 0 scatters
