@@ -435,6 +435,18 @@ __device__ __forceinline__ void resolve_limb(const KArgs& a, int y, int& poly, i
   row = i < m.split ? m.first_a + i : m.first_b + (i - m.split);
 }
 
+// which arithmetic a pass instantiates: both with a per-limb (wave-uniform) branch, or one alone
+constexpr int kKindAny = 0, kKindInt = 1, kKindF64 = 2;
+#ifndef PHX_NTT_SPLIT
+#define PHX_NTT_SPLIT 1
+#endif
+// processed limb y of the batch takes the FP64 path (q < 2^50); workgroup-uniform
+__device__ __forceinline__ bool limb_is_f64(const KArgs& a, int y) {
+  int poly, buf_limb, row;
+  resolve_limb(a, y, poly, buf_limb, row);
+  return a.modulus[__builtin_amdgcn_readfirstlane(row)] < (1ull << 50);
+}
+
 struct LimbCtx {
   uint64_t q;
   double qd, qinv;
@@ -547,8 +559,14 @@ __device__ __forceinline__ void epilogue_store(const KArgs& a, const TileRef& tr
 // epilogue's row pass.  One element per group (loads of the next element in flight) at 3 waves
 // (158 VGPRs, no spill) beat 4 per group at 2 waves (234 VGPRs): C3 relinearize 0.274-0.288 ->
 // 0.268-0.274 ms, bootstrap 23.41-23.57 -> 23.17-23.37 ms (profiles/r03/ks_waves/).
-constexpr int kKsKC = 1, kKsWaves = 3;
-constexpr int kKspWaves = 2;  // ... and of the inverse row pass with the key-switch prologue
+#ifndef PHX_KS_WAVES
+#define PHX_KS_WAVES 3
+#endif
+#ifndef PHX_KSP_WAVES
+#define PHX_KSP_WAVES 2
+#endif
+constexpr int kKsKC = 1, kKsWaves = PHX_KS_WAVES;
+constexpr int kKspWaves = PHX_KSP_WAVES;  // ... and of the inverse row pass with the key-switch prologue
 #ifndef PHX_EPI_WAVES
 #define PHX_EPI_WAVES 3
 #endif
@@ -792,7 +810,7 @@ template <int S1_LOG>
 constexpr int col_lds_words() { return (Sub<S1_LOG>::S + Sub<S1_LOG>::S / 16) * COLS; }
 
 // One column tile (the calling workgroup's threads tid < NT; `lds`: col_lds_words words).
-template <int S1_LOG, int S2_LOG, bool FWD, bool BCV, bool LZ, bool IO>
+template <int S1_LOG, int S2_LOG, bool FWD, bool BCV, bool LZ, int KIND>
 __device__ __forceinline__ void col_tile(const KArgs& a, int tile, uint64_t* lds, [[maybe_unused]] int sslot) {
   using SB = Sub<S1_LOG>;
   using P = Plan<S1_LOG, S2_LOG>;
@@ -819,7 +837,7 @@ __device__ __forceinline__ void col_tile(const KArgs& a, int tile, uint64_t* lds
 #pragma unroll
       for (int j = 0; j < E; ++j) x[j] = barrett_reduce_64(x[j], lc.q, r1);
     }
-    if (!IO && lc.f64) {
+    if (KIND == kKindF64 || (KIND == kKindAny && lc.f64)) {
       const double* tab = a.col + (size_t)tr.row * SB::S;
       double w[RN][E];
       static_for<RN>([&](auto rc) {
@@ -912,7 +930,16 @@ __global__ __launch_bounds__(CBLOCK, BCV ? 2 : IO ? kIoColWaves : kNttWavesPerEU
   if (tile >= a.limbs * CT) return;
   [[maybe_unused]] const int sslot = blockIdx.x * (CBLOCK / 64) + threadIdx.x / 64;
   if constexpr (FWD && !BCV) PHX_STAMP(sslot, 0, false);
-  col_tile<S1_LOG, S2_LOG, FWD, BCV, LZ, IO>(a, tile, lds, sslot);
+  if constexpr (IO) {
+    col_tile<S1_LOG, S2_LOG, FWD, BCV, LZ, kKindInt>(a, tile, lds, sslot);
+  } else if constexpr (PHX_NTT_SPLIT) {  // one code path per limb kind, chosen before any load
+    if (limb_is_f64(a, tile / CT))
+      col_tile<S1_LOG, S2_LOG, FWD, BCV, LZ, kKindF64>(a, tile, lds, sslot);
+    else
+      col_tile<S1_LOG, S2_LOG, FWD, BCV, LZ, kKindInt>(a, tile, lds, sslot);
+  } else {
+    col_tile<S1_LOG, S2_LOG, FWD, BCV, LZ, kKindAny>(a, tile, lds, sslot);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -965,7 +992,7 @@ struct RowShape {
 };
 
 // One row item (the calling wave's RW rows; lds: RowShape::LDS_WORDS words, tw0: RowShape::TW0).
-template <int S1_LOG, int S2_LOG, bool FWD, bool EPI, bool LZ, bool KS, bool IO>
+template <int S1_LOG, int S2_LOG, bool FWD, bool EPI, bool LZ, bool KS, int KIND>
 __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds, double* tw0,
                                          [[maybe_unused]] int sslot) {
   using SB = Sub<S2_LOG>;
@@ -991,7 +1018,7 @@ __device__ __forceinline__ void row_item(const KArgs& a, int item, uint64_t* lds
     const LimbCtx lc = limb_ctx(a, tr.row);
     uint64_t* dst = a.out + tr.off;
     [[maybe_unused]] EpiOperands eo;
-    if (!IO && lc.f64) {
+    if (KIND == kKindF64 || (KIND == kKindAny && lc.f64)) {
       const double* A = a.row_a + ((size_t)tr.row * S1 + r) * 16;
       const double* Bt = a.row_b + (size_t)tr.row * S2;
       // raw factors: round 0 (e = t + 1 + T k < 2^ER0) and every later round's slots
@@ -1180,7 +1207,16 @@ void ntt_row(KArgs a) {
   const int sslot = 0;
 #endif
   if constexpr (FWD && !EPI) PHX_STAMP(sslot, 0, false);
-  row_item<S1_LOG, S2_LOG, FWD, EPI, LZ, KS, IO>(a, item, lds, tw0, sslot);
+  if constexpr (IO) {
+    row_item<S1_LOG, S2_LOG, FWD, EPI, LZ, KS, kKindInt>(a, item, lds, tw0, sslot);
+  } else if constexpr (PHX_NTT_SPLIT) {  // one code path per limb kind, chosen before any load
+    if (limb_is_f64(a, item / RS::GROUPS))
+      row_item<S1_LOG, S2_LOG, FWD, EPI, LZ, KS, kKindF64>(a, item, lds, tw0, sslot);
+    else
+      row_item<S1_LOG, S2_LOG, FWD, EPI, LZ, KS, kKindInt>(a, item, lds, tw0, sslot);
+  } else {
+    row_item<S1_LOG, S2_LOG, FWD, EPI, LZ, KS, kKindAny>(a, item, lds, tw0, sslot);
+  }
 }
 // ---------------------------------------------------------------------------------------
 // 1-D path for small transforms, n = 2^8 .. 2^11 (the reference's radix-2 fnwt_1d / inwt_1d,
