@@ -30,6 +30,16 @@ size_t DevicePool::size_class(size_t bytes) {
   return c;
 }
 
+// The pool's events only order device work (hipStreamWaitEvent) and tell the host that a block's
+// last use has finished (hipEventQuery); nothing the host reads depends on them.  So they are
+// recorded without the system-scope release fence: with it, every record is a marker that writes
+// back the L2s before the stream's next kernel may start, and the frees of one operation (often
+// ten or more between two kernels) left 10-55 us idle gaps on the device per operation
+// (profiles/r06/pool_fence/).  Kernels end with a device-scope release, so a block's old contents
+// are in memory before its event completes.
+#ifndef PHX_POOL_SYSTEM_FENCE
+#define PHX_POOL_SYSTEM_FENCE 0
+#endif
 hipEvent_t DevicePool::take_event() {
   if (!spare_.empty()) {
     hipEvent_t e = spare_.back();
@@ -37,7 +47,7 @@ hipEvent_t DevicePool::take_event() {
     return e;
   }
   hipEvent_t e = nullptr;
-  PHX_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  PHX_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming | (PHX_POOL_SYSTEM_FENCE ? 0 : hipEventDisableSystemFence)));
   return e;
 }
 
@@ -54,19 +64,56 @@ static bool event_done(hipEvent_t e) {
 void DevicePool::add_use(Pending& pend, Use u) {
   for (Use& x : pend)
     if (x.first == u.first) {
-      if (u.seq > x.seq) std::swap(x, u);
-      spare_.push_back(u.second);  // the older of the two
+      if (u.stamp > x.stamp) x = u;
       return;
     }
   pend.push_back(u);
 }
 
+DevicePool::Use DevicePool::note_free(hipStream_t s) {
+  Stamps& st = stamps_[s];
+  st.dirty = true;
+  return Use{s, st.open};
+}
+
+void DevicePool::stamp_dirty() {
+  for (auto& kv : stamps_) {
+    Stamps& st = kv.second;
+    if (!st.dirty) continue;
+    hipEvent_t ev = take_event();
+    PHX_CHECK(hipEventRecord(ev, kv.first));
+    st.recorded.emplace_back(st.open, ev);
+    ++st.open;
+    st.dirty = false;
+  }
+}
+
+// a use is done when its stamp has completed; an unrecorded (open) stamp is not done
+bool DevicePool::use_done(const Use& u) {
+  Stamps& st = stamps_[u.first];
+  size_t k = 0;
+  while (u.stamp > st.done && k < st.recorded.size() && event_done(st.recorded[k].second)) {
+    st.done = st.recorded[k].first;
+    spare_.push_back(st.recorded[k].second);
+    ++k;
+  }
+  if (k) st.recorded.erase(st.recorded.begin(), st.recorded.begin() + static_cast<long>(k));
+  return u.stamp <= st.done;
+}
+
+void DevicePool::wait_use(hipStream_t s, const Use& u) {
+  if (use_done(u)) return;
+  for (const auto& r : stamps_[u.first].recorded)
+    if (r.first >= u.stamp) {  // (stamp_dirty ran first: the use's stamp is recorded)
+      PHX_CHECK(hipStreamWaitEvent(s, r.second, 0));
+      return;
+    }
+  PHX_CHECK(hipStreamSynchronize(u.first));  // (unreachable: an unrecorded stamp) wait on the host
+}
+
 void DevicePool::drop_done(Pending& pend) {
   for (size_t i = pend.size(); i-- > 0;)
-    if (event_done(pend[i].second)) {
-      spare_.push_back(pend[i].second);
-      pend.erase(pend.begin() + static_cast<long>(i));
-    }
+    if (use_done(pend[i])) pend.erase(pend.begin() + static_cast<long>(i));
 }
 
 // a block whose last uses were on `s` (stream order) or have completed may be reused on `s`
@@ -74,12 +121,10 @@ bool DevicePool::ready_for(Pending& pend, hipStream_t s) {
   bool ready = true;
   for (size_t i = pend.size(); i-- > 0;) {
     if (pend[i].first == s) continue;
-    if (event_done(pend[i].second)) {
-      spare_.push_back(pend[i].second);
+    if (use_done(pend[i]))
       pend.erase(pend.begin() + static_cast<long>(i));
-    } else {
+    else
       ready = false;
-    }
   }
   return ready;
 }
@@ -105,12 +150,13 @@ void DevicePool::note_live(long delta) {
 // `wait`, the best fit among all free blocks: `s` is made to wait (on the device) for the pending
 // uses of the block on other streams, as a stream-ordered allocator reuses another stream's block.
 void* DevicePool::carve(int dev, size_t c, hipStream_t s, bool wait) {
+  if (wait) stamp_dirty();  // (frees may have come in while grow() had the lock released)
   for (auto it = by_size_.lower_bound({dev, c}); it != by_size_.end() && it->first.first == dev; ++it) {
     Block* b = it->second;
     if (!ready_for(b->pending, s)) {
       if (!wait) continue;
-      for (auto& pe : b->pending)
-        if (pe.first != s) PHX_CHECK(hipStreamWaitEvent(s, pe.second, 0));
+      for (const Use& u : b->pending)
+        if (u.first != s) wait_use(s, u);
     }
     by_size_.erase(it);
     if (b->size > c) {  // the remainder stays free with the pending uses of the whole block
@@ -123,8 +169,7 @@ void* DevicePool::carve(int dev, size_t c, hipStream_t s, bool wait) {
       insert_free(r);
       b->size = c;
     }
-    for (auto& pe : b->pending) spare_.push_back(pe.second);  // (all on `s`: stream order covers them)
-    b->pending.clear();
+    b->pending.clear();  // (all on `s`, or waited for: stream order covers them)
     b->free = false;
     b->req = c;
     void* p = b->chunk->base + b->off;
@@ -172,17 +217,19 @@ void DevicePool::forget_stream(hipStream_t s) {
     for (Small& b : kv.second)
       if (b.stream == s) {
         // the caller has synchronised s: its blocks are free for any stream from now on
-        if (b.ev) spare_.push_back(b.ev);
-        b.ev = nullptr;
+        b.stamp = 0;
         b.stream = nullptr;
       }
   for (auto& kv : by_size_) {
     Pending& pend = kv.second->pending;
     for (size_t i = pend.size(); i-- > 0;)
-      if (pend[i].first == s) {
-        spare_.push_back(pend[i].second);
-        pend.erase(pend.begin() + static_cast<long>(i));
-      }
+      if (pend[i].first == s) pend.erase(pend.begin() + static_cast<long>(i));
+  }
+  // (a later stream may reuse the handle value: it starts with fresh stamps)
+  auto it = stamps_.find(s);
+  if (it != stamps_.end()) {
+    for (auto& r : it->second.recorded) spare_.push_back(r.second);
+    stamps_.erase(it);
   }
 }
 
@@ -202,11 +249,10 @@ void DevicePool::release_cached_locked() {
   for (auto& kv : small_free_) {
     std::vector<Small> keep;
     for (Small& b : kv.second) {
-      if (b.ev && !event_done(b.ev)) {
+      if (b.stamp && !use_done(Use{b.stream, b.stamp})) {
         keep.push_back(b);
         continue;
       }
-      if (b.ev) spare_.push_back(b.ev);
       (void)hipFree(b.p);
       st_.held -= kv.first.second;
       freed += kv.first.second;
@@ -238,6 +284,7 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
   if (bytes >= kArenaMin) {
     const size_t c = (bytes + kGrain - 1) / kGrain * kGrain;
     std::unique_lock<std::mutex> lk(mu_);
+    stamp_dirty();
     if (void* p = carve(dev, c, s)) return p;
     // Free blocks that are still in use by other streams: once the cached space exceeds the slack,
     // reuse one behind a device-side wait instead of growing (the held memory then tracks the live
@@ -251,7 +298,8 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
     release_cached_locked();
     if (grow(dev, c, lk)) return carve(dev, c, s);
     if (void* p = carve(dev, c, s, true)) return p;
-    PHX_CHECK(hipDeviceSynchronize());
+    stamp_dirty();
+    PHX_CHECK(hipDeviceSynchronize());  // every stamp recorded so far completes
     if (void* p = carve(dev, c, s)) return p;
     release_cached_locked();
     if (!grow(dev, c, lk)) PHX_CHECK(hipErrorOutOfMemory);
@@ -260,15 +308,15 @@ void* DevicePool::alloc(size_t bytes, hipStream_t s) {
   const size_t c = size_class(bytes);
   {
     std::lock_guard<std::mutex> lk(mu_);
+    stamp_dirty();
     auto it = small_free_.find({dev, c});
     if (it != small_free_.end()) {
       auto& v = it->second;
       for (size_t i = v.size(); i-- > 0;) {
         Small& b = v[i];
-        const bool ready = !b.ev || b.stream == s || event_done(b.ev);
+        const bool ready = !b.stamp || b.stream == s || use_done(Use{b.stream, b.stamp});
         if (!ready) continue;
         void* p = b.p;
-        if (b.ev) spare_.push_back(b.ev);
         v.erase(v.begin() + static_cast<long>(i));
         small_live_[p] = c;
         note_live(static_cast<long>(c));
@@ -314,11 +362,7 @@ void DevicePool::free(void* p, size_t bytes, hipStream_t s, bool completed) {
 #endif
     b->free = true;
     b->req = 0;
-    if (!completed) {
-      hipEvent_t ev = take_event();
-      PHX_CHECK(hipEventRecord(ev, s));
-      add_use(b->pending, Use{s, ev, ++seq_});
-    }
+    if (!completed) add_use(b->pending, note_free(s));
     // coalesce with free neighbours (their pending uses move into the merged block)
     auto& blocks = b->chunk->blocks;
     auto me = blocks.find(b->off);
@@ -356,14 +400,11 @@ void DevicePool::free(void* p, size_t bytes, hipStream_t s, bool completed) {
   const size_t cls = it->second;
   small_live_.erase(it);
   note_live(-static_cast<long>(cls));
-  Small b{p, s, nullptr};
+  Small b{p, s, 0};
 #ifdef PHX_GUARD
   if (!completed) PHX_CHECK(hipMemsetAsync(p, 0xFF, cls, s));
 #endif
-  if (!completed) {
-    b.ev = take_event();
-    PHX_CHECK(hipEventRecord(b.ev, s));
-  }
+  if (!completed) b.stamp = note_free(s).stamp;
   small_free_[{dev, cls}].push_back(b);
 }
 

@@ -54,18 +54,27 @@ class DevicePool {
   static constexpr size_t kSlackMin = size_t(2) << 30;  // cached arena space kept before waiting on reuse
 
  private:
-  // uses a block may still have: at most one per stream, the newest (an event recorded later on a
-  // stream completes after every earlier one there, so it alone covers the stream's uses)
+  // Uses a block may still have: at most one per stream, the newest.  A use is a stream and a
+  // stamp number: the free happened before that stream's stamp `stamp` (a marker event recorded on
+  // the stream after the free; a stream's stamps complete in order).  Frees only take the stream's
+  // open stamp number; the event is recorded once for all the frees since the last one, when the
+  // pool is next asked for memory (stamp_dirty), so a burst of frees costs one marker on the
+  // device instead of one each.
   struct Use {
     hipStream_t first;
-    hipEvent_t second;
-    uint64_t seq;  // record order (seq_)
+    uint64_t stamp;
   };
   using Pending = std::vector<Use>;
+  struct Stamps {
+    uint64_t open = 1;   // the stamp the next frees belong to (not recorded yet)
+    uint64_t done = 0;   // every stamp up to this one has completed
+    bool dirty = false;  // frees took `open` since it was last recorded
+    std::vector<std::pair<uint64_t, hipEvent_t>> recorded;  // in flight, oldest first
+  };
   struct Small {
     void* p;
     hipStream_t stream;
-    hipEvent_t ev;  // null when known complete
+    uint64_t stamp;  // 0 when known complete
   };
   struct Chunk;
   struct Block {
@@ -90,13 +99,17 @@ class DevicePool {
   std::multimap<std::pair<int, size_t>, Block*> by_size_;  // free arena blocks by (device, size)
   std::map<void*, Block*> live_;                           // handed-out arena blocks
   std::vector<hipEvent_t> spare_;
-  uint64_t seq_ = 0;
+  std::map<hipStream_t, Stamps> stamps_;
   Stats st_;
   static size_t size_class(size_t bytes);
   hipEvent_t take_event();
   bool ready_for(Pending& pend, hipStream_t s);  // drops completed uses
   void drop_done(Pending& pend);
   void add_use(Pending& pend, Use u);  // keeps the newest use per stream
+  Use note_free(hipStream_t s);        // the use a free on `s` leaves
+  void stamp_dirty();                  // records the open stamp of every stream with frees since its last
+  bool use_done(const Use& u);
+  void wait_use(hipStream_t s, const Use& u);  // device-side: `s` waits for the stamp of u
   Chunk* add_chunk(int dev, void* p, size_t sz);
   void insert_free(Block* b);
   void erase_free(Block* b);

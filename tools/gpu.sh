@@ -57,6 +57,17 @@ step_profboot() {  # kernel trace of ONE warm bootstrap and ONE lockstep group o
   local rc=$?; tail -2 "$OUT/profboot.log"; [ $rc -eq 0 ] || return $rc
   $PY tools/prof_windows.py "$(find "$OUT/profboot" -name '*kernel_trace.csv' | head -1)" "$OUT/boot_window"
 }
+step_proftrace() {  # kernel + HIP runtime trace of ONE warm bootstrap and ONE lockstep group of $GROUP
+  (cd /tmp && timeout -k 10 ${T_STATS:-300} rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv \
+     -d "$OUT/proftrace" -o run -- "$GRAFT_REPO_ROOT/phantom-fhe-boot_amd/bin/bootstrapping_example" prof 16 ${GROUP:-4} \
+     > "$OUT/proftrace.log" 2>&1)
+  local rc=$?; tail -2 "$OUT/proftrace.log"; return $rc
+}
+step_gaps() {  # idle gaps between kernels of the one-bootstrap window and of the group window of profboot
+  local t; t=$(find "$OUT/profboot" -name '*kernel_trace.csv' | head -1)
+  echo "single: $($PY tools/kernel_gaps.py "$t" -2)" | tee "$OUT/gaps.txt"
+  echo "group:  $($PY tools/kernel_gaps.py "$t" -1)" | tee -a "$OUT/gaps.txt"
+}
 step_profpmc() {  # FETCH_SIZE per dispatch over the same run (lt_bsgs_wide vs lt_bsgs_group)
   (cd /tmp && timeout -s KILL ${T_PMC:-240} rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv \
      -d "$OUT/profpmc" -o run -- "$GRAFT_REPO_ROOT/phantom-fhe-boot_amd/bin/bootstrapping_example" prof 16 ${GROUP:-4} \
