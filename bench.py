@@ -443,7 +443,7 @@ def c5_leg(dist, torch, world, rank, local_rank, total=1024, lanes=None, chain=2
 # HBM bytes per forward-NTT launch (column + row pass) from PMC counters: FETCH_SIZE and
 # WRITE_SIZE collected in separate rocprofv3 --pmc passes over the same NTT shape
 # (tools/gpu_pmc_traffic.sh), gfx950 FETCH_SIZE correction applied (tools/pmc_traffic.py).
-PMC_TRAFFIC_FILE = "profiles/r05/c2/ntt_pmc_traffic.json"
+PMC_TRAFFIC_FILE = "profiles/r06/c2/ntt_pmc_traffic.json"
 
 
 def pmc_traffic():
@@ -457,7 +457,7 @@ def pmc_traffic():
 
 # rocprofv3 kernel-trace average durations of the forward's two kernels at HEAD (bench.py's own C2
 # command profiled on MI355X): fwd_ms minus their sum is the column -> row launch gap
-KERNEL_SUM_SOURCE = "profiles/r05/c2/c2_fwd_kernels.json"
+KERNEL_SUM_SOURCE = "profiles/r06/c2/c2_fwd_kernels.json"
 
 
 def _kernel_sum_ms():
