@@ -225,3 +225,23 @@ def test_forward_fuse_moddown(rng, c3):
         diff = (cx[sl].astype(object) - nd[sl].astype(object)) % q
         want[sl] = (diff * pinv[l] % q).astype(np.uint64)
     assert np.array_equal(to_host(dct), want)
+
+
+@pytest.mark.parametrize("limbs,bits", [(264, 59), (256, 60)])
+def test_ntt_large_integer_batches(rng, limbs, bits):
+    """a C5-sized launch (a lockstep group's 256-480 limbs) of integer-only limbs below 2^60 (the
+    IO kernels), in place: forward, inverse of the result, and inverse of arbitrary canonical data
+    == the oracle (a one-workgroup-per-limb kernel, round 6, passed this and was slower: removed,
+    profiles/r06/ntt_limb/)"""
+    n = 1 << 16
+    mods = O.coeff_modulus_create(n, [bits] * limbs)
+    t = PA.NttTables(n, mods)
+    a = O.random_limbs(rng, n, mods)
+    d = to_dev(a)
+    _fwd(t, d, limbs)
+    assert np.array_equal(to_host(d), O.ntt_fwd(a, n, mods))
+    _inv(t, d, limbs)
+    assert np.array_equal(to_host(d), a)
+    d2 = to_dev(a)
+    _inv(t, d2, limbs)
+    assert np.array_equal(to_host(d2), O.ntt_inv(a, n, mods))

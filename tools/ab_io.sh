@@ -7,7 +7,8 @@ cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${TAG:-abio}; mkdir -p $OUT
 VARS=${VARS:-base}
 PYS=""; for v in $VARS; do PYS="$PYS tools/variants/$v/py"; done; PYS="$PYS phantom-fhe-boot_amd/py"
-for cfg in "60 1" "60 3" "50 1"; do
+IFS=';' read -ra CFGS <<< "${NTT_CFGS:-60 1;60 3;50 1}"
+for cfg in "${CFGS[@]}"; do
   set -- $cfg
   NTT_BITS=$1 NTT_REP=$2 timeout -k 10 400 python3 tools/ntt_ab.py $PYS > $OUT/ntt$1x$2.txt 2>&1 || { tail $OUT/ntt$1x$2.txt; exit 1; }
   tail -1 $OUT/ntt$1x$2.txt
