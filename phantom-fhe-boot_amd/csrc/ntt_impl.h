@@ -43,13 +43,16 @@
 namespace phx {
 namespace nttd {  // the 2-D NTT kernels and launch<>; ntt.hip dispatches, ntt_n*.hip instantiate
 
-constexpr int E_LOG = 4;  // elements per thread per round = 16 (radix-16 rounds)
+#ifndef PHX_E_LOG
+#define PHX_E_LOG 4
+#endif
+constexpr int E_LOG = PHX_E_LOG;  // elements per thread per round = 16 (radix-16 rounds)
 constexpr int E = 1 << E_LOG;
 // columns per column-pass tile: 16 x 8 B = one 128 B line per row (8 / 16 / 32 measured 36.7 /
 // 26.6 / 28.4 us for the 50-bit forward, profiles/r03/ntt_experiments/cols_*.txt)
 constexpr int COLS = 16;
 constexpr int BLOCK = 256;
-constexpr int CBLOCK = COLS * 16 > BLOCK ? COLS * 16 : BLOCK;  // column-pass workgroup bound
+constexpr int CBLOCK = COLS * (256 >> E_LOG) > BLOCK ? COLS * (256 >> E_LOG) : BLOCK;  // column-pass workgroup bound (S1 <= 256)
 constexpr int kNttWavesPerEU = 3;  // __launch_bounds__ occupancy target (waves per SIMD) of one-tile grids
 #ifndef PHX_ROW_WAVES
 #define PHX_ROW_WAVES 3
