@@ -249,7 +249,8 @@ int phantom_boot_run_grouped(phantom_boot_session* s, const uint8_t* dev_in, siz
   PHX_CAPI_GUARD({
     auto& b = session(s);
     if ((!dev_in || !dev_out) && count) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null pointer");
-    if (group < 1 || group > 8) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "group must be 1..8");
+    if (group < 1 || group > phx::kLtGroupMax)
+      return fail(PHANTOM_ERR_INVALID_ARGUMENT, "group must be 1..kLtGroupMax");
     std::vector<PhantomCiphertext> in;
     in.reserve(count);
     for (size_t i = 0; i < count; ++i) in.push_back(load_device(*b.ctx, dev_in + i * in_stride, in_stride));

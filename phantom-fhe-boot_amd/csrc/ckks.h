@@ -63,7 +63,10 @@ hipError_t lt_bsgs(const LtArgs& a, size_t n, hipStream_t s);
 // contiguous (baby j at baby0[c] + j baby_stride words), its inner sum 0 goes to acc[c] and inner
 // sum i >= 1 to giant1[c] + (i - 1) giant_stride; g == 32, b <= 8 (the bootstrap's levels).  Each
 // result equals its own lt_bsgs, bit for bit.
-constexpr int kLtGroupMax = 8;
+#ifndef PHX_GROUP_MAX
+#define PHX_GROUP_MAX 8  // ciphertexts of one lockstep group (the grouped kernels' argument arrays)
+#endif
+constexpr int kLtGroupMax = PHX_GROUP_MAX;
 struct LtGroupArgs {
   const uint64_t* const* pts = nullptr;
   const uint64_t* q = nullptr;

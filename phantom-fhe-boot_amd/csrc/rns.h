@@ -194,7 +194,10 @@ hipError_t keyswitch_rotate(const KsRotateArgs& a, int mode, size_t n, hipStream
 // keyswitch_rotate of `count` (2..kKsGroupMax) ciphertexts by the same rotation (evk, perm) in one
 // launch, their workgroups of an output block on one XCD so that the key is read from HBM about
 // once for all; each result equals its own keyswitch_rotate, bit for bit
-constexpr int kKsGroupMax = 8;
+#ifndef PHX_GROUP_MAX
+#define PHX_GROUP_MAX 8  // ciphertexts of one lockstep group (the grouped kernels' argument arrays)
+#endif
+constexpr int kKsGroupMax = PHX_GROUP_MAX;
 struct KsRotateGroupArgs {
   KsRotateArgs a[kKsGroupMax];
   int count = 1;

@@ -12,7 +12,8 @@ import bench  # noqa: E402
 
 torch.cuda.set_device(0)
 lanes = int(os.environ.get("C5_LANES", "3"))
-r = bench.c5_leg(None, torch, 1, 0, 0, total=int(os.environ.get("C5_TOTAL", "384")), lanes=lanes, verify=8)
+group = int(os.environ["C5_GROUP"]) if os.environ.get("C5_GROUP") else None
+r = bench.c5_leg(None, torch, 1, 0, 0, total=int(os.environ.get("C5_TOTAL", "384")), lanes=lanes, verify=8, group=group)
 free, total = torch.cuda.mem_get_info()
-print(os.path.basename(os.path.dirname(os.path.abspath(sys.argv[1]))), r["bootstraps_per_s"], r["min_avg_bits"],
+print(os.path.basename(os.path.dirname(os.path.abspath(sys.argv[1]))), lanes, r["lockstep_group"], r["bootstraps_per_s"], r["min_avg_bits"],
       "used_GiB %.1f" % ((total - free) / 2**30), flush=True)
