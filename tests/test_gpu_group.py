@@ -54,9 +54,10 @@ def _keys(rng, ctx):
     return keys, [to_dev(k) for k in keys]
 
 
-@pytest.mark.parametrize("chain,b,group", [(2, 8, 2), (3, 8, 4), (17, 8, 8), (18, 3, 8)])
+@pytest.mark.parametrize("chain,b,group", [(2, 8, 2), (3, 8, 4), (17, 8, 8), (18, 3, 8), (2, 8, 5), (18, 3, 7)])
 def test_lt_bsgs_group(c4, rng, chain, b, group):
-    """inner sums of `group` ciphertexts in one launch == or_lt_bsgs per ciphertext"""
+    """inner sums of `group` ciphertexts in one launch == or_lt_bsgs per ciphertext (odd group sizes:
+    the balanced lockstep groups of EvalBootstrapBatch)"""
     g = 32
     em = _ext_mods(c4, chain)
     W = 2 * len(em) * N
@@ -84,7 +85,7 @@ def test_lt_bsgs_group(c4, rng, chain, b, group):
             assert np.array_equal(giants[(i - 1) * W:i * W], want[i]), (c, i)
 
 
-@pytest.mark.parametrize("bits,b,group", [(61, 8, 2), (61, 3, 4), (59, 8, 4)])
+@pytest.mark.parametrize("bits,b,group", [(61, 8, 2), (61, 3, 3), (59, 8, 4)])
 def test_lt_bsgs_group_moduli(rng, bits, b, group):
     """grouped inner sums at the split partial sums' bounds: N = 4096, 8 + 2 moduli of `bits` bits
     (61-bit: folded every 4 products, LtGroupArgs::q60 = 0) == or_lt_bsgs per ciphertext"""
