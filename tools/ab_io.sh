@@ -13,7 +13,7 @@ for cfg in "${CFGS[@]}"; do
   NTT_BITS=$1 NTT_REP=$2 timeout -k 10 400 python3 tools/ntt_ab.py $PYS > $OUT/ntt$1x$2.txt 2>&1 || { tail $OUT/ntt$1x$2.txt; exit 1; }
   tail -1 $OUT/ntt$1x$2.txt
 done
-[ -n "$NO_C3" ] || for i in 1 2; do for v in $PYS; do
+[ -n "$NO_C3" ] || for i in $(seq 1 ${C3_REPS:-2}); do for v in $PYS; do
   timeout -k 10 200 python3 tools/time_c3.py $v 2>&1 | grep -v amdgpu.ids | tail -1 | tee -a $OUT/c3.txt || exit 1
 done; done
 [ -n "$NO_BOOT" ] || for i in 1 2; do for v in $VARS cur; do
