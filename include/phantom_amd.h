@@ -110,6 +110,11 @@ typedef struct phantom_context phantom_context;
 int phantom_context_create(size_t poly_modulus_degree, const uint64_t *moduli, size_t count,
                            size_t special_modulus_size, phantom_context **out);
 int phantom_context_destroy(phantom_context *ctx);
+/* Opt-in extension, no reference counterpart: on != 0 makes every moddown (and moddown +
+ * rescale) mean-unbiased by adding floor(ibase / 2) to each output coefficient (DESIGN.md §3,
+ * "Where the precision goes"); 0 (the default) restores the reference's arithmetic bit for bit.
+ * Also set by PHX_UNBIASED_MODDOWN=1 at phantom_context_create. */
+int phantom_context_set_unbiased_moddown(phantom_context *ctx, int on);
 /* number of data primes at chain_index (chain 0 = key level Q u P, 1 = Q, ...) */
 size_t phantom_context_coeff_modulus_size(const phantom_context *ctx, size_t chain_index);
 

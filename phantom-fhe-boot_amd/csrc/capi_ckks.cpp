@@ -91,6 +91,14 @@ int phantom_context_destroy(phantom_context* ctx) {
   return PHANTOM_OK;
 }
 
+int phantom_context_set_unbiased_moddown(phantom_context* ctx, int on) {
+  PHX_CAPI_GUARD({
+    if (!ctx) return fail(PHANTOM_ERR_INVALID_ARGUMENT, "null context");
+    ctx->ctx->set_unbiased_moddown(on != 0);
+    return PHANTOM_OK;
+  });
+}
+
 size_t phantom_context_coeff_modulus_size(const phantom_context* ctx, size_t chain_index) {
   if (!ctx || chain_index >= ctx->ctx->total_parm_size()) return 0;
   return ctx->ctx->get_context_data(chain_index).coeff_modulus_size();

@@ -30,6 +30,9 @@ hipError_t sample_ternary(uint64_t* out, const uint64_t* q, size_t n, size_t L, 
 // out[l][k] = in[l][k] * c[l] mod q[l] + (acc ? acc[l][k] : 0), Shoup constants c/c_shoup per limb
 hipError_t mul_scalar_add(const uint64_t* in, const uint64_t* c, const uint64_t* c_shoup, const uint64_t* acc,
                           uint64_t* out, const uint64_t* q, size_t n, size_t L, hipStream_t s);
+// out[p][l][k] += in[l][k] * c[l] mod q[l] for p < polys (out[p] at p poly_stride), one launch
+hipError_t mul_scalar_accumulate(const uint64_t* in, const uint64_t* c, const uint64_t* c_shoup, uint64_t* out,
+                                 size_t poly_stride, size_t polys, const uint64_t* q, size_t n, size_t L, hipStream_t s);
 
 }  // namespace phx
 

@@ -91,7 +91,11 @@ __global__ __launch_bounds__(kBlock) void small_kernel(uint64_t* out, const uint
 
 __global__ __launch_bounds__(kBlock) void mul_scalar_add_kernel(const uint64_t* in, const uint64_t* c,
                                                                 const uint64_t* cs, const uint64_t* acc, uint64_t* out,
-                                                                const uint64_t* q, uint32_t log_n, size_t total) {
+                                                                const uint64_t* q, uint32_t log_n, size_t total,
+                                                                size_t poly_stride) {
+  // blockIdx.y: polynomial (acc and out at y poly_stride; `in` shared)
+  if (acc) acc += blockIdx.y * poly_stride;
+  out += blockIdx.y * poly_stride;
   for (size_t e = blockIdx.x * (size_t)kBlock + threadIdx.x; e < total; e += (size_t)gridDim.x * kBlock) {
     const uint32_t l = static_cast<uint32_t>(e >> log_n);
     const uint64_t ql = q[l];
@@ -638,7 +642,16 @@ hipError_t sample_ternary(uint64_t* out, const uint64_t* q, size_t n, size_t L, 
 hipError_t mul_scalar_add(const uint64_t* in, const uint64_t* c, const uint64_t* c_shoup, const uint64_t* acc,
                           uint64_t* out, const uint64_t* q, size_t n, size_t L, hipStream_t s) {
   const size_t total = n * L;
-  mul_scalar_add_kernel<<<grid_for(total), kBlock, 0, s>>>(in, c, c_shoup, acc, out, q, __builtin_ctzll(n), total);
+  mul_scalar_add_kernel<<<grid_for(total), kBlock, 0, s>>>(in, c, c_shoup, acc, out, q, __builtin_ctzll(n), total, 0);
+  return hipGetLastError();
+}
+
+hipError_t mul_scalar_accumulate(const uint64_t* in, const uint64_t* c, const uint64_t* c_shoup, uint64_t* out,
+                                 size_t poly_stride, size_t polys, const uint64_t* q, size_t n, size_t L, hipStream_t s) {
+  const size_t total = n * L;
+  if (polys == 0 || total == 0) return hipSuccess;
+  const dim3 grid(static_cast<unsigned>(std::max<size_t>(1, grid_for(total) / polys)), static_cast<unsigned>(polys));
+  mul_scalar_add_kernel<<<grid, kBlock, 0, s>>>(in, c, c_shoup, out, out, q, __builtin_ctzll(n), total, poly_stride);
   return hipGetLastError();
 }
 

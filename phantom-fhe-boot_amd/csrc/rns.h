@@ -148,6 +148,7 @@ struct ModdownModupConsts {
   const uint64_t* pinv_shoup;
   const uint64_t* hatinv;
   const uint64_t* hatinv_shoup;
+  uint64_t bias = 0;  // added to every output coefficient (the opt-in unbiased moddown; 0 = off)
 };
 // `polys` independent ones per launch: c1 at p c1_stride, t_mod_up at p mod_up_stride, delta and
 // t_cks contiguous [polys][size_ql][n]

@@ -649,8 +649,12 @@ __global__ __launch_bounds__(kBlock) void moddown_modup_finish_kernel(const uint
     const uint32_t l = static_cast<uint32_t>(e >> log_n);
     const uint64_t m = k.q[l];
     const u64x2 c = ld2(c1 + e), d = ld2(delta + e);
-    const uint64_t yx = mul_shoup(sub_mod(c.x, d.x, m), k.pinv[l], k.pinv_shoup[l], m);
-    const uint64_t yy = mul_shoup(sub_mod(c.y, d.y, m), k.pinv[l], k.pinv_shoup[l], m);
+    uint64_t yx = mul_shoup(sub_mod(c.x, d.x, m), k.pinv[l], k.pinv_shoup[l], m);
+    uint64_t yy = mul_shoup(sub_mod(c.y, d.y, m), k.pinv[l], k.pinv_shoup[l], m);
+    if (k.bias) {  // uniform: the opt-in unbiased moddown
+      yx = add_mod(yx, k.bias, m);
+      yy = add_mod(yy, k.bias, m);
+    }
     st2(t_mod_up + (l / alpha) * qlp_n + e, yx, yy);
     st2(t_cks + e, mul_shoup(yx, k.hatinv[l], k.hatinv_shoup[l], m), mul_shoup(yy, k.hatinv[l], k.hatinv_shoup[l], m));
   }

@@ -1,6 +1,7 @@
 #include "context.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <thread>
 
@@ -78,6 +79,20 @@ PhantomContext::PhantomContext(const EncryptionParameters& params, hipStream_t s
     data_[c]->set_rns_tool(std::move(tools[c]));
   }
   PHX_CHECK(hipStreamSynchronize(s));
+  if (const char* e = std::getenv("PHX_UNBIASED_MODDOWN"); e && e[0] == '1') set_unbiased_moddown(true);
+}
+
+void PhantomContext::set_unbiased_moddown(bool on) {
+  hipStream_t s = stream_.s;
+  if (on && !ones_ntt_.get()) {
+    std::vector<uint64_t> h(size_Q_ * n_, 1);
+    ones_ntt_.upload(h, s);
+    PHX_CHECK(phx::ntt_forward(ntt_->get(), ones_ntt_.get(), ones_ntt_.get(),
+                               phx::LimbMap::contiguous(static_cast<int>(size_Q_), 0), s));
+  }
+  for (size_t c = 1; c <= size_Q_; ++c) data_[c]->gpu_rns_tool_mutable().set_unbias(on ? ones_ntt_.get() : nullptr, s);
+  PHX_CHECK(hipStreamSynchronize(s));
+  unbiased_ = on;
 }
 
 std::vector<uint32_t> PhantomContext::key_galois_elts() const {

@@ -58,6 +58,7 @@ class ContextData {
   const std::vector<uint64_t>& moduli() const { return moduli_; }
   size_t coeff_modulus_size() const { return moduli_.size(); }
   const RnsTool& gpu_rns_tool() const { return *rns_tool_; }
+  RnsTool& gpu_rns_tool_mutable() { return *rns_tool_; }
   bool has_rns_tool() const { return rns_tool_ != nullptr; }
   void set_rns_tool(std::unique_ptr<RnsTool> t) { rns_tool_ = std::move(t); }
 
@@ -177,6 +178,12 @@ class PhantomContext {
   // NTT(X^power) over the first L key moduli ([L][n]), cached per context
   const uint64_t* monomial_ntt(uint32_t power, size_t L) const;
 
+  // Opt-in mean-unbiased moddowns at every level (RnsTool::set_unbias): off by default, where each
+  // division is the reference's bit for bit.  PHX_UNBIASED_MODDOWN=1 in the environment turns it
+  // on at construction.  Call between operations, not while work on other streams is in flight.
+  void set_unbiased_moddown(bool on);
+  bool unbiased_moddown() const { return unbiased_; }
+
  private:
   OwnedStream stream_;  // first members: destroyed after everything that frees on them
   OwnedStream aux_[kLanes][kAuxStreams];
@@ -190,6 +197,8 @@ class PhantomContext {
   mutable std::mutex cache_mu_;
   mutable std::map<uint32_t, DeviceBuffer<uint32_t>> perms_;
   mutable std::map<std::pair<uint32_t, size_t>, DeviceBuffer<uint64_t>> monomials_;
+  DeviceBuffer<uint64_t> ones_ntt_;  // NTT(1, ..., 1) over Q, for the unbiased moddown
+  bool unbiased_ = false;
 };
 
 // runs the calling thread on lane `lane` of `cc`: its main stream (StreamScope) and aux streams

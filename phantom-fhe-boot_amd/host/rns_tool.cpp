@@ -6,13 +6,13 @@
 #include <stdexcept>
 
 #include "numth.h"
+#include "../csrc/ckks.h"
 
 #ifndef PHX_DIAG_CENTRED
 #define PHX_DIAG_CENTRED 0
 #endif
 #if PHX_DIAG_CENTRED
 #include <cstdio>
-#include "../csrc/ckks.h"
 #endif
 
 namespace phantom {
@@ -414,14 +414,15 @@ void RnsTool::moddown_add(uint64_t* ct, uint64_t* cx, bool accumulate, const phx
       bcv.ib[p] = (int)size_P_;
     }
     hip_ok(phx::ntt_forward_bconv(ntt, delta, dm, bcv, epi, s), "moddown bconv + NTT + finish");
-    return;
+  } else {
+    phx::BconvArgs ba = p_to_ql_.args(cp, delta, false);
+    ba.polys = np;
+    ba.in_stride = size_QlP * n_;
+    ba.out_stride = size_Ql * n_;
+    hip_ok(phx::bconv(ba, n_, s), "moddown bconv");
+    hip_ok(phx::ntt_forward_fused(ntt, delta, delta, dm, nullptr, 0, epi, s), "moddown NTT + finish");
   }
-  phx::BconvArgs ba = p_to_ql_.args(cp, delta, false);
-  ba.polys = np;
-  ba.in_stride = size_QlP * n_;
-  ba.out_stride = size_Ql * n_;
-  hip_ok(phx::bconv(ba, n_, s), "moddown bconv");
-  hip_ok(phx::ntt_forward_fused(ntt, delta, delta, dm, nullptr, 0, epi, s), "moddown NTT + finish");
+  if (unbiased()) unbias_ntt(ct, polys, size_Ql, size_Ql * n_, false, s);
 }
 
 void RnsTool::moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTables& ntt, hipStream_t s, size_t count,
@@ -453,7 +454,7 @@ void RnsTool::moddown_modup(uint64_t* t_mod_up, uint64_t* c1, const phx::NttTabl
   hip_ok(phx::bconv(ba, n_, s), "moddown-modup bconv P");
   uint64_t* t_cks = ws_->get(s, Workspace::kModupInv, count * size_Ql * n_);
   phx::ModdownModupConsts k{d_Ql_.get(), d_bigPInv_mod_q_.get(), d_bigPInv_mod_q_shoup_.get(), d_partQlHatInv_.get(),
-                            d_partQlHatInv_shoup_.get()};
+                            d_partQlHatInv_shoup_.get(), unbiased() ? k_md_ : 0};
   hip_ok(phx::moddown_modup_finish(c1, delta, k, t_cks, t_mod_up, n_, size_Ql, size_QlP, alpha, s, count, c1_stride,
                                    beta * size_QlP * n_),
          "moddown-modup finish");
@@ -534,14 +535,47 @@ void RnsTool::moddown_rescale(uint64_t* out, uint64_t* cx, const phx::NttTables&
       bcv.ib[p] = (int)(1 + size_P_);
     }
     hip_ok(phx::ntt_forward_bconv(ntt, delta, om, bcv, epi, s), "moddown-rescale bconv + NTT + finish");
-    return;
+  } else {
+    phx::BconvArgs ba = pq_to_ql1_.args(dropped, delta, false);
+    ba.polys = np;
+    ba.in_stride = size_QlP * n_;
+    ba.out_stride = Ln * n_;
+    hip_ok(phx::bconv(ba, n_, s), "moddown-rescale bconv");
+    hip_ok(phx::ntt_forward_fused(ntt, delta, delta, om, nullptr, 0, epi, s), "moddown-rescale NTT + finish");
   }
-  phx::BconvArgs ba = pq_to_ql1_.args(dropped, delta, false);
-  ba.polys = np;
-  ba.in_stride = size_QlP * n_;
-  ba.out_stride = Ln * n_;
-  hip_ok(phx::bconv(ba, n_, s), "moddown-rescale bconv");
-  hip_ok(phx::ntt_forward_fused(ntt, delta, delta, om, nullptr, 0, epi, s), "moddown-rescale NTT + finish");
+  if (unbiased()) {
+    if (epi.ks_prods > 1) {  // per-product outputs, [2][Ln][n] each
+      for (int k = 0; k < epi.ks_prods; ++k) unbias_ntt(epi.out_p[k], 2, Ln, Ln * n_, true, s);
+    } else {
+      unbias_ntt(out, polys, Ln, Ln * n_, true, s);
+    }
+  }
+}
+
+void RnsTool::set_unbias(const uint64_t* ones_ntt, hipStream_t s) {
+  ones_ntt_ = ones_ntt;
+  if (!ones_ntt) return;
+  const size_t size_Ql = base_Ql_.size();
+  k_md_ = size_P_ / 2;
+  k_mdr_ = (size_P_ + 1) / 2;
+  std::vector<uint64_t> a(size_Ql), as(size_Ql), b(size_Ql), bs(size_Ql);
+  for (size_t i = 0; i < size_Ql; ++i) {
+    const uint64_t q = base_Ql_[i];
+    a[i] = k_md_ % q;
+    as[i] = shoup(a[i], q);
+    b[i] = k_mdr_ % q;
+    bs[i] = shoup(b[i], q);
+  }
+  d_k_md_.upload(a, s);
+  d_k_md_shoup_.upload(as, s);
+  d_k_mdr_.upload(b, s);
+  d_k_mdr_shoup_.upload(bs, s);
+}
+
+void RnsTool::unbias_ntt(uint64_t* out, size_t polys, size_t limbs, size_t stride, bool rescale, hipStream_t s) const {
+  const uint64_t* k = rescale ? d_k_mdr_.get() : d_k_md_.get();
+  const uint64_t* ks = rescale ? d_k_mdr_shoup_.get() : d_k_md_shoup_.get();
+  hip_ok(phx::mul_scalar_accumulate(ones_ntt_, k, ks, out, stride, polys, d_Ql_.get(), n_, limbs, s), "unbiased moddown");
 }
 
 void RnsTool::rescale_ntt_to(const uint64_t* in, uint64_t* const* outs, size_t cts, const phx::NttTables& ntt,

@@ -83,6 +83,16 @@ class RnsTool {
   void rescale_ntt_to(const uint64_t* in, uint64_t* const* outs, size_t cts, const phx::NttTables& ntt,
                       hipStream_t s) const;
 
+  // Opt-in mean-unbiased moddown (PhantomContext::set_unbiased_moddown; DESIGN.md §3 "Where the
+  // precision goes").  A division by D = P (moddown) or P q_last (moddown + rescale) through the
+  // fast conversion of ibase limbs returns floor(c / D) - u with u the conversion's overflow, a
+  // mean bias of -1/2 - (ibase - 1) / 2 per coefficient (src/rns_bconv.cu:791-843 has no overflow
+  // correction).  With `ones_ntt` = NTT(1, ..., 1) over Q ([size_Q][n]), every such division adds
+  // floor(ibase / 2) to each output coefficient: zero mean for an even ibase, +-1/2 for an odd
+  // one (the plain rescale's own).  nullptr = off: the reference's arithmetic, bit for bit.
+  void set_unbias(const uint64_t* ones_ntt, hipStream_t s);
+  bool unbiased() const { return ones_ntt_ != nullptr; }
+
   // scratch space shared by the drivers (owned by the PhantomContext)
   void set_workspace(Workspace* ws) { ws_ = ws; }
   Workspace& workspace() const { return *ws_; }
@@ -116,6 +126,13 @@ class RnsTool {
   DeviceBuffer<uint64_t> d_bigP_mod_q_, d_bigP_mod_q_shoup_, d_bigPInv_mod_q_, d_bigPInv_mod_q_shoup_;
   // rescale
   DeviceBuffer<uint64_t> d_inv_qlast_, d_inv_qlast_shoup_;
+  // unbiased moddown (set_unbias): k mod q_l and its Shoup quotient over Ql, for the moddown
+  // (k = floor(size_P / 2)) and the moddown + rescale (k = floor((size_P + 1) / 2))
+  const uint64_t* ones_ntt_ = nullptr;
+  uint64_t k_md_ = 0, k_mdr_ = 0;
+  DeviceBuffer<uint64_t> d_k_md_, d_k_md_shoup_, d_k_mdr_, d_k_mdr_shoup_;
+  // out [polys][limbs][n] at poly stride `stride`, NTT form: += k NTT(1, ..., 1)
+  void unbias_ntt(uint64_t* out, size_t polys, size_t limbs, size_t stride, bool rescale, hipStream_t s) const;
 };
 
 }  // namespace phantom

@@ -37,6 +37,7 @@ _SIGS = {
     "phantom_context_create": (ctypes.c_int, [sz, u64p, sz, sz, ctypes.POINTER(vp)]),
     "phantom_context_destroy": (ctypes.c_int, [vp]),
     "phantom_context_coeff_modulus_size": (sz, [vp, sz]),
+    "phantom_context_set_unbiased_moddown": (ctypes.c_int, [vp, ctypes.c_int]),
     "phantom_multiply": (ctypes.c_int, [vp, sz, vp, vp, vp, vp]),
     "phantom_square": (ctypes.c_int, [vp, sz, vp, vp, vp]),
     "phantom_relinearize": (ctypes.c_int, [vp, sz, vp, ctypes.POINTER(vp), sz, vp]),
@@ -177,6 +178,10 @@ class Context:
 
     def ql(self, chain_index):
         return self.moduli[:self.size_Q - (chain_index - 1)]
+
+    def set_unbiased_moddown(self, on):
+        """Opt-in mean-unbiased moddowns (phantom_context_set_unbiased_moddown); off by default."""
+        check(load().phantom_context_set_unbiased_moddown(self.handle, 1 if on else 0))
 
     def close(self):
         if self.handle:

@@ -45,3 +45,33 @@ def test_precision_tail_is_slot_zero():
         if r["avg_bits"] < 9.5:
             assert min(abs(r["I0"]), abs(r["I_half"])) <= 4, r
     assert sum(r["avg_bits"] for r in rows) / len(rows) > 9.9
+
+
+def _tail_rows(env_extra, args):
+    env = dict(os.environ, TAIL_KEY_SEED="0x7A11", TAIL_ONLY_I0="1", **env_extra)
+    out = subprocess.run([EXE, "tail", *args], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    s_zeta = {l["key"]: abs(complex(*l["s_zeta"])) for l in lines if "s_zeta" in l}
+    return [dict(r, s=s_zeta[r["key"]]) for r in lines if "I_half" in r]
+
+
+def test_unbiased_moddown_removes_the_slot_zero_offset():
+    """The opt-in unbiased moddown (PHX_UNBIASED_MODDOWN=1, include/phantom_amd.h
+    phantom_context_set_unbiased_moddown) on the slot-0 events of three seeded keys (the same keys
+    and ciphertexts both times; profiles/r06/unbiased/): with the reference's arithmetic the
+    offset reaches 1.5e-5 |s(zeta)| and the worst event is below 9.5 bits (8.7 measured); with the
+    option every event stays within 2.5e-6 |s(zeta)| + 1e-4 (1.3e-6 measured) and above 9.6 bits
+    (9.81 measured)."""
+    off = _tail_rows({"PHX_UNBIASED_MODDOWN": "0"}, ["16", "6", "3"])
+    on = _tail_rows({"PHX_UNBIASED_MODDOWN": "1"}, ["16", "6", "3"])
+    assert len(off) == len(on) == 18
+    for a, b in zip(off, on):
+        assert (a["key"], a["I0"], a["I_half"]) == (b["key"], b["I0"], b["I_half"])  # same ciphertexts
+    # slot 0's deviation: coefficient 0 from the reference's -0.0027 constant, plus i coefficient N/2
+    dev = lambda r: abs(complex(r["e0"] + 2.7e-3, r["e_half"]))
+    assert min(r["avg_bits"] for r in off) < 9.5
+    assert max(dev(r) / r["s"] for r in off) > 1.0e-5
+    for r in on:
+        assert dev(r) <= 2.5e-6 * r["s"] + 1e-4, r
+        assert r["avg_bits"] > 9.6, r
