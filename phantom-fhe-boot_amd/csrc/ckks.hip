@@ -650,6 +650,7 @@ hipError_t mul_scalar_accumulate(const uint64_t* in, const uint64_t* c, const ui
                                  size_t poly_stride, size_t polys, const uint64_t* q, size_t n, size_t L, hipStream_t s) {
   const size_t total = n * L;
   if (polys == 0 || total == 0) return hipSuccess;
+  if (polys > 65535) return hipErrorInvalidValue;  // grid.y
   const dim3 grid(static_cast<unsigned>(std::max<size_t>(1, grid_for(total) / polys)), static_cast<unsigned>(polys));
   mul_scalar_add_kernel<<<grid, kBlock, 0, s>>>(in, c, c_shoup, out, out, q, __builtin_ctzll(n), total, poly_stride);
   return hipGetLastError();
